@@ -1,0 +1,302 @@
+/*
+ * rlp.h — C-ABI of the MI355X (gfx950) batched env-step + PPO2 rollout library (librlp.so).
+ *
+ * This is the drop-in boundary for the reference's on-policy hot path
+ * (HKPolyU-UAV/ReinforcementLearningPlatform). Every entry point replaces one
+ * piece of per-env Python/numpy/torch-CPU code; the reference interface it replaces is cited
+ * (path:line, relative to the reference root) next to each declaration.
+ *
+ * Conventions
+ *  - All array pointers are DEVICE pointers (e.g. torch.Tensor.data_ptr() on cuda), unless a
+ *    parameter is documented as host memory. Param structs are host memory and are passed to the
+ *    kernels by value.
+ *  - Physics state is float64, struct-of-arrays: state[d * n + i] is component d of env i.
+ *    Observations / actions are float32, env-major: obs[i * S + s].
+ *    Rollout buffers are time-major: buf[(t * n + i) * S + s]  (== RolloutBuffer rows, T*n of them).
+ *  - Every call is stream-ordered on `stream` (a hipStream_t; NULL = the legacy default stream)
+ *    and never synchronises the host unless documented.
+ *  - Return value: RLP_OK (0) on success; RLP_EINVAL / RLP_EUNSUPPORTED on bad arguments;
+ *    -(int)hipError_t for a HIP launch error. Nothing throws or aborts across the ABI.
+ *    rlp_last_error_string() returns a thread-local description of the last failure.
+ *  - The library allocates no device memory. Callers own every buffer.
+ */
+#ifndef RLP_H_
+#define RLP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *rlp_stream_t; /* hipStream_t */
+
+#define RLP_OK 0
+#define RLP_EINVAL (-1000)
+#define RLP_EUNSUPPORTED (-1001)
+
+#define RLP_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------------------------ */
+/* Environment kinds. Each kind is one specific reference env copy (copies diverge). */
+/* ------------------------------------------------------------------------------------------ */
+enum rlp_env_kind {
+    /* environment/CartPole/CartPole.py (== demonstration/PPO2/PPO2-4-CartPole/CartPole.py;
+       DPPO2 copy differs only in the reset law, expressed through the params). */
+    RLP_ENV_CARTPOLE = 1,
+    /* demonstration/PPO2/PPO2-4-CartPoleAngleOnly/cartpole_angleonly.py */
+    RLP_ENV_CARTPOLE_ANGLEONLY = 2,
+    /* environment/SecondOrderIntegration/SecondOrderIntegration.py (+ DPPO2/DDPG copy via params) */
+    RLP_ENV_SOI = 3,
+    /* environment/UGV/UGVForward.py (+ PPO2/DPPO2 copies via params) */
+    RLP_ENV_UGV_FORWARD = 4,
+    /* environment/UGV/UGVBidirectional.py (+ PPO2 copy via params) */
+    RLP_ENV_UGV_BIDIRECTIONAL = 5,
+    /* environment/UavRobust/UavHoverOuterLoop.py: 6-DoF rigid body (uav.py) + FNTSMC attitude
+       loop (FNTSMC.py) driven by an RL virtual-acceleration command. */
+    RLP_ENV_UAV_HOVER_OUTER_LOOP = 6,
+};
+
+/* Physics-state dimension D, observation dim S and action dim A per kind (also queryable). */
+#define RLP_CARTPOLE_D 5  /* theta, dtheta, x, dx, time */
+#define RLP_ANGLEONLY_D 5 /* theta, dtheta, x, dx, time */
+#define RLP_SOI_D 7       /* x, y, vx, vy, time, target_x, target_y */
+#define RLP_UGV_D 8       /* x, y, vel, phi, omega, time, target_x, target_y */
+#define RLP_UAV_D 22      /* x y z vx vy vz phi theta psi p q r | time | pos_ref[3] | s1[3] | att_ref[3] */
+
+/* CartPole.py:27-46 (physical constants), :187-217 get_reward literals, :273-274 reset law. */
+typedef struct rlp_cartpole_params {
+    double theta_max;   /* deg2rad(45) */
+    double dtheta_max;  /* deg2rad(90) */
+    double x_max;       /* 1.5 */
+    double dx_max;      /* 3 */
+    double static_gain; /* 2.0 */
+    double M, m, g, ell, kf;
+    double fm;       /* 8: action range [-fm, fm] */
+    double dt;       /* 0.02 */
+    double time_max; /* 5 */
+    double reset_theta_lo, reset_theta_hi; /* theta0 ~ U(lo, hi) */
+    double reset_x_lo, reset_x_hi;         /* x0 ~ U(lo, hi) */
+    double Q_x, Q_dx, Q_theta, Q_omega, R; /* get_reward :192-196 */
+    int32_t n_sub_div; /* h = dt / n_sub_div, `while time < tt` (CartPole.py:242-252) */
+    int32_t reserved;
+} rlp_cartpole_params;
+
+/* cartpole_angleonly.py:27-41, get_reward :170-195 (Q_theta, Q_omega, R), reset :245-279. */
+typedef struct rlp_angleonly_params {
+    double theta_max;   /* deg2rad(45) */
+    double static_gain; /* 2.0 */
+    double norm_dtheta; /* norm_4_boundless_state = 4 */
+    double M, m, g, ell, kf;
+    double fm;       /* 5 */
+    double dt;       /* 0.02: one RK4 step of h = dt (:218-229) */
+    double time_max; /* 5 */
+    double reset_theta_lo, reset_theta_hi;
+    double Q_theta, Q_omega, R; /* 10, 0, 0 */
+} rlp_angleonly_params;
+
+/* SecondOrderIntegration.py:13-60, reward :251-284, reset :328-352. */
+typedef struct rlp_soi_params {
+    double map_size[2]; /* 5, 5 */
+    double k;           /* 0.15 linear drag */
+    double mass;        /* 1.0 */
+    double dt;          /* 0.02 (one RK4 step: the `while` loop runs exactly once) */
+    double time_max;    /* 5.0 */
+    double v_max;       /* 3 (obs normaliser) */
+    double f_max;       /* 3: action range [-f_max, f_max]^2 */
+    double admissible_error; /* 0 */
+    double obs_gain;    /* 1 for the env file; 2 (static_gain) in the DPPO2/DDPG copies */
+    double reset_margin; /* 0.1: pos ~ U(0+m, map-m) */
+    double Q_pos, Q_vel, Q_acc; /* 1, 0.1, 0.05 (DPPO2/DDPG copies: 1, 0, 0) */
+    int32_t success_enabled;    /* 1: flag 3 on success (env file); 0 in the DPPO2/DDPG copies */
+    int32_t reserved;
+} rlp_soi_params;
+
+/* UGVForward.py / UGVBidirectional.py:34-63, reward :263-279, reset :334-362. */
+typedef struct rlp_ugv_params {
+    double map_size[2]; /* 5, 5 */
+    double dt;          /* 0.02 */
+    double time_max;    /* 10 (DPPO2 UGVForward copy: 5) */
+    double kf, kt;      /* 0.1, 0.1 */
+    double v_max;       /* 3 */
+    double omega_max;   /* 2*pi */
+    double a_linear_max;  /* 3 */
+    double a_angular_max; /* 2*pi */
+    double static_gain;   /* 1 */
+    double reset_margin;  /* 0.5 */
+    double Q_pos, Q_vel, Q_phi, Q_omega; /* 2, 0 (PPO2/DPPO2 copies: 0.1), 2, 1 */
+    int32_t phi_gate_abs; /* u_phi active if |e| > 0.1 (PPO2 Bidirectional copy) vs e > 0.1 */
+    int32_t reserved;
+} rlp_ugv_params;
+
+/* uav.py:12-31 uav_param; FNTSMC.py:4-15 fntsmc_param (attitude loop);
+   UavHoverOuterLoop.py:33-43 limits, :93-110 reward. Values of
+   demonstration/PPO/PPO-4-UavHoverOuterLoop/train.py:24-56. */
+typedef struct rlp_uav_hover_params {
+    double m, g;
+    double J[3];
+    double kr, kt;
+    double dt, time_max;
+    double pos0[3], vel0[3], angle0[3], pqr0[3];
+    double pos_zone[3][2];
+    double att_zone[3][2];
+    double att_k1[3], att_k2[3], att_alpha[3], att_beta[3], att_gamma[3], att_lmd[3];
+    double att_saturation[3];
+    double att_ctrl_dt;
+    double static_gain;
+    double e_pos_max[3], e_pos_min[3];
+    double vel_max[3], vel_min[3];
+    double dot_att_min[3], dot_att_max[3];
+    double u_min, u_max;
+    double target_offset; /* generate_random_point(offset=1.0) */
+    double Qx, Qv, R;     /* 1, 0.1, 0.02 */
+} rlp_uav_hover_params;
+
+/* Dimensions of a kind. Returns RLP_EINVAL for an unknown kind. Host-only, no device work. */
+int rlp_env_dims(int kind, int *D, int *S, int *A);
+
+/* rl_base.reset(random) — e.g. CartPole.py:266-295, UavHoverOuterLoop.py:152-214.
+ * For every env i with (mask == NULL || mask[i] != 0):
+ *   init_state != NULL : state[:, i] = init_state[:, i]            (f64, [D][n], teacher forcing)
+ *   init_state == NULL : reset law with a counter-based Philox4x32-10 stream keyed by
+ *                        (seed, counter, env_id0 + i): bit-identical on every rank/GPU.
+ * Hidden controller state that the reference carries across resets (UAV s1 / att_ref,
+ * UavHoverOuterLoop.py:152-208) is carried here too. */
+int rlp_env_reset(int kind, const void *params, double *state, int n, const uint8_t *mask,
+                  const double *init_state, uint64_t seed, uint64_t counter, uint64_t env_id0,
+                  rlp_stream_t stream);
+
+/* rl_base.get_state() (e.g. CartPole.py:145-153): obs[i*S+s] (f32). */
+int rlp_env_observe(int kind, const void *params, const double *state, int n, float *obs,
+                    rlp_stream_t stream);
+
+/* rl_base.step_update(action) (CartPole.py:257-264; SecondOrderIntegration.py:316-326;
+ * UGVForward.py:322-332; UavHoverOuterLoop.py:115-150), one env per lane, f64 physics.
+ * action [n][A] f32 (the dtype choose_action hands to step_update). Outputs:
+ *   obs_cur  [n][S] f32  current_state before the step (nullable)
+ *   obs_next [n][S] f32  next_state
+ *   reward   [n]    f64  env.reward
+ *   flag     [n]    i32  terminal_flag
+ *   done     [n]    u8   is_terminal                                                    */
+int rlp_env_step(int kind, const void *params, double *state, int n, const float *action,
+                 float *obs_cur, float *obs_next, double *reward, int32_t *flag, uint8_t *done,
+                 rlp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Policy / value networks: Linear(+tanh) stacks defined by the demo drivers                   */
+/* (demonstration/PPO2/PPO2-4-CartPole/train.py:39-125: fc1/fc2/mean_layer, fc1/fc2/fc3).      */
+/* ------------------------------------------------------------------------------------------ */
+#define RLP_MLP_MAX_LAYERS 8
+enum rlp_act { RLP_ACT_NONE = 0, RLP_ACT_TANH = 1, RLP_ACT_RELU = 2 };
+
+typedef struct rlp_mlp_desc {
+    int32_t n_layers;                    /* number of Linear layers */
+    int32_t dims[RLP_MLP_MAX_LAYERS + 1]; /* dims[0] = in, dims[l+1] = out of layer l */
+    int32_t act[RLP_MLP_MAX_LAYERS];     /* activation after layer l */
+} rlp_mlp_desc;
+
+/* Plain parameter layout: for each layer l: W_l row-major [out][in] then b_l [out]
+ * (== torch.cat([p.flatten() for p in module.parameters()]) for Linear stacks). */
+int64_t rlp_mlp_param_count(const rlp_mlp_desc *desc);
+
+/* Batched forward y[n][out] = MLP(x[n][in]) (nn.Sequential / driver forward()), fp32, MFMA
+ * (v_mfma_f32_16x16x4_f32) for every layer; rows with mask[i]==0 are skipped (mask nullable). */
+int rlp_mlp_forward(const rlp_mlp_desc *desc, const float *params, const float *x, float *y, int n,
+                    const uint8_t *mask, rlp_stream_t stream);
+
+/* Size (floats) and packing of the MFMA-fragment layout used by rlp_rollout for a
+ * [S -> H -> H -> A] tanh network (H in {64,128,256}). Returns RLP_EUNSUPPORTED otherwise. */
+int64_t rlp_mfma_packed_count(const rlp_mlp_desc *desc);
+int rlp_mfma_pack(const rlp_mlp_desc *desc, const float *params, float *packed, rlp_stream_t stream);
+
+/* Proximal_Policy_Optimization2.choose_action (Proximal_Policy_Optimization2.py:69-76):
+ *   a = clamp(mean + std*eps, a_min, a_max);  logp = Normal(mean, std).log_prob(a)  (per dim)
+ * eps from `noise` [n][A] if non-NULL, else Philox normals keyed (seed, counter, env_id0+i).
+ * std, a_min, a_max: HOST arrays of A floats. */
+int rlp_policy_sample(const float *mean, int n, int A, const float *std, const float *a_min,
+                      const float *a_max, const float *noise, uint64_t seed, uint64_t counter,
+                      uint64_t env_id0, float *action, float *logp, rlp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Fused batched rollout (demonstration/PPO2/PPO2-4-CartPole/train.py:184-217 for n envs):    */
+/* T x { auto-reset, actor forward + Gaussian sample, critic V(s), env step, buffer append }  */
+/* ------------------------------------------------------------------------------------------ */
+enum rlp_success_rule {
+    RLP_SUCCESS_DONE_AND_FLAG_NE = 0, /* done && flag != F  (PPO2 drivers, train.py:199-205) */
+    RLP_SUCCESS_FLAG_NE = 1,          /* flag != F, also on non-terminal steps (DPPO2 CartPole,
+                                         DPPO2-4-CartPole/Distributed_PPO2.py:138) */
+    RLP_SUCCESS_FLAG_EQ = 2,          /* flag == F  (PPO-4-UavHoverOuterLoop/train.py:217) */
+};
+
+typedef struct rlp_rollout_bufs {
+    float *obs;        /* [T][n][S] s_t                                     (RolloutBuffer.s)   */
+    float *obs_next;   /* [T][n][S] s'_t                                    (RolloutBuffer.s_)  */
+    float *action;     /* [T][n][A]                                         (RolloutBuffer.a)   */
+    float *logp;       /* [T][n][A]                                         (RolloutBuffer.a_lp)*/
+    float *reward;     /* [T][n]   raw env.reward (normalised later)        (RolloutBuffer.r)   */
+    float *value;      /* [T][n]   V(s_t)                                                        */
+    float *value_next; /* [T][n]   V(s'_t) where !done (== V(s_{t+1})); done rows left for
+                                   rlp_mlp_forward(mask=done) (critic on s'_t)                  */
+    uint8_t *done;     /* [T][n]                                            (RolloutBuffer.done)*/
+    uint8_t *success;  /* [T][n]                                            (RolloutBuffer.success)*/
+    int8_t *flag;      /* [T][n]   terminal_flag                                                 */
+} rlp_rollout_bufs;
+
+typedef struct rlp_rollout_cfg {
+    int32_t T;            /* steps per env in this segment */
+    int32_t n;            /* envs on this device */
+    uint64_t seed;        /* Philox key */
+    uint64_t step0;       /* global step counter of the first step (Philox counter) */
+    uint64_t env_id0;     /* global id of env 0 on this device (rank * n) */
+    int32_t success_rule; /* enum rlp_success_rule */
+    int32_t success_flag; /* F */
+    float std[4];         /* actor.std per action dim (host values) */
+    float a_min[4], a_max[4];
+} rlp_rollout_cfg;
+
+/* state: [D][n] f64 in/out, carried across segments. need_reset: [n] u8 in/out (1 = env is
+ * terminal / fresh and resets, with the reset law, before its next step; the reference driver's
+ * `if env.is_terminal: env.reset(random=True)`, train.py:187-191). actor/critic: MFMA-packed
+ * (rlp_mfma_pack). Supported kinds: RLP_ENV_CARTPOLE, RLP_ENV_CARTPOLE_ANGLEONLY,
+ * RLP_ENV_UGV_FORWARD, RLP_ENV_UGV_BIDIRECTIONAL, RLP_ENV_SOI, RLP_ENV_UAV_HOVER_OUTER_LOOP
+ * with actor [S->H->H->A] (tanh, tanh, tanh*gain+off) and critic [S->H->H->1]. */
+int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_reset,
+                const rlp_mlp_desc *actor_desc, const float *actor_packed,
+                const rlp_mlp_desc *critic_desc, const float *critic_packed,
+                const rlp_rollout_cfg *cfg, const rlp_rollout_bufs *bufs, rlp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Learn-side scans (Proximal_Policy_Optimization2.learn, :84-100; utils/classes.py:626-656)   */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Normalization(shape=1) over the rollout's reward stream (utils/classes.py:647-656):
+ * time step t's n rewards are merged into the running statistics in env order (Welford when
+ * n == 1, reproducing the reference exactly including the first-call std = x quirk; Chan's
+ * parallel merge otherwise), then every reward of step t is normalised with the statistics
+ * after that merge. rms: device f64[4] = {count, mean, S, std}, in/out across segments.
+ * work: device f64[3*T] scratch. reward_out may alias reward_in. */
+int rlp_reward_norm(const float *reward_in, int T, int n, double *rms, double *work,
+                    float *reward_out, rlp_stream_t stream);
+
+/* GAE(lambda) backward scan per env (Proximal_Policy_Optimization2.py:93-98), fp32 in the
+ * reference's exact operation order (bit-identical to the NumPy-2 loop):
+ *   delta = (r + ((float)gamma * (1 - success)) * v_next) - v
+ *   gae   = delta + ((float)(gamma*lambda) * gae) * (1 - done)
+ *   adv = gae; v_target = adv + v
+ * All arrays [T][n]. adv_stats (device f64[2], nullable): += {sum(adv), sum(adv^2)}. */
+int rlp_gae(const float *reward, const float *value, const float *value_next, const uint8_t *done,
+            const uint8_t *success, double gamma, double lambda, int T, int n, float *adv,
+            float *v_target, double *adv_stats, rlp_stream_t stream);
+
+/* adv = (adv - mean) / (std_unbiased + 1e-5) from adv_stats = {sum, sumsq} (Trick 1, :99-100). */
+int rlp_adv_normalize(float *adv, int64_t count, const double *adv_stats, rlp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------ */
+const char *rlp_last_error_string(void);
+int rlp_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RLP_H_ */

@@ -1,0 +1,525 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE's own Python code.
+
+Run only in the build container (the reference is mounted read-only at /root/reference and never
+travels to the GPU box):    python tests/golden/make_golden.py [/root/reference]
+
+What is recorded (inputs and expected outputs only — no reference source is copied):
+  * per env copy: teacher-forced single steps (state, float32 action -> next state, obs, reward,
+    terminal flag), incl. threshold-straddling states and both RK4 sub-step regimes (CartPole);
+  * UAV hover outer loop: multi-step sequences incl. the carried FNTSMC controller state;
+  * the PPO2-CartPole shipped actor/critic (datasave/net, loaded with weights_only=True):
+    forward on random inputs, choose_action samples, and the deterministic closed-loop
+    known answer;
+  * Proximal_Policy_Optimization2.learn()'s GAE / v_target / advantage normalisation;
+  * utils.classes.Normalization on a reward stream.
+cv2 is absent here and only used for drawing: it is replaced by a no-op module.
+"""
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+
+sys.dont_write_bytecode = True
+REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _install_cv2_stub():
+    cv2 = types.ModuleType("cv2")
+
+    def _noop(*a, **k):
+        return -1
+    for name in ("imshow", "waitKey", "rectangle", "line", "circle", "putText", "destroyAllWindows",
+                 "VideoWriter", "VideoWriter_fourcc", "fillPoly", "ellipse", "arrowedLine",
+                 "polylines", "namedWindow", "imwrite"):
+        setattr(cv2, name, _noop)
+    cv2.FONT_HERSHEY_COMPLEX = 0
+    cv2.FONT_HERSHEY_SIMPLEX = 0
+    cv2.LINE_AA = 0
+    sys.modules["cv2"] = cv2
+
+
+_install_cv2_stub()
+for p in (REF, os.path.join(REF, "environment/UavRobust")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402  (after the stub; seeds are set after all imports)
+
+
+def load(path, name):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REF, path))
+    mod = importlib.util.module_from_spec(spec)
+    sys.path.insert(0, os.path.dirname(os.path.join(REF, path)))
+    try:
+        spec.loader.exec_module(mod)
+    finally:
+        sys.path.pop(0)
+    return mod
+
+
+import contextlib, io  # noqa: E402
+
+
+@contextlib.contextmanager
+def quiet():
+    with contextlib.redirect_stdout(io.StringIO()):
+        yield
+
+
+# ---------------------------------------------------------------------------------------------
+mods = {}
+with quiet():
+    mods["cp_ppo2"] = load("demonstration/PPO2/PPO2-4-CartPole/CartPole.py", "ref_cp_ppo2")
+    mods["cp_dppo2"] = load("demonstration/DPPO2/DPPO2-4-CartPole/CartPole.py", "ref_cp_dppo2")
+    mods["ao_ppo2"] = load("demonstration/PPO2/PPO2-4-CartPoleAngleOnly/cartpole_angleonly.py",
+                           "ref_ao_ppo2")
+    mods["soi_env"] = load("environment/SecondOrderIntegration/SecondOrderIntegration.py", "ref_soi")
+    mods["soi_dppo2"] = load("demonstration/DPPO2/DPPO2-4-SecondOrderIntegration/"
+                             "SecondOrderIntegration.py", "ref_soi_dppo2")
+    mods["ugvf_env"] = load("environment/UGV/UGVForward.py", "ref_ugvf")
+    mods["ugvf_ppo2"] = load("demonstration/PPO2/PPO2-4-UGVForward/UGVForward.py", "ref_ugvf_ppo2")
+    mods["ugvf_dppo2"] = load("demonstration/DPPO2/DPPO2-4-UGVForward/UGVForward.py",
+                              "ref_ugvf_dppo2")
+    mods["ugvb_env"] = load("environment/UGV/UGVBidirectional.py", "ref_ugvb")
+    mods["ugvb_ppo2"] = load("demonstration/PPO2/PPO2-4-UGVBidirectional/UGVBidirectional.py",
+                             "ref_ugvb_ppo2")
+    import environment.UavRobust.UavHoverOuterLoop as uav_mod  # noqa: E402
+    from environment.UavRobust.uav import uav_param  # noqa: E402
+    from environment.UavRobust.FNTSMC import fntsmc_param  # noqa: E402
+    ppo2_mod = load("algorithm/policy_base/Proximal_Policy_Optimization2.py", "ref_ppo2")
+    cls_mod = load("utils/classes.py", "ref_classes")
+    drv = load("demonstration/PPO2/PPO2-4-CartPole/train.py", "ref_ppo2_cartpole_train")
+
+rng = np.random.default_rng(3407)
+torch.manual_seed(3407)
+np.random.seed(3407)
+
+
+def f32(x):
+    return np.asarray(x, dtype=np.float32)
+
+
+# ---------------------------------------------------------------------------------------------
+# CartPole (PPO2 copy == env dir; DPPO2 copy)
+# ---------------------------------------------------------------------------------------------
+def cartpole_time_table(mod, steps):
+    env = mod.CartPole(0., 0.)
+    env.reset(False)
+    times = []
+    for _ in range(steps):
+        times.append(env.time)
+        env.rk44(np.array([np.float32(0.)]))
+    return np.array(times)
+
+
+def gen_cartpole(key, mod, n=600):
+    env = mod.CartPole(0., 0.)
+    tt = cartpole_time_table(mod, 245)
+    rows = {k: [] for k in ("state", "action", "state_next", "obs_cur", "obs_next", "reward",
+                            "flag", "done")}
+    th_hi = env.theta_max + np.pi / 180
+    th_lo = -env.dtheta_max - np.pi / 180
+    for i in range(n):
+        k = int(rng.integers(0, 245))
+        th = rng.uniform(-0.9, 0.9)
+        x = rng.uniform(-1.4, 1.4)
+        dth, dx = rng.uniform(-3, 3), rng.uniform(-3, 3)
+        kind = i % 8
+        if kind == 1:
+            th = th_hi + rng.uniform(-2e-3, 2e-3); dth = rng.uniform(-0.05, 0.05)
+        elif kind == 2:
+            th = th_lo + rng.uniform(-5e-3, 5e-3); dth = rng.uniform(-0.05, 0.05)
+        elif kind == 3:
+            x = np.sign(rng.uniform(-1, 1)) * (env.x_max + rng.uniform(-2e-3, 2e-3))
+            dx = rng.uniform(-0.05, 0.05)
+        elif kind == 4:
+            k = int(rng.integers(230, 245))
+        elif kind == 5:
+            th, dth, x, dx = [rng.uniform(-2e-3, 2e-3) for _ in range(4)]
+        a = np.float32(rng.uniform(-8, 8))
+        if i % 13 == 0:
+            a = np.float32(rng.choice([-8, 8]))
+        env.reset(False)
+        env.theta, env.dtheta, env.x, env.dx, env.time = th, dth, x, dx, tt[k]
+        env.etheta, env.ex = 0. - th, 0. - x
+        rows["state"].append([th, dth, x, dx, tt[k]])
+        env.step_update(np.array([a], dtype=np.float32))
+        rows["action"].append([a])
+        rows["state_next"].append([env.theta, env.dtheta, env.x, env.dx, env.time])
+        rows["obs_cur"].append(env.current_state)
+        rows["obs_next"].append(env.next_state)
+        rows["reward"].append(float(env.reward))
+        rows["flag"].append(env.terminal_flag)
+        rows["done"].append(int(env.is_terminal))
+    out = {k: np.array(v) for k, v in rows.items()}
+    out["action"] = out["action"].astype(np.float32)
+    out["time_table"] = tt
+    np.savez(os.path.join(OUT, f"{key}.npz"), **out)
+    print(key, {k: v.shape for k, v in out.items()}, "flags", np.bincount(out["flag"]))
+
+
+def gen_angleonly(key, mod, n=400):
+    env = mod.CartPoleAngleOnly(0.)
+    rows = {k: [] for k in ("state", "action", "state_next", "obs_cur", "obs_next", "reward",
+                            "flag", "done")}
+    th_hi = env.thetaMax + np.pi / 180
+    for i in range(n):
+        k = int(rng.integers(0, 252))
+        th, dth = rng.uniform(-0.85, 0.85), rng.uniform(-4, 4)
+        x, dx = rng.uniform(-2, 2), rng.uniform(-2, 2)
+        if i % 6 == 1:
+            th = np.sign(rng.uniform(-1, 1)) * (th_hi + rng.uniform(-2e-3, 2e-3))
+            dth = rng.uniform(-0.05, 0.05)
+        elif i % 6 == 2:
+            k = int(rng.integers(245, 252))
+        elif i % 6 == 3:
+            th, dth = rng.uniform(-2e-3, 2e-3), rng.uniform(-2e-3, 2e-3)
+        tm = 0.
+        for _ in range(k):
+            tm += env.dt
+        a = np.float32(rng.uniform(-5, 5))
+        with quiet():
+            env.reset(False)
+            env.theta, env.dtheta, env.x, env.dx, env.time = th, dth, x, dx, tm
+            rows["state"].append([th, dth, x, dx, tm])
+            env.step_update(np.array([a], dtype=np.float32))
+        rows["action"].append([a])
+        rows["state_next"].append([env.theta, env.dtheta, env.x, env.dx, env.time])
+        rows["obs_cur"].append(env.current_state)
+        rows["obs_next"].append(env.next_state)
+        rows["reward"].append(float(env.reward))
+        rows["flag"].append(env.terminal_flag)
+        rows["done"].append(int(env.is_terminal))
+    out = {k: np.array(v) for k, v in rows.items()}
+    out["action"] = out["action"].astype(np.float32)
+    np.savez(os.path.join(OUT, f"{key}.npz"), **out)
+    print(key, "flags", np.bincount(out["flag"]))
+
+
+def gen_soi(key, mod, n=400):
+    env = mod.SecondOrderIntegration()
+    rows = {k: [] for k in ("state", "action", "state_next", "obs_cur", "obs_next", "reward",
+                            "flag", "done")}
+    for i in range(n):
+        k = int(rng.integers(0, 252))
+        tm = 0.
+        for _ in range(k):
+            tm += env.dt
+        pos = rng.uniform(-0.1, 5.1, 2)
+        vel = rng.uniform(-3, 3, 2)
+        if i % 5 == 1:
+            pos = np.array([2.5, 2.5]) + rng.uniform(-0.03, 0.03, 2); vel = rng.uniform(-0.03, 0.03, 2)
+        elif i % 5 == 2:
+            k = int(rng.integers(245, 252))
+        a = f32(rng.uniform(-3, 3, 2))
+        with quiet():
+            env.reset(False)
+            env.pos = pos.copy(); env.vel = vel.copy(); env.time = tm
+            env.target = np.array([2.5, 2.5])
+            rows["state"].append([pos[0], pos[1], vel[0], vel[1], tm, 2.5, 2.5])
+            env.step_update(a)
+        rows["action"].append(a)
+        rows["state_next"].append([env.pos[0], env.pos[1], env.vel[0], env.vel[1], env.time,
+                                   env.target[0], env.target[1]])
+        rows["obs_cur"].append(env.current_state)
+        rows["obs_next"].append(env.next_state)
+        rows["reward"].append(float(env.reward))
+        rows["flag"].append(env.terminal_flag)
+        rows["done"].append(int(env.is_terminal))
+    out = {k: np.array(v) for k, v in rows.items()}
+    out["action"] = out["action"].astype(np.float32)
+    np.savez(os.path.join(OUT, f"{key}.npz"), **out)
+    print(key, "flags", np.bincount(out["flag"]))
+
+
+def gen_ugv(key, cls, n=400):
+    env = cls()
+    rows = {k: [] for k in ("state", "action", "state_next", "obs_cur", "obs_next", "reward",
+                            "flag", "done")}
+    for i in range(n):
+        k = int(rng.integers(0, 502))
+        tm = 0.
+        for _ in range(k):
+            tm += env.dt
+        pos = rng.uniform(-0.05, 5.05, 2)
+        vel = rng.uniform(-1, 3)
+        phi = rng.uniform(-np.pi, np.pi)
+        om = rng.uniform(-3, 3)
+        if i % 6 == 1:
+            pos = np.array([2.5, 2.5]) + rng.uniform(-0.04, 0.04, 2); vel = rng.uniform(-0.02, 0.02)
+        elif i % 6 == 2:
+            k = int(rng.integers(250, 502))
+            tm = 0.
+            for _ in range(k):
+                tm += env.dt
+        elif i % 6 == 3:
+            phi = np.sign(rng.uniform(-1, 1)) * (np.pi - rng.uniform(0, 0.02)); om = 3 * np.sign(phi)
+        a = f32([rng.uniform(-3, 3), rng.uniform(-2 * np.pi, 2 * np.pi)])
+        with quiet():
+            env.reset(False)
+            env.pos = pos.copy(); env.vel = vel; env.phi = phi; env.omega = om; env.time = tm
+            env.target = np.array([2.5, 2.5])
+            rows["state"].append([pos[0], pos[1], vel, phi, om, tm, 2.5, 2.5])
+            env.step_update(a)
+        rows["action"].append(a)
+        rows["state_next"].append([env.pos[0], env.pos[1], env.vel, env.phi, env.omega, env.time,
+                                   env.target[0], env.target[1]])
+        rows["obs_cur"].append(env.current_state)
+        rows["obs_next"].append(env.next_state)
+        rows["reward"].append(float(env.reward))
+        rows["flag"].append(env.terminal_flag)
+        rows["done"].append(int(env.is_terminal))
+    out = {k: np.array(v) for k, v in rows.items()}
+    out["action"] = out["action"].astype(np.float32)
+    np.savez(os.path.join(OUT, f"{key}.npz"), **out)
+    print(key, "flags", np.bincount(out["flag"]))
+
+
+# ---------------------------------------------------------------------------------------------
+# UAV hover outer loop (params of demonstration/PPO/PPO-4-UavHoverOuterLoop/train.py:24-56)
+# ---------------------------------------------------------------------------------------------
+def make_uav():
+    up = uav_param()
+    up.m = 0.8; up.g = 9.8; up.J = np.array([4.212e-3, 4.212e-3, 8.255e-3]); up.d = 0.12
+    up.CT = 2.168e-6; up.CM = 2.136e-8; up.J0 = 1.01e-5; up.kr = 1e-3; up.kt = 1e-3
+    up.pos0 = np.array([0, 0, 0]); up.vel0 = np.array([0, 0, 0]); up.angle0 = np.array([0, 0, 0])
+    up.pqr0 = np.array([0, 0, 0]); up.dt = 0.01; up.time_max = 10
+    up.pos_zone = np.atleast_2d([[-5, 5], [-5, 5], [0, 5]])
+    ap = fntsmc_param()
+    ap.k1 = np.array([25, 25, 40]); ap.k2 = np.array([0.1, 0.1, 0.2])
+    ap.alpha = np.array([2.5, 2.5, 2.5]); ap.beta = np.array([0.99, 0.99, 0.99])
+    ap.gamma = np.array([1.5, 1.5, 1.2]); ap.lmd = np.array([2.0, 2.0, 2.0]); ap.dim = 3
+    ap.dt = 0.01; ap.ctrl0 = np.array([0., 0., 0.]); ap.saturation = np.array([0.3, 0.3, 0.3])
+    with quiet():
+        env = uav_mod.uav_hover_outer_loop(up, fntsmc_param(), ap, target0=np.array([-1, 3, 2]))
+    env.msg_print_flag = False
+    return env
+
+
+def uav_full_state(env):
+    return np.concatenate([env.uav_state_call_back(), [env.time], env.pos_ref, env.att_ctrl.s1,
+                           env.att_ref])
+
+
+def gen_uav(key, n_seq=24, seq_len=60):
+    env = make_uav()
+    seqs = {k: [] for k in ("state", "action", "state_next", "obs_cur", "obs_next", "reward",
+                            "flag", "done")}
+    for q in range(n_seq):
+        with quiet():
+            env.reset(random=True)
+        # perturb the fresh episode so both calm and aggressive regimes are covered
+        env.x, env.y, env.z = rng.uniform(-1, 1), rng.uniform(-1, 1), rng.uniform(0.5, 3)
+        env.vx, env.vy, env.vz = rng.uniform(-1, 1, 3)
+        env.phi, env.theta, env.psi = rng.uniform(-0.3, 0.3, 3)
+        env.p, env.q, env.r = rng.uniform(-1, 1, 3)
+        env.att_ctrl.s1 = rng.uniform(-0.2, 0.2, 3)
+        env.att_ref = rng.uniform(-0.2, 0.2, 3)
+        if q % 6 == 1:  # heading for the floor: position-out (flag 2)
+            env.z, env.vz = rng.uniform(0.02, 0.2), -1.5
+        elif q % 6 == 2:  # rolling hard: attitude-out (flag 3)
+            env.phi, env.p = 0.7, 4.0
+        elif q % 6 == 4:  # yawing past the +-120 deg zone
+            env.psi, env.r = 2.05, 3.0
+        env.error = env.uav_pos() - env.pos_ref
+        if q % 4 == 3:
+            t0 = 0.
+            for _ in range(1000 - seq_len // 2):
+                t0 += env.dt
+            env.time = t0
+        for t in range(seq_len):
+            a = f32(rng.uniform(-8, 8, 3)) if q % 2 else f32(rng.uniform(-2, 2, 3))
+            seqs["state"].append(uav_full_state(env))
+            with quiet():
+                env.step_update(a)
+            seqs["action"].append(a)
+            seqs["state_next"].append(uav_full_state(env))
+            seqs["obs_cur"].append(env.current_state)
+            seqs["obs_next"].append(env.next_state)
+            seqs["reward"].append(float(env.reward))
+            seqs["flag"].append(env.terminal_flag)
+            seqs["done"].append(int(env.is_terminal))
+            if env.is_terminal:
+                break
+    out = {k: np.array(v) for k, v in seqs.items()}
+    out["action"] = out["action"].astype(np.float32)
+    np.savez(os.path.join(OUT, f"{key}.npz"), **out)
+    print(key, out["state"].shape, "flags", np.bincount(out["flag"]))
+
+
+# ---------------------------------------------------------------------------------------------
+# Shipped PPO2-CartPole nets: forward, choose_action, closed-loop known answer
+# ---------------------------------------------------------------------------------------------
+def gen_nets():
+    net_dir = os.path.join(REF, "demonstration/PPO2/PPO2-4-CartPole/datasave/net")
+    env = mods["cp_ppo2"].CartPole(0., 0.)
+    actor = drv.PPOActor_Gaussian(state_dim=4, action_dim=1,
+                                  a_min=np.array(env.action_range)[:, 0],
+                                  a_max=np.array(env.action_range)[:, 1], init_std=env.fm / 3,
+                                  use_orthogonal_init=True)
+    critic = drv.PPOCritic(state_dim=4, use_orthogonal_init=True)
+    actor.load_state_dict(torch.load(os.path.join(net_dir, "actor"), weights_only=True))
+    critic.load_state_dict(torch.load(os.path.join(net_dir, "critic"), weights_only=True))
+    flat = lambda m: torch.cat([p.detach().flatten() for p in m.parameters()]).numpy()
+    x = f32(rng.uniform(-2.2, 2.2, (512, 4)))
+    x[0] = [0.1, -0.2, 0.3, 0.05]
+    with torch.no_grad():
+        xa = torch.tensor(x)
+        pre = actor.mean_layer(torch.tanh(actor.fc2(torch.tanh(actor.fc1(xa)))))
+        mean = actor(xa).numpy()
+        v = critic(xa).numpy()
+    # choose_action samples (torch RNG), via the reference agent
+    ppo_msg = {'gamma': 0.999, 'K_epochs': 30, 'eps_clip': 0.2, 'buffer_size': 1000,
+               'state_dim': 4, 'action_dim': 1, 'a_lr': 3e-4, 'c_lr': 1e-3, 'set_adam_eps': True,
+               'lmd': 0.95, 'use_adv_norm': True, 'mini_batch_size': 64, 'entropy_coef': 0.01,
+               'use_grad_clip': False, 'use_lr_decay': False, 'max_train_steps': int(5e6),
+               'using_mini_batch': False}
+    env_msg = {'state_dim': 4, 'action_dim': 1, 'name': 'CartPole', 'action_range': env.action_range}
+    agent = ppo2_mod.Proximal_Policy_Optimization2(env_msg, ppo_msg, actor=actor, critic=critic)
+    torch.manual_seed(11)
+    sa, slp = [], []
+    for i in range(256):
+        a, lp = agent.choose_action(x[i].astype(np.float64))
+        sa.append(a); slp.append(lp)
+    # closed loop, deterministic actor (SURVEY §4 known answers)
+    loops = {}
+    for name, (th0, x0) in {"a": (0.3, 0.5), "b": (-0.2, -0.6)}.items():
+        e = mods["cp_ppo2"].CartPole(th0, x0)
+        e.reset(False)
+        obs, acts, rews, flags = [], [], [], []
+        while not e.is_terminal:
+            e.current_state = e.next_state.copy()
+            a = agent.evaluate(e.current_state)
+            obs.append(e.current_state); acts.append(a)
+            e.step_update(a)
+            rews.append(e.reward); flags.append(e.terminal_flag)
+        loops[name] = dict(obs=np.array(obs), action=np.array(acts, np.float32),
+                           reward=np.array(rews), flag=np.array(flags), init=np.array([th0, x0]))
+        print("closed loop", name, len(rews), "steps, return %.6f" % np.sum(rews))
+    np.savez(os.path.join(OUT, "ppo2_cartpole_nets.npz"), actor_params=flat(actor),
+             critic_params=flat(critic), x=x, actor_pre=pre.numpy(), actor_mean=mean,
+             critic_v=v, sample_a=np.array(sa), sample_logp=np.array(slp), std=np.float32(env.fm / 3),
+             **{f"loop_{k}_{q}": v for k, d in loops.items() for q, v in d.items()})
+
+
+# ---------------------------------------------------------------------------------------------
+# PPO2.learn GAE / v_target / adv-norm, via the reference's own learn() with probes
+# ---------------------------------------------------------------------------------------------
+class _TorchProbe:
+    """Stands in for the `torch` name inside the reference PPO2 module to observe learn()'s
+    intermediate tensors (GAE list, normalised advantage); everything else is real torch."""
+
+    def __init__(self, rec):
+        self._rec = rec
+
+    def __getattr__(self, name):
+        return getattr(torch, name)
+
+    def tensor(self, data, *a, **k):
+        if isinstance(data, list):
+            self._rec["gae_list"] = np.array([float(d) for d in data], np.float32)
+        return torch.tensor(data, *a, **k)
+
+    def min(self, a, b):
+        self._rec.setdefault("adv_norm", a.detach().numpy().copy())
+        return torch.min(a, b)
+
+
+class _TableCritic(torch.nn.Module):
+    def __init__(self, table):
+        super().__init__()
+        self.table = torch.tensor(table, dtype=torch.float32)
+        self.w = torch.nn.Parameter(torch.zeros(1))
+
+    def forward(self, s):
+        return self.table[s[:, 0].long()].view(-1, 1) + 0 * self.w
+
+
+class _ConstActor(torch.nn.Module):
+    """get_dist(s).log_prob(a) returns the stored a_lp exactly => ratios == 1, surr1 == adv."""
+
+    def __init__(self, a_lp):
+        super().__init__()
+        self.a_lp = torch.tensor(a_lp, dtype=torch.float32)
+        self.w = torch.nn.Parameter(torch.zeros(1))
+
+    def get_dist(self, s):
+        outer = self
+
+        class D:
+            def entropy(self):
+                return torch.zeros(len(s), 1) + 0 * outer.w
+
+            def log_prob(self, a):
+                return outer.a_lp + 0 * outer.w
+        return D()
+
+
+def gen_gae(n_cases=4, B=1000):
+    cases = []
+    for c in range(n_cases):
+        r = rng.normal(0, 1, B)
+        v = f32(rng.normal(40, 5, B))
+        vn = f32(rng.normal(40, 5, B))
+        done = (rng.uniform(0, 1, B) < [0.004, 0.02, 0.1, 0.3][c]).astype(np.float64)
+        success = done * (rng.uniform(0, 1, B) < 0.5)
+        if c == 3:
+            success = (rng.uniform(0, 1, B) < 0.7).astype(np.float64)  # DPPO2 rule: also non-terminal
+        rec = {}
+        ppo_msg = {'gamma': 0.999, 'K_epochs': 1, 'eps_clip': 0.2, 'buffer_size': B,
+                   'state_dim': 1, 'action_dim': 1, 'a_lr': 3e-4, 'c_lr': 1e-3,
+                   'set_adam_eps': True, 'lmd': 0.95, 'use_adv_norm': True,
+                   'mini_batch_size': 64, 'entropy_coef': 0.01, 'use_grad_clip': False,
+                   'use_lr_decay': False, 'max_train_steps': int(5e6), 'using_mini_batch': False}
+        env_msg = {'state_dim': 1, 'action_dim': 1, 'name': 'gae', 'action_range': [[-1, 1]]}
+        a_lp = rng.normal(0, 1, (B, 1))
+        table = np.concatenate([v, vn])
+        agent = ppo2_mod.Proximal_Policy_Optimization2(env_msg, ppo_msg, actor=_ConstActor(a_lp),
+                                                       critic=_TableCritic(table))
+        for i in range(B):
+            agent.buffer.append(s=np.array([i]), a=np.array([0.]), log_prob=a_lp[i], r=r[i],
+                                s_=np.array([B + i]), done=done[i], success=success[i], index=i)
+        real = ppo2_mod.torch
+        ppo2_mod.torch = _TorchProbe(rec)
+        try:
+            agent.learn(0, buf_num=1)
+        finally:
+            ppo2_mod.torch = real
+        cases.append(dict(r=f32(r), v=v, vn=vn, done=done.astype(np.uint8),
+                          success=success.astype(np.uint8), adv=rec["gae_list"],
+                          v_target=(torch.tensor(rec["gae_list"]) + torch.tensor(v)).numpy(),
+                          adv_norm=rec["adv_norm"].reshape(-1)))
+    np.savez(os.path.join(OUT, "gae.npz"), gamma=0.999, lmd=0.95,
+             **{f"c{i}_{k}": v for i, c in enumerate(cases) for k, v in c.items()})
+    print("gae", len(cases), "cases")
+
+
+def gen_reward_norm():
+    norm = cls_mod.Normalization(shape=1)
+    xs = np.concatenate([[-3., -1., -2.], rng.normal(-1, 2, 2000), rng.normal(-50, 30, 300)])
+    out = np.array([np.asarray(norm(x)).item() for x in xs])
+    np.savez(os.path.join(OUT, "reward_norm.npz"), x=xs, y=out)
+    print("reward_norm", out[:3])
+
+
+if __name__ == "__main__":
+    gen_cartpole("cartpole_ppo2", mods["cp_ppo2"])
+    gen_cartpole("cartpole_dppo2", mods["cp_dppo2"], n=100)
+    gen_angleonly("angleonly_ppo2", mods["ao_ppo2"])
+    gen_soi("soi_env", mods["soi_env"])
+    gen_soi("soi_dppo2", mods["soi_dppo2"], n=200)
+    gen_ugv("ugvf_env", mods["ugvf_env"].UGVForward)
+    gen_ugv("ugvf_ppo2", mods["ugvf_ppo2"].UGVForward, n=200)
+    gen_ugv("ugvf_dppo2", mods["ugvf_dppo2"].UGVForward, n=200)
+    gen_ugv("ugvb_env", mods["ugvb_env"].UGVBidirectional)
+    gen_ugv("ugvb_ppo2", mods["ugvb_ppo2"].UGVBidirectional, n=200)
+    gen_uav("uav_hover")
+    gen_nets()
+    gen_gae()
+    gen_reward_norm()
+    with open(os.path.join(OUT, "VERSIONS.txt"), "w") as f:
+        f.write(f"numpy {np.__version__}\ntorch {torch.__version__}\npython {sys.version.split()[0]}\n"
+                f"reference {REF} (HKPolyU-UAV/ReinforcementLearningPlatform @ 2025-02-28)\n")
