@@ -1,0 +1,226 @@
+"""bench.py — env-steps/s of the CartPole PPO2 rollout hot path on 1..8 MI355X (one process per GPU).
+
+One bench "step" = one PPO2 rollout iteration over the config's synthetic env batch, entirely on
+the GPU: T env-steps x n envs of {auto-reset, actor forward + Gaussian sample, critic V(s), RK4 env
+step, buffer append} in the fused HIP kernel (rlp_rollout), then the critic on terminal s', reward
+normalisation, GAE(lambda) and advantage normalisation — everything learn() consumes
+(SURVEY.md §8a rows a1-a6, a14, a15, a17-a19). `value` = env-steps/s of the whole job.
+With --e2e the K-epoch PPO update (torch autograd on the same GPU) is also timed and reported
+separately under "e2e".
+
+Launch: python bench.py [--gpus 1]   |   torchrun --nproc-per-node N bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from reinforcementlearningplatform_amd import _abi as A  # noqa: E402
+from reinforcementlearningplatform_amd import _native  # noqa: E402
+from reinforcementlearningplatform_amd import kernels as K  # noqa: E402
+
+METRIC = "env-steps/sec (whole node), CartPole+UavRobust PPO2 @ 1/2/4/8 MI355X"
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
+PEAK_HBM_GBS = 8000.0
+
+ENVS = {
+    "cartpole": (A.RLP_ENV_CARTPOLE, lambda: A.cartpole_params("ppo2"), 3),
+    "uav": (A.RLP_ENV_UAV_HOVER_OUTER_LOOP, A.uav_hover_params, 1),
+    "angleonly": (A.RLP_ENV_CARTPOLE_ANGLEONLY, A.angleonly_params, 3),
+    "soi": (A.RLP_ENV_SOI, lambda: A.soi_params("env"), 2),
+    "ugv": (A.RLP_ENV_UGV_FORWARD, lambda: A.ugv_params(A.RLP_ENV_UGV_FORWARD, "ppo2"), 2),
+}
+
+
+def orthogonal_params(desc, gains, seed):
+    """PPOActor_Gaussian / PPOCritic init (demonstration/PPO2/PPO2-4-CartPole/train.py:59-70):
+    orthogonal weights, zero bias; flattened in nn.Module.parameters() order."""
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    ds = desc.layer_dims()
+    for i in range(desc.n_layers):
+        w = torch.empty(ds[i + 1], ds[i])
+        torch.nn.init.orthogonal_(w, gain=gains[i], generator=g)
+        out += [w.flatten(), torch.zeros(ds[i + 1])]
+    return torch.cat(out)
+
+
+def mlp_flops(desc):
+    ds = desc.layer_dims()
+    return sum(2 * ds[i] * ds[i + 1] for i in range(desc.n_layers))
+
+
+class Segment:
+    """Device-resident state + buffers of one rank's env batch."""
+
+    def __init__(self, env, n, T, seed, env_id0, H=256):
+        kind, pf, timeout_flag = ENVS[env]
+        self.kind, self.params = kind, pf()
+        D, S, Ad = A.ENV_DIMS[kind]
+        self.S, self.Ad, self.n, self.T = S, Ad, n, T
+        self.ad = A.MLPDesc.make([S, H, H, Ad], [A.RLP_ACT_TANH] * 3)
+        self.cd = A.MLPDesc.make([S, H, H, 1], [A.RLP_ACT_TANH, A.RLP_ACT_TANH, A.RLP_ACT_NONE])
+        self.actor = orthogonal_params(self.ad, [1.0, 1.0, 0.01], seed).cuda()
+        self.critic = orthogonal_params(self.cd, [1.0, 1.0, 1.0], seed + 1).cuda()
+        self.apk = K.mfma_pack(self.ad, self.actor)
+        self.cpk = K.mfma_pack(self.cd, self.critic)
+        lo, hi = A.action_bounds(kind, self.params)
+        self.std = [(h - l) / 2 / 3 for l, h in zip(lo, hi)]   # init_std = fm/3 (train.py:169)
+        self.lo, self.hi = lo, hi
+        self.seed, self.env_id0 = seed, env_id0
+        self.rule, self.flag = A.RLP_SUCCESS_DONE_AND_FLAG_NE, timeout_flag
+        self.state = K.new_state(kind, n)
+        self.need = torch.ones(n, dtype=torch.uint8, device="cuda")
+        self.bufs = K.rollout_buffers(kind, T, n)
+        self.rms = torch.zeros(4, dtype=torch.float64, device="cuda")
+        self.work = torch.empty(3 * T, dtype=torch.float64, device="cuda")
+        self.rnorm = torch.empty((T, n), dtype=torch.float32, device="cuda")
+        self.adv = torch.empty((T, n), dtype=torch.float32, device="cuda")
+        self.vt = torch.empty((T, n), dtype=torch.float32, device="cuda")
+        self.stats = torch.zeros(2, dtype=torch.float64, device="cuda")
+        self.step0 = 0
+
+    def rollout(self):
+        cfg = K.make_rollout_cfg(self.T, self.n, self.seed, self.step0, self.env_id0, self.std,
+                                 self.lo, self.hi, self.rule, self.flag)
+        K.rollout(self.kind, self.params, self.state, self.need, self.ad, self.apk, self.cd,
+                  self.cpk, cfg, self.bufs)
+        self.step0 += self.T
+
+    def learn_side(self):
+        b = self.bufs
+        # V(s'_t) of terminal transitions (non-terminal ones were written by the rollout)
+        K.mlp_forward(self.cd, self.critic, b["obs_next"].view(-1, self.S),
+                      mask=b["done"].view(-1), out=b["value_next"].view(-1, 1))
+        K.reward_norm(b["reward"], self.rms, self.work, out=self.rnorm)
+        self.stats.zero_()
+        K.gae(self.rnorm, b["value"], b["value_next"], b["done"], b["success"], 0.999, 0.95,
+              adv=self.adv, v_target=self.vt, stats=self.stats)
+        K.adv_normalize(self.adv, self.stats)
+
+    def iteration(self):
+        self.rollout()
+        self.learn_side()
+
+
+def cpu_baseline(env, seconds=10.0):
+    """Oracle (plain-C port of the reference loop, 1 thread) on a bounded sample of the same
+    workload: actor + critic forward, sampling and env step per env-step."""
+    from oracle import oracle
+    kind, pf, tflag = ENVS[env]
+    p = pf()
+    D, S, Ad = A.ENV_DIMS[kind]
+    ad = A.MLPDesc.make([S, 256, 256, Ad], [1, 1, 1])
+    cd = A.MLPDesc.make([S, 256, 256, 1], [1, 1, 0])
+    ap = orthogonal_params(ad, [1.0, 1.0, 0.01], 1).numpy()
+    cp = orthogonal_params(cd, [1.0, 1.0, 1.0], 2).numpy()
+    lo, hi = A.action_bounds(kind, p)
+    std = [(h - l) / 6 for l, h in zip(lo, hi)]
+
+    def run(n, T):
+        cfg = K.make_rollout_cfg(T, n, 3407, 0, 0, std, lo, hi, A.RLP_SUCCESS_DONE_AND_FLAG_NE, tflag)
+        st = np.zeros((D, n))
+        need = np.ones(n, np.uint8)
+        t0 = time.perf_counter()
+        oracle.rollout(kind, p, st, need, ad, ap, cd, cp, cfg, want_buffers=True)
+        return time.perf_counter() - t0
+
+    dt = run(16, 8)
+    n = max(16, int(16 * seconds / max(dt, 1e-6) / 64))
+    T = 64
+    dt = run(n, T)
+    return {"value": n * T / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/rlp_oracle.c rollout (actor+critic 256x256 fp32 MLP, Philox sample, "
+                      f"f64 RK4 {env} step) for {n} envs x {T} steps = {n * T} env-steps in "
+                      f"{dt:.1f} s on 1 host thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--env", default="cartpole", choices=sorted(ENVS))
+    ap.add_argument("--envs-per-gpu", type=int, default=65536)
+    ap.add_argument("--T", type=int, default=128, help="rollout segment length (steps per env)")
+    ap.add_argument("--sub", type=int, default=0, help="16-env sub-blocks per wave (2|4; 0=lib default)")
+    ap.add_argument("--seed", type=int, default=3407)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.sub:
+        _native.set_rollout_sub(args.sub)
+
+    n, T = args.envs_per_gpu, args.T
+    seg = Segment(args.env, n, T, args.seed, env_id0=rank * n)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        seg.iteration()
+    barrier()
+    t0 = time.perf_counter()
+    ev = []
+    for _ in range(args.steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        seg.rollout()
+        e1.record()
+        seg.learn_side()
+        ev.append((e0, e1))
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    rollout_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    env_steps = n * T * world * args.steps
+    value = env_steps / elapsed
+    flop_launch = n * T * (mlp_flops(seg.ad) + mlp_flops(seg.cd)) + n * mlp_flops(seg.cd)
+    achieved = flop_launch / (rollout_ms * 1e-3) / 1e12
+    out = {
+        "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic",
+        "config": {"workload": f"{args.env}_ppo2_rollout", "envs_per_gpu": n, "global_envs": n * world,
+                   "T": T, "env_steps_per_iteration": n * T * world,
+                   "nets": "actor [S,256,256,A] tanh, critic [S,256,256,1]",
+                   "parallelism": f"dp{world} (env shards, no data-path collective)",
+                   "physics": "f64", "mlp": "fp32 MFMA"},
+        "roofline": {"bound": "mfma", "kernel": "rlp::rollout_kernel", "achieved": achieved,
+                     "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+                     "avg_launch_ms": rollout_ms, "flop_per_launch": flop_launch},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.env, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

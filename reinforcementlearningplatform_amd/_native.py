@@ -1,0 +1,94 @@
+"""ctypes binding of librlp.so (the HIP/gfx950 library behind include/rlp.h).
+
+There is no CPU fallback: if the library is missing or a call fails, this module raises. Device
+buffers are torch tensors on a ROCm device; every call is ordered on the caller's current stream.
+"""
+import ctypes as C
+import os
+
+import torch  # import first: its libamdhip64 is the runtime librlp.so binds to (same SONAME)
+
+from . import _abi
+
+_LIB_NAME = "librlp.so"
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+class RLPError(RuntimeError):
+    pass
+
+
+def lib_path():
+    return os.environ.get("RLP_LIBRARY", os.path.join(_HERE, _LIB_NAME))
+
+
+def _declare(lib):
+    vp, i32, i64, u64, dbl = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_double
+    sig = {
+        "rlp_abi_version": (i32, []),
+        "rlp_last_error_string": (C.c_char_p, []),
+        "rlp_struct_size": (i64, [i32]),
+        "rlp_env_dims": (i32, [i32, vp, vp, vp]),
+        "rlp_env_reset": (i32, [i32, vp, vp, i32, vp, vp, u64, u64, u64, vp]),
+        "rlp_env_observe": (i32, [i32, vp, vp, i32, vp, vp]),
+        "rlp_env_step": (i32, [i32, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]),
+        "rlp_mlp_param_count": (i64, [vp]),
+        "rlp_mlp_forward": (i32, [vp, vp, vp, vp, i32, vp, vp]),
+        "rlp_mfma_packed_count": (i64, [vp]),
+        "rlp_mfma_pack": (i32, [vp, vp, vp, vp]),
+        "rlp_policy_sample": (i32, [vp, i32, i32, vp, vp, vp, vp, u64, u64, u64, vp, vp, vp]),
+        "rlp_rollout": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "rlp_set_rollout_sub": (i32, [i32]),
+        "rlp_reward_norm": (i32, [vp, i32, i32, vp, vp, vp, vp]),
+        "rlp_gae": (i32, [vp, vp, vp, vp, vp, dbl, dbl, i32, i32, vp, vp, vp, vp]),
+        "rlp_adv_normalize": (i32, [vp, i64, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype, f.argtypes = res, args
+
+
+def lib():
+    """Load librlp.so (raises if it is absent: the HIP path has no fallback)."""
+    global _lib
+    if _lib is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise RLPError(f"{path} not found: build it with `make -C "
+                           f"reinforcementlearningplatform_amd/csrc` or __graft_entry__.build()")
+        _lib = C.CDLL(path)
+        _declare(_lib)
+        if _lib.rlp_abi_version() != 1:
+            raise RLPError("librlp ABI version mismatch")
+        for i, (name, size) in enumerate(_abi.check_struct_sizes().items()):
+            if _lib.rlp_struct_size(i) != size:
+                raise RLPError(f"struct layout mismatch for {name}: C {_lib.rlp_struct_size(i)} "
+                               f"vs ctypes {size}")
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().rlp_last_error_string().decode(errors="replace")
+        raise RLPError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RLPError("librlp takes device tensors only (got a CPU tensor)")
+    if not t.is_contiguous():
+        raise RLPError("librlp takes contiguous tensors only")
+    return C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def set_rollout_sub(sub):
+    check(lib().rlp_set_rollout_sub(int(sub)), "rlp_set_rollout_sub")

@@ -1,0 +1,109 @@
+// rlp_common.hpp — shared device/host helpers for librlp (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rlp.h"
+
+namespace rlp {
+
+// ------------------------------------------------------------------------------------------
+// error plumbing (never throw across the C-ABI)
+// ------------------------------------------------------------------------------------------
+void set_error(const char *fmt, ...);
+int fail(int code, const char *fmt, ...);
+
+#define RLP_CHECK_LAUNCH(what)                                                            \
+    do {                                                                                  \
+        hipError_t e_ = hipGetLastError();                                                \
+        if (e_ != hipSuccess) return ::rlp::fail(-(int)e_, "%s: %s", what, hipGetErrorString(e_)); \
+    } while (0)
+
+#define RLP_REQUIRE(cond, ...)                                          \
+    do {                                                                \
+        if (!(cond)) return ::rlp::fail(RLP_EINVAL, __VA_ARGS__);      \
+    } while (0)
+
+inline hipStream_t as_stream(rlp_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------
+// Philox4x32-10 counter-based RNG: (seed, counter, env_id, tag) -> 4 x u32. Identical stream on
+// every rank, so sharding envs over GPUs never changes any env's trajectory.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void philox_block(uint64_t seed, uint64_t counter, uint64_t env_id,
+                                             uint32_t tag, uint32_t out[4]) {
+    uint32_t c0 = (uint32_t)counter;
+    uint32_t c1 = (uint32_t)(counter >> 32) ^ ((uint32_t)(env_id >> 32) << 16);
+    uint32_t c2 = (uint32_t)env_id;
+    uint32_t c3 = tag;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        uint32_t n0 = hi1 ^ c1 ^ k0;
+        uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+// two doubles in [0,1) with 53 random bits each (bit-identical to the CPU oracle)
+__device__ __forceinline__ void philox_u01_f64x2(uint64_t seed, uint64_t counter, uint64_t env_id,
+                                                 uint32_t tag, double u[2]) {
+    uint32_t r[4];
+    philox_block(seed, counter, env_id, tag, r);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        uint64_t bits = ((uint64_t)r[2 * k] << 21) ^ (uint64_t)(r[2 * k + 1] >> 11);
+        bits &= ((uint64_t)1 << 53) - 1;
+        u[k] = (double)bits * (1.0 / 9007199254740992.0);
+    }
+}
+
+// standard normals (Box-Muller, fp32), block j = 0,1 gives eps[2j], eps[2j+1]
+template <int A>
+__device__ __forceinline__ void philox_normal_f32(uint64_t seed, uint64_t counter, uint64_t env_id,
+                                                  float *eps) {
+#pragma unroll
+    for (int j = 0; 2 * j < A; ++j) {
+        uint32_t r[4];
+        philox_block(seed, counter, env_id, 0x100u + (uint32_t)j, r);
+        float u1 = (float)(r[0] >> 8) * 5.9604644775390625e-08f + 2.98023223876953125e-08f;
+        float u2 = (float)(r[1] >> 8) * 5.9604644775390625e-08f;
+        float rad = sqrtf(-2.0f * logf(u1));
+        float th = 6.28318530717958647692f * u2;
+        eps[2 * j] = rad * cosf(th);
+        if (2 * j + 1 < A) eps[2 * j + 1] = rad * sinf(th);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// fp32 activations
+// ------------------------------------------------------------------------------------------
+// Hidden-layer tanh: 1 - 2/(exp(2|x|)+1) on v_exp_f32 / v_rcp_f32 (7 VALU ops). Absolute error
+// <= ~1.2e-7, which is below the fp32 rounding noise of the 256-term dot products it feeds.
+__device__ __forceinline__ float tanh_fast(float x) {
+    float ax = fabsf(x);
+    float e = __builtin_amdgcn_exp2f(ax * -2.8853900817779268f);  // exp(-2|x|)
+    float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
+    return __builtin_copysignf(t, x);
+}
+
+// torch.distributions.Normal(mean, std).log_prob(a) in its fp32 expression order
+__device__ __forceinline__ float normal_logp(float a, float mean, float std) {
+    float var = std * std;
+    float d = a - mean;
+    return -(d * d) / (2.0f * var) - logf(std) - 0.91893853320467274178f;
+}
+
+__device__ __forceinline__ float mfma16(float a, float b, floatx4 &c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    return 0.f;
+}
+
+}  // namespace rlp

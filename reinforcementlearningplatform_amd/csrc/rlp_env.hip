@@ -1,0 +1,199 @@
+// rlp_env.hip — batched env step / observe / reset kernels and the shared C-ABI plumbing.
+//
+// Layout: physics state f64 SoA [D][n] (one env per lane => every component load/store is a
+// coalesced 512 B wave access); actions/observations f32 env-major [n][A] / [n][S].
+// Roofline: HBM-bound for every kind except CartPole (whose 10-11 RK4 sub-steps with fp64
+// sincos make it VALU-bound); per-env bytes and FLOPs are listed in DESIGN.md.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <type_traits>
+
+#include "rlp_envs.hpp"
+
+namespace rlp {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+template <int KIND>
+__global__ void __launch_bounds__(256) env_step_kernel(typename Env<KIND>::P p, double *state,
+                                                       int n, const float *__restrict__ action,
+                                                       float *obs_cur, float *obs_next,
+                                                       double *reward, int32_t *flag,
+                                                       uint8_t *done) {
+    using E = Env<KIND>;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s[E::D];
+#pragma unroll
+    for (int d = 0; d < E::D; ++d) s[d] = state[(size_t)d * n + i];
+    float a[E::A], on[E::S];
+#pragma unroll
+    for (int j = 0; j < E::A; ++j) a[j] = action[(size_t)i * E::A + j];
+    if (obs_cur) {
+        float oc[E::S];
+        E::observe(p, s, oc);
+#pragma unroll
+        for (int j = 0; j < E::S; ++j) obs_cur[(size_t)i * E::S + j] = oc[j];
+    }
+    double r;
+    int f;
+    bool dn;
+    E::step(p, s, a, on, r, f, dn);
+#pragma unroll
+    for (int d = 0; d < E::D; ++d) state[(size_t)d * n + i] = s[d];
+#pragma unroll
+    for (int j = 0; j < E::S; ++j) obs_next[(size_t)i * E::S + j] = on[j];
+    reward[i] = r;
+    flag[i] = f;
+    done[i] = dn ? 1 : 0;
+}
+
+template <int KIND>
+__global__ void __launch_bounds__(256) env_observe_kernel(typename Env<KIND>::P p,
+                                                          const double *state, int n, float *obs) {
+    using E = Env<KIND>;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s[E::D];
+#pragma unroll
+    for (int d = 0; d < E::D; ++d) s[d] = state[(size_t)d * n + i];
+    float o[E::S];
+    E::observe(p, s, o);
+#pragma unroll
+    for (int j = 0; j < E::S; ++j) obs[(size_t)i * E::S + j] = o[j];
+}
+
+template <int KIND>
+__global__ void __launch_bounds__(256) env_reset_kernel(typename Env<KIND>::P p, double *state,
+                                                        int n, const uint8_t *mask,
+                                                        const double *init, uint64_t seed,
+                                                        uint64_t counter, uint64_t env_id0) {
+    using E = Env<KIND>;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (mask && !mask[i]) return;
+    if (init) {
+#pragma unroll
+        for (int d = 0; d < E::D; ++d) state[(size_t)d * n + i] = init[(size_t)d * n + i];
+        return;
+    }
+    double s[E::D];
+#pragma unroll
+    for (int d = 0; d < E::D; ++d) s[d] = state[(size_t)d * n + i];
+    E::reset(p, s, seed, counter, env_id0 + (uint64_t)i);
+#pragma unroll
+    for (int d = 0; d < E::D; ++d) state[(size_t)d * n + i] = s[d];
+}
+
+// kind -> template dispatch
+template <typename F>
+int dispatch_kind(int kind, F &&f) {
+    switch (kind) {
+    case RLP_ENV_CARTPOLE: return f(std::integral_constant<int, RLP_ENV_CARTPOLE>());
+    case RLP_ENV_CARTPOLE_ANGLEONLY: return f(std::integral_constant<int, RLP_ENV_CARTPOLE_ANGLEONLY>());
+    case RLP_ENV_SOI: return f(std::integral_constant<int, RLP_ENV_SOI>());
+    case RLP_ENV_UGV_FORWARD: return f(std::integral_constant<int, RLP_ENV_UGV_FORWARD>());
+    case RLP_ENV_UGV_BIDIRECTIONAL: return f(std::integral_constant<int, RLP_ENV_UGV_BIDIRECTIONAL>());
+    case RLP_ENV_UAV_HOVER_OUTER_LOOP: return f(std::integral_constant<int, RLP_ENV_UAV_HOVER_OUTER_LOOP>());
+    }
+    return fail(RLP_EINVAL, "unknown env kind %d", kind);
+}
+
+}  // namespace rlp
+
+using namespace rlp;
+
+extern "C" {
+
+const char *rlp_last_error_string(void) { return g_err; }
+int rlp_abi_version(void) { return RLP_ABI_VERSION; }
+
+int rlp_env_dims(int kind, int *D, int *S, int *A) {
+    return dispatch_kind(kind, [&](auto k) {
+        using E = Env<decltype(k)::value>;
+        if (D) *D = E::D;
+        if (S) *S = E::S;
+        if (A) *A = E::A;
+        return RLP_OK;
+    });
+}
+
+// sizes of the ABI structs as compiled here (the Python mirror checks against them)
+int64_t rlp_struct_size(int which) {
+    switch (which) {
+    case 0: return sizeof(rlp_cartpole_params);
+    case 1: return sizeof(rlp_angleonly_params);
+    case 2: return sizeof(rlp_soi_params);
+    case 3: return sizeof(rlp_ugv_params);
+    case 4: return sizeof(rlp_uav_hover_params);
+    case 5: return sizeof(rlp_mlp_desc);
+    case 6: return sizeof(rlp_rollout_cfg);
+    case 7: return sizeof(rlp_rollout_bufs);
+    }
+    return -1;
+}
+
+int rlp_env_step(int kind, const void *params, double *state, int n, const float *action,
+                 float *obs_cur, float *obs_next, double *reward, int32_t *flag, uint8_t *done,
+                 rlp_stream_t stream) {
+    RLP_REQUIRE(params && state && action && obs_next && reward && flag && done,
+                "rlp_env_step: null argument");
+    RLP_REQUIRE(n >= 0, "rlp_env_step: n < 0");
+    if (n == 0) return RLP_OK;
+    return dispatch_kind(kind, [&](auto k) {
+        constexpr int K = decltype(k)::value;
+        const auto &p = *static_cast<const typename Env<K>::P *>(params);
+        env_step_kernel<K><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
+            p, state, n, action, obs_cur, obs_next, reward, flag, done);
+        RLP_CHECK_LAUNCH("rlp_env_step");
+        return RLP_OK;
+    });
+}
+
+int rlp_env_observe(int kind, const void *params, const double *state, int n, float *obs,
+                    rlp_stream_t stream) {
+    RLP_REQUIRE(params && state && obs, "rlp_env_observe: null argument");
+    RLP_REQUIRE(n >= 0, "rlp_env_observe: n < 0");
+    if (n == 0) return RLP_OK;
+    return dispatch_kind(kind, [&](auto k) {
+        constexpr int K = decltype(k)::value;
+        const auto &p = *static_cast<const typename Env<K>::P *>(params);
+        env_observe_kernel<K><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(p, state, n, obs);
+        RLP_CHECK_LAUNCH("rlp_env_observe");
+        return RLP_OK;
+    });
+}
+
+int rlp_env_reset(int kind, const void *params, double *state, int n, const uint8_t *mask,
+                  const double *init_state, uint64_t seed, uint64_t counter, uint64_t env_id0,
+                  rlp_stream_t stream) {
+    RLP_REQUIRE(params && state, "rlp_env_reset: null argument");
+    RLP_REQUIRE(n >= 0, "rlp_env_reset: n < 0");
+    if (n == 0) return RLP_OK;
+    return dispatch_kind(kind, [&](auto k) {
+        constexpr int K = decltype(k)::value;
+        const auto &p = *static_cast<const typename Env<K>::P *>(params);
+        env_reset_kernel<K><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
+            p, state, n, mask, init_state, seed, counter, env_id0);
+        RLP_CHECK_LAUNCH("rlp_env_reset");
+        return RLP_OK;
+    });
+}
+
+}  // extern "C"

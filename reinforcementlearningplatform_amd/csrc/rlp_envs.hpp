@@ -1,0 +1,580 @@
+// rlp_envs.hpp — batched environment dynamics, one env per lane, float64 physics in registers.
+//
+// Each Env<KIND> restates one reference env copy's step_update / get_state / reset
+// (citations per function, relative to the reference root). Expression order follows the
+// reference (numpy evaluates left to right and never fuses multiply-adds; the library is built
+// with -ffp-contract=off), float32-action quirks under NumPy-2 promotion included, so results match
+// the reference numpy step() to ~1 ulp of libm rather than to the 1e-5 the contract allows.
+#pragma once
+#include "rlp_common.hpp"
+
+namespace rlp {
+
+constexpr double kPi = 3.141592653589793;
+__device__ __forceinline__ double deg2rad(double d) { return d * kPi / 180.; }
+__device__ __forceinline__ double clipd(double x, double lo, double hi) {
+    return x < lo ? lo : (x > hi ? hi : x);
+}
+
+template <int KIND> struct Env;
+
+// ==========================================================================================
+// CartPole — environment/CartPole/CartPole.py (PPO2 and DPPO2 demo copies via params)
+// state: theta, dtheta, x, dx, time
+// ==========================================================================================
+template <> struct Env<RLP_ENV_CARTPOLE> {
+    using P = rlp_cartpole_params;
+    static constexpr int D = RLP_CARTPOLE_D, S = 4, A = 1;
+
+    // CartPole.ode :219-238
+    __device__ static __forceinline__ void ode(const P &p, double force, const double xx[4],
+                                               double d[4]) {
+        double th = xx[0], dth = xx[1], dx = xx[3];
+        double Sv, Cv;
+        sincos(th, &Sv, &Cv);
+        double num = force + p.m * p.ell * (dth * dth) * Sv;
+        num = num - p.kf * dx;
+        num = num - 3.0 / 4.0 * p.m * p.g * Sv * Cv;
+        double den = p.M + p.m - 3.0 / 4.0 * p.m * (Cv * Cv);
+        double ddx = num / den;
+        double ddth = 3.0 / 4.0 / p.m / p.ell * (p.m * p.g * Sv - p.m * ddx * Cv);
+        d[0] = dth; d[1] = ddth; d[2] = dx; d[3] = ddx;
+    }
+    // get_state :145-153
+    __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
+        o[0] = (float)((s[0] / p.theta_max) * p.static_gain);
+        o[1] = (float)((s[1] / p.dtheta_max) * p.static_gain);
+        o[2] = (float)((s[2] / p.x_max) * p.static_gain);
+        o[3] = (float)((s[3] / p.dx_max) * p.static_gain);
+    }
+    // step_update :257-264 -> rk44 :240-255, is_Terminal :160-185, get_reward :187-217
+    __device__ static __forceinline__ void step(const P &p, double *s, const float *a, float *on,
+                                                double &reward, int &flag, bool &done) {
+        const float af = a[0];
+        const double force = (double)af;
+        const double h = p.dt / (double)p.n_sub_div;
+        double time = s[4];
+        const double tt = time + p.dt;
+        double xx[4] = {s[0], s[1], s[2], s[3]};
+        while (time < tt) {  // fp64 time accumulation => 10 or 11 sub-steps
+            double K1[4], K2[4], K3[4], K4[4], tmp[4], d[4];
+            ode(p, force, xx, d);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { K1[i] = h * d[i]; tmp[i] = xx[i] + K1[i] / 2; }
+            ode(p, force, tmp, d);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { K2[i] = h * d[i]; tmp[i] = xx[i] + K2[i] / 2; }
+            ode(p, force, tmp, d);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { K3[i] = h * d[i]; tmp[i] = xx[i] + K3[i]; }
+            ode(p, force, tmp, d);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                K4[i] = h * d[i];
+                xx[i] = xx[i] + (K1[i] + 2 * K2[i] + 2 * K3[i] + K4[i]) / 6;
+            }
+            time += h;
+        }
+        s[0] = xx[0]; s[1] = xx[1]; s[2] = xx[2]; s[3] = xx[3]; s[4] = time;
+        const double th = xx[0], dth = xx[1], x = xx[2], dx = xx[3];
+        const double eth = 0. - th, ex = 0. - x;
+        int f = 0;
+        if ((th > p.theta_max + deg2rad(1)) || th < -p.dtheta_max - deg2rad(1)) f = 1;  // :167 (sic)
+        if (x > p.x_max || x < -p.x_max) f = 2;
+        if (time > p.time_max) f = 3;
+        if (sqrt(ex * ex + dx * dx + eth * eth + dth * dth) < 1e-2) f = 4;
+        observe(p, s, on);
+        const double r_x = -fabs(x) * p.Q_x;
+        const double r_dx = -fabs(dx) * p.Q_dx;
+        const double r_th = -fabs(th) * p.Q_theta;
+        const double r_om = -fabs(dth) * p.Q_omega;
+        const double r_f = (double)(-fabsf(af) * (float)p.R);  // float32 (np.float32 force)
+        double r_extra = 0.;
+        if (f == 1 || f == 2) {
+            const double n_ = (p.time_max - time) / p.dt;
+            r_extra = n_ * (r_x + r_dx + r_th + r_om + r_f);
+        }
+        reward = r_x + r_dx + r_th + r_om + r_f + r_extra;
+        flag = f;
+        done = f != 0;
+    }
+    // reset(random=True) :272-282
+    __device__ static __forceinline__ void reset(const P &p, double *s, uint64_t seed,
+                                                 uint64_t counter, uint64_t env_id) {
+        double u[2];
+        philox_u01_f64x2(seed, counter, env_id, 0x200u, u);
+        s[0] = p.reset_theta_lo + (p.reset_theta_hi - p.reset_theta_lo) * u[0];
+        s[1] = 0.;
+        s[2] = p.reset_x_lo + (p.reset_x_hi - p.reset_x_lo) * u[1];
+        s[3] = 0.;
+        s[4] = 0.;
+    }
+};
+
+// ==========================================================================================
+// CartPoleAngleOnly — demonstration/PPO2/PPO2-4-CartPoleAngleOnly/cartpole_angleonly.py
+// ==========================================================================================
+template <> struct Env<RLP_ENV_CARTPOLE_ANGLEONLY> {
+    using P = rlp_angleonly_params;
+    static constexpr int D = RLP_ANGLEONLY_D, S = 2, A = 1;
+
+    __device__ static __forceinline__ void ode(const P &p, double force, const double xx[4],
+                                               double d[4]) {  // :197-216
+        double th = xx[0], dth = xx[1], dx = xx[3];
+        double Sv, Cv;
+        sincos(th, &Sv, &Cv);
+        double num = force + p.m * p.ell * (dth * dth) * Sv;
+        num = num - p.kf * dx;
+        num = num - 3.0 / 4.0 * p.m * p.g * Sv * Cv;
+        double den = p.M + p.m - 3.0 / 4.0 * p.m * (Cv * Cv);
+        double ddx = num / den;
+        double ddth = 3.0 / 4.0 / p.m / p.ell * (p.m * p.g * Sv - p.m * ddx * Cv);
+        d[0] = dth; d[1] = ddth; d[2] = dx; d[3] = ddx;
+    }
+    __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
+        o[0] = (float)((s[0] / p.theta_max) * p.static_gain);  // :137-143
+        o[1] = (float)((s[1] / p.norm_dtheta) * p.static_gain);
+    }
+    __device__ static __forceinline__ void step(const P &p, double *s, const float *a, float *on,
+                                                double &reward, int &flag, bool &done) {
+        const float af = a[0];
+        const double force = (double)af, dt = p.dt;
+        double xx[4] = {s[0], s[1], s[2], s[3]};
+        double K1[4], K2[4], K3[4], K4[4], tmp[4], d[4];
+        ode(p, force, xx, d);  // rk44 :218-229 (one RK4 step of dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { K1[i] = dt * d[i]; tmp[i] = xx[i] + K1[i] / 2; }
+        ode(p, force, tmp, d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { K2[i] = dt * d[i]; tmp[i] = xx[i] + K2[i] / 2; }
+        ode(p, force, tmp, d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { K3[i] = dt * d[i]; tmp[i] = xx[i] + K3[i]; }
+        ode(p, force, tmp, d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            K4[i] = dt * d[i];
+            xx[i] = xx[i] + (K1[i] + 2 * K2[i] + 2 * K3[i] + K4[i]) / 6;
+        }
+        const double time = s[4] + dt;
+        s[0] = xx[0]; s[1] = xx[1]; s[2] = xx[2]; s[3] = xx[3]; s[4] = time;
+        const double th = xx[0], dth = xx[1], eth = 0. - th;
+        int f = 0;  // is_Terminal :150-168
+        if ((th > p.theta_max + deg2rad(1)) || th < -p.theta_max - deg2rad(1)) f = 1;
+        if (time > p.time_max) f = 3;
+        if (sqrt(eth * eth + dth * dth) < 1e-2) f = 4;
+        observe(p, s, on);
+        const double r1 = -(th * th) * p.Q_theta;  // get_reward :170-195
+        const double r2 = -(dth * dth) * p.Q_omega;
+        const double r3 = (double)(-(af * af) * (float)p.R);
+        double r4 = 0.;
+        if (f == 1) {
+            const double n_ = (p.time_max - time) / p.dt;
+            r4 = n_ * (r1 + r2 + r3);
+        }
+        reward = r1 + r2 + r3 + r4;
+        flag = f;
+        done = f != 0;
+    }
+    __device__ static __forceinline__ void reset(const P &p, double *s, uint64_t seed,
+                                                 uint64_t counter, uint64_t env_id) {
+        double u[2];  // reset :245-279
+        philox_u01_f64x2(seed, counter, env_id, 0x200u, u);
+        s[0] = p.reset_theta_lo + (p.reset_theta_hi - p.reset_theta_lo) * u[0];
+        s[1] = 0.; s[2] = 0.; s[3] = 0.; s[4] = 0.;
+    }
+};
+
+// ==========================================================================================
+// SecondOrderIntegration — environment/SecondOrderIntegration/SecondOrderIntegration.py
+// state: x, y, vx, vy, time, tx, ty
+// ==========================================================================================
+template <> struct Env<RLP_ENV_SOI> {
+    using P = rlp_soi_params;
+    static constexpr int D = RLP_SOI_D, S = 4, A = 2;
+
+    __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
+        const double ex = s[5] - s[0], ey = s[6] - s[1];  // get_state :211-219
+        o[0] = (float)((ex / p.map_size[0]) * p.obs_gain);
+        o[1] = (float)((ey / p.map_size[1]) * p.obs_gain);
+        o[2] = (float)((-s[2] / p.v_max) * p.obs_gain);
+        o[3] = (float)((-s[3] / p.v_max) * p.obs_gain);
+    }
+    __device__ static __forceinline__ void step(const P &p, double *s, const float *a, float *on,
+                                                double &reward, int &flag, bool &done) {
+        const double f0 = (double)a[0], f1 = (double)a[1];
+        const double h = p.dt / 1;
+        double time = s[4];
+        const double tt = time + p.dt;
+        while (time < tt) {  // rk44 :298-314 (the loop runs once)
+            const double x0 = s[0], x1 = s[1], x2 = s[2], x3 = s[3];
+            double K1[4], K2[4], K3[4], K4[4];
+            K1[0] = h * x2; K1[1] = h * x3; K1[2] = h * (f0 - p.k * x2); K1[3] = h * (f1 - p.k * x3);
+            double t2 = x2 + K1[2] / 2, t3 = x3 + K1[3] / 2;
+            K2[0] = h * t2; K2[1] = h * t3; K2[2] = h * (f0 - p.k * t2); K2[3] = h * (f1 - p.k * t3);
+            t2 = x2 + K2[2] / 2; t3 = x3 + K2[3] / 2;
+            K3[0] = h * t2; K3[1] = h * t3; K3[2] = h * (f0 - p.k * t2); K3[3] = h * (f1 - p.k * t3);
+            t2 = x2 + K3[2]; t3 = x3 + K3[3];
+            K4[0] = h * t2; K4[1] = h * t3; K4[2] = h * (f0 - p.k * t2); K4[3] = h * (f1 - p.k * t3);
+            s[0] = x0 + (K1[0] + 2 * K2[0] + 2 * K3[0] + K4[0]) / 6;
+            s[1] = x1 + (K1[1] + 2 * K2[1] + 2 * K3[1] + K4[1]) / 6;
+            s[2] = x2 + (K1[2] + 2 * K2[2] + 2 * K3[2] + K4[2]) / 6;
+            s[3] = x3 + (K1[3] + 2 * K2[3] + 2 * K3[3] + K4[3]) / 6;
+            time += h;
+        }
+        s[4] = time;
+        const double accx = (f0 - p.k * s[2]) / p.mass, accy = (f1 - p.k * s[3]) / p.mass;
+        const double ex = s[5] - s[0], ey = s[6] - s[1];
+        const double adm = p.admissible_error;
+        int f = 0;  // is_Terminal :235-249
+        if (s[0] > p.map_size[0] + adm || s[0] < 0 - adm || s[1] > p.map_size[1] + adm ||
+            s[1] < 0 - adm)
+            f = 1;
+        if (time > p.time_max) f = 2;
+        const double e_pos = sqrt(ex * ex + ey * ey), e_vel = sqrt(s[2] * s[2] + s[3] * s[3]);
+        if (p.success_enabled && e_pos <= 0.05 && e_vel < 0.05) f = 3;
+        observe(p, s, on);
+        const double acc = sqrt(accx * accx + accy * accy);  // get_reward :251-284
+        const double u_pos = -e_pos * p.Q_pos, u_vel = -e_vel * p.Q_vel, u_acc = -acc * p.Q_acc;
+        double u_extra = 0.;
+        if (f == 1) {
+            const double n_ = (p.time_max - time) / p.dt;
+            u_extra = n_ * (u_pos + u_vel + u_acc);
+        }
+        reward = u_pos + u_vel + u_acc + u_extra;
+        flag = f;
+        done = f != 0;
+    }
+    __device__ static __forceinline__ void reset(const P &p, double *s, uint64_t seed,
+                                                 uint64_t counter, uint64_t env_id) {
+        double u[2];  // reset :328-352
+        philox_u01_f64x2(seed, counter, env_id, 0x200u, u);
+        const double lo = 0 + p.reset_margin;
+        s[0] = lo + ((p.map_size[0] - p.reset_margin) - lo) * u[0];
+        s[1] = lo + ((p.map_size[1] - p.reset_margin) - lo) * u[1];
+        s[2] = 0.; s[3] = 0.; s[4] = 0.;
+        s[5] = p.map_size[0] / 2; s[6] = p.map_size[1] / 2;
+    }
+};
+
+// ==========================================================================================
+// UGVForward / UGVBidirectional — environment/UGV/UGVForward.py, UGVBidirectional.py
+// state: x, y, vel, phi, omega, time, tx, ty
+// ==========================================================================================
+template <bool BIDIR> struct UGV {
+    using P = rlp_ugv_params;
+    static constexpr int D = RLP_UGV_D, S = 4, A = 2;
+
+    __device__ static __forceinline__ double get_e(const double *s, double c, double sn) {
+        const double ex = s[6] - s[0], ey = s[7] - s[1];
+        const double v = sqrt(ex * ex + ey * ey);
+        if (!BIDIR) return v;  // UGVForward.get_e :315-317
+        const double dot = c * ex + sn * ey;  // UGVBidirectional.get_e
+        return (dot > 0 ? 1.0 : (dot < 0 ? -1.0 : 0.0)) * v;
+    }
+    // get_e_phi -> utils/functions.py:49-60 cal_vector_rad_oriented (+ Bidirectional fold)
+    __device__ static __forceinline__ double get_e_phi(const double *s, double c, double sn) {
+        const double x2 = s[6] - s[0], y2 = s[7] - s[1];
+        double ph;
+        if (sqrt(x2 * x2 + y2 * y2) < 1e-4 || sqrt(c * c + sn * sn) < 1e-4) {
+            ph = 0;
+        } else {
+            const double dot = c * x2 + sn * y2;
+            const double det = c * y2 - sn * x2;
+            ph = atan2(det, dot);
+        }
+        if (BIDIR) {
+            ph = ph >= kPi / 2 ? ph - kPi : ph;
+            ph = ph <= -kPi / 2 ? ph + kPi : ph;
+        }
+        return ph;
+    }
+    __device__ static __forceinline__ void obs_from(const P &p, const double *s, double e,
+                                                    double eph, float *o) {  // get_state :217-227
+        const double e_max = sqrt(p.map_size[0] * p.map_size[0] + p.map_size[1] * p.map_size[1]) / 2;
+        double s0, s1;
+        if (!BIDIR) {
+            s0 = 2 / e_max * e - 1;
+            s1 = 2 / p.v_max * s[2] - 1;
+        } else {
+            s0 = e / e_max;
+            s1 = s[2] / p.v_max;
+        }
+        o[0] = (float)(s0 * p.static_gain);
+        o[1] = (float)(s1 * p.static_gain);
+        o[2] = (float)((eph / kPi) * p.static_gain);
+        o[3] = (float)((s[4] / p.omega_max) * p.static_gain);
+    }
+    __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
+        double sn, c;
+        sincos(s[3], &sn, &c);
+        obs_from(p, s, get_e(s, c, sn), get_e_phi(s, c, sn), o);
+    }
+    __device__ static __forceinline__ void ode(const P &p, double al, double aa, const double *x,
+                                               double *d) {  // ode :281-292
+        double sn, c;
+        sincos(x[3], &sn, &c);
+        d[0] = x[2] * c;
+        d[1] = x[2] * sn;
+        d[2] = al - p.kf * x[2];
+        d[3] = x[4];
+        d[4] = aa - p.kt * x[4];
+    }
+    __device__ static __forceinline__ void step(const P &p, double *s, const float *a, float *on,
+                                                double &reward, int &flag, bool &done) {
+        const double al = (double)a[0], aa = (double)a[1], dt = p.dt;
+        double xx[5] = {s[0], s[1], s[2], s[3], s[4]};
+        double K1[5], K2[5], K3[5], K4[5], t[5], d[5];
+        ode(p, al, aa, xx, d);  // rk44 :294-313
+#pragma unroll
+        for (int i = 0; i < 5; ++i) { K1[i] = dt * d[i]; t[i] = xx[i] + K1[i] / 2; }
+        ode(p, al, aa, t, d);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) { K2[i] = dt * d[i]; t[i] = xx[i] + K2[i] / 2; }
+        ode(p, al, aa, t, d);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) { K3[i] = dt * d[i]; t[i] = xx[i] + K3[i]; }
+        ode(p, al, aa, t, d);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            K4[i] = dt * d[i];
+            s[i] = xx[i] + (K1[i] + 2 * K2[i] + 2 * K3[i] + K4[i]) / 6;
+        }
+        if (!BIDIR && s[2] < 0.) s[2] = 0.;
+        const double time = s[5] + dt;
+        s[5] = time;
+        if (s[3] > kPi) s[3] -= 2 * kPi;
+        if (s[3] < -kPi) s[3] += 2 * kPi;
+        double sn, c;
+        sincos(s[3], &sn, &c);
+        const double e = get_e(s, c, sn), eph = get_e_phi(s, c, sn);
+        int f = 0;  // is_Terminal :247-261
+        if (s[0] > p.map_size[0] || s[0] < 0 || s[1] > p.map_size[1] || s[1] < 0) f = 1;
+        if (time > p.time_max) f = 2;
+        if (fabs(e) <= 0.05 && fabs(s[2]) < 0.01) f = 3;
+        obs_from(p, s, e, eph, on);
+        const double u_pos = -fabs(e) * p.Q_pos;  // get_reward :263-279
+        const double u_vel = -fabs(s[2]) * p.Q_vel;
+        const double gate = p.phi_gate_abs ? fabs(e) : e;
+        const double u_phi = gate > 0.1 ? -fabs(eph) * p.Q_phi : 0.0;
+        const double u_om = -fabs(s[4]) * p.Q_omega;
+        double u_psi = 0.;
+        if (f == 1) {
+            const double n_ = (p.time_max - time) / p.dt;
+            u_psi = n_ * (u_pos + u_vel + u_phi + u_om);
+        }
+        reward = u_pos + u_vel + u_phi + u_om + u_psi;
+        flag = f;
+        done = f != 0;
+    }
+    __device__ static __forceinline__ void reset(const P &p, double *s, uint64_t seed,
+                                                 uint64_t counter, uint64_t env_id) {
+        double u[2], u2[2];  // reset :334-362
+        philox_u01_f64x2(seed, counter, env_id, 0x200u, u);
+        philox_u01_f64x2(seed, counter, env_id, 0x201u, u2);
+        const double d0 = p.reset_margin;
+        s[0] = d0 + ((p.map_size[0] - d0) - d0) * u[0];
+        s[1] = d0 + ((p.map_size[1] - d0) - d0) * u[1];
+        s[3] = -kPi + (kPi - -kPi) * u2[0];
+        s[2] = 0.; s[4] = 0.; s[5] = 0.;
+        s[6] = p.map_size[0] / 2; s[7] = p.map_size[1] / 2;
+    }
+};
+template <> struct Env<RLP_ENV_UGV_FORWARD> : UGV<false> {};
+template <> struct Env<RLP_ENV_UGV_BIDIRECTIONAL> : UGV<true> {};
+
+// ==========================================================================================
+// UAV hover outer loop — environment/UavRobust/UavHoverOuterLoop.py (+ uav.py, uav_pos_ctrl.py,
+// FNTSMC.py). state: x y z vx vy vz phi theta psi p q r | time | pos_ref[3] | s1[3] | att_ref[3]
+// ==========================================================================================
+template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
+    using P = rlp_uav_hover_params;
+    static constexpr int D = RLP_UAV_D, S = 6, A = 3;
+    enum { X = 0, VX = 3, PHI = 6, THE = 7, PSI = 8, PP = 9, T = 12, REF = 13, S1 = 16, AREF = 19 };
+
+    // UAV.ode uav.py:429-460 (J0 = 0, ideal: dis = 0)
+    __device__ static __forceinline__ void ode(const P &p, double thr, const double tq[3],
+                                               const double *x, double *d) {
+        const double vx = x[3], vy = x[4], vz = x[5], phi = x[6], th = x[7], psi = x[8];
+        const double pp = x[9], q = x[10], r = x[11];
+        const double dp = (-p.kr * pp - q * r * (p.J[2] - p.J[1]) + tq[0]) / p.J[0];
+        const double dq = (-p.kr * q - pp * r * (p.J[0] - p.J[2]) + tq[1]) / p.J[1];
+        const double dr = (-p.kr * r - pp * q * (p.J[1] - p.J[0]) + tq[2]) / p.J[2];
+        double sphi, cphi, sth, cth, spsi, cpsi;
+        sincos(phi, &sphi, &cphi);
+        sincos(th, &sth, &cth);
+        sincos(psi, &spsi, &cpsi);
+        const double tth = tan(th);
+        const double R01 = tth * sphi, R02 = tth * cphi, R11 = cphi, R12 = -sphi;
+        const double R21 = sphi / cth, R22 = cphi / cth;
+        d[6] = 1 * pp + R01 * q + R02 * r;
+        d[7] = 0 * pp + R11 * q + R12 * r;
+        d[8] = 0 * pp + R21 * q + R22 * r;
+        d[0] = vx; d[1] = vy; d[2] = vz;
+        d[3] = (thr * (cpsi * sth * cphi + spsi * sphi) - p.kt * vx + 0.0) / p.m;
+        d[4] = (thr * (spsi * sth * cphi - cpsi * sphi) - p.kt * vy + 0.0) / p.m;
+        d[5] = -p.g + (thr * cphi * cth - p.kt * vz + 0.0) / p.m;
+        d[9] = dp; d[10] = dq; d[11] = dr;
+    }
+    __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {  // get_state :81-91
+            const double e = s[X + i] - s[REF + i];
+            o[i] = (float)(e / (p.e_pos_max[i] - p.e_pos_min[i]) * p.static_gain);
+            o[3 + i] = (float)(2 * s[VX + i] / (p.vel_max[i] - p.vel_min[i]) * p.static_gain);
+        }
+    }
+    __device__ static __forceinline__ void step(const P &p, double *s, const float *a, float *on,
+                                                double &reward, int &flag, bool &done) {
+        const double phi = s[PHI], th = s[THE], psi = s[PSI];
+        const double pp = s[PP], q = s[PP + 1], r = s[PP + 2];
+        double sphi, cphi, sth, cth, spsi, cpsi;
+        sincos(phi, &sphi, &cphi);
+        sincos(th, &sth, &cth);
+        sincos(psi, &spsi, &cpsi);
+        // uo_2_ref_angle_throttle uav_pos_ctrl.py:67-76; (uz + g) * m in float32 (NEP 50)
+        const double ux = (double)a[0], uy = (double)a[1];
+        const float uzg = (a[2] + (float)p.g) * (float)p.m;
+        const double uf = (double)uzg / (cphi * cth);
+        const double phi_d0 = asin(clipd((ux * spsi - uy * cpsi) * p.m / uf, -1, 1));
+        const double th_d0 = asin(clipd((ux * cpsi + uy * spsi) * p.m / (uf * cos(phi_d0)), -1, 1));
+        const double phi_d = clipd(phi_d0, p.att_zone[0][0], p.att_zone[0][1]);  // :126-127
+        const double th_d = clipd(th_d0, p.att_zone[1][0], p.att_zone[1][1]);
+        const double aref_new[3] = {phi_d, th_d, 0.0};
+        double daref[3], aref[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {  // attitude-reference rate limit :130-134
+            const double old = s[AREF + i];
+            daref[i] = clipd((aref_new[i] - old) / p.dt, p.dot_att_min[i], p.dot_att_max[i]);
+            aref[i] = daref[i] * p.dt + old;
+        }
+        // att_control uav_pos_ctrl.py:46-65 -> fntsmc_att.control_update FNTSMC.py:80-106
+        const double tth = tan(th);
+        const double f1[3][3] = {{1., sphi * tth, cphi * tth}, {0., cphi, -sphi},
+                                 {0., sphi / cth, cphi / cth}};
+        const double rho2[3] = {pp, q, r};
+        double drho1[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            drho1[i] = f1[i][0] * rho2[0] + f1[i][1] * rho2[1] + f1[i][2] * rho2[2];
+        const double f2[3] = {(p.kr * pp + q * r * (p.J[1] - p.J[2])) / p.J[0],  // uav.py:630-641
+                              (p.kr * q + pp * r * (p.J[2] - p.J[0])) / p.J[1],
+                              (p.kr * r + pp * q * (p.J[0] - p.J[1])) / p.J[2]};
+        const double c2 = cth * cth;  // F uav.py:668-686
+        double dF[3][3] = {{0., 0., 0.}, {0., 0., 0.}, {0., 0., 0.}};
+        dF[0][1] = drho1[0] * tth * cphi + drho1[1] * sphi / c2;
+        dF[0][2] = -drho1[0] * tth * sphi + drho1[1] * cphi / c2;
+        dF[1][1] = -drho1[0] * sphi;
+        dF[1][2] = -drho1[0] * cphi;
+        dF[2][1] = (drho1[0] * cphi * cth + drho1[1] * sphi * sth) / c2;
+        dF[2][2] = (-drho1[0] * sphi * cth + drho1[1] * cphi * sth) / c2;
+        const double rho1[3] = {phi, th, psi};
+        double u12[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const double sec = (dF[i][0] * rho2[0] + dF[i][1] * rho2[1] + dF[i][2] * rho2[2]) +
+                               (f1[i][0] * f2[0] + f1[i][1] * f2[1] + f1[i][2] * f2[2]);
+            const double e = rho1[i] - aref[i];
+            const double de = drho1[i] - daref[i];
+            const double ss = 1 * de + p.att_k1[i] * e +
+                              p.att_gamma[i] * pow(fabs(e), p.att_alpha[i]) * tanh(5 * e);
+            const double ds1 = pow(fabs(ss), p.att_beta[i]) * tanh(5 * ss);
+            s[S1 + i] += ds1 * p.att_ctrl_dt;
+            const double sigma = ss + p.att_lmd[i] * s[S1 + i];
+            const double u1 = sec + 0.0 + p.att_k1[i] * de +
+                              p.att_gamma[i] * p.att_alpha[i] * pow(fabs(e), p.att_alpha[i] - 1) * de +
+                              p.att_lmd[i] * ds1;
+            const double u2 = -p.att_k2[i] * tanh(10 * sigma);
+            u12[i] = u1 + u2;
+        }
+        // -inv(f1 diag(1/J)) (u1+u2) = -diag(J) f1^-1 (u1+u2); f1^-1 of the Euler-rate matrix
+        const double fi[3][3] = {{1., 0., -sth}, {0., cphi, sphi * cth}, {0., -sphi, cphi * cth}};
+        double tq[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const double v = p.J[i] * fi[i][0] * u12[0] + p.J[i] * fi[i][1] * u12[1] +
+                             p.J[i] * fi[i][2] * u12[2];
+            tq[i] = clipd(-v, -p.att_saturation[i], p.att_saturation[i]);
+            s[AREF + i] = aref[i];
+        }
+        // update -> rk44(n=1) uav.py:462-483
+        const double h = p.dt / 1;
+        double xx[12], K1[12], K2[12], K3[12], t[12], d[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) xx[i] = s[i];
+        ode(p, uf, tq, xx, d);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) { K1[i] = h * d[i]; t[i] = xx[i] + K1[i] / 2; }
+        ode(p, uf, tq, t, d);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) { K2[i] = h * d[i]; t[i] = xx[i] + K2[i] / 2; }
+        ode(p, uf, tq, t, d);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) { K3[i] = h * d[i]; t[i] = xx[i] + K3[i]; }
+        ode(p, uf, tq, t, d);
+#pragma unroll
+        for (int i = 0; i < 12; ++i)
+            s[i] = xx[i] + (K1[i] + 2 * K2[i] + 2 * K3[i] + h * d[i]) / 6;
+        s[T] += p.dt;
+        if (s[PSI] > kPi) s[PSI] -= 2 * kPi;
+        if (s[PSI] < -kPi) s[PSI] += 2 * kPi;
+        int f = 0;  // is_episode_Terminal uav.py:543-560
+        if (s[T] > p.time_max - p.dt / 2) f = 1;
+        bool po = false, ao = false;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            po |= (s[X + i] < p.pos_zone[i][0]) || (s[X + i] > p.pos_zone[i][1]);
+            ao |= (s[PHI + i] < p.att_zone[i][0]) || (s[PHI + i] > p.att_zone[i][1]);
+        }
+        if (po) f = 2;
+        if (ao) f = 3;
+        observe(p, s, on);
+        double nte = 0, ne = 0, ntv = 0, nv = 0;  // get_reward :93-110
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const double e = s[X + i] - s[REF + i], v = s[VX + i];
+            const double te = tanh(10 * e), tv = tanh(10 * v);
+            nte += te * te; ne += e * e; ntv += tv * tv; nv += v * v;
+        }
+        nte = sqrt(nte); ne = sqrt(ne); ntv = sqrt(ntv); nv = sqrt(nv);
+        const float na = sqrtf(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);  // float32 action norm
+        const double r1 = -(nte * nte) * 0.5 * p.Qx - ne * ne * 0.5 * p.Qx;
+        const double r2 = -(ntv * ntv) * 0.5 * p.Qx - nv * nv * 0.5 * p.Qv;
+        const double r3 = (double)(-(na * na) * (float)p.R);
+        double r4 = 0;
+        if (po || ao)
+            r4 = -(p.time_max - s[T]) / p.dt *
+                 (p.Qx * (ne * ne) + p.Qv * (nv * nv) + (double)((float)p.R * (na * na)));
+        reward = r1 + r2 + r3 + r4;
+        flag = f;
+        done = f != 0;
+    }
+    // reset(random=True) :152-214; FNTSMC s1 and att_ref are carried over, as in the reference
+    __device__ static __forceinline__ void reset(const P &p, double *s, uint64_t seed,
+                                                 uint64_t counter, uint64_t env_id) {
+        double u[2], u2[2];
+        philox_u01_f64x2(seed, counter, env_id, 0x200u, u);
+        philox_u01_f64x2(seed, counter, env_id, 0x201u, u2);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            s[X + i] = p.pos0[i]; s[VX + i] = p.vel0[i];
+            s[PHI + i] = p.angle0[i]; s[PP + i] = p.pqr0[i];
+        }
+        s[T] = 0.;
+        const double uu[3] = {u[0], u[1], u2[0]};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const double lo = p.pos_zone[i][0] + p.target_offset, hi = p.pos_zone[i][1] - p.target_offset;
+            s[REF + i] = lo + (hi - lo) * uu[i];
+        }
+    }
+};
+
+// success rule of the driver
+__device__ __forceinline__ bool success_of(int rule, int F, bool done, int flag) {
+    return rule == RLP_SUCCESS_FLAG_NE ? (flag != F)
+         : rule == RLP_SUCCESS_FLAG_EQ ? (flag == F)
+                                       : (done && flag != F);
+}
+
+}  // namespace rlp

@@ -1,0 +1,235 @@
+// rlp_mlp.hip — actor/critic MLP forward on fp32 MFMA (v_mfma_f32_16x16x4_f32), the packer for
+// the fused-rollout weight layout, and Gaussian policy sampling.
+//
+// Orientation used everywhere ("env on the lane"): a layer computes H_out^T = W · H_in^T, so the
+// MFMA A operand is a weight fragment (lane l: W[16 j + (l&15)][k]) and the B operand an activation
+// fragment (lane l: H_in[env l&15][k]); the 16x16 C tile lands as lane l: H_out[env l&15]
+// [neuron 16 j + 4 (l>>4) + r], r = 0..3. MFMA numerics are an exact k-ordered fp32 fma chain.
+#include "rlp_mfma_layout.hpp"
+
+namespace rlp {
+
+// ------------------------------------------------------------------------------------------
+// Generic forward: any Linear(+act) stack, one wave per 16 rows, activations in LDS.
+// ------------------------------------------------------------------------------------------
+constexpr int kMlpMaxW = 512;
+
+struct MlpArgs {
+    rlp_mlp_desc d;
+};
+
+__device__ __forceinline__ float act_apply(int act, float v) {
+    return act == RLP_ACT_TANH ? tanhf(v) : (act == RLP_ACT_RELU ? fmaxf(v, 0.f) : v);
+}
+
+__global__ void __launch_bounds__(64) mlp_forward_kernel(MlpArgs args, const float *__restrict__ P,
+                                                         const float *__restrict__ x, float *y, int n,
+                                                         const uint8_t *mask, int ldw) {
+    extern __shared__ float lds[];  // [2][16][ldw]
+    const rlp_mlp_desc &d = args.d;
+    const int lane = threadIdx.x;
+    const int g = lane >> 4, e = lane & 15;
+    const int row0 = blockIdx.x * 16;
+    const int row = row0 + e;
+    bool active = row < n && (!mask || mask[row]);
+    if (!__any(active)) return;  // wave-uniform skip of fully masked 16-row groups
+    float *buf0 = lds, *buf1 = lds + 16 * ldw;
+    // stage input rows (zero padded)
+    const int in0 = d.dims[0];
+    for (int idx = lane; idx < 16 * ldw; idx += 64) {
+        const int r = idx / ldw, k = idx % ldw;
+        const int gr = row0 + r;
+        buf0[idx] = (gr < n && k < in0) ? x[(size_t)gr * in0 + k] : 0.f;
+    }
+    __syncthreads();
+    const float *pw = P;
+    float *cur = buf0, *nxt = buf1;
+    for (int l = 0; l < d.n_layers; ++l) {
+        const int in = d.dims[l], out = d.dims[l + 1];
+        const float *W = pw, *b = pw + (size_t)in * out;
+        const int ks_n = (in + 3) / 4, jt_n = (out + 15) / 16;
+        for (int jt = 0; jt < jt_n; ++jt) {
+            floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+            const int wrow = 16 * jt + e;
+            for (int ks = 0; ks < ks_n; ++ks) {
+                const int k = 4 * ks + g;
+                const float a = (wrow < out && k < in) ? W[(size_t)wrow * in + k] : 0.f;
+                const float bv = cur[e * ldw + k];
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int nr = 16 * jt + 4 * g + r;
+                float v = 0.f;
+                if (nr < out) v = act_apply(d.act[l], acc[r] + b[nr]);
+                nxt[e * ldw + nr] = v;
+            }
+        }
+        // zero the k-padding of the next layer's input
+        const int pad_to = ((out + 3) / 4) * 4;
+        for (int k = jt_n * 16; k < pad_to; ++k) nxt[e * ldw + k] = 0.f;
+        __syncthreads();
+        pw += (size_t)in * out + out;
+        float *t = cur; cur = nxt; nxt = t;
+    }
+    const int outn = d.dims[d.n_layers];
+    if (active) {
+        for (int j = g; j < outn; j += 4) y[(size_t)row * outn + j] = cur[e * ldw + j];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused-layout packer (see rlp_mfma_layout.hpp for the layout)
+// ------------------------------------------------------------------------------------------
+__global__ void mfma_pack_kernel(MfmaNet net, const float *__restrict__ P, float *out) {
+    const int total = (int)net.count;
+    const int S = net.S, H = net.H, A = net.A, NT = H / 16, KS1 = net.ks1;
+    const float *W1 = P, *b1 = W1 + S * H, *W2 = b1 + H, *b2 = W2 + H * H, *W3 = b2 + H,
+                *b3 = W3 + H * A;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += gridDim.x * blockDim.x) {
+        float v = 0.f;
+        if (idx < net.off_b1) {  // W1p [t][kk][lane]
+            const int lane = idx & 63, kk = (idx >> 6) % KS1, t = (idx >> 6) / KS1;
+            const int k = 4 * kk + (lane >> 4), j = 16 * t + (lane & 15);
+            v = k < S ? W1[j * S + k] : 0.f;
+        } else if (idx < net.off_w2) {  // B1p [t][lane][4]
+            const int q = idx - net.off_b1;
+            const int r = q & 3, lane = (q >> 2) & 63, t = q >> 8;
+            v = b1[16 * t + 4 * (lane >> 4) + r];
+        } else if (idx < net.off_b2) {  // W2p [t][r][jq][lane][4]
+            const int q = idx - net.off_w2;
+            const int qq = q & 3, lane = (q >> 2) & 63, jq = (q >> 8) % (NT / 4);
+            const int r = ((q >> 8) / (NT / 4)) & 3, t = ((q >> 8) / (NT / 4)) >> 2;
+            const int j = 16 * (4 * jq + qq) + (lane & 15);
+            const int k = 16 * t + 4 * (lane >> 4) + r;
+            v = W2[j * H + k];
+        } else if (idx < net.off_w3) {  // B2p [j][lane][4]
+            const int q = idx - net.off_b2;
+            const int r = q & 3, lane = (q >> 2) & 63, j = q >> 8;
+            v = b2[16 * j + 4 * (lane >> 4) + r];
+        } else if (idx < net.off_b3) {  // W3p [a][j][lane][4]
+            const int q = idx - net.off_w3;
+            const int r = q & 3, lane = (q >> 2) & 63, j = (q >> 8) % NT, a = (q >> 8) / NT;
+            v = W3[a * H + 16 * j + 4 * (lane >> 4) + r];
+        } else {  // b3 [a] (padded to 4)
+            const int a = idx - net.off_b3;
+            v = a < A ? b3[a] : 0.f;
+        }
+        out[idx] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Gaussian policy sample (Proximal_Policy_Optimization2.choose_action :69-76)
+// ------------------------------------------------------------------------------------------
+struct SampleArgs {
+    float std[8], a_min[8], a_max[8];
+};
+
+template <int A>
+__global__ void __launch_bounds__(256) policy_sample_kernel(const float *__restrict__ mean, int n,
+                                                            SampleArgs sa, const float *noise,
+                                                            uint64_t seed, uint64_t counter,
+                                                            uint64_t env_id0, float *action,
+                                                            float *logp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float eps[A];
+    if (noise) {
+#pragma unroll
+        for (int j = 0; j < A; ++j) eps[j] = noise[(size_t)i * A + j];
+    } else {
+        philox_normal_f32<A>(seed, counter, env_id0 + (uint64_t)i, eps);
+    }
+#pragma unroll
+    for (int j = 0; j < A; ++j) {
+        const float m = mean[(size_t)i * A + j];
+        float a = m + sa.std[j] * eps[j];
+        a = fmaxf(fminf(a, sa.a_max[j]), sa.a_min[j]);
+        action[(size_t)i * A + j] = a;
+        logp[(size_t)i * A + j] = normal_logp(a, m, sa.std[j]);
+    }
+}
+
+}  // namespace rlp
+
+using namespace rlp;
+
+extern "C" {
+
+int64_t rlp_mlp_param_count(const rlp_mlp_desc *desc) {
+    if (!desc || desc->n_layers < 1 || desc->n_layers > RLP_MLP_MAX_LAYERS) return RLP_EINVAL;
+    int64_t c = 0;
+    for (int l = 0; l < desc->n_layers; ++l)
+        c += (int64_t)desc->dims[l] * desc->dims[l + 1] + desc->dims[l + 1];
+    return c;
+}
+
+int rlp_mlp_forward(const rlp_mlp_desc *desc, const float *params, const float *x, float *y,
+                    int n, const uint8_t *mask, rlp_stream_t stream) {
+    RLP_REQUIRE(desc && params && x && y, "rlp_mlp_forward: null argument");
+    RLP_REQUIRE(desc->n_layers >= 1 && desc->n_layers <= RLP_MLP_MAX_LAYERS,
+                "rlp_mlp_forward: n_layers %d", desc->n_layers);
+    int maxw = 0;
+    for (int l = 0; l <= desc->n_layers; ++l) {
+        RLP_REQUIRE(desc->dims[l] >= 1 && desc->dims[l] <= kMlpMaxW,
+                    "rlp_mlp_forward: width %d not in [1, %d]", desc->dims[l], kMlpMaxW);
+        maxw = desc->dims[l] > maxw ? desc->dims[l] : maxw;
+    }
+    if (n <= 0) return n == 0 ? RLP_OK : RLP_EINVAL;
+    // row stride: multiple of 32 (+2) so the B-operand reads (16 rows x 2 k per half-wave) hit
+    // 32 distinct banks
+    const int ldw = ((maxw + 31) / 32) * 32 + 2;
+    const size_t lds = sizeof(float) * 2 * 16 * ldw;
+    MlpArgs args{*desc};
+    mlp_forward_kernel<<<(n + 15) / 16, 64, lds, as_stream(stream)>>>(args, params, x, y, n, mask,
+                                                                      ldw);
+    RLP_CHECK_LAUNCH("rlp_mlp_forward");
+    return RLP_OK;
+}
+
+int64_t rlp_mfma_packed_count(const rlp_mlp_desc *desc) {
+    MfmaNet net;
+    if (!desc || !mfma_net_from_desc(*desc, &net)) return RLP_EUNSUPPORTED;
+    return net.count;
+}
+
+int rlp_mfma_pack(const rlp_mlp_desc *desc, const float *params, float *packed,
+                  rlp_stream_t stream) {
+    RLP_REQUIRE(desc && params && packed, "rlp_mfma_pack: null argument");
+    MfmaNet net;
+    if (!mfma_net_from_desc(*desc, &net))
+        return fail(RLP_EUNSUPPORTED, "rlp_mfma_pack: need [S<=8 -> H -> H -> A<=4], H in {64,128,256}");
+    const int blocks = (int)((net.count + 255) / 256);
+    mfma_pack_kernel<<<blocks < 1024 ? blocks : 1024, 256, 0, as_stream(stream)>>>(net, params,
+                                                                                  packed);
+    RLP_CHECK_LAUNCH("rlp_mfma_pack");
+    return RLP_OK;
+}
+
+int rlp_policy_sample(const float *mean, int n, int A, const float *std, const float *a_min,
+                      const float *a_max, const float *noise, uint64_t seed, uint64_t counter,
+                      uint64_t env_id0, float *action, float *logp, rlp_stream_t stream) {
+    RLP_REQUIRE(mean && std && a_min && a_max && action && logp, "rlp_policy_sample: null argument");
+    RLP_REQUIRE(A >= 1 && A <= 4, "rlp_policy_sample: A = %d not in [1, 4]", A);
+    if (n <= 0) return n == 0 ? RLP_OK : RLP_EINVAL;
+    SampleArgs sa;
+    for (int j = 0; j < 8; ++j) {
+        sa.std[j] = j < A ? std[j] : 1.f;
+        sa.a_min[j] = j < A ? a_min[j] : 0.f;
+        sa.a_max[j] = j < A ? a_max[j] : 0.f;
+    }
+    const dim3 grid((n + 255) / 256), block(256);
+    hipStream_t s = as_stream(stream);
+    switch (A) {
+    case 1: policy_sample_kernel<1><<<grid, block, 0, s>>>(mean, n, sa, noise, seed, counter, env_id0, action, logp); break;
+    case 2: policy_sample_kernel<2><<<grid, block, 0, s>>>(mean, n, sa, noise, seed, counter, env_id0, action, logp); break;
+    case 3: policy_sample_kernel<3><<<grid, block, 0, s>>>(mean, n, sa, noise, seed, counter, env_id0, action, logp); break;
+    case 4: policy_sample_kernel<4><<<grid, block, 0, s>>>(mean, n, sa, noise, seed, counter, env_id0, action, logp); break;
+    }
+    RLP_CHECK_LAUNCH("rlp_policy_sample");
+    return RLP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,255 @@
+// rlp_rollout.hip — fused batched rollout: the reference driver loop
+// (demonstration/PPO2/PPO2-4-CartPole/train.py:184-217) for n envs and T steps in ONE launch.
+//
+// Per wave: WENV = 16*SUB envs, env state resident in registers (f64) for all T steps. Per step:
+//   auto-reset (need_reset)            train.py:187-191, env.reset(random=True)
+//   obs = get_state()                  CartPole.py:145-153 (etc.)
+//   actor forward -> mean; sample      Proximal_Policy_Optimization2.py:69-76 (Philox eps)
+//   critic forward -> V(s_t)           (learn() :91, same params => same values)
+//   env.step_update(a)                 CartPole.py:257-264 (etc.)
+//   buffer.append(...)                 utils/classes.py:264-272, time-major [T][n][...]
+// The two MLPs are fp32 MFMA (v_mfma_f32_16x16x4_f32): this kernel is MFMA-bound.
+#include "rlp_envs.hpp"
+#include "rlp_mfma_layout.hpp"
+
+namespace rlp {
+
+struct RolloutArgs {
+    int T, n;
+    uint64_t seed, step0, env_id0;
+    int success_rule, success_flag;
+    float std_[4], a_min[4], a_max[4], gain[4], off[4];
+};
+
+template <int KIND, int H, int SUB>
+__global__ void __launch_bounds__(256, (SUB == 4 ? 1 : 2))
+rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__restrict__ need_reset,
+               const float *__restrict__ actor, MfmaNet an, const float *__restrict__ critic,
+               MfmaNet cn, RolloutArgs ra, rlp_rollout_bufs b) {
+    using E = Env<KIND>;
+    constexpr int S = E::S, A = E::A, D = E::D, KS1 = (S + 3) / 4, WENV = 16 * SUB;
+    __shared__ float sobs[4][WENV][8];
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, e = lane & 15;
+    const int n = ra.n;
+    const int env = (blockIdx.x * 4 + wave) * WENV + lane;  // physics lane -> env
+    const bool phys = lane < WENV && env < n;
+    const uint64_t eid = ra.env_id0 + (uint64_t)env;
+
+    double s[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) s[d] = phys ? state[(size_t)d * n + env] : 0.0;
+    bool need = phys ? need_reset[env] != 0 : false;
+    bool prev_done = true;  // no value_next write before step 0
+
+    for (int t = 0; t < ra.T; ++t) {
+        const uint64_t gstep = ra.step0 + (uint64_t)t;
+        const size_t k = (size_t)t * n + env;
+        if (phys && need) {
+            E::reset(p, s, ra.seed, gstep, eid);
+            need = false;
+        }
+        float o[S];
+        E::observe(p, s, o);
+        if (lane < WENV) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sobs[wave][lane][j] = (phys && j < S) ? o[j] : 0.f;
+        }
+        __syncthreads();
+        float bobs[SUB][KS1];
+#pragma unroll
+        for (int sb = 0; sb < SUB; ++sb)
+#pragma unroll
+            for (int kk = 0; kk < KS1; ++kk) bobs[sb][kk] = sobs[wave][16 * sb + e][4 * kk + g];
+        __syncthreads();
+
+        // actor then critic through ONE copy of the fused forward (one register allocation)
+        float mraw[A], v = 0.f;
+#pragma unroll 1
+        for (int which = 0; which < 2; ++which) {
+            float out[SUB][A];
+            mlp_fused_forward<H, SUB, KS1, A>(which ? critic : actor, which ? cn : an,
+                                              which ? 1 : A, bobs, out);
+            // the physics lane (sub-block g, env e) owns out[g]
+            float sel[A];
+#pragma unroll
+            for (int a = 0; a < A; ++a) sel[a] = out[0][a];
+#pragma unroll
+            for (int sb = 1; sb < SUB; ++sb)
+                if (g == sb) {
+#pragma unroll
+                    for (int a = 0; a < A; ++a) sel[a] = out[sb][a];
+                }
+            if (which) {
+                v = sel[0];
+            } else {
+#pragma unroll
+                for (int a = 0; a < A; ++a) mraw[a] = sel[a];
+            }
+        }
+        if (phys) {
+            float eps[A], act[A], lp[A];
+            philox_normal_f32<A>(ra.seed, gstep, eid, eps);
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                const float m = (an.out_tanh ? tanhf(mraw[a]) : mraw[a]) * ra.gain[a] + ra.off[a];
+                float x = m + ra.std_[a] * eps[a];
+                x = fmaxf(fminf(x, ra.a_max[a]), ra.a_min[a]);
+                act[a] = x;
+                lp[a] = normal_logp(x, m, ra.std_[a]);
+            }
+            float on[S];
+            double r;
+            int f;
+            bool dn;
+            E::step(p, s, act, on, r, f, dn);
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                b.obs[k * S + j] = o[j];
+                b.obs_next[k * S + j] = on[j];
+            }
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                b.action[k * A + a] = act[a];
+                b.logp[k * A + a] = lp[a];
+            }
+            b.reward[k] = (float)r;
+            b.value[k] = v;
+            b.done[k] = dn;
+            b.success[k] = success_of(ra.success_rule, ra.success_flag, dn, f);
+            b.flag[k] = (int8_t)f;
+            if (!prev_done) b.value_next[k - n] = v;  // V(s'_{t-1}) == V(s_t) when no reset
+            prev_done = dn;
+            need = dn;
+        }
+    }
+
+    // bootstrap V(s'_{T-1}) for envs that did not terminate on the last step
+    float o[S];
+    E::observe(p, s, o);
+    if (lane < WENV) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sobs[wave][lane][j] = (phys && j < S) ? o[j] : 0.f;
+    }
+    __syncthreads();
+    float bobs[SUB][KS1];
+#pragma unroll
+    for (int sb = 0; sb < SUB; ++sb)
+#pragma unroll
+        for (int kk = 0; kk < KS1; ++kk) bobs[sb][kk] = sobs[wave][16 * sb + e][4 * kk + g];
+    float cv[SUB][A];
+    mlp_fused_forward<H, SUB, KS1, A>(critic, cn, 1, bobs, cv);
+    float v = cv[0][0];
+#pragma unroll
+    for (int sb = 1; sb < SUB; ++sb)
+        if (g == sb) v = cv[sb][0];
+    if (phys) {
+        if (!prev_done) b.value_next[(size_t)(ra.T - 1) * n + env] = v;
+#pragma unroll
+        for (int d = 0; d < D; ++d) state[(size_t)d * n + env] = s[d];
+        need_reset[env] = need ? 1 : 0;
+    }
+}
+
+template <int KIND, int H, int SUB>
+static int launch_rollout(const void *params, double *state, uint8_t *need_reset,
+                          const float *actor, const MfmaNet &an, const float *critic,
+                          const MfmaNet &cn, const RolloutArgs &ra, const rlp_rollout_bufs &b,
+                          hipStream_t stream) {
+    const auto &p = *static_cast<const typename Env<KIND>::P *>(params);
+    constexpr int envs_per_block = 4 * 16 * SUB;
+    const int blocks = (ra.n + envs_per_block - 1) / envs_per_block;
+    rollout_kernel<KIND, H, SUB><<<blocks, 256, 0, stream>>>(p, state, need_reset, actor, an,
+                                                             critic, cn, ra, b);
+    RLP_CHECK_LAUNCH("rlp_rollout");
+    return RLP_OK;
+}
+
+template <int KIND>
+static int rollout_kind(const void *params, double *state, uint8_t *need_reset, const float *actor,
+                        const MfmaNet &an, const float *critic, const MfmaNet &cn,
+                        const RolloutArgs &ra, const rlp_rollout_bufs &b, int sub,
+                        hipStream_t stream) {
+    using E = Env<KIND>;
+    if (an.S != E::S || cn.S != E::S || an.A != E::A || cn.A != 1)
+        return fail(RLP_EINVAL, "rlp_rollout: net dims (S=%d,A=%d / S=%d,A=%d) != env (S=%d,A=%d)",
+                    an.S, an.A, cn.S, cn.A, E::S, E::A);
+    if (an.H != 256 || cn.H != 256)
+        return fail(RLP_EUNSUPPORTED, "rlp_rollout: hidden width %d/%d (built for 256)", an.H, cn.H);
+    if (sub == 2)
+        return launch_rollout<KIND, 256, 2>(params, state, need_reset, actor, an, critic, cn, ra, b,
+                                            stream);
+    return launch_rollout<KIND, 256, 4>(params, state, need_reset, actor, an, critic, cn, ra, b,
+                                        stream);
+}
+
+static int g_rollout_sub = 4;
+
+}  // namespace rlp
+
+using namespace rlp;
+
+extern "C" {
+
+// tuning knob (envs per wave = 16 * sub); sub in {2, 4}
+int rlp_set_rollout_sub(int sub) {
+    if (sub != 2 && sub != 4) return fail(RLP_EINVAL, "rlp_set_rollout_sub: %d", sub);
+    g_rollout_sub = sub;
+    return RLP_OK;
+}
+
+int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_reset,
+                const rlp_mlp_desc *actor_desc, const float *actor_packed,
+                const rlp_mlp_desc *critic_desc, const float *critic_packed,
+                const rlp_rollout_cfg *cfg, const rlp_rollout_bufs *bufs, rlp_stream_t stream) {
+    RLP_REQUIRE(env_params && state && need_reset && actor_desc && actor_packed && critic_desc &&
+                    critic_packed && cfg && bufs,
+                "rlp_rollout: null argument");
+    const rlp_rollout_bufs &b = *bufs;
+    RLP_REQUIRE(b.obs && b.obs_next && b.action && b.logp && b.reward && b.value && b.value_next &&
+                    b.done && b.success && b.flag,
+                "rlp_rollout: null buffer");
+    RLP_REQUIRE(cfg->T >= 1 && cfg->n >= 0, "rlp_rollout: T=%d n=%d", cfg->T, cfg->n);
+    if (cfg->n == 0) return RLP_OK;
+    MfmaNet an, cn;
+    if (!mfma_net_from_desc(*actor_desc, &an) || !mfma_net_from_desc(*critic_desc, &cn))
+        return fail(RLP_EUNSUPPORTED, "rlp_rollout: nets must be [S->H->H->A] tanh MLPs");
+    RolloutArgs ra;
+    ra.T = cfg->T; ra.n = cfg->n;
+    ra.seed = cfg->seed; ra.step0 = cfg->step0; ra.env_id0 = cfg->env_id0;
+    ra.success_rule = cfg->success_rule; ra.success_flag = cfg->success_flag;
+    for (int a = 0; a < 4; ++a) {
+        ra.std_[a] = cfg->std[a];
+        ra.a_min[a] = cfg->a_min[a];
+        ra.a_max[a] = cfg->a_max[a];
+        ra.off[a] = (cfg->a_min[a] + cfg->a_max[a]) / 2.0f;  // PPOActor_Gaussian: (a_min+a_max)/2
+        ra.gain[a] = cfg->a_max[a] - ra.off[a];              //                   a_max - off
+    }
+    hipStream_t s = as_stream(stream);
+    const int sub = g_rollout_sub;
+    switch (kind) {
+    case RLP_ENV_CARTPOLE:
+        return rollout_kind<RLP_ENV_CARTPOLE>(env_params, state, need_reset, actor_packed, an,
+                                              critic_packed, cn, ra, b, sub, s);
+    case RLP_ENV_CARTPOLE_ANGLEONLY:
+        return rollout_kind<RLP_ENV_CARTPOLE_ANGLEONLY>(env_params, state, need_reset, actor_packed,
+                                                        an, critic_packed, cn, ra, b, sub, s);
+    case RLP_ENV_SOI:
+        return rollout_kind<RLP_ENV_SOI>(env_params, state, need_reset, actor_packed, an,
+                                         critic_packed, cn, ra, b, sub, s);
+    case RLP_ENV_UGV_FORWARD:
+        return rollout_kind<RLP_ENV_UGV_FORWARD>(env_params, state, need_reset, actor_packed, an,
+                                                 critic_packed, cn, ra, b, sub, s);
+    case RLP_ENV_UGV_BIDIRECTIONAL:
+        return rollout_kind<RLP_ENV_UGV_BIDIRECTIONAL>(env_params, state, need_reset, actor_packed,
+                                                       an, critic_packed, cn, ra, b, sub, s);
+    case RLP_ENV_UAV_HOVER_OUTER_LOOP:
+        return rollout_kind<RLP_ENV_UAV_HOVER_OUTER_LOOP>(env_params, state, need_reset,
+                                                          actor_packed, an, critic_packed, cn, ra,
+                                                          b, sub, s);
+    }
+    return fail(RLP_EINVAL, "rlp_rollout: unknown env kind %d", kind);
+}
+
+}  // extern "C"

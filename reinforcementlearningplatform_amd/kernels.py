@@ -1,0 +1,150 @@
+"""Tensor-level wrappers of librlp's C-ABI (one function per entry point of include/rlp.h).
+
+All tensors live on the ROCm device. Nothing here falls back to the CPU.
+"""
+import ctypes as C
+
+import torch
+
+from . import _abi
+from ._native import check, lib, ptr, stream_ptr
+
+
+def dims(kind):
+    return _abi.ENV_DIMS[kind]
+
+
+def _dev(device):
+    return torch.device(device) if device is not None else torch.device("cuda")
+
+
+def new_state(kind, n, device=None):
+    D, _, _ = dims(kind)
+    return torch.zeros((D, n), dtype=torch.float64, device=_dev(device))
+
+
+def env_reset(kind, params, state, mask=None, init_state=None, seed=0, counter=0, env_id0=0):
+    n = state.shape[1]
+    check(lib().rlp_env_reset(kind, C.byref(params), ptr(state), n, ptr(mask), ptr(init_state),
+                              seed, counter, env_id0, stream_ptr()), "rlp_env_reset")
+
+
+def env_observe(kind, params, state, out=None):
+    _, S, _ = dims(kind)
+    n = state.shape[1]
+    out = out if out is not None else torch.empty((n, S), dtype=torch.float32, device=state.device)
+    check(lib().rlp_env_observe(kind, C.byref(params), ptr(state), n, ptr(out), stream_ptr()),
+          "rlp_env_observe")
+    return out
+
+
+def env_step(kind, params, state, action, want_obs_cur=True):
+    _, S, A = dims(kind)
+    n = state.shape[1]
+    dev = state.device
+    action = action.to(device=dev, dtype=torch.float32).reshape(n, A).contiguous()
+    oc = torch.empty((n, S), dtype=torch.float32, device=dev) if want_obs_cur else None
+    on = torch.empty((n, S), dtype=torch.float32, device=dev)
+    r = torch.empty(n, dtype=torch.float64, device=dev)
+    f = torch.empty(n, dtype=torch.int32, device=dev)
+    d = torch.empty(n, dtype=torch.uint8, device=dev)
+    check(lib().rlp_env_step(kind, C.byref(params), ptr(state), n, ptr(action), ptr(oc), ptr(on),
+                             ptr(r), ptr(f), ptr(d), stream_ptr()), "rlp_env_step")
+    return oc, on, r, f, d
+
+
+def mlp_forward(desc, params, x, mask=None, out=None):
+    n = x.shape[0]
+    outn = desc.dims[desc.n_layers]
+    out = out if out is not None else torch.empty((n, outn), dtype=torch.float32, device=x.device)
+    check(lib().rlp_mlp_forward(C.byref(desc), ptr(params), ptr(x.contiguous()), ptr(out), n,
+                                ptr(mask), stream_ptr()), "rlp_mlp_forward")
+    return out
+
+
+def mfma_pack(desc, params, out=None):
+    cnt = lib().rlp_mfma_packed_count(C.byref(desc))
+    if cnt < 0:
+        check(int(cnt), "rlp_mfma_packed_count")
+    out = out if out is not None else torch.empty(cnt, dtype=torch.float32, device=params.device)
+    check(lib().rlp_mfma_pack(C.byref(desc), ptr(params), ptr(out), stream_ptr()), "rlp_mfma_pack")
+    return out
+
+
+def _host_f32(v, A):
+    arr = (C.c_float * A)()
+    vals = list(v) if hasattr(v, "__len__") else [v] * A
+    for i in range(A):
+        arr[i] = float(vals[i])
+    return arr
+
+
+def policy_sample(mean, std, a_min, a_max, noise=None, seed=0, counter=0, env_id0=0):
+    n, A = mean.shape
+    a = torch.empty_like(mean)
+    lp = torch.empty_like(mean)
+    check(lib().rlp_policy_sample(ptr(mean.contiguous()), n, A, _host_f32(std, A),
+                                  _host_f32(a_min, A), _host_f32(a_max, A), ptr(noise), seed,
+                                  counter, env_id0, ptr(a), ptr(lp), stream_ptr()),
+          "rlp_policy_sample")
+    return a, lp
+
+
+def rollout_buffers(kind, T, n, device=None):
+    _, S, A = dims(kind)
+    dev = _dev(device)
+    f32 = dict(dtype=torch.float32, device=dev)
+    u8 = dict(dtype=torch.uint8, device=dev)
+    return dict(obs=torch.empty((T, n, S), **f32), obs_next=torch.empty((T, n, S), **f32),
+                action=torch.empty((T, n, A), **f32), logp=torch.empty((T, n, A), **f32),
+                reward=torch.empty((T, n), **f32), value=torch.empty((T, n), **f32),
+                value_next=torch.zeros((T, n), **f32), done=torch.empty((T, n), **u8),
+                success=torch.empty((T, n), **u8), flag=torch.empty((T, n), dtype=torch.int8,
+                                                                    device=dev))
+
+
+def rollout(kind, params, state, need_reset, actor_desc, actor_packed, critic_desc, critic_packed,
+            cfg, bufs):
+    cb = _abi.RolloutBufs(**{k: v.data_ptr() for k, v in bufs.items()})
+    check(lib().rlp_rollout(kind, C.byref(params), ptr(state), ptr(need_reset), C.byref(actor_desc),
+                            ptr(actor_packed), C.byref(critic_desc), ptr(critic_packed),
+                            C.byref(cfg), C.byref(cb), stream_ptr()), "rlp_rollout")
+
+
+def make_rollout_cfg(T, n, seed, step0, env_id0, std, a_min, a_max, success_rule, success_flag):
+    cfg = _abi.RolloutCfg()
+    cfg.T, cfg.n, cfg.seed, cfg.step0, cfg.env_id0 = T, n, seed, step0, env_id0
+    cfg.success_rule, cfg.success_flag = success_rule, success_flag
+    A = len(a_min)
+    stdv = list(std) if hasattr(std, "__len__") else [std] * A
+    for i in range(4):
+        cfg.std[i] = float(stdv[i]) if i < A else 1.0
+        cfg.a_min[i] = float(a_min[i]) if i < A else 0.0
+        cfg.a_max[i] = float(a_max[i]) if i < A else 0.0
+    return cfg
+
+
+def reward_norm(reward, rms, work=None, out=None):
+    """reward [T][n] f32 -> normalised (in `out`, may alias); rms: f64[4] device running stats."""
+    T, n = reward.shape
+    work = work if work is not None else torch.empty(3 * T, dtype=torch.float64, device=reward.device)
+    out = out if out is not None else torch.empty_like(reward)
+    check(lib().rlp_reward_norm(ptr(reward), T, n, ptr(rms), ptr(work), ptr(out), stream_ptr()),
+          "rlp_reward_norm")
+    return out
+
+
+def gae(reward, value, value_next, done, success, gamma, lmd, adv=None, v_target=None, stats=None):
+    T, n = reward.shape
+    adv = adv if adv is not None else torch.empty_like(reward)
+    v_target = v_target if v_target is not None else torch.empty_like(reward)
+    check(lib().rlp_gae(ptr(reward), ptr(value), ptr(value_next), ptr(done), ptr(success),
+                        float(gamma), float(lmd), T, n, ptr(adv), ptr(v_target), ptr(stats),
+                        stream_ptr()), "rlp_gae")
+    return adv, v_target
+
+
+def adv_normalize(adv, stats):
+    check(lib().rlp_adv_normalize(ptr(adv), adv.numel(), ptr(stats), stream_ptr()),
+          "rlp_adv_normalize")
+    return adv

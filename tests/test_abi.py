@@ -1,0 +1,63 @@
+"""CPU-side checks of the drop-in boundary: librlp.so loads, exports every entry point that
+include/rlp.h declares, agrees with the ctypes struct mirror, and rejects bad arguments with a
+status code (host-side validation only — no kernel is launched here)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from reinforcementlearningplatform_amd import _abi, _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "rlp.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(rlp_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.lib()
+    names = header_functions()
+    assert len(names) >= 15, names
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, f"declared in include/rlp.h but not exported: {missing}"
+
+
+def test_struct_layouts_match():
+    lib = _native.lib()
+    for i, (name, size) in enumerate(_abi.check_struct_sizes().items()):
+        assert lib.rlp_struct_size(i) == size, name
+
+
+@pytest.mark.parametrize("kind", sorted(_abi.ENV_DIMS))
+def test_env_dims(kind):
+    lib = _native.lib()
+    D, S, A = C.c_int(), C.c_int(), C.c_int()
+    assert lib.rlp_env_dims(kind, C.byref(D), C.byref(S), C.byref(A)) == 0
+    assert (D.value, S.value, A.value) == _abi.ENV_DIMS[kind]
+
+
+def test_bad_arguments_return_status():
+    lib = _native.lib()
+    assert lib.rlp_env_dims(99, None, None, None) == _abi.RLP_EINVAL
+    assert b"unknown env kind" in lib.rlp_last_error_string()
+    rc = lib.rlp_env_step(1, None, None, 4, None, None, None, None, None, None, None)
+    assert rc == _abi.RLP_EINVAL and b"null" in lib.rlp_last_error_string()
+    d = _abi.MLPDesc.make([4, 100, 100, 1], [1, 1, 1])
+    assert lib.rlp_mfma_packed_count(C.byref(d)) == _abi.RLP_EUNSUPPORTED
+    d = _abi.MLPDesc.make([4, 256, 256, 1], [1, 1, 0])
+    assert lib.rlp_mfma_packed_count(C.byref(d)) > 256 * 256
+    assert lib.rlp_mlp_param_count(C.byref(d)) == d.param_count() == 67329
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(ROOT, "reinforcementlearningplatform_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
+                src = open(os.path.join(dp, f)).read()
+                assert "oracle" not in re.sub(r"#.*|//.*", "", src).lower().replace(
+                    "oracle_free", ""), f"{f} references the oracle"

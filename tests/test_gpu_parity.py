@@ -1,0 +1,216 @@
+"""GPU parity: librlp.so's HIP kernels against the CPU oracle and the reference's golden vectors.
+
+Tolerances: physics is float64 on both sides, so env outputs must match the
+reference numpy step() to ~1 ulp of libm (checked at rtol 1e-9); float32 observations to 1 ulp;
+MLP outputs (fp32 MFMA vs the reference's fp32 torch) at rtol 1e-5 + atol 1e-6-ish; GAE is
+bit-exact; Philox resets are bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from reinforcementlearningplatform_amd import _abi as A
+from reinforcementlearningplatform_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+from test_oracle_golden import ENV_CASES  # noqa: E402
+
+
+def dev(x, dtype=None):
+    t = torch.as_tensor(np.ascontiguousarray(x))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+def close(a, b, rtol, atol, what):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    bad = np.abs(a - b) > atol + rtol * np.abs(b)
+    assert not bad.any(), f"{what}: {bad.sum()} mismatches, max abs err {np.max(np.abs(a - b))}"
+
+
+@pytest.mark.parametrize("name,kind,pf", ENV_CASES, ids=[c[0] for c in ENV_CASES])
+def test_env_step_vs_reference_golden(golden, name, kind, pf):
+    g = golden(name)
+    p = pf()
+    st = dev(g["state"].T)
+    oc, on, r, f, d = K.env_step(kind, p, st, dev(g["action"]))
+    torch.cuda.synchronize()
+    close(host(st).T, g["state_next"], 1e-9, 1e-12, "state_next")
+    close(host(oc), g["obs_cur"].astype(np.float32), 1e-6, 1e-7, "obs_cur")
+    close(host(on), g["obs_next"].astype(np.float32), 1e-6, 1e-7, "obs_next")
+    close(host(r), g["reward"], 1e-7, 1e-9, "reward")
+    np.testing.assert_array_equal(host(f), g["flag"])
+    np.testing.assert_array_equal(host(d), g["done"])
+
+
+def _random_states(kind, n, rng):
+    D, S, Ad = A.ENV_DIMS[kind]
+    p = A.default_params(kind)
+    st = np.zeros((D, n))
+    oracle.env_reset(kind, p, st, seed=123, counter=7)
+    # spread the states, incl. out-of-bounds neighbourhoods
+    if kind in (A.RLP_ENV_CARTPOLE, A.RLP_ENV_CARTPOLE_ANGLEONLY):
+        st[0] = rng.uniform(-0.85, 0.85, n); st[1] = rng.uniform(-3, 3, n)
+        st[2] = rng.uniform(-1.6, 1.6, n); st[3] = rng.uniform(-3, 3, n)
+        st[4] = rng.integers(0, 250, n) * 0.02
+    elif kind == A.RLP_ENV_SOI:
+        st[0:2] = rng.uniform(-0.1, 5.1, (2, n)); st[2:4] = rng.uniform(-3, 3, (2, n))
+        st[4] = rng.integers(0, 250, n) * 0.02
+    elif kind in (A.RLP_ENV_UGV_FORWARD, A.RLP_ENV_UGV_BIDIRECTIONAL):
+        st[0:2] = rng.uniform(-0.1, 5.1, (2, n)); st[2] = rng.uniform(-0.5, 3, n)
+        st[3] = rng.uniform(-np.pi, np.pi, n); st[4] = rng.uniform(-3, 3, n)
+        st[5] = rng.integers(0, 500, n) * 0.02
+    else:
+        st[0:3] = rng.uniform(-4.9, 4.9, (3, n)); st[2] = rng.uniform(0.05, 4.9, n)
+        st[3:6] = rng.uniform(-2, 2, (3, n)); st[6:9] = rng.uniform(-0.6, 0.6, (3, n))
+        st[9:12] = rng.uniform(-2, 2, (3, n)); st[12] = rng.integers(0, 999, n) * 0.01
+        st[16:22] = rng.uniform(-0.3, 0.3, (6, n))
+    lo, hi = A.action_bounds(kind, p)
+    act = rng.uniform(lo, hi, (n, Ad)).astype(np.float32)
+    return p, st, act
+
+
+@pytest.mark.parametrize("kind", sorted(A.ENV_DIMS))
+def test_env_step_vs_oracle_large(kind):
+    rng = np.random.default_rng(kind)
+    n = 1 << 16
+    p, st, act = _random_states(kind, n, rng)
+    g = dev(st)
+    oc, on, r, f, d = K.env_step(kind, p, g, dev(act))
+    o_oc, o_on, o_r, o_f, o_d = oracle.env_step(kind, p, st, act)
+    torch.cuda.synchronize()
+    close(host(g), st, 1e-9, 1e-12, "state")
+    close(host(oc), o_oc, 1e-6, 1e-7, "obs_cur")
+    close(host(on), o_on, 1e-6, 1e-7, "obs_next")
+    close(host(r), o_r, 1e-8, 1e-9, "reward")
+    # flags may only differ where a threshold is straddled within float64 rounding
+    assert (host(f) != o_f).mean() < 1e-4
+    assert (host(d) != o_d).mean() < 1e-4
+
+
+@pytest.mark.parametrize("kind", sorted(A.ENV_DIMS))
+def test_reset_bit_exact_and_observe(kind):
+    D, S, _ = A.ENV_DIMS[kind]
+    p = A.default_params(kind)
+    n = 100_003
+    rng = np.random.default_rng(5)
+    mask = (rng.uniform(0, 1, n) < 0.7).astype(np.uint8)
+    st0 = rng.uniform(-1, 1, (D, n))
+    g = dev(st0)
+    K.env_reset(kind, p, g, mask=dev(mask), seed=3407, counter=11, env_id0=1000)
+    o = st0.copy()
+    oracle.env_reset(kind, p, o, mask=mask, seed=3407, counter=11, env_id0=1000)
+    np.testing.assert_array_equal(host(g), o)
+    obs = K.env_observe(kind, p, g)
+    close(host(obs), oracle.env_observe(kind, p, o), 1e-6, 1e-7, "observe")
+
+
+def test_mlp_forward_shipped_nets(golden):
+    g = golden("ppo2_cartpole_nets")
+    ad = A.MLPDesc.make([4, 256, 256, 1], [1, 1, 1])
+    cd = A.MLPDesc.make([4, 256, 256, 1], [1, 1, 0])
+    x = dev(g["x"])
+    mean = host(K.mlp_forward(ad, dev(g["actor_params"]), x)) * np.float32(8)
+    v = host(K.mlp_forward(cd, dev(g["critic_params"]), x))
+    close(mean, g["actor_mean"], 1e-5, 2e-6, "actor mean vs torch")
+    close(v, g["critic_v"], 1e-5, 2e-5, "critic v vs torch")
+
+
+@pytest.mark.parametrize("dims,acts", [
+    ([4, 128, 64, 32, 2], [1, 1, 1, 1]),      # PPO2-4-SecondOrderIntegration actor
+    ([6, 128, 64, 3], [1, 1, 1]),             # PPO-4-UavHoverOuterLoop actor
+    ([2, 256, 256, 1], [1, 1, 0]),            # AngleOnly critic
+    ([41, 256, 256, 2], [1, 1, 1]),           # UGV obstacle-avoidance actor (41 inputs)
+    ([5, 33, 17, 1], [2, 1, 0]),              # ragged widths, relu
+])
+def test_mlp_forward_generic_vs_oracle(dims, acts):
+    rng = np.random.default_rng(len(dims) * 100 + dims[0])
+    d = A.MLPDesc.make(dims, acts)
+    prm = (rng.normal(0, 1, d.param_count()) / 8).astype(np.float32)
+    n = 3001
+    x = rng.uniform(-2, 2, (n, dims[0])).astype(np.float32)
+    mask = (rng.uniform(0, 1, n) < 0.5).astype(np.uint8)
+    y = K.mlp_forward(d, dev(prm), dev(x), mask=dev(mask), out=torch.full((n, dims[-1]), 7.0,
+                                                                           device="cuda"))
+    ref = oracle.mlp_forward(d, prm, x)
+    yh = host(y)
+    close(yh[mask == 1], ref[mask == 1], 1e-5, 2e-6, "masked rows")
+    assert (yh[mask == 0] == 7.0).all()
+
+
+def test_policy_sample_philox_and_noise(golden):
+    rng = np.random.default_rng(2)
+    n, Ad = 70_000, 3
+    mean = rng.uniform(-9, 9, (n, Ad)).astype(np.float32)
+    std, lo, hi = [2.6, 1.0, 0.5], [-8, -8, -8], [8, 8, 8]
+    a, lp = K.policy_sample(dev(mean), std, lo, hi, seed=3407, counter=99, env_id0=5)
+    oa, olp = oracle.policy_sample(mean, std, lo, hi, seed=3407, counter=99, env_id0=5)
+    close(host(a), oa, 1e-6, 2e-6, "philox action")
+    close(host(lp), olp, 1e-6, 2e-6, "philox logp")
+    eps = rng.normal(0, 1, (n, Ad)).astype(np.float32)
+    a, lp = K.policy_sample(dev(mean), std, lo, hi, noise=dev(eps))
+    oa, olp = oracle.policy_sample(mean, std, lo, hi, noise=eps)
+    close(host(a), oa, 0, 1e-6, "noise action")
+    close(host(lp), olp, 1e-6, 1e-6, "noise logp")
+    # reference log_prob semantics on the shipped-net samples
+    g = golden("ppo2_cartpole_nets")
+    m = g["actor_mean"][:256]
+    e = (g["sample_a"].astype(np.float64) - m) / float(g["std"])
+    cl = np.abs(g["sample_a"]) >= 8
+    e[cl] = np.sign(g["sample_a"][cl]) * (np.abs(e[cl]) + 1)
+    a, lp = K.policy_sample(dev(m), float(g["std"]), [-8], [8], noise=dev(e.astype(np.float32)))
+    close(host(a), g["sample_a"], 0, 2e-6, "sample a vs torch")
+    close(host(lp), g["sample_logp"], 0, 2e-6, "sample logp vs torch")
+
+
+def test_gae_bit_exact_vs_reference(golden):
+    g = golden("gae")
+    for c in range(4):
+        k = lambda s: g[f"c{c}_{s}"]
+        T = len(k("r"))
+        col = lambda x, dt: dev(x.reshape(T, 1), dt)
+        stats = torch.zeros(2, dtype=torch.float64, device="cuda")
+        adv, vt = K.gae(col(k("r"), torch.float32), col(k("v"), torch.float32),
+                        col(k("vn"), torch.float32), col(k("done"), torch.uint8),
+                        col(k("success"), torch.uint8), float(g["gamma"]), float(g["lmd"]),
+                        stats=stats)
+        np.testing.assert_array_equal(host(adv).ravel(), k("adv"))
+        np.testing.assert_array_equal(host(vt).ravel(), k("v_target"))
+        K.adv_normalize(adv, stats)
+        close(host(adv).ravel(), k("adv_norm"), 2e-5, 2e-6, "adv_norm")
+
+
+def test_gae_batched_bit_exact_vs_oracle():
+    rng = np.random.default_rng(9)
+    T, n = 200, 40_000
+    r = rng.normal(0, 1, (T, n)).astype(np.float32)
+    v = rng.normal(30, 5, (T, n)).astype(np.float32)
+    vn = rng.normal(30, 5, (T, n)).astype(np.float32)
+    done = (rng.uniform(0, 1, (T, n)) < 0.01).astype(np.uint8)
+    succ = (done * (rng.uniform(0, 1, (T, n)) < 0.6)).astype(np.uint8)
+    adv, vt = K.gae(dev(r), dev(v), dev(vn), dev(done), dev(succ), 0.999, 0.95)
+    oadv, ovt = oracle.gae(r, v, vn, done, succ, 0.999, 0.95)
+    np.testing.assert_array_equal(host(adv), oadv)
+    np.testing.assert_array_equal(host(vt), ovt)
+
+
+@pytest.mark.parametrize("T,n", [(1000, 1), (64, 10_000), (3, 65_536)])
+def test_reward_norm_vs_oracle(golden, T, n):
+    rng = np.random.default_rng(T)
+    r = rng.normal(-2, 3, (T, n)).astype(np.float32)
+    rms = torch.zeros(4, dtype=torch.float64, device="cuda")
+    out = host(K.reward_norm(dev(r), rms))
+    o, orms = oracle.reward_norm(r)
+    close(out, o, 1e-6, 1e-6, "normalised reward")
+    close(host(rms), orms, 1e-9, 1e-9, "running stats")
+    if n == 1:
+        gg = golden("reward_norm")
+        rms = torch.zeros(4, dtype=torch.float64, device="cuda")
+        out = host(K.reward_norm(dev(gg["x"].astype(np.float32).reshape(-1, 1)), rms)).ravel()
+        close(out, gg["y"], 1e-5, 1e-6, "vs reference Normalization")
