@@ -97,8 +97,7 @@ class Segment:
     def learn_side(self):
         b = self.bufs
         # V(s'_t) of terminal transitions (non-terminal ones were written by the rollout)
-        K.mlp_forward(self.cd, self.critic, b["obs_next"].view(-1, self.S),
-                      mask=b["done"].view(-1), out=b["value_next"].view(-1, 1))
+        K.value_fixup(self.cd, self.cpk, b["obs_next"], b["done"], b["success"], b["value_next"])
         K.reward_norm(b["reward"], self.rms, self.work, out=self.rnorm)
         self.stats.zero_()
         K.gae(self.rnorm, b["value"], b["value_next"], b["done"], b["success"], 0.999, 0.95,
@@ -133,8 +132,8 @@ def cpu_baseline(env, seconds=10.0):
         return time.perf_counter() - t0
 
     dt = run(16, 8)
-    n = max(16, int(16 * seconds / max(dt, 1e-6) / 64))
     T = 64
+    n = max(16, int(16 * 8 * seconds / max(dt, 1e-6) / T))
     dt = run(n, T)
     return {"value": n * T / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": f"oracle/rlp_oracle.c rollout (actor+critic 256x256 fp32 MLP, Philox sample, "

@@ -236,8 +236,8 @@ typedef struct rlp_rollout_bufs {
     float *logp;       /* [T][n][A]                                         (RolloutBuffer.a_lp)*/
     float *reward;     /* [T][n]   raw env.reward (normalised later)        (RolloutBuffer.r)   */
     float *value;      /* [T][n]   V(s_t)                                                        */
-    float *value_next; /* [T][n]   V(s'_t) where !done (== V(s_{t+1})); done rows left for
-                                   rlp_mlp_forward(mask=done) (critic on s'_t)                  */
+    float *value_next; /* [T][n]   V(s'_t) where !done (== V(s_{t+1})); done rows are left to
+                                   rlp_value_fixup (critic on s'_t where the GAE needs it)       */
     uint8_t *done;     /* [T][n]                                            (RolloutBuffer.done)*/
     uint8_t *success;  /* [T][n]                                            (RolloutBuffer.success)*/
     int8_t *flag;      /* [T][n]   terminal_flag                                                 */
@@ -265,6 +265,18 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
                 const rlp_mlp_desc *actor_desc, const float *actor_packed,
                 const rlp_mlp_desc *critic_desc, const float *critic_packed,
                 const rlp_rollout_cfg *cfg, const rlp_rollout_bufs *bufs, rlp_stream_t stream);
+
+/* Batched forward of an MFMA-packed [S->H->H->A] net (H = 256): y[rows][A] (last-layer act
+ * applied). Proximal_Policy_Optimization2.evaluate (:63-67) / critic(s) in learn() (:91-92). */
+int rlp_mfma_forward(const rlp_mlp_desc *desc, const float *packed, const float *x, float *y,
+                     int64_t rows, rlp_stream_t stream);
+
+/* Bootstrap values the rollout kernel cannot provide: value_next[i] = critic(obs_next[i]) for
+ * rows with done[i] && !success[i] (e.g. CartPole time-outs); every other row is either written by
+ * rlp_rollout (V(s'_t) == V(s_{t+1})) or multiplied by (1 - success) = 0 in the GAE (:93). */
+int rlp_value_fixup(const rlp_mlp_desc *critic_desc, const float *critic_packed,
+                    const float *obs_next, const uint8_t *done, const uint8_t *success,
+                    float *value_next, int64_t rows, rlp_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Learn-side scans (Proximal_Policy_Optimization2.learn, :84-100; utils/classes.py:626-656)   */
@@ -295,6 +307,11 @@ int rlp_adv_normalize(float *adv, int64_t count, const double *adv_stats, rlp_st
 /* ------------------------------------------------------------------------------------------ */
 const char *rlp_last_error_string(void);
 int rlp_abi_version(void);
+/* sizeof of the ABI structs as compiled into the library (0 cartpole, 1 angleonly, 2 soi, 3 ugv,
+ * 4 uav, 5 mlp_desc, 6 rollout_cfg, 7 rollout_bufs): FFI bindings verify their mirrors with it. */
+int64_t rlp_struct_size(int which);
+/* Tuning knob of rlp_rollout: 16-env sub-blocks per wave (2 or 4; default 2). */
+int rlp_set_rollout_sub(int sub);
 
 #ifdef __cplusplus
 }

@@ -39,6 +39,8 @@ def _declare(lib):
         "rlp_mfma_pack": (i32, [vp, vp, vp, vp]),
         "rlp_policy_sample": (i32, [vp, i32, i32, vp, vp, vp, vp, u64, u64, u64, vp, vp, vp]),
         "rlp_rollout": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "rlp_mfma_forward": (i32, [vp, vp, vp, vp, i64, vp]),
+        "rlp_value_fixup": (i32, [vp, vp, vp, vp, vp, vp, i64, vp]),
         "rlp_set_rollout_sub": (i32, [i32]),
         "rlp_reward_norm": (i32, [vp, i32, i32, vp, vp, vp, vp]),
         "rlp_gae": (i32, [vp, vp, vp, vp, vp, dbl, dbl, i32, i32, vp, vp, vp, vp]),

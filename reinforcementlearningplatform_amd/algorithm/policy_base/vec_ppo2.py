@@ -1,0 +1,215 @@
+"""VecPPO2 — PPO2 over a batch of n envs on one GPU: the DPPO2 worker loop
+(demonstration/DPPO2/DPPO2-4-CartPole/Distributed_PPO2.py:115-172) with the per-env Python loop
+replaced by one fused HIP rollout launch per segment.
+
+One iteration:
+  rollout     rlp_rollout: T steps x n envs (reset, actor + sample, critic, env step, append)
+  advantages  rlp_value_fixup (V(s') of time-outs), rlp_reward_norm (Normalization, per rank as
+              each DPPO2 worker keeps its own), rlp_gae + rlp_adv_normalize
+  update      K epochs of the PPO2 clipped objective (Proximal_Policy_Optimization2.py:102-160)
+              in torch autograd on the GPU; under torch.distributed the actor+critic gradients are
+              averaged in ONE flat all-reduce per step (RCCL over xGMI) — synchronous data
+              parallelism instead of the reference's Hogwild shared-memory updates.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ... import _abi
+from ... import kernels as K
+from ...utils.classes import GPUNet
+
+DEFAULT_PPO_MSG = {
+    # demonstration/PPO2/PPO2-4-CartPole/train.py:145-161
+    'gamma': 0.999, 'K_epochs': 30, 'eps_clip': 0.2, 'a_lr': 3e-4, 'c_lr': 1e-3,
+    'set_adam_eps': True, 'lmd': 0.95, 'use_adv_norm': True, 'mini_batch_size': 64,
+    'entropy_coef': 0.01, 'use_grad_clip': False, 'use_lr_decay': False,
+    'max_train_steps': int(5e6), 'using_mini_batch': False,
+}
+
+
+class PPO2Learner:
+    """The K-epoch PPO2 update (Proximal_Policy_Optimization2.py:102-174) on any torch device, with
+    synchronous data-parallel gradient averaging under torch.distributed (one flat all-reduce of the
+    actor+critic gradients per optimiser step: ~539 KB for the CartPole nets, latency-bound on
+    xGMI, so one bucket)."""
+
+    def __init__(self, actor, critic, msg, process_group=None, device=None):
+        self.msg = msg
+        self.device = torch.device(device) if device is not None else next(actor.parameters()).device
+        self.actor, self.critic = actor.to(self.device), critic.to(self.device)
+        for name in ("a_min", "a_max", "off", "gain", "std"):
+            v = getattr(self.actor, name, None)
+            if torch.is_tensor(v):
+                setattr(self.actor, name, v.to(self.device))
+        self.pg = process_group
+        self.distributed = process_group is not None or (
+            torch.distributed.is_available() and torch.distributed.is_initialized()
+            and torch.distributed.get_world_size() > 1)
+        self.world = torch.distributed.get_world_size(process_group) if self.distributed else 1
+        if self.distributed:
+            self.broadcast_params()
+        eps = dict(eps=1e-5) if msg['set_adam_eps'] else {}
+        self.opt_a = torch.optim.Adam(self.actor.parameters(), lr=msg['a_lr'], **eps)
+        self.opt_c = torch.optim.Adam(self.critic.parameters(), lr=msg['c_lr'], **eps)
+        self.total_steps = 0
+
+    def params(self):
+        return list(self.actor.parameters()) + list(self.critic.parameters())
+
+    def broadcast_params(self):
+        """Every rank starts from rank 0's replica (the reference's global nets)."""
+        src = 0 if self.pg is None else torch.distributed.get_global_rank(self.pg, 0)
+        with torch.no_grad():
+            flat = torch.cat([p.data.reshape(-1) for p in self.params()])
+            torch.distributed.broadcast(flat, src=src, group=self.pg)
+            off = 0
+            for p in self.params():
+                p.data.copy_(flat[off:off + p.numel()].view_as(p))
+                off += p.numel()
+
+    def _allreduce_grads(self):
+        params = [p for p in self.params() if p.grad is not None]
+        flat = torch.cat([p.grad.reshape(-1) for p in params])
+        torch.distributed.all_reduce(flat, group=self.pg)
+        flat /= self.world
+        off = 0
+        for p in params:
+            p.grad.copy_(flat[off:off + p.numel()].view_as(p.grad))
+            off += p.numel()
+
+    def step(self, s, a, a_lp, adv, vt):
+        m = self.msg
+        dist = self.actor.get_dist(s)
+        ent = dist.entropy().sum(1, keepdim=True)
+        ratios = torch.exp(dist.log_prob(a).sum(1, keepdim=True) - a_lp.sum(1, keepdim=True))
+        surr1 = ratios * adv
+        surr2 = torch.clamp(ratios, 1 - m['eps_clip'], 1 + m['eps_clip']) * adv
+        actor_loss = (-torch.min(surr1, surr2) - m['entropy_coef'] * ent).mean()
+        critic_loss = F.mse_loss(vt, self.critic(s))
+        self.opt_a.zero_grad()
+        self.opt_c.zero_grad()
+        actor_loss.backward()
+        critic_loss.backward()   # the critic loss does not depend on the actor: order is free
+        if self.distributed:
+            self._allreduce_grads()
+        if m['use_grad_clip']:
+            torch.nn.utils.clip_grad_norm_(self.actor.parameters(), 0.5)
+            torch.nn.utils.clip_grad_norm_(self.critic.parameters(), 0.5)
+        self.opt_a.step()
+        self.opt_c.step()
+        return actor_loss.detach(), critic_loss.detach()
+
+    def update(self, s, a, a_lp, adv, vt, generator=None):
+        m = self.msg
+        N = s.shape[0]
+        losses = None
+        for _ in range(m['K_epochs']):
+            if m['using_mini_batch']:
+                perm = torch.randperm(N, device=s.device, generator=generator)
+                mb = m['mini_batch_size']
+                for i in range(0, max(N - mb + 1, 1), mb):
+                    idx = perm[i:i + mb]
+                    losses = self.step(s[idx], a[idx], a_lp[idx], adv[idx], vt[idx])
+            else:
+                losses = self.step(s, a, a_lp, adv, vt)
+        return losses
+
+    def lr_decay(self, total_steps):
+        if not self.msg['use_lr_decay']:
+            return
+        frac = max(1 - total_steps / self.msg['max_train_steps'], 0)
+        for g, lr in ((self.opt_a, self.msg['a_lr']), (self.opt_c, self.msg['c_lr'])):
+            for p in g.param_groups:
+                p['lr'] = max(lr * frac, 1e-6)
+
+
+class VecPPO2:
+    def __init__(self, env, actor, critic, ppo_msg=None, T=128, success_rule=None, seed=None,
+                 process_group=None, device=None):
+        self.env = env
+        self.kind, self.params = env.KIND, env.params
+        self.n, self.T = env.n_envs, int(T)
+        self.device = torch.device(device) if device is not None else env.device
+        self.msg = dict(DEFAULT_PPO_MSG, **(ppo_msg or {}))
+        if 'k_epo' in self.msg:                       # DPPO2 drivers name it k_epo
+            self.msg['K_epochs'] = self.msg['k_epo']
+        self.learner = PPO2Learner(actor, critic, self.msg, process_group, self.device)
+        self.actor, self.critic = self.learner.actor, self.learner.critic
+        self.world = self.learner.world
+        self.gpu_actor = GPUNet(self.actor, True, self.device)
+        self.gpu_critic = GPUNet(self.critic, False, self.device)
+        if not (self.gpu_actor.mfma_ok and self.gpu_critic.mfma_ok):
+            raise ValueError("VecPPO2 needs [S->256->256->A] actor / [S->256->256->1] critic nets "
+                             "for the fused rollout kernel")
+        rule, flag = success_rule or (_abi.RLP_SUCCESS_DONE_AND_FLAG_NE, _abi.timeout_flag(self.kind))
+        self.rule, self.flag = rule, flag
+        lo, hi = _abi.action_bounds(self.kind, self.params)
+        self.lo, self.hi = lo, hi
+        self.seed = int(seed) if seed is not None else env.seed
+        self.env_id0 = env.env_id0
+        self.step0 = 0
+        self.need = torch.ones(self.n, dtype=torch.uint8, device=self.device)
+        self.bufs = K.rollout_buffers(self.kind, self.T, self.n, self.device)
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.rnorm = torch.empty((self.T, self.n), **f32)
+        self.adv = torch.empty((self.T, self.n), **f32)
+        self.v_target = torch.empty((self.T, self.n), **f32)
+        self.rms = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self.work = torch.empty(3 * self.T, dtype=torch.float64, device=self.device)
+        self.stats = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(self.seed + 7919 * (self.env_id0 + 1))
+        self.total_steps = 0
+
+    # ------------------------------------------------------------------------------------------
+    def std_list(self):
+        std = torch.as_tensor(self.actor.std, dtype=torch.float32).reshape(-1).cpu().numpy()
+        return list(np.broadcast_to(std, (len(self.lo),)))
+
+    def rollout(self):
+        cfg = K.make_rollout_cfg(self.T, self.n, self.seed, self.step0, self.env_id0,
+                                 self.std_list(), self.lo, self.hi, self.rule, self.flag)
+        K.rollout(self.kind, self.params, self.env.state, self.need, self.gpu_actor.desc,
+                  self.gpu_actor.packed, self.gpu_critic.desc, self.gpu_critic.packed, cfg, self.bufs)
+        self.step0 += self.T
+        self.total_steps += self.T * self.n * self.world
+
+    def advantages(self):
+        b = self.bufs
+        K.value_fixup(self.gpu_critic.desc, self.gpu_critic.packed, b["obs_next"], b["done"],
+                      b["success"], b["value_next"])
+        K.reward_norm(b["reward"], self.rms, self.work, out=self.rnorm)
+        self.stats.zero_()
+        K.gae(self.rnorm, b["value"], b["value_next"], b["done"], b["success"], self.msg['gamma'],
+              self.msg['lmd'], adv=self.adv, v_target=self.v_target, stats=self.stats)
+        if self.msg['use_adv_norm']:
+            K.adv_normalize(self.adv, self.stats)
+
+    def update(self):
+        b = self.bufs
+        S, Ad = self.env.state_dim, self.env.action_dim
+        losses = self.learner.update(b["obs"].view(-1, S), b["action"].view(-1, Ad),
+                                     b["logp"].view(-1, Ad), self.adv.view(-1, 1),
+                                     self.v_target.view(-1, 1), self.gen)
+        self.gpu_actor.refresh()
+        self.gpu_critic.refresh()
+        self.learner.lr_decay(self.total_steps)
+        return losses
+
+    def iteration(self, learn=True):
+        self.rollout()
+        self.advantages()
+        out = {}
+        if learn:
+            al, cl = self.update()
+            out = {"actor_loss": al, "critic_loss": cl}
+        return out
+
+    def episode_stats(self):
+        """(finished episodes, sum of their raw rewards is not tracked per-episode on device) —
+        mean raw reward per env-step and terminal-flag histogram of the last segment."""
+        b = self.bufs
+        flags = torch.bincount(b["flag"].view(-1).to(torch.int64) + 0, minlength=5)
+        return {"mean_reward": float(b["reward"].mean()), "episodes": int(b["done"].sum()),
+                "flags": flags.cpu().tolist()}

@@ -152,6 +152,79 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Packed-net forward over rows (evaluate(), learn()'s V(s) / V(s'), the value fix-up).
+// Each wave walks 16*SUB-row groups (grid-stride); with a row predicate, groups without an
+// active row are skipped wave-uniformly.
+// ------------------------------------------------------------------------------------------
+template <int H, int SUB, int KS1, int NOUT, int MODE>  // MODE 0: all rows; 1: done && !success
+__global__ void __launch_bounds__(256, (SUB == 4 ? 1 : 2))
+packed_forward_kernel(const float *__restrict__ P, MfmaNet net, const float *__restrict__ x,
+                      float *__restrict__ y, int64_t rows, const uint8_t *__restrict__ done,
+                      const uint8_t *__restrict__ success, int apply_out_act) {
+    constexpr int WROWS = 16 * SUB;
+    const int lane = threadIdx.x & 63, g = lane >> 4, e = lane & 15;
+    const int S = net.S;
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    for (int64_t grp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); grp * WROWS < rows;
+         grp += nwaves) {
+        const int64_t r0 = grp * WROWS;
+        bool act_row = false;
+        if (lane < WROWS && r0 + lane < rows)
+            act_row = MODE == 0 ? true : (done[r0 + lane] && !success[r0 + lane]);
+        if (!__any(act_row)) continue;  // wave-uniform
+        float bobs[SUB][KS1];
+#pragma unroll
+        for (int sb = 0; sb < SUB; ++sb)
+#pragma unroll
+            for (int kk = 0; kk < KS1; ++kk) {
+                const int64_t row = r0 + 16 * sb + e;
+                const int k = 4 * kk + g;
+                bobs[sb][kk] = (row < rows && k < S) ? x[row * S + k] : 0.f;
+            }
+        float out[SUB][NOUT];
+        mlp_fused_forward<H, SUB, KS1, NOUT>(P, net, net.A, bobs, out);
+        // lane (sub-block g, row e) owns out[g]; lanes 0..WROWS-1 store their row
+        float sel[NOUT];
+#pragma unroll
+        for (int a = 0; a < NOUT; ++a) sel[a] = out[0][a];
+#pragma unroll
+        for (int sb = 1; sb < SUB; ++sb)
+            if (g == sb) {
+#pragma unroll
+                for (int a = 0; a < NOUT; ++a) sel[a] = out[sb][a];
+            }
+        if (act_row) {
+            const int64_t row = r0 + lane;
+            for (int a = 0; a < net.A; ++a)
+                y[row * net.A + a] = (apply_out_act && net.out_tanh) ? tanhf(sel[a]) : sel[a];
+        }
+    }
+}
+
+template <int MODE>
+static int launch_packed_forward(const MfmaNet &net, const float *P, const float *x, float *y,
+                                 int64_t rows, const uint8_t *done, const uint8_t *success,
+                                 int apply_out_act, hipStream_t s) {
+    if (net.H != 256) return fail(RLP_EUNSUPPORTED, "packed forward: hidden width %d", net.H);
+    constexpr int SUB = MODE == 0 ? 4 : 1;
+    const int64_t groups = (rows + 16 * SUB - 1) / (16 * SUB);
+    int64_t blocks = (groups + 3) / 4;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) return RLP_OK;
+#define RLP_PF(KS1, NOUT)                                                                       \
+    packed_forward_kernel<256, SUB, KS1, NOUT, MODE><<<(int)blocks, 256, 0, s>>>(             \
+        P, net, x, y, rows, done, success, apply_out_act)
+    if (net.ks1 == 1) {
+        if (net.A == 1) RLP_PF(1, 1); else if (net.A == 2) RLP_PF(1, 2); else if (net.A == 3) RLP_PF(1, 3); else RLP_PF(1, 4);
+    } else {
+        if (net.A == 1) RLP_PF(2, 1); else if (net.A == 2) RLP_PF(2, 2); else if (net.A == 3) RLP_PF(2, 3); else RLP_PF(2, 4);
+    }
+#undef RLP_PF
+    RLP_CHECK_LAUNCH("packed forward");
+    return RLP_OK;
+}
+
 template <int KIND, int H, int SUB>
 static int launch_rollout(const void *params, double *state, uint8_t *need_reset,
                           const float *actor, const MfmaNet &an, const float *critic,
@@ -184,7 +257,7 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
                                         stream);
 }
 
-static int g_rollout_sub = 4;
+static int g_rollout_sub = 2;
 
 }  // namespace rlp
 
@@ -197,6 +270,29 @@ int rlp_set_rollout_sub(int sub) {
     if (sub != 2 && sub != 4) return fail(RLP_EINVAL, "rlp_set_rollout_sub: %d", sub);
     g_rollout_sub = sub;
     return RLP_OK;
+}
+
+int rlp_mfma_forward(const rlp_mlp_desc *desc, const float *packed, const float *x, float *y,
+                     int64_t rows, rlp_stream_t stream) {
+    RLP_REQUIRE(desc && packed && x && y, "rlp_mfma_forward: null argument");
+    MfmaNet net;
+    if (!mfma_net_from_desc(*desc, &net))
+        return fail(RLP_EUNSUPPORTED, "rlp_mfma_forward: need a [S->H->H->A] tanh MLP");
+    if (rows <= 0) return rows == 0 ? RLP_OK : RLP_EINVAL;
+    return launch_packed_forward<0>(net, packed, x, y, rows, nullptr, nullptr, 1, as_stream(stream));
+}
+
+int rlp_value_fixup(const rlp_mlp_desc *critic_desc, const float *critic_packed,
+                    const float *obs_next, const uint8_t *done, const uint8_t *success,
+                    float *value_next, int64_t rows, rlp_stream_t stream) {
+    RLP_REQUIRE(critic_desc && critic_packed && obs_next && done && success && value_next,
+                "rlp_value_fixup: null argument");
+    MfmaNet net;
+    if (!mfma_net_from_desc(*critic_desc, &net) || net.A != 1)
+        return fail(RLP_EUNSUPPORTED, "rlp_value_fixup: need a [S->H->H->1] critic");
+    if (rows <= 0) return rows == 0 ? RLP_OK : RLP_EINVAL;
+    return launch_packed_forward<1>(net, critic_packed, obs_next, value_next, rows, done, success,
+                                    1, as_stream(stream));
 }
 
 int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_reset,

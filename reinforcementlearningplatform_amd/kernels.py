@@ -71,6 +71,25 @@ def mfma_pack(desc, params, out=None):
     return out
 
 
+def mfma_forward(desc, packed, x, out=None):
+    """Forward of an MFMA-packed [S->H->H->A] net (last-layer activation applied)."""
+    rows = x.shape[0]
+    outn = desc.dims[desc.n_layers]
+    out = out if out is not None else torch.empty((rows, outn), dtype=torch.float32, device=x.device)
+    check(lib().rlp_mfma_forward(C.byref(desc), ptr(packed), ptr(x.contiguous()), ptr(out), rows,
+                                 stream_ptr()), "rlp_mfma_forward")
+    return out
+
+
+def value_fixup(critic_desc, critic_packed, obs_next, done, success, value_next):
+    """value_next[i] = critic(obs_next[i]) where done & !success (flattened [T*n] rows)."""
+    rows = done.numel()
+    check(lib().rlp_value_fixup(C.byref(critic_desc), ptr(critic_packed), ptr(obs_next),
+                                ptr(done), ptr(success), ptr(value_next), rows, stream_ptr()),
+          "rlp_value_fixup")
+    return value_next
+
+
 def _host_f32(v, A):
     arr = (C.c_float * A)()
     vals = list(v) if hasattr(v, "__len__") else [v] * A

@@ -1,0 +1,277 @@
+"""Buffers, normalisers and the PPO2 driver networks (utils/classes.py of the reference, the parts on
+the PPO2 hot path), plus GPUNet: the adapter that runs a driver-defined Linear/Tanh network through
+librlp's MFMA kernels.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import _abi
+from .. import kernels as K
+
+
+# ---------------------------------------------------------------------------------------------
+# Running statistics (utils/classes.py:626-673)
+# ---------------------------------------------------------------------------------------------
+class RunningMeanStd:
+    """Welford running mean/std; the first sample sets std = x (reference behaviour, :634-637)."""
+
+    def __init__(self, shape):
+        self.n = 0
+        self.mean = np.zeros(shape)
+        self.S = np.zeros(shape)
+        self.std = np.sqrt(self.S)
+
+    def update(self, x):
+        x = np.array(x)
+        self.n += 1
+        if self.n == 1:
+            self.mean, self.std = x, x
+            return
+        prev = self.mean.copy()
+        self.mean = prev + (x - prev) / self.n
+        self.S = self.S + (x - prev) * (x - self.mean)
+        self.std = np.sqrt(self.S / self.n)
+
+
+class Normalization:
+    def __init__(self, shape):
+        self.running_ms = RunningMeanStd(shape=shape)
+
+    def __call__(self, x, update=True):
+        if update:
+            self.running_ms.update(x)
+        return (x - self.running_ms.mean) / (self.running_ms.std + 1e-8)
+
+
+class RewardScaling:
+    def __init__(self, shape, gamma):
+        self.shape, self.gamma = shape, gamma
+        self.running_ms = RunningMeanStd(shape=shape)
+        self.R = np.zeros(shape)
+
+    def __call__(self, x):
+        self.R = self.gamma * self.R + x
+        self.running_ms.update(self.R)
+        return x / (self.running_ms.std + 1e-8)
+
+    def reset(self):
+        self.R = np.zeros(self.shape)
+
+
+# ---------------------------------------------------------------------------------------------
+# Rollout buffer (utils/classes.py:250-310): same API; the storage is a float64 host array as in
+# the reference (a single env appends one row per step), to_tensor() hands fp32 tensors to the
+# learner's device.
+# ---------------------------------------------------------------------------------------------
+class RolloutBuffer:
+    FIELDS = ("s", "a", "a_lp", "r", "s_", "done", "success")
+
+    def __init__(self, batch_size: int, state_dim: int, action_dim: int, device=None):
+        self.batch_size, self.state_dim, self.action_dim = batch_size, state_dim, action_dim
+        self.device = device
+        self.s = np.zeros((batch_size, state_dim))
+        self.a = np.zeros((batch_size, action_dim))
+        self.a_lp = np.zeros((batch_size, action_dim))
+        self.r = np.zeros((batch_size, 1))
+        self.s_ = np.zeros((batch_size, state_dim))
+        self.done = np.zeros((batch_size, 1))
+        self.success = np.zeros((batch_size, 1))
+        self.index = 0
+
+    def append(self, s, a, log_prob, r, s_, done, success, index):
+        self.s[index], self.a[index], self.a_lp[index] = s, a, log_prob
+        self.r[index], self.s_[index] = r, s_
+        self.done[index], self.success[index] = done, success
+
+    def append_traj(self, s, a, log_prob, r, s_, done, success):
+        for i in range(len(done)):
+            if self.index == self.batch_size:
+                self.index = 0
+                return True
+            self.append(s[i], a[i], log_prob[i], r[i], s_[i], done[i], success[i], self.index)
+            self.index += 1
+        return False
+
+    def to_tensor(self, device=None):
+        dev = device or self.device or "cpu"
+        return tuple(torch.tensor(getattr(self, f), dtype=torch.float, device=dev) for f in self.FIELDS)
+
+    def print_size(self):
+        print('==== RolloutBuffer ====')
+        for f in self.FIELDS:
+            print(f'{f}: {getattr(self, f).size}')
+
+
+class RolloutBuffer2:
+    """Growing trajectory buffer (utils/classes.py:313-376)."""
+
+    def __init__(self, state_dim: int, action_dim: int):
+        self.state_dim, self.action_dim = state_dim, action_dim
+        self.clean()
+
+    def clean(self):
+        self.index = 0
+        for f in RolloutBuffer.FIELDS:
+            setattr(self, f, np.atleast_2d([]).astype(np.float32))
+
+    def append_traj(self, s, a, log_prob, r, s_, done, success):
+        vals = dict(s=s, a=a, a_lp=log_prob, r=r, s_=s_, done=done, success=success)
+        for f, v in vals.items():
+            v = np.atleast_2d(v).astype(np.float32)
+            setattr(self, f, v if self.index == 0 else np.vstack((getattr(self, f), v)))
+        self.index += len(done)
+
+    def to_tensor(self, device=None):
+        return tuple(torch.tensor(getattr(self, f), dtype=torch.float, device=device or "cpu")
+                     for f in RolloutBuffer.FIELDS)
+
+
+# ---------------------------------------------------------------------------------------------
+# PPO2 driver networks (demonstration/PPO2/PPO2-4-CartPole/train.py:39-125): same constructor
+# arguments and parameter names (fc1 / fc2 / mean_layer, fc1 / fc2 / fc3) so the shipped
+# datasave/net checkpoints load unchanged.
+# ---------------------------------------------------------------------------------------------
+def _orthogonal(layer, gain=1.0):
+    nn.init.orthogonal_(layer.weight, gain=gain)
+    nn.init.constant_(layer.bias, 0)
+
+
+class PPOActor_Gaussian(nn.Module):
+    def __init__(self, state_dim: int = 3, action_dim: int = 3, a_min=np.zeros(3), a_max=np.ones(3),
+                 init_std: float = 0.5, use_orthogonal_init: bool = True, hidden: int = 256):
+        super().__init__()
+        self.fc1 = nn.Linear(state_dim, hidden)
+        self.fc2 = nn.Linear(hidden, hidden)
+        self.mean_layer = nn.Linear(hidden, action_dim)
+        self.activate_func = nn.Tanh()
+        self.a_min = torch.tensor(a_min, dtype=torch.float)
+        self.a_max = torch.tensor(a_max, dtype=torch.float)
+        self.off = (self.a_min + self.a_max) / 2.0
+        self.gain = self.a_max - self.off
+        self.action_dim = action_dim
+        self.std = torch.tensor(init_std, dtype=torch.float)
+        if use_orthogonal_init:
+            self.orthogonal_init_all()
+
+    def orthogonal_init_all(self):
+        _orthogonal(self.fc1)
+        _orthogonal(self.fc2)
+        _orthogonal(self.mean_layer, gain=0.01)
+
+    def _apply(self, fn, *args, **kwargs):  # keep the non-parameter tensors on the module's device
+        super()._apply(fn, *args, **kwargs)
+        self.a_min, self.a_max = fn(self.a_min), fn(self.a_max)
+        self.off, self.gain = fn(self.off), fn(self.gain)
+        self.std = fn(self.std) if torch.is_tensor(self.std) else self.std
+        return self
+
+    def forward(self, s):
+        s = self.activate_func(self.fc1(s))
+        s = self.activate_func(self.fc2(s))
+        return torch.tanh(self.mean_layer(s)) * self.gain + self.off
+
+    def get_dist(self, s):
+        mean = self.forward(s)
+        std = torch.as_tensor(self.std, dtype=mean.dtype, device=mean.device).expand_as(mean)
+        return torch.distributions.Normal(mean, std)
+
+    def evaluate(self, state):
+        with torch.no_grad():
+            t = torch.tensor(state, dtype=torch.float, device=self.fc1.weight.device).unsqueeze(0)
+            return self.forward(t).cpu().numpy().flatten()
+
+
+class PPOCritic(nn.Module):
+    def __init__(self, state_dim=3, use_orthogonal_init: bool = True, hidden: int = 256):
+        super().__init__()
+        self.fc1 = nn.Linear(state_dim, hidden)
+        self.fc2 = nn.Linear(hidden, hidden)
+        self.fc3 = nn.Linear(hidden, 1)
+        self.activate_func = nn.Tanh()
+        if use_orthogonal_init:
+            self.orthogonal_init_all()
+
+    def orthogonal_init_all(self):
+        _orthogonal(self.fc1)
+        _orthogonal(self.fc2)
+        _orthogonal(self.fc3)
+
+    def forward(self, s):
+        s = self.activate_func(self.fc1(s))
+        s = self.activate_func(self.fc2(s))
+        return self.fc3(s)
+
+    def init(self, use_orthogonal_init):
+        if use_orthogonal_init:
+            self.orthogonal_init_all()
+        else:
+            for m in (self.fc1, self.fc2, self.fc3):
+                m.reset_parameters()
+
+
+# ---------------------------------------------------------------------------------------------
+# GPUNet: a driver-defined Linear/Tanh stack on librlp's MFMA kernels
+# ---------------------------------------------------------------------------------------------
+class GPUNet:
+    """Runs `module`'s forward through librlp: the Linear layers (registration order) become an
+    rlp_mlp_desc with tanh hidden activations; an actor with `gain`/`off` gets tanh * gain + off on
+    the last layer, a critic the identity. The mapping is verified against module(x) on a probe
+    batch when built; an architecture that does not match raises instead of silently diverging."""
+
+    def __init__(self, module: nn.Module, is_actor: bool, device="cuda"):
+        self.module = module
+        self.is_actor = is_actor
+        self.device = torch.device(device)
+        self.linears = [m for m in module.modules() if isinstance(m, nn.Linear)]
+        if not self.linears:
+            raise ValueError("GPUNet: module has no nn.Linear layers")
+        dims = [self.linears[0].in_features] + [l.out_features for l in self.linears]
+        for a, b in zip(self.linears[:-1], self.linears[1:]):
+            if a.out_features != b.in_features:
+                raise ValueError("GPUNet: Linear layers do not chain")
+        acts = [_abi.RLP_ACT_TANH] * (len(self.linears) - 1)
+        acts.append(_abi.RLP_ACT_TANH if is_actor else _abi.RLP_ACT_NONE)
+        self.desc = _abi.MLPDesc.make(dims, acts)
+        self.packed = None
+        self.flat = None
+        self.refresh()
+        self._verify()
+
+    @property
+    def mfma_ok(self):
+        return self.packed is not None
+
+    def refresh(self):
+        """Re-read the module's parameters (call after every optimiser step)."""
+        with torch.no_grad():
+            self.flat = torch.cat([t.detach().reshape(-1).to(self.device, torch.float32)
+                                   for l in self.linears for t in (l.weight, l.bias)]).contiguous()
+            cnt = K.lib().rlp_mfma_packed_count(__import__("ctypes").byref(self.desc))
+            self.packed = K.mfma_pack(self.desc, self.flat, out=self.packed) if cnt > 0 else None
+
+    def raw(self, x):
+        """Last-layer output (tanh already applied for an actor, before gain/off)."""
+        x = x.to(self.device, torch.float32).contiguous()
+        if self.packed is not None and self.desc.dims[1] == 256:
+            return K.mfma_forward(self.desc, self.packed, x)
+        return K.mlp_forward(self.desc, self.flat, x)
+
+    def __call__(self, x):
+        y = self.raw(x)
+        if self.is_actor:
+            gain = torch.as_tensor(self.module.gain, device=self.device)
+            off = torch.as_tensor(self.module.off, device=self.device)
+            y = y * gain + off
+        return y
+
+    def _verify(self):
+        g = torch.Generator().manual_seed(0)
+        x = torch.rand(64, self.desc.dims[0], generator=g) * 4 - 2
+        with torch.no_grad():
+            p = next(self.module.parameters())
+            ref = self.module(x.to(p.device, p.dtype)).float().to(self.device)
+        got = self(x.to(self.device))
+        if not torch.allclose(got, ref, rtol=1e-4, atol=1e-4):
+            raise ValueError("GPUNet: module forward is not a Linear/Tanh stack this adapter maps "
+                             f"(max diff {float((got - ref).abs().max()):.3g})")

@@ -147,3 +147,26 @@ def test_rollout_segments_chain():
         outs.append((torch.cat(acts), st.clone()))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("kind", [A.RLP_ENV_CARTPOLE, A.RLP_ENV_UAV_HOVER_OUTER_LOOP,
+                                  A.RLP_ENV_CARTPOLE_ANGLEONLY])
+def test_mfma_forward_and_value_fixup(kind):
+    D, S, Ad = A.ENV_DIMS[kind]
+    ad, ap, cd, cp = nets(S, Ad, seed=11)
+    rng = np.random.default_rng(kind)
+    rows = 50_000 + 7
+    x = rng.uniform(-2, 2, (rows, S)).astype(np.float32)
+    apk, cpk = K.mfma_pack(ad, dev(ap)), K.mfma_pack(cd, dev(cp))
+    m = host(K.mfma_forward(ad, apk, dev(x)))
+    v = host(K.mfma_forward(cd, cpk, dev(x)))
+    np.testing.assert_allclose(m, oracle.mlp_forward(ad, ap, x), rtol=1e-5, atol=2e-6)
+    np.testing.assert_allclose(v, oracle.mlp_forward(cd, cp, x), rtol=1e-5, atol=2e-5)
+    done = (rng.uniform(0, 1, rows) < 0.05).astype(np.uint8)
+    succ = (done * (rng.uniform(0, 1, rows) < 0.5)).astype(np.uint8)
+    vn = torch.full((rows,), -123.0, device="cuda")
+    K.value_fixup(cd, cpk, dev(x), dev(done), dev(succ), vn)
+    vn = host(vn)
+    need = (done == 1) & (succ == 0)
+    np.testing.assert_allclose(vn[need], v[need, 0], rtol=1e-6, atol=1e-6)
+    assert (vn[~need] == -123.0).all()
