@@ -57,6 +57,20 @@ def mlp_flops(desc):
     return sum(2 * ds[i] * ds[i + 1] for i in range(desc.n_layers))
 
 
+def pmc_traffic(workload, n, T):
+    """HBM bytes per rollout launch from the committed rocprofv3 PMC pass of this workload
+    (profiles/pmc_traffic.json: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    e = d.get(workload)
+    if not e or e.get("envs_per_gpu") != n or e.get("T") != T:
+        return None
+    return e["hbm_bytes_per_launch"]
+
+
 class Segment:
     """Device-resident state + buffers of one rank's env batch."""
 
@@ -109,6 +123,43 @@ class Segment:
         self.learn_side()
 
 
+def e2e_iterations(seg, iters, k_epochs=6):
+    """Whole PPO2 iterations: rollout + advantages + K full-batch epochs of the clipped-surrogate /
+    MSE update (torch autograd + Adam on this GPU; the DPPO2 CartPole drivers' k_epo = 6,
+    demonstration/DPPO2/DPPO2-4-CartPole/train.py:161). Returns env-steps/s of this rank."""
+    from reinforcementlearningplatform_amd.algorithm.policy_base.vec_ppo2 import (DEFAULT_PPO_MSG,
+                                                                                   PPO2Learner)
+    from reinforcementlearningplatform_amd.utils.classes import PPOActor_Gaussian, PPOCritic
+    actor = PPOActor_Gaussian(seg.S, seg.Ad, np.array(seg.lo), np.array(seg.hi), init_std=seg.std[0])
+    critic = PPOCritic(seg.S)
+    with torch.no_grad():   # start from the bench nets
+        for m, flat in ((actor, seg.actor), (critic, seg.critic)):
+            off = 0
+            for p in m.parameters():
+                p.copy_(flat[off:off + p.numel()].view_as(p).cpu())
+                off += p.numel()
+    learner = PPO2Learner(actor, critic, dict(DEFAULT_PPO_MSG, K_epochs=k_epochs), device="cuda")
+    b = seg.bufs
+
+    def one():
+        seg.iteration()
+        learner.update(b["obs"].view(-1, seg.S), b["action"].view(-1, seg.Ad),
+                       b["logp"].view(-1, seg.Ad), seg.adv.view(-1, 1), seg.vt.view(-1, 1))
+        with torch.no_grad():   # the rollout's packed nets follow the learner
+            seg.actor.copy_(torch.cat([p.reshape(-1) for p in actor.parameters()]))
+            seg.critic.copy_(torch.cat([p.reshape(-1) for p in critic.parameters()]))
+            K.mfma_pack(seg.ad, seg.actor, out=seg.apk)
+            K.mfma_pack(seg.cd, seg.critic, out=seg.cpk)
+    one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        one()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return seg.n * seg.T * iters / dt, dt / iters
+
+
 def cpu_baseline(env, seconds=10.0):
     """Oracle (plain-C port of the reference loop, 1 thread) on a bounded sample of the same
     workload: actor + critic forward, sampling and env step per env-step."""
@@ -153,16 +204,26 @@ def main():
     ap.add_argument("--seed", type=int, default=3407)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--e2e", type=int, default=2, help="PPO2 iterations incl. the K-epoch update to time (0: skip)")
+    ap.add_argument("--uav", type=int, default=1, help="also time the UavRobust rollout (32768 envs/GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; RLP_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks folded
+    # onto the visible devices) — the driver's runs use RCCL ("nccl") with one GPU per rank
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("RLP_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     if args.sub:
         _native.set_rollout_sub(args.sub)
 
@@ -213,6 +274,33 @@ def main():
                      "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
                      "avg_launch_ms": rollout_ms, "flop_per_launch": flop_launch},
     }
+    traffic = pmc_traffic(out["config"]["workload"], n, T)
+    if traffic is not None:
+        out["roofline"]["traffic"] = traffic
+    if args.uav and args.env == "cartpole":
+        useg = Segment("uav", 32768, 64, args.seed + 1, env_id0=rank * 32768)
+        for _ in range(2):
+            useg.iteration()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(3):
+            useg.iteration()
+        torch.cuda.synchronize()
+        uel = time.perf_counter() - t1
+        if dist is not None:
+            t = torch.tensor([uel], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            uel = float(t.item())
+        out["uav_ppo2_rollout"] = {"value": 32768 * 64 * 3 * world / uel, "unit": "env-steps/s",
+                                   "envs_per_gpu": 32768, "global_envs": 32768 * world, "T": 64,
+                                   "config": "UavRobust hover outer loop (6-DoF + FNTSMC), PPO2 [6,256,256,3]"}
+        del useg
+    if args.e2e:
+        v, it_s = e2e_iterations(seg, args.e2e)
+        v_all = v * world
+        out["e2e"] = {"value": v_all, "unit": "env-steps/s", "s_per_iteration": it_s,
+                      "update": "K=6 full-batch epochs (torch autograd+Adam, fp32) per iteration",
+                      "note": "rollout + GAE + PPO update; `value` above is the rollout hot path"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.env, args.cpu_seconds)
     if rank == 0:

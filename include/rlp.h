@@ -312,6 +312,10 @@ int rlp_abi_version(void);
 int64_t rlp_struct_size(int which);
 /* Tuning knob of rlp_rollout: 16-env sub-blocks per wave (2 or 4; default 2). */
 int rlp_set_rollout_sub(int sub);
+/* Tuning knob of rlp_rollout: one-time start delay (shader cycles) of the second wave of each
+ * SIMD so the two waves' VALU phases interleave with each other's MFMA phases (default 40000,
+ * or the RLP_STAGGER environment variable). */
+int rlp_set_rollout_stagger(int cycles);
 
 #ifdef __cplusplus
 }

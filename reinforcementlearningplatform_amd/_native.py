@@ -42,6 +42,7 @@ def _declare(lib):
         "rlp_mfma_forward": (i32, [vp, vp, vp, vp, i64, vp]),
         "rlp_value_fixup": (i32, [vp, vp, vp, vp, vp, vp, i64, vp]),
         "rlp_set_rollout_sub": (i32, [i32]),
+        "rlp_set_rollout_stagger": (i32, [i32]),
         "rlp_reward_norm": (i32, [vp, i32, i32, vp, vp, vp, vp]),
         "rlp_gae": (i32, [vp, vp, vp, vp, vp, dbl, dbl, i32, i32, vp, vp, vp, vp]),
         "rlp_adv_normalize": (i32, [vp, i64, vp, vp]),
@@ -90,6 +91,10 @@ def ptr(t):
 def stream_ptr(stream=None):
     s = stream if stream is not None else torch.cuda.current_stream()
     return C.c_void_p(s.cuda_stream)
+
+
+def set_rollout_stagger(cycles):
+    check(lib().rlp_set_rollout_stagger(int(cycles)), "rlp_set_rollout_stagger")
 
 
 def set_rollout_sub(sub):

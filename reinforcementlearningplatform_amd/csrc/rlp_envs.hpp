@@ -16,6 +16,37 @@ __device__ __forceinline__ double clipd(double x, double lo, double hi) {
     return x < lo ? lo : (x > hi ? hi : x);
 }
 
+// fp64 sin and cos of one argument: Cody-Waite reduction by pi/2 (three-part constant, FMA) and
+// the classic minimax kernels on [-pi/4, pi/4] (fdlibm __kernel_sin/__kernel_cos coefficients),
+// <= 1 ulp like libm for |x| < 2^20 (accuracy degrades beyond: no live episode gets there, every
+// env terminates at |angle| of a few rad). ~30 VALU ops instead of the general-purpose routine's
+// ~150 plus its call — the physics' sub-step loops call it 4x per sub-step.
+__device__ __forceinline__ void sincos_fast(double x, double *sp, double *cp) {
+    const double kd = rint(x * 0.63661977236758134308);
+    double r = fma(-kd, 1.5707963267948966192, x);
+    r = fma(-kd, 6.123233995736766036e-17, r);
+    r = fma(-kd, -1.4973849048591698e-33, r);
+    const double z = r * r;
+    // sin(r) = r + r^3 (S1 + z (S2 + ... z S6))
+    const double ps = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                        2.75573137070700676789e-06), -1.98412698298579493134e-04),
+                          8.33333333332248946124e-03);
+    const double sr = r + (z * r) * fma(z, ps, -1.66666666666666324348e-01);
+    // cos(r) = w + ((1 - w) - z/2 + z^2 (C1 + z (C2 + ... z C6))), w = 1 - z/2
+    const double pc = z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11,
+                                                           2.08757232129817482790e-09),
+                                                    -2.75573143513906633035e-07),
+                                             2.48015872894767294178e-05),
+                                      -1.38888888888741095749e-03),
+                               4.16666666666666019037e-02);
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    const double cr = w + (((1.0 - w) - hz) + z * pc);
+    const int q = ((int)kd) & 3;
+    const double s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
+    *sp = (q & 2) ? -s0 : s0;
+    *cp = ((q + 1) & 2) ? -c0 : c0;
+}
+
 template <int KIND> struct Env;
 
 // ==========================================================================================
@@ -31,7 +62,7 @@ template <> struct Env<RLP_ENV_CARTPOLE> {
                                                double d[4]) {
         double th = xx[0], dth = xx[1], dx = xx[3];
         double Sv, Cv;
-        sincos(th, &Sv, &Cv);
+        sincos_fast(th, &Sv, &Cv);
         double num = force + p.m * p.ell * (dth * dth) * Sv;
         num = num - p.kf * dx;
         num = num - 3.0 / 4.0 * p.m * p.g * Sv * Cv;
@@ -122,7 +153,7 @@ template <> struct Env<RLP_ENV_CARTPOLE_ANGLEONLY> {
                                                double d[4]) {  // :197-216
         double th = xx[0], dth = xx[1], dx = xx[3];
         double Sv, Cv;
-        sincos(th, &Sv, &Cv);
+        sincos_fast(th, &Sv, &Cv);
         double num = force + p.m * p.ell * (dth * dth) * Sv;
         num = num - p.kf * dx;
         num = num - 3.0 / 4.0 * p.m * p.g * Sv * Cv;
@@ -307,13 +338,13 @@ template <bool BIDIR> struct UGV {
     }
     __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
         double sn, c;
-        sincos(s[3], &sn, &c);
+        sincos_fast(s[3], &sn, &c);
         obs_from(p, s, get_e(s, c, sn), get_e_phi(s, c, sn), o);
     }
     __device__ static __forceinline__ void ode(const P &p, double al, double aa, const double *x,
                                                double *d) {  // ode :281-292
         double sn, c;
-        sincos(x[3], &sn, &c);
+        sincos_fast(x[3], &sn, &c);
         d[0] = x[2] * c;
         d[1] = x[2] * sn;
         d[2] = al - p.kf * x[2];
@@ -346,7 +377,7 @@ template <bool BIDIR> struct UGV {
         if (s[3] > kPi) s[3] -= 2 * kPi;
         if (s[3] < -kPi) s[3] += 2 * kPi;
         double sn, c;
-        sincos(s[3], &sn, &c);
+        sincos_fast(s[3], &sn, &c);
         const double e = get_e(s, c, sn), eph = get_e_phi(s, c, sn);
         int f = 0;  // is_Terminal :247-261
         if (s[0] > p.map_size[0] || s[0] < 0 || s[1] > p.map_size[1] || s[1] < 0) f = 1;
@@ -401,10 +432,10 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
         const double dq = (-p.kr * q - pp * r * (p.J[0] - p.J[2]) + tq[1]) / p.J[1];
         const double dr = (-p.kr * r - pp * q * (p.J[1] - p.J[0]) + tq[2]) / p.J[2];
         double sphi, cphi, sth, cth, spsi, cpsi;
-        sincos(phi, &sphi, &cphi);
-        sincos(th, &sth, &cth);
-        sincos(psi, &spsi, &cpsi);
-        const double tth = tan(th);
+        sincos_fast(phi, &sphi, &cphi);
+        sincos_fast(th, &sth, &cth);
+        sincos_fast(psi, &spsi, &cpsi);
+        const double tth = sth / cth;
         const double R01 = tth * sphi, R02 = tth * cphi, R11 = cphi, R12 = -sphi;
         const double R21 = sphi / cth, R22 = cphi / cth;
         d[6] = 1 * pp + R01 * q + R02 * r;
@@ -429,9 +460,9 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
         const double phi = s[PHI], th = s[THE], psi = s[PSI];
         const double pp = s[PP], q = s[PP + 1], r = s[PP + 2];
         double sphi, cphi, sth, cth, spsi, cpsi;
-        sincos(phi, &sphi, &cphi);
-        sincos(th, &sth, &cth);
-        sincos(psi, &spsi, &cpsi);
+        sincos_fast(phi, &sphi, &cphi);
+        sincos_fast(th, &sth, &cth);
+        sincos_fast(psi, &spsi, &cpsi);
         // uo_2_ref_angle_throttle uav_pos_ctrl.py:67-76; (uz + g) * m in float32 (NEP 50)
         const double ux = (double)a[0], uy = (double)a[1];
         const float uzg = (a[2] + (float)p.g) * (float)p.m;
@@ -449,7 +480,7 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
             aref[i] = daref[i] * p.dt + old;
         }
         // att_control uav_pos_ctrl.py:46-65 -> fntsmc_att.control_update FNTSMC.py:80-106
-        const double tth = tan(th);
+        const double tth = sth / cth;
         const double f1[3][3] = {{1., sphi * tth, cphi * tth}, {0., cphi, -sphi},
                                  {0., sphi / cth, cphi / cth}};
         const double rho2[3] = {pp, q, r};

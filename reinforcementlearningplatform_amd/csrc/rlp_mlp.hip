@@ -89,30 +89,24 @@ __global__ void mfma_pack_kernel(MfmaNet net, const float *__restrict__ P, float
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
          idx += gridDim.x * blockDim.x) {
         float v = 0.f;
-        if (idx < net.off_b1) {  // W1p [t][kk][lane]
-            const int lane = idx & 63, kk = (idx >> 6) % KS1, t = (idx >> 6) / KS1;
-            const int k = 4 * kk + (lane >> 4), j = 16 * t + (lane & 15);
-            v = k < S ? W1[j * S + k] : 0.f;
-        } else if (idx < net.off_w2) {  // B1p [t][lane][4]
-            const int q = idx - net.off_b1;
-            const int r = q & 3, lane = (q >> 2) & 63, t = q >> 8;
-            v = b1[16 * t + 4 * (lane >> 4) + r];
-        } else if (idx < net.off_b2) {  // W2p [t][r][jq][lane][4]
-            const int q = idx - net.off_w2;
+        if (idx < net.off_w1) {  // W2p [t][r][jq][lane][4]
+            const int q = idx;
             const int qq = q & 3, lane = (q >> 2) & 63, jq = (q >> 8) % (NT / 4);
             const int r = ((q >> 8) / (NT / 4)) & 3, t = ((q >> 8) / (NT / 4)) >> 2;
             const int j = 16 * (4 * jq + qq) + (lane & 15);
             const int k = 16 * t + 4 * (lane >> 4) + r;
             v = W2[j * H + k];
-        } else if (idx < net.off_w3) {  // B2p [j][lane][4]
-            const int q = idx - net.off_b2;
-            const int r = q & 3, lane = (q >> 2) & 63, j = q >> 8;
-            v = b2[16 * j + 4 * (lane >> 4) + r];
-        } else if (idx < net.off_b3) {  // W3p [a][j][lane][4]
-            const int q = idx - net.off_w3;
-            const int r = q & 3, lane = (q >> 2) & 63, j = (q >> 8) % NT, a = (q >> 8) / NT;
-            v = W3[a * H + 16 * j + 4 * (lane >> 4) + r];
-        } else {  // b3 [a] (padded to 4)
+        } else if (idx < net.off_b1) {  // W1c [H][4*KS1]
+            const int q = idx - net.off_w1;
+            const int j = q / (4 * KS1), k = q % (4 * KS1);
+            v = k < S ? W1[j * S + k] : 0.f;
+        } else if (idx < net.off_b2) {  // B1c [H]
+            v = b1[idx - net.off_b1];
+        } else if (idx < net.off_w3) {  // B2c [H]
+            v = b2[idx - net.off_b2];
+        } else if (idx < net.off_b3) {  // W3c [A][H]
+            v = W3[idx - net.off_w3];
+        } else {  // b3 [4]
             const int a = idx - net.off_b3;
             v = a < A ? b3[a] : 0.f;
         }

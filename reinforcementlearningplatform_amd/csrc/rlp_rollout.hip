@@ -9,31 +9,68 @@
 //   env.step_update(a)                 CartPole.py:257-264 (etc.)
 //   buffer.append(...)                 utils/classes.py:264-272, time-major [T][n][...]
 // The two MLPs are fp32 MFMA (v_mfma_f32_16x16x4_f32): this kernel is MFMA-bound.
+#include <stdlib.h>
+
 #include "rlp_envs.hpp"
 #include "rlp_mfma_layout.hpp"
 
 namespace rlp {
 
+// Each wave stages only its own envs' observations in LDS, so a wave-level fence suffices; no
+// block barrier keeps the two waves of a SIMD in lockstep (one's f64 physics overlaps the other's
+// MFMAs).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 struct RolloutArgs {
     int T, n;
+    int stagger_cycles;  // one-time start delay of waves 4..7 (SIMD partners of waves 0..3)
     uint64_t seed, step0, env_id0;
     int success_rule, success_flag;
     float std_[4], a_min[4], a_max[4], gain[4], off[4];
 };
 
+// Block = 4 waves per SIMD-partner set: SUB == 4 -> 256 threads (1 wave per SIMD); SUB == 2 ->
+// 512 threads, waves w and w+4 share a SIMD (MI355X_MICROARCH.md "Two waves per SIMD").
+template <int SUB> constexpr int rollout_block() { return SUB == 4 ? 256 : 512; }
+
+constexpr int RING = 3;  // W2 k-phases in flight per wave: 2 ahead of the one being consumed
+
 template <int KIND, int H, int SUB>
-__global__ void __launch_bounds__(256, (SUB == 4 ? 1 : 2))
+__global__ void __launch_bounds__(rollout_block<SUB>(), 1)
 rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__restrict__ need_reset,
                const float *__restrict__ actor, MfmaNet an, const float *__restrict__ critic,
                MfmaNet cn, RolloutArgs ra, rlp_rollout_bufs b) {
     using E = Env<KIND>;
     constexpr int S = E::S, A = E::A, D = E::D, KS1 = (S + 3) / 4, WENV = 16 * SUB;
-    __shared__ float sobs[4][WENV][8];
+    constexpr int WAVES = rollout_block<SUB>() / 64;
+    constexpr int SMALL = mlp_small_floats<H, KS1, A>(), PF = mlp_phase_floats<H>();
+    // ONE __shared__ object (a second one next to the LDS-DMA ring can make hipcc drain vmcnt
+    // before every ds_read): [actor small | critic small | obs staging | per-wave W2 rings]
+    __shared__ __attribute__((aligned(16))) float lds[2 * SMALL + WAVES * WENV * 8 + WAVES * RING * PF];
+    float *small_a = lds, *small_c = lds + SMALL;
+    float(*sobs)[WENV][8] = reinterpret_cast<float(*)[WENV][8]>(lds + 2 * SMALL);
+    float *ring = lds + 2 * SMALL + WAVES * WENV * 8 + (threadIdx.x >> 6) * RING * PF;
+    mlp_small_to_lds(actor, an, small_a);
+    mlp_small_to_lds(critic, cn, small_c);
+    __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, e = lane & 15;
     const int n = ra.n;
-    const int env = (blockIdx.x * 4 + wave) * WENV + lane;  // physics lane -> env
+    const int env = (blockIdx.x * WAVES + wave) * WENV + lane;  // physics lane -> env
+
+    // The two waves of a SIMD run the same program; started together they stay phase-locked and
+    // their VALU phases (f64 physics, activations) coincide while the matrix pipe idles. A one-time
+    // delay of the partner waves puts one wave's VALU phase under the other's MFMA phase.
+    if (WAVES == 8 && wave >= 4 && ra.stagger_cycles > 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)ra.stagger_cycles)
+            __builtin_amdgcn_s_sleep(4);
+    }
     const bool phys = lane < WENV && env < n;
     const uint64_t eid = ra.env_id0 + (uint64_t)env;
 
@@ -56,21 +93,21 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
 #pragma unroll
             for (int j = 0; j < 8; ++j) sobs[wave][lane][j] = (phys && j < S) ? o[j] : 0.f;
         }
-        __syncthreads();
+        wave_sync();
         float bobs[SUB][KS1];
 #pragma unroll
         for (int sb = 0; sb < SUB; ++sb)
 #pragma unroll
             for (int kk = 0; kk < KS1; ++kk) bobs[sb][kk] = sobs[wave][16 * sb + e][4 * kk + g];
-        __syncthreads();
+        wave_sync();
 
         // actor then critic through ONE copy of the fused forward (one register allocation)
         float mraw[A], v = 0.f;
 #pragma unroll 1
         for (int which = 0; which < 2; ++which) {
             float out[SUB][A];
-            mlp_fused_forward<H, SUB, KS1, A>(which ? critic : actor, which ? cn : an,
-                                              which ? 1 : A, bobs, out);
+            mlp_fused_forward<H, SUB, KS1, A, RING>(which ? critic : actor, which ? small_c : small_a,
+                                                    ring, which ? cn : an, which ? 1 : A, bobs, out);
             // the physics lane (sub-block g, env e) owns out[g]
             float sel[A];
 #pragma unroll
@@ -132,14 +169,14 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
 #pragma unroll
         for (int j = 0; j < 8; ++j) sobs[wave][lane][j] = (phys && j < S) ? o[j] : 0.f;
     }
-    __syncthreads();
+    wave_sync();
     float bobs[SUB][KS1];
 #pragma unroll
     for (int sb = 0; sb < SUB; ++sb)
 #pragma unroll
         for (int kk = 0; kk < KS1; ++kk) bobs[sb][kk] = sobs[wave][16 * sb + e][4 * kk + g];
     float cv[SUB][A];
-    mlp_fused_forward<H, SUB, KS1, A>(critic, cn, 1, bobs, cv);
+    mlp_fused_forward<H, SUB, KS1, A, RING>(critic, small_c, ring, cn, 1, bobs, cv);
     float v = cv[0][0];
 #pragma unroll
     for (int sb = 1; sb < SUB; ++sb)
@@ -163,6 +200,11 @@ packed_forward_kernel(const float *__restrict__ P, MfmaNet net, const float *__r
                       float *__restrict__ y, int64_t rows, const uint8_t *__restrict__ done,
                       const uint8_t *__restrict__ success, int apply_out_act) {
     constexpr int WROWS = 16 * SUB;
+    constexpr int SMALL = mlp_small_floats<H, KS1, NOUT>(), PF = mlp_phase_floats<H>();
+    __shared__ __attribute__((aligned(16))) float lds[SMALL + 4 * RING * PF];
+    float *small = lds, *ring = lds + SMALL + (threadIdx.x >> 6) * RING * PF;
+    mlp_small_to_lds(P, net, small);
+    __syncthreads();
     const int lane = threadIdx.x & 63, g = lane >> 4, e = lane & 15;
     const int S = net.S;
     const int64_t nwaves = (int64_t)gridDim.x * 4;
@@ -183,7 +225,7 @@ packed_forward_kernel(const float *__restrict__ P, MfmaNet net, const float *__r
                 bobs[sb][kk] = (row < rows && k < S) ? x[row * S + k] : 0.f;
             }
         float out[SUB][NOUT];
-        mlp_fused_forward<H, SUB, KS1, NOUT>(P, net, net.A, bobs, out);
+        mlp_fused_forward<H, SUB, KS1, NOUT, RING>(P, small, ring, net, net.A, bobs, out);
         // lane (sub-block g, row e) owns out[g]; lanes 0..WROWS-1 store their row
         float sel[NOUT];
 #pragma unroll
@@ -231,10 +273,11 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
                           const MfmaNet &cn, const RolloutArgs &ra, const rlp_rollout_bufs &b,
                           hipStream_t stream) {
     const auto &p = *static_cast<const typename Env<KIND>::P *>(params);
-    constexpr int envs_per_block = 4 * 16 * SUB;
+    constexpr int threads = rollout_block<SUB>();
+    constexpr int envs_per_block = threads / 64 * 16 * SUB;
     const int blocks = (ra.n + envs_per_block - 1) / envs_per_block;
-    rollout_kernel<KIND, H, SUB><<<blocks, 256, 0, stream>>>(p, state, need_reset, actor, an,
-                                                             critic, cn, ra, b);
+    rollout_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor, an,
+                                                                 critic, cn, ra, b);
     RLP_CHECK_LAUNCH("rlp_rollout");
     return RLP_OK;
 }
@@ -258,6 +301,7 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
 }
 
 static int g_rollout_sub = 2;
+static int g_stagger_cycles = -1;  // -1: from RLP_STAGGER env (default 40000 cycles)
 
 }  // namespace rlp
 
@@ -266,6 +310,11 @@ using namespace rlp;
 extern "C" {
 
 // tuning knob (envs per wave = 16 * sub); sub in {2, 4}
+int rlp_set_rollout_stagger(int cycles) {
+    g_stagger_cycles = cycles < 0 ? 0 : cycles;
+    return RLP_OK;
+}
+
 int rlp_set_rollout_sub(int sub) {
     if (sub != 2 && sub != 4) return fail(RLP_EINVAL, "rlp_set_rollout_sub: %d", sub);
     g_rollout_sub = sub;
@@ -322,6 +371,11 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
         ra.off[a] = (cfg->a_min[a] + cfg->a_max[a]) / 2.0f;  // PPOActor_Gaussian: (a_min+a_max)/2
         ra.gain[a] = cfg->a_max[a] - ra.off[a];              //                   a_max - off
     }
+    if (g_stagger_cycles < 0) {
+        const char *e = getenv("RLP_STAGGER");
+        g_stagger_cycles = e ? atoi(e) : 40000;
+    }
+    ra.stagger_cycles = g_stagger_cycles;
     hipStream_t s = as_stream(stream);
     const int sub = g_rollout_sub;
     switch (kind) {
