@@ -28,6 +28,9 @@ from reinforcementlearningplatform_amd import kernels as K  # noqa: E402
 
 METRIC = "env-steps/sec (whole node), CartPole+UavRobust PPO2 @ 1/2/4/8 MI355X"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
+PEAK_F16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS   # f16/bf16 dense MFMA = 16x the f32 rate
+# f16x3 split: 3 f16 MFMAs per fp32-equivalent product -> the path's fp32-equivalent ceiling
+PEAK_F16X3_TFLOPS = PEAK_F16_MFMA_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0
 
 ENVS = {
@@ -206,6 +209,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e", type=int, default=2, help="PPO2 iterations incl. the K-epoch update to time (0: skip)")
     ap.add_argument("--uav", type=int, default=1, help="also time the UavRobust rollout (32768 envs/GPU)")
+    ap.add_argument("--fp32-leg", type=int, default=1, help="also time the exact-f32 MLP path")
+    ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
+                    help="rollout hidden-layer arithmetic (include/rlp.h rlp_set_mlp_precision)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -226,6 +232,8 @@ def main():
             dist.init_process_group(backend)
     if args.sub:
         _native.set_rollout_sub(args.sub)
+    prec = _native.MLP_F16X3 if args.precision == "f16x3" else _native.MLP_FP32
+    _native.set_mlp_precision(prec)
 
     n, T = args.envs_per_gpu, args.T
     seg = Segment(args.env, n, T, args.seed, env_id0=rank * n)
@@ -235,45 +243,65 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    def timed(steps):
+        barrier()
+        t0 = time.perf_counter()
+        ev = []
+        for _ in range(steps):
+            # HIP events on the stream the rollout kernel is launched on (torch's current stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            seg.rollout()
+            e1.record()
+            seg.learn_side()
+            ev.append((e0, e1))
+        barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([el], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
     for _ in range(args.warmup):
         seg.iteration()
-    barrier()
-    t0 = time.perf_counter()
-    ev = []
-    for _ in range(args.steps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        seg.rollout()
-        e1.record()
-        seg.learn_side()
-        ev.append((e0, e1))
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    rollout_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    elapsed, rollout_ms = timed(args.steps)
 
     env_steps = n * T * world * args.steps
     value = env_steps / elapsed
     flop_launch = n * T * (mlp_flops(seg.ad) + mlp_flops(seg.cd)) + n * mlp_flops(seg.cd)
     achieved = flop_launch / (rollout_ms * 1e-3) / 1e12
+    if prec == _native.MLP_F16X3:
+        peak, basis = PEAK_F16X3_TFLOPS, ("f16 dense MFMA %.1f TF / 3 (f16x3 split: 3 f16 MFMAs per "
+                                          "fp32-equivalent product)" % PEAK_F16_MFMA_TFLOPS)
+        dtype, mlp = "fp32 (f16x3 split MFMA)", "f16x3 split MFMA, f32 accumulate (fp32-class error)"
+    else:
+        peak, basis = PEAK_FP32_MFMA_TFLOPS, "f32 MFMA dense (v_mfma_f32_16x16x4_f32)"
+        dtype, mlp = "fp32", "fp32 MFMA (exact f32)"
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dtype,
         "data": "synthetic",
         "config": {"workload": f"{args.env}_ppo2_rollout", "envs_per_gpu": n, "global_envs": n * world,
                    "T": T, "env_steps_per_iteration": n * T * world,
                    "nets": "actor [S,256,256,A] tanh, critic [S,256,256,1]",
                    "parallelism": f"dp{world} (env shards, no data-path collective)",
-                   "physics": "f64", "mlp": "fp32 MFMA"},
+                   "physics": "f64", "mlp": mlp},
         "roofline": {"bound": "mfma", "kernel": "rlp::rollout_kernel", "achieved": achieved,
-                     "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
-                     "avg_launch_ms": rollout_ms, "flop_per_launch": flop_launch},
+                     "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+                     "peak_basis": basis, "avg_launch_ms": rollout_ms, "flop_per_launch": flop_launch},
     }
+    if prec == _native.MLP_F16X3 and args.fp32_leg:
+        # the exact-f32 MFMA path on the same workload, for reference (include/rlp.h)
+        _native.set_mlp_precision(_native.MLP_FP32)
+        seg.iteration()
+        el32, ms32 = timed(max(2, args.steps // 2))
+        _native.set_mlp_precision(prec)
+        ach32 = flop_launch / (ms32 * 1e-3) / 1e12
+        out["fp32_mfma_path"] = {"value": n * T * world * max(2, args.steps // 2) / el32,
+                                 "unit": "env-steps/s", "avg_launch_ms": ms32, "achieved": ach32,
+                                 "peak": PEAK_FP32_MFMA_TFLOPS, "frac": ach32 / PEAK_FP32_MFMA_TFLOPS}
     traffic = pmc_traffic(out["config"]["workload"], n, T)
     if traffic is not None:
         out["roofline"]["traffic"] = traffic

@@ -312,10 +312,16 @@ int rlp_abi_version(void);
 int64_t rlp_struct_size(int which);
 /* Tuning knob of rlp_rollout: 16-env sub-blocks per wave (2 or 4; default 2). */
 int rlp_set_rollout_sub(int sub);
-/* Tuning knob of rlp_rollout: one-time start delay (shader cycles) of the second wave of each
- * SIMD so the two waves' VALU phases interleave with each other's MFMA phases (default 40000,
- * or the RLP_STAGGER environment variable). */
-int rlp_set_rollout_stagger(int cycles);
+/* Arithmetic of rlp_rollout's hidden layer (the [256 x 256] GEMM, 99 % of its FLOPs):
+ *   RLP_MLP_F16X3 (default): error-compensated split, w*x = wh*xh + wh*xl + wl*xh on f16 MFMA with
+ *     f32 accumulation — fp32-class accuracy (see tests/test_gpu_rollout.py) at 16/3 x the f32
+ *     MFMA rate;
+ *   RLP_MLP_FP32: exact f32-input MFMA (v_mfma_f32_16x16x4_f32).
+ * The other kernels (rlp_mfma_forward, rlp_value_fixup, rlp_mlp_forward) are always fp32. */
+#define RLP_MLP_FP32 0
+#define RLP_MLP_F16X3 1
+int rlp_set_mlp_precision(int mode);
+int rlp_get_mlp_precision(void);
 
 #ifdef __cplusplus
 }

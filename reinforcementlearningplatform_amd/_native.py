@@ -42,7 +42,8 @@ def _declare(lib):
         "rlp_mfma_forward": (i32, [vp, vp, vp, vp, i64, vp]),
         "rlp_value_fixup": (i32, [vp, vp, vp, vp, vp, vp, i64, vp]),
         "rlp_set_rollout_sub": (i32, [i32]),
-        "rlp_set_rollout_stagger": (i32, [i32]),
+        "rlp_set_mlp_precision": (i32, [i32]),
+        "rlp_get_mlp_precision": (i32, []),
         "rlp_reward_norm": (i32, [vp, i32, i32, vp, vp, vp, vp]),
         "rlp_gae": (i32, [vp, vp, vp, vp, vp, dbl, dbl, i32, i32, vp, vp, vp, vp]),
         "rlp_adv_normalize": (i32, [vp, i64, vp, vp]),
@@ -93,8 +94,16 @@ def stream_ptr(stream=None):
     return C.c_void_p(s.cuda_stream)
 
 
-def set_rollout_stagger(cycles):
-    check(lib().rlp_set_rollout_stagger(int(cycles)), "rlp_set_rollout_stagger")
+MLP_FP32, MLP_F16X3 = 0, 1
+
+
+def set_mlp_precision(mode):
+    """rlp_rollout's hidden-layer arithmetic: MLP_F16X3 (default) or MLP_FP32 (include/rlp.h)."""
+    check(lib().rlp_set_mlp_precision(int(mode)), "rlp_set_mlp_precision")
+
+
+def get_mlp_precision():
+    return int(lib().rlp_get_mlp_precision())
 
 
 def set_rollout_sub(sub):

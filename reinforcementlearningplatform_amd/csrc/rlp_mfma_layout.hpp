@@ -16,17 +16,23 @@
 // Packed layout (floats), NT = H/16, NJQ = NT/4, KS1 = ceil(S/4):
 //   W2p [t][r][jq][lane][4]   W2[16(4jq+q) + (l&15)][16t + 4(l>>4) + r]      (offset 0)
 //   W1c [H][4*KS1]            W1[j][k] (0 for k >= S)                         (LDS-resident part:)
-//   B1c [H], B2c [H], W3c [A][H], b3 [4]
+//   B1c [H], B2c [H], W3c [A][H], b3 [4], info [4] = {2^sw, 2^(sw+SH), 2^-(sw+SH), 0}
+//   X3  (256-B aligned)       W2 * 2^sw split into f16 hi + lo, the f16x3 path's chunks
+//                             (rlp_mfma_x3.hpp)
 #pragma once
 #include "rlp_common.hpp"
 
 namespace rlp {
 
+// f16x3 path: hidden activations h in [-1, 1] are scaled by 2^SH before the f16 split
+constexpr float kX3HScale = 4096.f;
+
 struct MfmaNet {
     int S, H, A, ks1;
     int out_tanh;  // last layer activation is tanh (actor) vs identity (critic)
-    int off_w1, off_b1, off_b2, off_w3, off_b3;  // offsets of the LDS-resident part
-    int small_count;                               // floats from off_w1 to the end
+    int off_w1, off_b1, off_b2, off_w3, off_b3, off_info;  // offsets of the LDS-resident part
+    int small_count;                                         // floats from off_w1 to info's end
+    int off_x3;                                              // f16 hi/lo W2 chunks (H*H floats)
     int64_t count;
 };
 
@@ -45,14 +51,16 @@ inline bool mfma_net_from_desc(const rlp_mlp_desc &d, MfmaNet *net) {
     net->off_b2 = net->off_b1 + H;
     net->off_w3 = net->off_b2 + H;
     net->off_b3 = net->off_w3 + A * H;
-    net->count = net->off_b3 + 4;
-    net->small_count = (int)(net->count - net->off_w1);
+    net->off_info = net->off_b3 + 4;
+    net->small_count = net->off_info + 4 - net->off_w1;
+    net->off_x3 = (net->off_info + 4 + 63) / 64 * 64;
+    net->count = net->off_x3 + (int64_t)H * H;
     return true;
 }
 
 // LDS floats of one net's resident part (upper bound used for static carving)
 template <int H, int KS1, int NOUT>
-constexpr int mlp_small_floats() { return H * 4 * KS1 + 2 * H + NOUT * H + 4; }
+constexpr int mlp_small_floats() { return H * 4 * KS1 + 2 * H + NOUT * H + 8; }
 template <int H>
 constexpr int mlp_phase_floats() { return H / 64 * 256; }  // one k-phase of W2 fragments
 

@@ -1,0 +1,180 @@
+// rlp_mfma_x3.hpp — f16x3 split-MFMA forward of the [S -> 256 -> 256 -> A] tanh MLP (the PPO2
+// drivers' actor/critic, demonstration/PPO2/PPO2-4-CartPole/train.py:39-125): layer 2 (99 % of the
+// FLOPs) on v_mfma_f32_16x16x32_f16 at 16x the f32-MFMA rate, with fp32-class accuracy.
+//
+// Split: w = 2^sw W2 and x = 2^SH h1 are each written as hi + lo with hi = f16(v), lo = f16(v - hi)
+// (hi, lo normal f16 for every term that matters: 2^sw puts max|W2| in [2^13, 2^14), h1 is a tanh
+// in [-1, 1]). w x = wh xh + wh xl + wl xh + wl xl; the three MFMAs keep the first three terms
+// (f16 x f16 products are exact in the f32 accumulator), so the dropped wl xl and the rounding of
+// lo leave ~3 * 2^-22 |w x| per product — the same order as the f32 MFMA's own accumulation
+// rounding (MI355X_MICROARCH.md "FP32-input MFMA": 0.75-1.5e-7 sum|ab|). The accumulator carries
+// 2^(sw + SH) (bias pre-scaled, removed inside the output tanh's exponent constant, exact powers
+// of two). tests/test_gpu_rollout.py measures the error of both paths against float64.
+//
+// Operands ("env on lane", as rlp_mfma_layout.hpp): for phase P (K = 32 neurons), lane (g, e) of
+// sub-block sb holds B[k = 8g + i][env e] = x(neuron 32P + 4g + i) for i < 4 (layer-1 tile 2P, its
+// C registers) and x(32P + 16 + 4g + i - 4) for i >= 4 (tile 2P + 1); the packed A fragments
+// (X3 region, mfma_pack_kernel) use the same k permutation.
+//
+// Staging: 16 chunks of 16 KiB per net (phase P, half hf: 8 output tiles x {hi, lo} x 64 lanes x
+// 16 B). The kX3Waves waves of a block share one LDS ring of kX3Ring chunks: each wave DMAs a
+// quarter of every chunk (global_load_lds_dwordx4, 4 x 1 KiB), waits for its own part with a
+// counted vmcnt, and one s_barrier per chunk publishes the chunk and frees the slot the next DMA
+// overwrites. Sharing divides the L2 -> CU weight stream by kX3Waves (at the f16 rate a per-wave
+// stream would exceed the L2 bandwidth).
+#pragma once
+#include "rlp_mfma_layout.hpp"
+
+namespace rlp {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+constexpr int kX3Waves = 4;             // waves per block sharing the W2 ring
+constexpr int kX3Ring = 3;              // chunks resident in the ring
+constexpr int kX3ChunkFloats = 4096;    // 16 KiB
+constexpr int kX3RingFloats = kX3Ring * kX3ChunkFloats;
+
+__device__ __forceinline__ void block_barrier_raw() {
+    // s_barrier without the compiler's vmcnt(0) drain: the counted waits above it already cover
+    // exactly the DMA this barrier publishes, and later chunks stay in flight.
+    asm volatile("s_barrier" ::: "memory");
+}
+
+// Every wave of the block must call this the same number of times (it contains block barriers).
+template <int H, int SUB, int KS1, int NOUT>
+__device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, const float *small,
+                                               float *ring, const MfmaNet &net, const int nout,
+                                               const float (&bobs)[SUB][KS1],
+                                               float (&out)[SUB][NOUT]) {
+    static_assert(H == 256, "chunking assumes H = 256 (2 chunks of 8 output tiles per phase)");
+    constexpr int NT = H / 16, NPH = H / 32, NC = 2 * NPH;
+    const int lane = threadIdx.x & 63, wv = (threadIdx.x >> 6) & (kX3Waves - 1);
+    const int g = lane >> 4, e = lane & 15;
+    const float *Pg = P0;
+    asm volatile("" : "+s"(Pg));
+    const gptr<float> X = as_global(Pg) + net.off_x3 + wv * 4 * 256 + lane * 4;
+    float *const my_part = ring + wv * 4 * 256;
+    const float *W1c = small;
+    const float *B1c = small + (net.off_b1 - net.off_w1);
+    const float *B2c = small + (net.off_b2 - net.off_w1);
+    const float *W3c = small + (net.off_w3 - net.off_w1);
+    const float *b3c = small + (net.off_b3 - net.off_w1);
+    const float *info = small + (net.off_info - net.off_w1);
+    const float acc_scale = info[1];
+    const float k_out = 2.8853900817779268f * info[2];  // exp(2x) constant with 2^-(sw+SH) folded
+
+    auto issue = [&](int c) {
+        float *slot = my_part + (c % kX3Ring) * kX3ChunkFloats;
+        const gptr<float> src = X + c * kX3ChunkFloats;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
+    };
+    block_barrier_raw();  // every wave is done reading the ring (previous call)
+    issue(0);
+    issue(1);
+
+    floatx4 acc[SUB][NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        floatx4 b2 = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b2[r] *= acc_scale;
+#pragma unroll
+        for (int sb = 0; sb < SUB; ++sb) acc[sb][j] = b2;
+    }
+    auto layer1 = [&](int t, floatx4(&c)[SUB]) {
+        float w1[KS1];
+#pragma unroll
+        for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[(16 * t + e) * (4 * KS1) + 4 * kk + g];
+        const floatx4 b1 = *reinterpret_cast<const floatx4 *>(B1c + 16 * t + 4 * g);
+#pragma unroll
+        for (int sb = 0; sb < SUB; ++sb) {
+            c[sb] = b1;
+#pragma unroll
+            for (int kk = 0; kk < KS1; ++kk)
+                c[sb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[kk], bobs[sb][kk], c[sb], 0, 0, 0);
+        }
+    };
+    floatx4 hp0[SUB], hp1[SUB];
+    layer1(0, hp0);
+    layer1(1, hp1);
+
+#pragma unroll 1
+    for (int P = 0; P < NPH; ++P) {
+        half8 bh[SUB], bl[SUB];
+#pragma unroll
+        for (int sb = 0; sb < SUB; ++sb)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float pre = i < 4 ? hp0[sb][i] : hp1[sb][i - 4];
+                // 2^SH tanh(pre), bit-identical to kX3HScale * tanh_fast(pre)
+                const float ex = __builtin_amdgcn_exp2f(pre * 2.8853900817779268f);
+                const float x = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + ex),
+                                               kX3HScale);
+                const _Float16 hi = (_Float16)x;
+                bh[sb][i] = hi;
+                bl[sb][i] = (_Float16)(x - (float)hi);
+            }
+        if (P + 1 < NPH) {  // next phase's layer-1 tiles, under this phase's MFMAs
+            layer1(2 * P + 2, hp0);
+            layer1(2 * P + 3, hp1);
+        }
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            const int c = 2 * P + hf;
+            if (c + 1 < NC) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // own part of c landed
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            block_barrier_raw();  // all parts of c landed; everyone is done with chunk c - 1
+            if (c + 2 < NC) issue(c + 2);  // into chunk c - 1's slot
+            const float *slot = ring + (c % kX3Ring) * kX3ChunkFloats + lane * 4;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const half8 ah = *reinterpret_cast<const half8 *>(slot + (2 * jj) * 256);
+                const half8 al = *reinterpret_cast<const half8 *>(slot + (2 * jj + 1) * 256);
+#pragma unroll
+                for (int sb = 0; sb < SUB; ++sb) {
+                    floatx4 a = acc[sb][8 * hf + jj];
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[sb], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[sb], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[sb], a, 0, 0, 0);
+                    acc[sb][8 * hf + jj] = a;
+                }
+            }
+        }
+    }
+
+    // ---- layer 3: out[a][env] = sum_n W3[a][n] tanh(H2^T[n][env]) + b3[a]
+    float part[SUB][NOUT];
+#pragma unroll
+    for (int sb = 0; sb < SUB; ++sb)
+#pragma unroll
+        for (int a = 0; a < NOUT; ++a) part[sb][a] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        floatx4 w3[NOUT];
+#pragma unroll
+        for (int a = 0; a < NOUT; ++a)
+            w3[a] = a < nout ? *reinterpret_cast<const floatx4 *>(W3c + a * H + 16 * j + 4 * g)
+                             : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int sb = 0; sb < SUB; ++sb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float ex = __builtin_amdgcn_exp2f(acc[sb][j][r] * k_out);
+                const float h = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + ex), 1.0f);
+#pragma unroll
+                for (int a = 0; a < NOUT; ++a) part[sb][a] = __builtin_fmaf(w3[a][r], h, part[sb][a]);
+            }
+    }
+#pragma unroll
+    for (int sb = 0; sb < SUB; ++sb)
+#pragma unroll
+        for (int a = 0; a < NOUT; ++a) {
+            float v = part[sb][a];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            out[sb][a] = v + (a < nout ? b3c[a] : 0.f);
+        }
+}
+
+}  // namespace rlp

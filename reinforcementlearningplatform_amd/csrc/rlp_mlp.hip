@@ -81,11 +81,40 @@ __global__ void __launch_bounds__(64) mlp_forward_kernel(MlpArgs args, const flo
 // ------------------------------------------------------------------------------------------
 // Fused-layout packer (see rlp_mfma_layout.hpp for the layout)
 // ------------------------------------------------------------------------------------------
+// info[] = {2^sw, 2^sw * 2^SH, 2^-(sw + SH), 0}: 2^sw puts max|W2| in [2^13, 2^14), far inside f16
+// range, so the hi and lo f16 halves of every weight that matters stay normal (rlp_mfma_x3.hpp).
+__global__ void __launch_bounds__(256) mfma_scale_kernel(MfmaNet net, const float *__restrict__ P,
+                                                         float *out) {
+    const int S = net.S, H = net.H;
+    const float *W2 = P + S * H + H;
+    float m = 0.f;
+    for (int i = threadIdx.x; i < H * H; i += blockDim.x) m = fmaxf(m, fabsf(W2[i]));
+    __shared__ float red[256];
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int e = 0;
+        if (red[0] > 0.f) frexpf(red[0], &e);  // max = f * 2^e, f in [0.5, 1)
+        e = e < -60 ? -60 : (e > 60 ? 60 : e);
+        const float sw = ldexpf(1.f, 14 - e);
+        float *info = out + net.off_info;
+        info[0] = sw;
+        info[1] = sw * kX3HScale;
+        info[2] = 1.f / (sw * kX3HScale);
+        info[3] = 0.f;
+    }
+}
+
 __global__ void mfma_pack_kernel(MfmaNet net, const float *__restrict__ P, float *out) {
     const int total = (int)net.count;
     const int S = net.S, H = net.H, A = net.A, NT = H / 16, KS1 = net.ks1;
     const float *W1 = P, *b1 = W1 + S * H, *W2 = b1 + H, *b2 = W2 + H * H, *W3 = b2 + H,
                 *b3 = W3 + H * A;
+    const float sw = out[net.off_info];  // written by mfma_scale_kernel (same stream)
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
          idx += gridDim.x * blockDim.x) {
         float v = 0.f;
@@ -106,9 +135,26 @@ __global__ void mfma_pack_kernel(MfmaNet net, const float *__restrict__ P, float
             v = b2[idx - net.off_b2];
         } else if (idx < net.off_b3) {  // W3c [A][H]
             v = W3[idx - net.off_w3];
-        } else {  // b3 [4]
+        } else if (idx < net.off_info) {  // b3 [4]
             const int a = idx - net.off_b3;
             v = a < A ? b3[a] : 0.f;
+        } else if (idx < net.off_x3) {  // info (mfma_scale_kernel) + alignment pad
+            continue;
+        } else {  // X3 [P][j][part][lane][8 halfs]: two halfs per float slot
+            const int q = idx - net.off_x3;
+            const int i = 2 * (q & 3), lane = (q >> 2) & 63, part = (q >> 8) & 1;
+            const int j = (q >> 9) % NT, Pp = (q >> 9) / NT;
+            const int row = 16 * j + (lane & 15), g = lane >> 4;
+            _Float16 h2[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int ii = i + u;
+                const int k = 32 * Pp + (ii < 4 ? 4 * g + ii : 16 + 4 * g + ii - 4);
+                const float w = W2[row * H + k] * sw;
+                const _Float16 hi = (_Float16)w;
+                h2[u] = part == 0 ? hi : (_Float16)(w - (float)hi);
+            }
+            __builtin_memcpy(&v, h2, 4);
         }
         out[idx] = v;
     }
@@ -196,6 +242,7 @@ int rlp_mfma_pack(const rlp_mlp_desc *desc, const float *params, float *packed,
     if (!mfma_net_from_desc(*desc, &net))
         return fail(RLP_EUNSUPPORTED, "rlp_mfma_pack: need [S<=8 -> H -> H -> A<=4], H in {64,128,256}");
     const int blocks = (int)((net.count + 255) / 256);
+    mfma_scale_kernel<<<1, 256, 0, as_stream(stream)>>>(net, params, packed);
     mfma_pack_kernel<<<blocks < 1024 ? blocks : 1024, 256, 0, as_stream(stream)>>>(net, params,
                                                                                   packed);
     RLP_CHECK_LAUNCH("rlp_mfma_pack");

@@ -9,10 +9,13 @@
 //   env.step_update(a)                 CartPole.py:257-264 (etc.)
 //   buffer.append(...)                 utils/classes.py:264-272, time-major [T][n][...]
 // The two MLPs are fp32 MFMA (v_mfma_f32_16x16x4_f32): this kernel is MFMA-bound.
-#include <stdlib.h>
-
 #include "rlp_envs.hpp"
 #include "rlp_mfma_layout.hpp"
+#include "rlp_mfma_x3.hpp"
+
+#ifndef RLP_EXPERIMENT
+#define RLP_EXPERIMENT 0
+#endif
 
 namespace rlp {
 
@@ -27,33 +30,35 @@ __device__ __forceinline__ void wave_sync() {
 
 struct RolloutArgs {
     int T, n;
-    int stagger_cycles;  // one-time start delay of waves 4..7 (SIMD partners of waves 0..3)
     uint64_t seed, step0, env_id0;
     int success_rule, success_flag;
     float std_[4], a_min[4], a_max[4], gain[4], off[4];
 };
 
-// Block = 4 waves per SIMD-partner set: SUB == 4 -> 256 threads (1 wave per SIMD); SUB == 2 ->
-// 512 threads, waves w and w+4 share a SIMD (MI355X_MICROARCH.md "Two waves per SIMD").
-template <int SUB> constexpr int rollout_block() { return SUB == 4 ? 256 : 512; }
+// fp32 path: SUB == 4 -> 256 threads (1 wave per SIMD); SUB == 2 -> 512 threads, waves w and w+4
+// share a SIMD (MI355X_MICROARCH.md "Two waves per SIMD"); one block per CU, per-wave W2 rings.
+// f16x3 path: 4-wave blocks sharing one W2 ring, two blocks per CU (2 waves per SIMD).
+template <int SUB, bool X3> constexpr int rollout_block() { return X3 ? 256 : (SUB == 4 ? 256 : 512); }
+template <bool X3> constexpr int rollout_min_blocks() { return X3 ? 2 : 1; }
 
-constexpr int RING = 3;  // W2 k-phases in flight per wave: 2 ahead of the one being consumed
+constexpr int RING = 3;  // fp32 path: W2 k-phases in flight per wave
 
-template <int KIND, int H, int SUB>
-__global__ void __launch_bounds__(rollout_block<SUB>(), 1)
+template <int KIND, int H, int SUB, bool X3>
+__global__ void __launch_bounds__((rollout_block<SUB, X3>()), (rollout_min_blocks<X3>()))
 rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__restrict__ need_reset,
                const float *__restrict__ actor, MfmaNet an, const float *__restrict__ critic,
                MfmaNet cn, RolloutArgs ra, rlp_rollout_bufs b) {
     using E = Env<KIND>;
     constexpr int S = E::S, A = E::A, D = E::D, KS1 = (S + 3) / 4, WENV = 16 * SUB;
-    constexpr int WAVES = rollout_block<SUB>() / 64;
+    constexpr int WAVES = rollout_block<SUB, X3>() / 64;
     constexpr int SMALL = mlp_small_floats<H, KS1, A>(), PF = mlp_phase_floats<H>();
+    constexpr int RINGF = X3 ? kX3RingFloats : WAVES * RING * PF;
     // ONE __shared__ object (a second one next to the LDS-DMA ring can make hipcc drain vmcnt
-    // before every ds_read): [actor small | critic small | obs staging | per-wave W2 rings]
-    __shared__ __attribute__((aligned(16))) float lds[2 * SMALL + WAVES * WENV * 8 + WAVES * RING * PF];
+    // before every ds_read): [actor small | critic small | obs staging | W2 ring(s)]
+    __shared__ __attribute__((aligned(16))) float lds[2 * SMALL + WAVES * WENV * 8 + RINGF];
     float *small_a = lds, *small_c = lds + SMALL;
     float(*sobs)[WENV][8] = reinterpret_cast<float(*)[WENV][8]>(lds + 2 * SMALL);
-    float *ring = lds + 2 * SMALL + WAVES * WENV * 8 + (threadIdx.x >> 6) * RING * PF;
+    float *ring = lds + 2 * SMALL + WAVES * WENV * 8 + (X3 ? 0 : (threadIdx.x >> 6) * RING * PF);
     mlp_small_to_lds(actor, an, small_a);
     mlp_small_to_lds(critic, cn, small_c);
     __syncthreads();
@@ -63,14 +68,6 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
     const int n = ra.n;
     const int env = (blockIdx.x * WAVES + wave) * WENV + lane;  // physics lane -> env
 
-    // The two waves of a SIMD run the same program; started together they stay phase-locked and
-    // their VALU phases (f64 physics, activations) coincide while the matrix pipe idles. A one-time
-    // delay of the partner waves puts one wave's VALU phase under the other's MFMA phase.
-    if (WAVES == 8 && wave >= 4 && ra.stagger_cycles > 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memtime();
-        while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)ra.stagger_cycles)
-            __builtin_amdgcn_s_sleep(4);
-    }
     const bool phys = lane < WENV && env < n;
     const uint64_t eid = ra.env_id0 + (uint64_t)env;
 
@@ -106,8 +103,17 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
 #pragma unroll 1
         for (int which = 0; which < 2; ++which) {
             float out[SUB][A];
-            mlp_fused_forward<H, SUB, KS1, A, RING>(which ? critic : actor, which ? small_c : small_a,
-                                                    ring, which ? cn : an, which ? 1 : A, bobs, out);
+#if RLP_EXPERIMENT == 1  // timing experiment only: MLP skipped
+            for (int sb = 0; sb < SUB; ++sb) for (int a = 0; a < A; ++a) out[sb][a] = bobs[sb][0] * 0.5f;
+#else
+            if constexpr (X3)
+                mlp_x3_forward<H, SUB, KS1, A>(which ? critic : actor, which ? small_c : small_a,
+                                               ring, which ? cn : an, which ? 1 : A, bobs, out);
+            else
+                mlp_fused_forward<H, SUB, KS1, A, RING>(which ? critic : actor,
+                                                        which ? small_c : small_a, ring,
+                                                        which ? cn : an, which ? 1 : A, bobs, out);
+#endif
             // the physics lane (sub-block g, env e) owns out[g]
             float sel[A];
 #pragma unroll
@@ -140,7 +146,11 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
             double r;
             int f;
             bool dn;
+#if RLP_EXPERIMENT == 2  // timing experiment only: env dynamics skipped
+            s[0] += 1e-3 * act[0]; E::observe(p, s, on); r = s[0]; f = 0; dn = false;
+#else
             E::step(p, s, act, on, r, f, dn);
+#endif
 #pragma unroll
             for (int j = 0; j < S; ++j) {
                 b.obs[k * S + j] = o[j];
@@ -176,7 +186,10 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
 #pragma unroll
         for (int kk = 0; kk < KS1; ++kk) bobs[sb][kk] = sobs[wave][16 * sb + e][4 * kk + g];
     float cv[SUB][A];
-    mlp_fused_forward<H, SUB, KS1, A, RING>(critic, small_c, ring, cn, 1, bobs, cv);
+    if constexpr (X3)
+        mlp_x3_forward<H, SUB, KS1, A>(critic, small_c, ring, cn, 1, bobs, cv);
+    else
+        mlp_fused_forward<H, SUB, KS1, A, RING>(critic, small_c, ring, cn, 1, bobs, cv);
     float v = cv[0][0];
 #pragma unroll
     for (int sb = 1; sb < SUB; ++sb)
@@ -267,16 +280,16 @@ static int launch_packed_forward(const MfmaNet &net, const float *P, const float
     return RLP_OK;
 }
 
-template <int KIND, int H, int SUB>
+template <int KIND, int H, int SUB, bool X3>
 static int launch_rollout(const void *params, double *state, uint8_t *need_reset,
                           const float *actor, const MfmaNet &an, const float *critic,
                           const MfmaNet &cn, const RolloutArgs &ra, const rlp_rollout_bufs &b,
                           hipStream_t stream) {
     const auto &p = *static_cast<const typename Env<KIND>::P *>(params);
-    constexpr int threads = rollout_block<SUB>();
+    constexpr int threads = rollout_block<SUB, X3>();
     constexpr int envs_per_block = threads / 64 * 16 * SUB;
     const int blocks = (ra.n + envs_per_block - 1) / envs_per_block;
-    rollout_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor, an,
+    rollout_kernel<KIND, H, SUB, X3><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor, an,
                                                                  critic, cn, ra, b);
     RLP_CHECK_LAUNCH("rlp_rollout");
     return RLP_OK;
@@ -285,7 +298,7 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
 template <int KIND>
 static int rollout_kind(const void *params, double *state, uint8_t *need_reset, const float *actor,
                         const MfmaNet &an, const float *critic, const MfmaNet &cn,
-                        const RolloutArgs &ra, const rlp_rollout_bufs &b, int sub,
+                        const RolloutArgs &ra, const rlp_rollout_bufs &b, int sub, int prec,
                         hipStream_t stream) {
     using E = Env<KIND>;
     if (an.S != E::S || cn.S != E::S || an.A != E::A || cn.A != 1)
@@ -293,15 +306,18 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
                     an.S, an.A, cn.S, cn.A, E::S, E::A);
     if (an.H != 256 || cn.H != 256)
         return fail(RLP_EUNSUPPORTED, "rlp_rollout: hidden width %d/%d (built for 256)", an.H, cn.H);
+    if (prec == RLP_MLP_F16X3)
+        return launch_rollout<KIND, 256, 2, true>(params, state, need_reset, actor, an, critic, cn,
+                                                  ra, b, stream);
     if (sub == 2)
-        return launch_rollout<KIND, 256, 2>(params, state, need_reset, actor, an, critic, cn, ra, b,
-                                            stream);
-    return launch_rollout<KIND, 256, 4>(params, state, need_reset, actor, an, critic, cn, ra, b,
-                                        stream);
+        return launch_rollout<KIND, 256, 2, false>(params, state, need_reset, actor, an, critic, cn,
+                                                   ra, b, stream);
+    return launch_rollout<KIND, 256, 4, false>(params, state, need_reset, actor, an, critic, cn, ra,
+                                               b, stream);
 }
 
 static int g_rollout_sub = 2;
-static int g_stagger_cycles = -1;  // -1: from RLP_STAGGER env (default 40000 cycles)
+static int g_mlp_precision = RLP_MLP_F16X3;
 
 }  // namespace rlp
 
@@ -309,11 +325,16 @@ using namespace rlp;
 
 extern "C" {
 
-// tuning knob (envs per wave = 16 * sub); sub in {2, 4}
-int rlp_set_rollout_stagger(int cycles) {
-    g_stagger_cycles = cycles < 0 ? 0 : cycles;
+int rlp_set_mlp_precision(int mode) {
+    if (mode != RLP_MLP_FP32 && mode != RLP_MLP_F16X3)
+        return fail(RLP_EINVAL, "rlp_set_mlp_precision: %d", mode);
+    g_mlp_precision = mode;
     return RLP_OK;
 }
+
+int rlp_get_mlp_precision(void) { return g_mlp_precision; }
+
+// tuning knob of the fp32 path (envs per wave = 16 * sub); sub in {2, 4}
 
 int rlp_set_rollout_sub(int sub) {
     if (sub != 2 && sub != 4) return fail(RLP_EINVAL, "rlp_set_rollout_sub: %d", sub);
@@ -371,33 +392,28 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
         ra.off[a] = (cfg->a_min[a] + cfg->a_max[a]) / 2.0f;  // PPOActor_Gaussian: (a_min+a_max)/2
         ra.gain[a] = cfg->a_max[a] - ra.off[a];              //                   a_max - off
     }
-    if (g_stagger_cycles < 0) {
-        const char *e = getenv("RLP_STAGGER");
-        g_stagger_cycles = e ? atoi(e) : 40000;
-    }
-    ra.stagger_cycles = g_stagger_cycles;
     hipStream_t s = as_stream(stream);
-    const int sub = g_rollout_sub;
+    const int sub = g_rollout_sub, prec = g_mlp_precision;
     switch (kind) {
     case RLP_ENV_CARTPOLE:
         return rollout_kind<RLP_ENV_CARTPOLE>(env_params, state, need_reset, actor_packed, an,
-                                              critic_packed, cn, ra, b, sub, s);
+                                              critic_packed, cn, ra, b, sub, prec, s);
     case RLP_ENV_CARTPOLE_ANGLEONLY:
         return rollout_kind<RLP_ENV_CARTPOLE_ANGLEONLY>(env_params, state, need_reset, actor_packed,
-                                                        an, critic_packed, cn, ra, b, sub, s);
+                                                        an, critic_packed, cn, ra, b, sub, prec, s);
     case RLP_ENV_SOI:
         return rollout_kind<RLP_ENV_SOI>(env_params, state, need_reset, actor_packed, an,
-                                         critic_packed, cn, ra, b, sub, s);
+                                         critic_packed, cn, ra, b, sub, prec, s);
     case RLP_ENV_UGV_FORWARD:
         return rollout_kind<RLP_ENV_UGV_FORWARD>(env_params, state, need_reset, actor_packed, an,
-                                                 critic_packed, cn, ra, b, sub, s);
+                                                 critic_packed, cn, ra, b, sub, prec, s);
     case RLP_ENV_UGV_BIDIRECTIONAL:
         return rollout_kind<RLP_ENV_UGV_BIDIRECTIONAL>(env_params, state, need_reset, actor_packed,
-                                                       an, critic_packed, cn, ra, b, sub, s);
+                                                       an, critic_packed, cn, ra, b, sub, prec, s);
     case RLP_ENV_UAV_HOVER_OUTER_LOOP:
         return rollout_kind<RLP_ENV_UAV_HOVER_OUTER_LOOP>(env_params, state, need_reset,
                                                           actor_packed, an, critic_packed, cn, ra,
-                                                          b, sub, s);
+                                                          b, sub, prec, s);
     }
     return fail(RLP_EINVAL, "rlp_rollout: unknown env kind %d", kind);
 }

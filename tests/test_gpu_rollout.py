@@ -170,3 +170,38 @@ def test_mfma_forward_and_value_fixup(kind):
     need = (done == 1) & (succ == 0)
     np.testing.assert_allclose(vn[need], v[need, 0], rtol=1e-6, atol=1e-6)
     assert (vn[~need] == -123.0).all()
+
+
+@pytest.mark.parametrize("kind", [A.RLP_ENV_CARTPOLE, A.RLP_ENV_UAV_HOVER_OUTER_LOOP])
+def test_mlp_precision_modes_vs_float64(kind):
+    """rlp_rollout's two hidden-layer arithmetics against a float64 evaluation of the critic on the
+    observations each run recorded: the f16x3 split (default) must stay within a small factor of
+    the exact f32-MFMA path's own error, and well inside the 1e-5 parity tolerance."""
+    D, S, Ad = A.ENV_DIMS[kind]
+    p = A.default_params(kind)
+    ad, ap, cd, cp = nets(S, Ad, seed=5)
+    lo, hi = A.action_bounds(kind, p)
+    std = [(h - l) / 6 for l, h in zip(lo, hi)]
+    n, T = 8192, 8
+    cfg = K.make_rollout_cfg(T, n, 11, 0, 0, std, lo, hi, A.RLP_SUCCESS_DONE_AND_FLAG_NE,
+                             A.timeout_flag(kind))
+    apk, cpk = K.mfma_pack(ad, dev(ap)), K.mfma_pack(cd, dev(cp))
+    errs = {}
+    old = _native.get_mlp_precision()
+    try:
+        for mode in (_native.MLP_FP32, _native.MLP_F16X3):
+            _native.set_mlp_precision(mode)
+            st = K.new_state(kind, n)
+            need = torch.ones(n, dtype=torch.uint8, device="cuda")
+            bufs = K.rollout_buffers(kind, T, n)
+            K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs)
+            obs = host(bufs["obs"]).reshape(-1, S)
+            v64 = oracle.mlp_forward(cd, cp, obs)[:, 0]
+            v = host(bufs["value"]).reshape(-1).astype(np.float64)
+            errs[mode] = np.abs(v - v64) / (np.abs(v64) + 1.0)
+    finally:
+        _native.set_mlp_precision(old)
+    e32, ex3 = errs[_native.MLP_FP32], errs[_native.MLP_F16X3]
+    assert e32.max() < 1e-5 and ex3.max() < 1e-5
+    assert ex3.max() <= 4 * e32.max() + 1e-7, (ex3.max(), e32.max())
+    assert ex3.mean() <= 4 * e32.mean() + 1e-8, (ex3.mean(), e32.mean())
