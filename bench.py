@@ -126,10 +126,11 @@ class Segment:
         self.learn_side()
 
 
-def e2e_iterations(seg, iters, k_epochs=6):
+def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
     """Whole PPO2 iterations: rollout + advantages + K full-batch epochs of the clipped-surrogate /
     MSE update (torch autograd + Adam on this GPU; the DPPO2 CartPole drivers' k_epo = 6,
     demonstration/DPPO2/DPPO2-4-CartPole/train.py:161). Returns env-steps/s of this rank."""
+    from reinforcementlearningplatform_amd.algorithm.policy_base.native_ppo2 import NativePPO2Learner
     from reinforcementlearningplatform_amd.algorithm.policy_base.vec_ppo2 import (DEFAULT_PPO_MSG,
                                                                                    PPO2Learner)
     from reinforcementlearningplatform_amd.utils.classes import PPOActor_Gaussian, PPOCritic
@@ -141,7 +142,8 @@ def e2e_iterations(seg, iters, k_epochs=6):
             for p in m.parameters():
                 p.copy_(flat[off:off + p.numel()].view_as(p).cpu())
                 off += p.numel()
-    learner = PPO2Learner(actor, critic, dict(DEFAULT_PPO_MSG, K_epochs=k_epochs), device="cuda")
+    cls = NativePPO2Learner if learner == "native" else PPO2Learner
+    learner = cls(actor, critic, dict(DEFAULT_PPO_MSG, K_epochs=k_epochs), device="cuda")
     b = seg.bufs
 
     def one():
@@ -210,6 +212,8 @@ def main():
     ap.add_argument("--e2e", type=int, default=2, help="PPO2 iterations incl. the K-epoch update to time (0: skip)")
     ap.add_argument("--uav", type=int, default=1, help="also time the UavRobust rollout (32768 envs/GPU)")
     ap.add_argument("--fp32-leg", type=int, default=1, help="also time the exact-f32 MLP path")
+    ap.add_argument("--learner", default="native", choices=["native", "torch"],
+                    help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="rollout hidden-layer arithmetic (include/rlp.h rlp_set_mlp_precision)")
     args = ap.parse_args()
@@ -324,10 +328,12 @@ def main():
                                    "config": "UavRobust hover outer loop (6-DoF + FNTSMC), PPO2 [6,256,256,3]"}
         del useg
     if args.e2e:
-        v, it_s = e2e_iterations(seg, args.e2e)
+        v, it_s = e2e_iterations(seg, args.e2e, learner=args.learner)
         v_all = v * world
         out["e2e"] = {"value": v_all, "unit": "env-steps/s", "s_per_iteration": it_s,
-                      "update": "K=6 full-batch epochs (torch autograd+Adam, fp32) per iteration",
+                      "update": ("K=6 full-batch epochs per iteration, " +
+                                 ("librlp rlp_ppo2_grad + rlp_adam_step" if args.learner == "native"
+                                  else "torch autograd + Adam (fp32)")),
                       "note": "rollout + GAE + PPO update; `value` above is the rollout hot path"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.env, args.cpu_seconds)

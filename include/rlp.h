@@ -305,10 +305,51 @@ int rlp_gae(const float *reward, const float *value, const float *value_next, co
 int rlp_adv_normalize(float *adv, int64_t count, const double *adv_stats, rlp_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
+/* PPO2 update (Proximal_Policy_Optimization2.learn, algorithm/policy_base/
+ * Proximal_Policy_Optimization2.py:102-163) for the drivers' [S -> 256 -> 256 -> A] tanh nets
+ * (PPOActor_Gaussian / PPOCritic, demonstration/PPO2/PPO2-4-CartPole/train.py:39-125).
+ * rlp_ppo2_grad writes the gradient of ONE optimiser step's loss over `rows` samples, in the
+ * flat torch parameter order (W1, b1, W2, b2, W3, b3 = rlp_mlp_forward's layout):
+ *   RLP_LOSS_ACTOR:  mean(-min(r*adv, clamp(r, 1-eps, 1+eps)*adv) - entropy_coef * entropy),
+ *                    r = exp(sum_a logN(a; mu(s), std) - sum_a a_logprob)  (:141-148; std is a
+ *                    constant, so the entropy term has no parameter gradient)
+ *   RLP_LOSS_CRITIC: mean((v_target - V(s))^2)  (:155-156)
+ * `index` (nullable) gathers the rows of a mini-batch (:110-111 BatchSampler); `loss_sum` (+=)
+ * receives the summed per-row loss (divide by rows for the reported loss). `packed` is
+ * rlp_mfma_pack(params). The hidden-layer GEMMs use the f16x3 split (RLP_MLP_F16X3 accuracy),
+ * the weight-gradient GEMMs exact f32 MFMA. `workspace` holds rlp_ppo2_workspace_floats(). */
+#define RLP_LOSS_ACTOR 0
+#define RLP_LOSS_CRITIC 1
+typedef struct rlp_ppo2_loss_cfg {
+    int32_t kind;            /* RLP_LOSS_ACTOR | RLP_LOSS_CRITIC */
+    float eps_clip;          /* ppo_msg['eps_clip'] */
+    float entropy_coef;      /* ppo_msg['entropy_coef'] */
+    float std[4];            /* actor.std per action dim */
+    float a_min[4], a_max[4];/* actor.a_min / a_max (mean = tanh(.) * gain + off) */
+} rlp_ppo2_loss_cfg;
+int64_t rlp_ppo2_workspace_floats(const rlp_mlp_desc *desc, int64_t rows);
+int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_loss_cfg *cfg,
+                  const float *s, const float *a, const float *a_logprob, const float *adv,
+                  const float *v_target, const int64_t *index, int64_t rows, float *grad,
+                  double *loss_sum, float *workspace, rlp_stream_t stream);
+/* out[0] += sum(grad^2) (torch.nn.utils.clip_grad_norm_'s total norm, squared). */
+int rlp_grad_sqnorm(const float *grad, int64_t n, double *out, rlp_stream_t stream);
+/* torch.optim.Adam step (exp_avg.lerp_, exp_avg_sq.mul_.addcmul_, bias corrections, addcdiv).
+ * With clip_sqnorm != NULL the gradient is first scaled by min(1, max_norm / (sqrt(*clip_sqnorm)
+ * + 1e-6)) (clip_grad_norm_, :150-151), evaluated on the device. */
+typedef struct rlp_adam_cfg {
+    float lr, beta1, beta2, eps, max_norm;
+    int32_t step;            /* 1-based step count after this update (bias corrections) */
+} rlp_adam_cfg;
+int rlp_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                  const rlp_adam_cfg *cfg, const double *clip_sqnorm, rlp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------ */
 const char *rlp_last_error_string(void);
 int rlp_abi_version(void);
 /* sizeof of the ABI structs as compiled into the library (0 cartpole, 1 angleonly, 2 soi, 3 ugv,
- * 4 uav, 5 mlp_desc, 6 rollout_cfg, 7 rollout_bufs): FFI bindings verify their mirrors with it. */
+ * 4 uav, 5 mlp_desc, 6 rollout_cfg, 7 rollout_bufs, 8 ppo2_loss_cfg, 9 adam_cfg): FFI bindings
+ * verify their mirrors with it. */
 int64_t rlp_struct_size(int which);
 /* Tuning knob of rlp_rollout: 16-env sub-blocks per wave (2 or 4; default 2). */
 int rlp_set_rollout_sub(int sub);

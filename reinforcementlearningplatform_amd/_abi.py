@@ -123,6 +123,19 @@ class RolloutBufs(C.Structure):
         "flag")]
 
 
+RLP_LOSS_ACTOR, RLP_LOSS_CRITIC = 0, 1
+
+
+class PPO2LossCfg(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("eps_clip", C.c_float), ("entropy_coef", C.c_float),
+                ("std", C.c_float * 4), ("a_min", C.c_float * 4), ("a_max", C.c_float * 4)]
+
+
+class AdamCfg(C.Structure):
+    _fields_ = [("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
+                ("max_norm", C.c_float), ("step", C.c_int32)]
+
+
 PARAM_TYPES = {
     RLP_ENV_CARTPOLE: CartPoleParams,
     RLP_ENV_CARTPOLE_ANGLEONLY: AngleOnlyParams,
@@ -297,7 +310,8 @@ def check_struct_sizes():
     return {"cartpole": C.sizeof(CartPoleParams), "angleonly": C.sizeof(AngleOnlyParams),
             "soi": C.sizeof(SOIParams), "ugv": C.sizeof(UGVParams),
             "uav": C.sizeof(UAVHoverParams), "mlp_desc": C.sizeof(MLPDesc),
-            "rollout_cfg": C.sizeof(RolloutCfg), "rollout_bufs": C.sizeof(RolloutBufs)}
+            "rollout_cfg": C.sizeof(RolloutCfg), "rollout_bufs": C.sizeof(RolloutBufs),
+            "ppo2_loss_cfg": C.sizeof(PPO2LossCfg), "adam_cfg": C.sizeof(AdamCfg)}
 
 
 _ = math  # keep import for callers doing deg arithmetic

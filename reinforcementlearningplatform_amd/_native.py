@@ -47,6 +47,10 @@ def _declare(lib):
         "rlp_reward_norm": (i32, [vp, i32, i32, vp, vp, vp, vp]),
         "rlp_gae": (i32, [vp, vp, vp, vp, vp, dbl, dbl, i32, i32, vp, vp, vp, vp]),
         "rlp_adv_normalize": (i32, [vp, i64, vp, vp]),
+        "rlp_ppo2_workspace_floats": (i64, [vp, i64]),
+        "rlp_ppo2_grad": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp]),
+        "rlp_grad_sqnorm": (i32, [vp, i64, vp, vp]),
+        "rlp_adam_step": (i32, [vp, vp, vp, vp, i64, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

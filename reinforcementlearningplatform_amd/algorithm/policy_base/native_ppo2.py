@@ -1,0 +1,161 @@
+"""NativePPO2Learner — the K-epoch PPO2 update (Proximal_Policy_Optimization2.learn,
+algorithm/policy_base/Proximal_Policy_Optimization2.py:102-174) on librlp's HIP kernels.
+
+Per optimiser step and net: rlp_mfma_pack (packed weights), rlp_ppo2_grad (forward + loss
+gradient + backward + weight gradients on MFMA, include/rlp.h), optional RCCL all-reduce of the
+actor+critic gradients (one flat buffer, as PPO2Learner), rlp_grad_sqnorm + rlp_adam_step
+(clip_grad_norm_ and torch.optim.Adam, evaluated on the device). Same interface and semantics as
+PPO2Learner (vec_ppo2.py), which stays as the torch-autograd reference the parity tests compare
+against.
+
+The modules' parameters become views of the learner's flat fp32 buffers, so `actor.state_dict()`
+(save_ac), GPUNet.refresh and evaluation see every update without a copy.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ... import _abi
+from ... import kernels as K
+
+
+class _Net:
+    def __init__(self, module, is_actor, device):
+        lin = [m for m in module.modules() if isinstance(m, nn.Linear)]
+        dims = [lin[0].in_features] + [l.out_features for l in lin] if lin else []
+        if len(lin) != 3 or dims[1] != 256 or dims[2] != 256 or dims[0] > 8 or dims[3] > 4:
+            raise ValueError(f"NativePPO2Learner: needs a [S<=8 -> 256 -> 256 -> A<=4] Linear/Tanh "
+                             f"stack (got {dims})")
+        acts = [_abi.RLP_ACT_TANH, _abi.RLP_ACT_TANH,
+                _abi.RLP_ACT_TANH if is_actor else _abi.RLP_ACT_NONE]
+        self.desc = _abi.MLPDesc.make(dims, acts)
+        params = [p for l in lin for p in (l.weight, l.bias)]
+        self.flat = torch.cat([p.detach().reshape(-1).to(device, torch.float32)
+                               for p in params]).contiguous()
+        off = 0
+        for p in params:  # the module's parameters are views of the flat buffer from now on
+            p.data = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.grad = torch.zeros_like(self.flat)
+        self.exp_avg = torch.zeros_like(self.flat)
+        self.exp_avg_sq = torch.zeros_like(self.flat)
+        self.packed = K.mfma_pack(self.desc, self.flat)
+        self.sqnorm = torch.zeros(1, dtype=torch.float64, device=device)
+        self.step = 0
+
+
+class NativePPO2Learner:
+    """PPO2Learner on librlp's kernels; synchronous data parallelism under torch.distributed."""
+
+    def __init__(self, actor, critic, msg, process_group=None, device=None):
+        self.msg = msg
+        self.device = torch.device(device) if device is not None else next(actor.parameters()).device
+        self.actor, self.critic = actor.to(self.device), critic.to(self.device)
+        for name in ("a_min", "a_max", "off", "gain", "std"):
+            v = getattr(self.actor, name, None)
+            if torch.is_tensor(v):
+                setattr(self.actor, name, v.to(self.device))
+        self.net_a = _Net(self.actor, True, self.device)
+        self.net_c = _Net(self.critic, False, self.device)
+        self.pg = process_group
+        self.distributed = process_group is not None or (
+            torch.distributed.is_available() and torch.distributed.is_initialized()
+            and torch.distributed.get_world_size() > 1)
+        self.world = torch.distributed.get_world_size(process_group) if self.distributed else 1
+        if self.distributed:
+            self.broadcast_params()
+        self.lr = {"a": msg['a_lr'], "c": msg['c_lr']}
+        self.eps = 1e-5 if msg['set_adam_eps'] else 1e-8
+        self.loss = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self.ws = None
+        self.total_steps = 0
+
+    # same accessors as PPO2Learner
+    def params(self):
+        return list(self.actor.parameters()) + list(self.critic.parameters())
+
+    def broadcast_params(self):
+        src = 0 if self.pg is None else torch.distributed.get_global_rank(self.pg, 0)
+        flat = torch.cat([self.net_a.flat, self.net_c.flat])
+        torch.distributed.broadcast(flat, src=src, group=self.pg)
+        na = self.net_a.flat.numel()
+        self.net_a.flat.copy_(flat[:na])
+        self.net_c.flat.copy_(flat[na:])
+
+    def _actor_cfg(self):
+        A = self.net_a.desc.dims[3]
+        std = np.broadcast_to(torch.as_tensor(self.actor.std, dtype=torch.float32).reshape(-1)
+                              .cpu().numpy(), (A,))
+        lo = torch.as_tensor(self.actor.a_min, dtype=torch.float32).reshape(-1).cpu().numpy()
+        hi = torch.as_tensor(self.actor.a_max, dtype=torch.float32).reshape(-1).cpu().numpy()
+        lo, hi = np.broadcast_to(lo, (A,)), np.broadcast_to(hi, (A,))
+        return K.ppo2_loss_cfg(_abi.RLP_LOSS_ACTOR, self.msg['eps_clip'], self.msg['entropy_coef'],
+                               std, lo, hi)
+
+    def _workspace(self, rows):
+        need = max(K.lib().rlp_ppo2_workspace_floats(__import__("ctypes").byref(n.desc), rows)
+                   for n in (self.net_a, self.net_c))
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(int(need), dtype=torch.float32, device=self.device)
+        return self.ws
+
+    def grads(self, s, a, a_lp, adv, vt, index=None):
+        """Gradients of one step's actor and critic losses into net.grad (no optimiser step)."""
+        rows = int(index.shape[0]) if index is not None else int(s.shape[0])
+        ws = self._workspace(rows)
+        self.loss.zero_()
+        adv, vt = adv.reshape(-1), vt.reshape(-1)
+        na, nc = self.net_a, self.net_c
+        K.mfma_pack(na.desc, na.flat, out=na.packed)
+        K.ppo2_grad(na.desc, na.packed, self._actor_cfg(), s, a=a, a_logprob=a_lp, adv=adv,
+                    index=index, grad=na.grad, loss_sum=self.loss[0:1], workspace=ws)
+        K.mfma_pack(nc.desc, nc.flat, out=nc.packed)
+        K.ppo2_grad(nc.desc, nc.packed, K.ppo2_loss_cfg(_abi.RLP_LOSS_CRITIC), s, v_target=vt,
+                    index=index, grad=nc.grad, loss_sum=self.loss[1:2], workspace=ws)
+        return rows
+
+    def _allreduce_grads(self):
+        flat = torch.cat([self.net_a.grad, self.net_c.grad])
+        torch.distributed.all_reduce(flat, group=self.pg)
+        flat /= self.world
+        na = self.net_a.grad.numel()
+        self.net_a.grad.copy_(flat[:na])
+        self.net_c.grad.copy_(flat[na:])
+
+    def step(self, s, a, a_lp, adv, vt, index=None):
+        rows = self.grads(s, a, a_lp, adv, vt, index)
+        if self.distributed:
+            self._allreduce_grads()
+        clip = self.msg['use_grad_clip']
+        for net, lr in ((self.net_a, self.lr["a"]), (self.net_c, self.lr["c"])):
+            sq = None
+            if clip:  # clip_grad_norm_(params, 0.5), :150-151 / :158-159
+                net.sqnorm.zero_()
+                K.grad_sqnorm(net.grad, net.sqnorm)
+                sq = net.sqnorm
+            net.step += 1
+            K.adam_step(net.flat, net.grad, net.exp_avg, net.exp_avg_sq, lr, net.step, eps=self.eps,
+                        clip_sqnorm=sq, max_norm=0.5)
+        return self.loss[0] / rows, self.loss[1] / rows
+
+    def update(self, s, a, a_lp, adv, vt, generator=None):
+        m = self.msg
+        N = s.shape[0]
+        losses = None
+        s, a, a_lp = s.contiguous(), a.contiguous(), a_lp.contiguous()
+        adv, vt = adv.reshape(-1).contiguous(), vt.reshape(-1).contiguous()
+        for _ in range(m['K_epochs']):
+            if m['using_mini_batch']:
+                perm = torch.randperm(N, device=s.device, generator=generator)
+                mb = m['mini_batch_size']
+                for i in range(0, N, mb):  # BatchSampler(..., drop_last=False)
+                    losses = self.step(s, a, a_lp, adv, vt, index=perm[i:i + mb].contiguous())
+            else:
+                losses = self.step(s, a, a_lp, adv, vt)
+        return losses
+
+    def lr_decay(self, total_steps):
+        if not self.msg['use_lr_decay']:
+            return
+        frac = max(1 - total_steps / self.msg['max_train_steps'], 0)
+        self.lr = {"a": max(self.msg['a_lr'] * frac, 1e-6), "c": max(self.msg['c_lr'] * frac, 1e-6)}

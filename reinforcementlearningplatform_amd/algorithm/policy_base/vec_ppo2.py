@@ -108,7 +108,7 @@ class PPO2Learner:
             if m['using_mini_batch']:
                 perm = torch.randperm(N, device=s.device, generator=generator)
                 mb = m['mini_batch_size']
-                for i in range(0, max(N - mb + 1, 1), mb):
+                for i in range(0, N, mb):  # BatchSampler(..., drop_last=False)
                     idx = perm[i:i + mb]
                     losses = self.step(s[idx], a[idx], a_lp[idx], adv[idx], vt[idx])
             else:

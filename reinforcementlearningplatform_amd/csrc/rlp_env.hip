@@ -145,6 +145,8 @@ int64_t rlp_struct_size(int which) {
     case 5: return sizeof(rlp_mlp_desc);
     case 6: return sizeof(rlp_rollout_cfg);
     case 7: return sizeof(rlp_rollout_bufs);
+    case 8: return sizeof(rlp_ppo2_loss_cfg);
+    case 9: return sizeof(rlp_adam_cfg);
     }
     return -1;
 }

@@ -19,6 +19,7 @@
 //   B1c [H], B2c [H], W3c [A][H], b3 [4], info [4] = {2^sw, 2^(sw+SH), 2^-(sw+SH), 0}
 //   X3  (256-B aligned)       W2 * 2^sw split into f16 hi + lo, the f16x3 path's chunks
 //                             (rlp_mfma_x3.hpp)
+//   X3T                       the same for W2^T (the PPO2 update's backward GEMM, rlp_update.hip)
 #pragma once
 #include "rlp_common.hpp"
 
@@ -33,6 +34,7 @@ struct MfmaNet {
     int off_w1, off_b1, off_b2, off_w3, off_b3, off_info;  // offsets of the LDS-resident part
     int small_count;                                         // floats from off_w1 to info's end
     int off_x3;                                              // f16 hi/lo W2 chunks (H*H floats)
+    int off_x3t;                                             // the same for W2^T
     int64_t count;
 };
 
@@ -54,7 +56,8 @@ inline bool mfma_net_from_desc(const rlp_mlp_desc &d, MfmaNet *net) {
     net->off_info = net->off_b3 + 4;
     net->small_count = net->off_info + 4 - net->off_w1;
     net->off_x3 = (net->off_info + 4 + 63) / 64 * 64;
-    net->count = net->off_x3 + (int64_t)H * H;
+    net->off_x3t = net->off_x3 + H * H;
+    net->count = net->off_x3t + (int64_t)H * H;
     return true;
 }
 

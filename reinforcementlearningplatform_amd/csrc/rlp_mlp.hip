@@ -140,8 +140,9 @@ __global__ void mfma_pack_kernel(MfmaNet net, const float *__restrict__ P, float
             v = a < A ? b3[a] : 0.f;
         } else if (idx < net.off_x3) {  // info (mfma_scale_kernel) + alignment pad
             continue;
-        } else {  // X3 [P][j][part][lane][8 halfs]: two halfs per float slot
-            const int q = idx - net.off_x3;
+        } else {  // X3 / X3T [P][j][part][lane][8 halfs]: two halfs per float slot
+            const bool tr = idx >= net.off_x3t;
+            const int q = idx - (tr ? net.off_x3t : net.off_x3);
             const int i = 2 * (q & 3), lane = (q >> 2) & 63, part = (q >> 8) & 1;
             const int j = (q >> 9) % NT, Pp = (q >> 9) / NT;
             const int row = 16 * j + (lane & 15), g = lane >> 4;
@@ -150,7 +151,7 @@ __global__ void mfma_pack_kernel(MfmaNet net, const float *__restrict__ P, float
             for (int u = 0; u < 2; ++u) {
                 const int ii = i + u;
                 const int k = 32 * Pp + (ii < 4 ? 4 * g + ii : 16 + 4 * g + ii - 4);
-                const float w = W2[row * H + k] * sw;
+                const float w = (tr ? W2[k * H + row] : W2[row * H + k]) * sw;
                 const _Float16 hi = (_Float16)w;
                 h2[u] = part == 0 ? hi : (_Float16)(w - (float)hi);
             }

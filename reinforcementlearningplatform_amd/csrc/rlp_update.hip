@@ -1,0 +1,657 @@
+// rlp_update.hip — gradients of one PPO2 optimiser step on MFMA (Proximal_Policy_Optimization2.learn,
+// algorithm/policy_base/Proximal_Policy_Optimization2.py:102-163) for the drivers'
+// [S -> 256 -> 256 -> A] tanh actor (PPOActor_Gaussian, demonstration/PPO2/PPO2-4-CartPole/
+// train.py:39-88) and critic (PPOCritic, :91-125), plus clip_grad_norm_ and torch.optim.Adam.
+//
+// Two kernels per net and step:
+//   ppo2_fd_kernel    per 64-row tile (4 waves x 16 rows, env-on-lane like the rollout): forward
+//                     z2 = W2 h1 (f16x3 through the block's W2 chunk ring), h2, z3, the loss's
+//                     gradient g3 = dL/dz3 per row, dW3/db3 partials (registers), g2 = W3^T g3 *
+//                     (1 - h2^2), backward dh1 = W2^T g2 (f16x3 over the W2^T chunks, per-row
+//                     power-of-two scaling of g2), g1 = dh1 * (1 - h1^2); G2, G1 -> HBM in a
+//                     [tile][neuron][64 rows] layout (rows contiguous: the reduction operand of
+//                     the next kernel).
+//   ppo2_wgrad_kernel dW2 = sum_r g2 h1^T (exact f32 MFMA, h1 recomputed bit-identically from s),
+//                     dW1 | db1 = sum_r g1 [s | 1]^T, db2 = sum_r g2; per-block partials.
+// A deterministic reduce assembles the flat gradient (torch parameter order).
+#include "rlp_mfma_x3.hpp"
+
+namespace rlp {
+
+constexpr int kUpdRows = 64;          // rows per block tile (4 waves x 16)
+constexpr int kUpdH = 256;
+constexpr int kUpdTileFloats = kUpdH * kUpdRows;
+
+struct Ppo2Args {
+    const float *packed;
+    MfmaNet net;
+    const float *s, *a, *lp, *adv, *vt;
+    const int64_t *index;
+    int64_t rows;
+    float inv_rows, eps_clip, ent_row;  // ent_row = entropy_coef * sum_a entropy_a (constant)
+    float std_[4], gain[4], off[4];
+    float *g2t, *g1t;   // [tiles][256][64]
+    float *part3;       // [grid * 4][A * 256 + A]: per-wave dW3 | db3 partials
+    double *loss_sum;
+};
+
+// wave-level 256x256 GEMM of 16 rows through the block's chunk ring (all 4 waves call it in step):
+// acc[j] += A-chunks(Xw) x B(P), B(P) = bop(P) as f16 hi/lo (rlp_mfma_x3.hpp layout)
+template <class BOp>
+__device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, float *my_part,
+                                          floatx4 (&acc)[16], BOp &&bop) {
+    constexpr int NC = 16;
+    const int lane = threadIdx.x & 63;
+    auto issue = [&](int c) {
+        float *slot = my_part + (c % kX3Ring) * kX3ChunkFloats;
+        const gptr<float> src = Xw + c * kX3ChunkFloats;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
+    };
+    block_barrier_raw();  // every wave is done reading the ring
+    issue(0);
+    issue(1);
+#pragma unroll 1
+    for (int P = 0; P < 8; ++P) {
+        half8 bh, bl;
+        bop(P, bh, bl);
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            const int c = 2 * P + hf;
+            if (c + 1 < NC) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            block_barrier_raw();
+            if (c + 2 < NC) issue(c + 2);
+            const float *slot = ring + (c % kX3Ring) * kX3ChunkFloats + lane * 4;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const half8 ah = *reinterpret_cast<const half8 *>(slot + (2 * jj) * 256);
+                const half8 al = *reinterpret_cast<const half8 *>(slot + (2 * jj + 1) * 256);
+                floatx4 v = acc[8 * hf + jj];
+                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, v, 0, 0, 0);
+                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, v, 0, 0, 0);
+                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, v, 0, 0, 0);
+                acc[8 * hf + jj] = v;
+            }
+        }
+    }
+}
+
+// wave-scope LDS fence + barrier (the staging buffer is private to the wave)
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void split8(const float (&x)[8], half8 &bh, half8 &bl) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const _Float16 hi = (_Float16)x[i];
+        bh[i] = hi;
+        bl[i] = (_Float16)(x[i] - (float)hi);
+    }
+}
+
+template <int KS1, int A, int LOSS>
+__global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
+    constexpr int H = kUpdH, SMALL = mlp_small_floats<H, KS1, A>();
+    constexpr int STG = 20;  // staging row pitch: conflict-free b32 writes, 16-B aligned b128 reads
+    __shared__ __attribute__((aligned(16))) float lds[SMALL + kX3RingFloats + 4 * H * STG + 4 * 16 * 4];
+    float *small = lds, *ring = lds + SMALL;
+    float *const stg = lds + SMALL + kX3RingFloats + (threadIdx.x >> 6) * H * STG;
+    float *const g3s = lds + SMALL + kX3RingFloats + 4 * H * STG + (threadIdx.x >> 6) * 64;  // [16][4]
+    const MfmaNet &net = g.net;
+    mlp_small_to_lds(g.packed, net, small);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, gq = lane >> 4, e = lane & 15;
+    const int S = net.S;
+    const float *info = small + (net.off_info - net.off_w1);
+    const float sw = info[0], acc_scale = info[1];
+    const float k_out = 2.8853900817779268f * info[2];
+    float *const my_part = ring + wv * 4 * 256;
+    // this wave's [256 neurons][16 rows] tile (staged in LDS) -> G[tile][n][64 rows] columns
+    // 16 wv .. 16 wv + 15, as 16 coalesced float4 stores per lane
+    auto store_tile = [&](float *Gt) {
+        wave_sync_lds();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int f = i * 64 + lane, n = f >> 2, c = f & 3;
+            const floatx4 v = *reinterpret_cast<const floatx4 *>(stg + n * STG + 4 * c);
+            *reinterpret_cast<floatx4 *>(Gt + n * kUpdRows + 16 * wv + 4 * c) = v;
+        }
+        wave_sync_lds();
+    };
+
+    float dW3p[A][4];  // neurons 64 c + lane
+    float db3p[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        db3p[a] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dW3p[a][c] = 0.f;
+    }
+    double lsum = 0.0;
+
+    const int64_t ntiles = (g.rows + kUpdRows - 1) / kUpdRows;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        // opaque per iteration: keeps the 2 x 64 chunk addresses from being hoisted (and spilled)
+        const float *Pg = g.packed;
+        asm volatile("" : "+s"(Pg));
+        const gptr<float> Xf = as_global(Pg) + net.off_x3 + wv * 4 * 256 + lane * 4;
+        const gptr<float> Xb = as_global(Pg) + net.off_x3t + wv * 4 * 256 + lane * 4;
+        float *g2base = g.g2t, *g1base = g.g1t;
+        asm volatile("" : "+s"(g2base), "+s"(g1base));
+        // the small weights are re-read from LDS per use, not hoisted into ~300 registers
+        const float *sm = small;
+        asm volatile("" : "+s"(sm));
+        const float *W1c = sm;
+        const float *B1c = sm + (net.off_b1 - net.off_w1);
+        const float *B2c = sm + (net.off_b2 - net.off_w1);
+        const float *W3c = sm + (net.off_w3 - net.off_w1);
+        const float *b3c = sm + (net.off_b3 - net.off_w1);
+        const int64_t r = tile * kUpdRows + 16 * wv + e;
+        const bool valid = r < g.rows;
+        const int64_t src = valid ? (g.index ? g.index[r] : r) : 0;
+        float bobs[KS1];
+#pragma unroll
+        for (int kk = 0; kk < KS1; ++kk) {
+            const int k = 4 * kk + gq;
+            bobs[kk] = (valid && k < S) ? g.s[src * S + k] : 0.f;
+        }
+        auto layer1 = [&](int t) {
+            float w1[KS1];
+#pragma unroll
+            for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[(16 * t + e) * (4 * KS1) + 4 * kk + gq];
+            floatx4 c = *reinterpret_cast<const floatx4 *>(B1c + 16 * t + 4 * gq);
+#pragma unroll
+            for (int kk = 0; kk < KS1; ++kk)
+                c = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[kk], bobs[kk], c, 0, 0, 0);
+            return c;
+        };
+
+        // ---- forward: z2 (scaled by 2^(sw+SH)) = W2 h1 + b2
+        floatx4 acc[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            floatx4 b2 = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * gq);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b2[q] *= acc_scale;
+            acc[j] = b2;
+        }
+        x3_gemm16(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
+            const floatx4 p0 = layer1(2 * P), p1 = layer1(2 * P + 1);
+            float x[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float pre = i < 4 ? p0[i] : p1[i - 4];
+                const float ex = __builtin_amdgcn_exp2f(pre * 2.8853900817779268f);
+                x[i] = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + ex), kX3HScale);
+            }
+            split8(x, bh, bl);
+        });
+        // ---- h2 = tanh(z2), z3 = W3 h2 + b3 (every lane group ends with its row's z3)
+        float z3[A];
+#pragma unroll
+        for (int a = 0; a < A; ++a) z3[a] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float ex = __builtin_amdgcn_exp2f(acc[j][q] * k_out);
+                const float h = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + ex), 1.0f);
+                acc[j][q] = h;
+#pragma unroll
+                for (int a = 0; a < A; ++a)
+                    z3[a] = __builtin_fmaf(W3c[a * H + 16 * j + 4 * gq + q], h, z3[a]);
+            }
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            z3[a] += __shfl_xor(z3[a], 16);
+            z3[a] += __shfl_xor(z3[a], 32);
+            z3[a] += b3c[a];
+        }
+        // ---- head gradient g3 = dL/dz3 of this row (mean over rows folded in)
+        float g3[A];
+        float lrow = 0.f;
+        if constexpr (LOSS == RLP_LOSS_ACTOR) {
+            float t[A], d[A], lp_now = 0.f, lp_old = 0.f;
+            float adv = valid ? g.adv[src] : 0.f;
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                t[a] = tanhf(z3[a]);
+                const float mean = t[a] * g.gain[a] + g.off[a];
+                const float act = valid ? g.a[src * A + a] : mean;
+                d[a] = act - mean;
+                lp_now += normal_logp(act, mean, g.std_[a]);
+                lp_old += valid ? g.lp[src * A + a] : 0.f;
+            }
+            const float ratio = expf(lp_now - lp_old);
+            const float lo = 1.f - g.eps_clip, hi = 1.f + g.eps_clip;
+            const float s1 = ratio * adv;
+            const float rc = fminf(fmaxf(ratio, lo), hi);
+            const float s2 = rc * adv;
+            // torch.min backward: the smaller operand takes the gradient, a tie splits it
+            const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+            const float w2 = s2 < s1 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+            const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;  // clamp backward
+            const float dl_dratio = -adv * (w1 + w2 * inr);
+            const float dl_dlp = dl_dratio * ratio * g.inv_rows;
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                const float var = g.std_[a] * g.std_[a];
+                g3[a] = valid ? dl_dlp * (d[a] / var) * g.gain[a] * (1.f - t[a] * t[a]) : 0.f;
+            }
+            lrow = valid ? -fminf(s1, s2) - g.ent_row : 0.f;
+        } else {
+            const float v = z3[0];
+            const float diff = valid ? v - g.vt[src] : 0.f;
+            g3[0] = 2.f * diff * g.inv_rows;
+            lrow = diff * diff;
+        }
+        if (gq == 0) {
+            lsum += (double)lrow;
+#pragma unroll
+            for (int a = 0; a < A; ++a) db3p[a] += g3[a];
+        }
+        // ---- dW3 = sum_rows g3 h2^T through the staging tile (transpose: lane owns neurons
+        // 64 c + lane and sums over the wave's 16 rows); g2 = (W3^T g3) * (1 - h2^2) in place
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) stg[(16 * j + 4 * gq + q) * STG + e] = acc[j][q];
+        if (gq == 0) {
+#pragma unroll
+            for (int a = 0; a < A; ++a) g3s[e * 4 + a] = g3[a];
+        }
+        wave_sync_lds();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float *hrow = stg + (64 * c + lane) * STG;
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const floatx4 h = *reinterpret_cast<const floatx4 *>(hrow + 4 * q4);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const floatx4 gr = *reinterpret_cast<const floatx4 *>(g3s + (4 * q4 + u) * 4);
+#pragma unroll
+                    for (int a = 0; a < A; ++a) dW3p[a][c] = __builtin_fmaf(gr[a], h[u], dW3p[a][c]);
+                }
+            }
+        }
+        wave_sync_lds();
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float h = acc[j][q];
+                float dh = 0.f;
+#pragma unroll
+                for (int a = 0; a < A; ++a)
+                    dh = __builtin_fmaf(W3c[a * H + 16 * j + 4 * gq + q], g3[a], dh);
+                acc[j][q] = dh * (1.f - h * h);
+            }
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) stg[(16 * j + 4 * gq + q) * STG + e] = acc[j][q];
+        store_tile(g2base + tile * kUpdTileFloats);
+
+        // ---- backward: dh1 = W2^T g2, with g2 scaled per row into f16 range
+        float m = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) m = fmaxf(m, fabsf(acc[j][q]));
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        const int ex = m > 0.f ? __builtin_amdgcn_frexp_expf(m) : 0;  // m in [2^(ex-1), 2^ex)
+        const float sc = __builtin_amdgcn_ldexpf(1.f, 14 - ex);
+        const float unscale = __builtin_amdgcn_ldexpf(1.f, ex - 14) / sw;  // exact powers of two
+        floatx4 dh1[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) dh1[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // B operands from the staged g2 tile (still in stg after store_tile): row e, neurons
+        // 32P + 4gq + i and 32P + 16 + 4gq + i
+        x3_gemm16(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
+            float x[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                x[i] = stg[(32 * P + 4 * gq + i) * STG + e] * sc;
+                x[i + 4] = stg[(32 * P + 16 + 4 * gq + i) * STG + e] * sc;
+            }
+            split8(x, bh, bl);
+        });
+        wave_sync_lds();  // stg is rewritten with g1 below
+        // ---- g1 = dh1 * (1 - h1^2), h1 recomputed (bit-identical to the forward's)
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const floatx4 pre = layer1(t);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float h1 = tanh_fast(pre[q]);
+                stg[(16 * t + 4 * gq + q) * STG + e] = dh1[t][q] * unscale * (1.f - h1 * h1);
+            }
+        }
+        store_tile(g1base + tile * kUpdTileFloats);
+    }
+
+    // ---- per-wave partials: dW3 (lane's neurons) | db3 summed over the 16 row lanes; loss
+    float *out = g.part3 + (size_t)(blockIdx.x * 4 + wv) * (A * H + A);
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) out[a * H + 64 * c + lane] = dW3p[a][c];
+        float b = db3p[a];
+        b += __shfl_xor(b, 1);
+        b += __shfl_xor(b, 2);
+        b += __shfl_xor(b, 4);
+        b += __shfl_xor(b, 8);
+        if (lane == 0) out[A * H + a] = b;
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) lsum += __shfl_xor(lsum, o);
+    if (lane == 0 && g.loss_sum) atomicAdd(g.loss_sum, lsum);
+}
+
+struct WArgs {
+    const float *packed;
+    MfmaNet net;
+    const float *s;
+    const int64_t *index;
+    int64_t rows;
+    const float *g2t, *g1t;
+    float *part;  // [grid][H*H + H*S + 2H]: dW2 | dW1 | db1 | db2
+};
+
+template <int KS1>
+__global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
+    constexpr int H = kUpdH, SP = 4 * KS1;
+    __shared__ float srow[kUpdRows][SP];
+    __shared__ float w1s[H][SP + 1];
+    __shared__ float b1s[H];
+    const MfmaNet &net = w.net;
+    const int S = net.S;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, gq = lane >> 4, e = lane & 15;
+    {
+        const float *W1c = w.packed + net.off_w1, *B1c = w.packed + net.off_b1;
+        for (int i = threadIdx.x; i < H * SP; i += blockDim.x) w1s[i / SP][i % SP] = W1c[i];
+        for (int i = threadIdx.x; i < H; i += blockDim.x) b1s[i] = B1c[i];
+    }
+    floatx4 acc2[4][16], acc1[4], accb[4];
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) {
+        acc1[jt] = accb[jt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int nt = 0; nt < 16; ++nt) acc2[jt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int64_t ntiles = (w.rows + kUpdRows - 1) / kUpdRows;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < kUpdRows * SP; i += blockDim.x) {
+            const int rr = i / SP, k = i % SP;
+            const int64_t r = tile * kUpdRows + rr;
+            float v = 0.f;
+            if (r < w.rows && k < S) v = w.s[(w.index ? w.index[r] : r) * S + k];
+            srow[rr][k] = v;
+        }
+        __syncthreads();
+        // A operands: G[tile][j][16 gq + q], j = 64 wv + 16 jt + e (MFMA step q <-> row 16 gq + q)
+        float a2[4][16];
+        const float *g2base = w.g2t, *g1base = w.g1t;
+        asm volatile("" : "+s"(g2base), "+s"(g1base));
+        const float *G2 = g2base + tile * kUpdTileFloats + 16 * gq;
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt) {
+            const gptr<float> src = as_global(G2 + (64 * wv + 16 * jt + e) * kUpdRows);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const floatx4 v = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 4 * q4);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) a2[jt][4 * q4 + u] = v[u];
+            }
+        }
+#pragma unroll
+        for (int nt = 0; nt < 16; ++nt) {
+            const int n = 16 * nt + e;
+            float w1[SP];
+#pragma unroll
+            for (int k = 0; k < SP; ++k) w1[k] = w1s[n][k];
+            const float b1 = b1s[n];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                // h1 of row 16 gq + q, neuron n: the k-ordered f32 fma chain of the forward's MFMA
+                float pre = b1;
+#pragma unroll
+                for (int k = 0; k < SP; ++k) pre = __builtin_fmaf(w1[k], srow[16 * gq + q][k], pre);
+                const float h1 = tanh_fast(pre);
+#pragma unroll
+                for (int jt = 0; jt < 4; ++jt)
+                    acc2[jt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[jt][q], h1, acc2[jt][nt], 0, 0, 0);
+            }
+        }
+        // [s | 1] operand: column e < S -> s, e == S -> 1 (db), else 0
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const float bs = e < S ? srow[16 * gq + q][e < SP ? e : 0] : (e == S ? 1.f : 0.f);
+#pragma unroll
+            for (int jt = 0; jt < 4; ++jt)
+                accb[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[jt][q], bs, accb[jt], 0, 0, 0);
+        }
+        const float *G1 = g1base + tile * kUpdTileFloats + 16 * gq;
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt) {
+            const gptr<float> src = as_global(G1 + (64 * wv + 16 * jt + e) * kUpdRows);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const floatx4 v = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 4 * q4);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) a2[jt][4 * q4 + u] = v[u];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const float bs = e < S ? srow[16 * gq + q][e < SP ? e : 0] : (e == S ? 1.f : 0.f);
+#pragma unroll
+            for (int jt = 0; jt < 4; ++jt)
+                acc1[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[jt][q], bs, acc1[jt], 0, 0, 0);
+        }
+    }
+    // C layout: lane holds rows m = 4 gq + q (j = 64 wv + 16 jt + m), column e
+    float *out = w.part + (size_t)blockIdx.x * (H * H + H * S + 2 * H);
+    float *dW1 = out + H * H, *db1 = dW1 + H * S, *db2 = db1 + H;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = 64 * wv + 16 * jt + 4 * gq + q;
+#pragma unroll
+            for (int nt = 0; nt < 16; ++nt) out[j * H + 16 * nt + e] = acc2[jt][nt][q];
+            if (e < S) dW1[j * S + e] = acc1[jt][q];
+            if (e == S) {
+                db1[j] = acc1[jt][q];
+                db2[j] = accb[jt][q];
+            }
+        }
+}
+
+// grad (torch order W1 b1 W2 b2 W3 b3) = sum over blocks of the partials, in block order
+__global__ void ppo2_reduce_kernel(MfmaNet net, const float *__restrict__ part, int nw,
+                                   const float *__restrict__ part3, int n3, float *grad) {
+    const int H = net.H, S = net.S, A = net.A;
+    const int64_t total = (int64_t)H * S + H + (int64_t)H * H + H + (int64_t)A * H + A;
+    const int pw = H * H + H * S + 2 * H, p3 = A * H + A;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float *src;
+        int stride, cnt;
+        int64_t off;
+        if (i < H * S) { src = part; off = H * H + i; stride = pw; cnt = nw; }                     // W1
+        else if (i < H * S + H) { src = part; off = H * H + H * S + (i - H * S); stride = pw; cnt = nw; }  // b1
+        else if (i < H * S + H + H * H) { src = part; off = i - (H * S + H); stride = pw; cnt = nw; }     // W2
+        else if (i < H * S + 2 * H + H * H) { src = part; off = H * H + H * S + H + (i - (H * S + H + H * H)); stride = pw; cnt = nw; }  // b2
+        else { src = part3; off = i - (H * S + 2 * H + H * H); stride = p3; cnt = n3; }              // W3, b3
+        float acc = 0.f;
+        for (int b = 0; b < cnt; ++b) acc += src[(size_t)b * stride + off];
+        grad[i] = acc;
+    }
+}
+
+__global__ void sqnorm_kernel(const float *__restrict__ g, int64_t n, double *out) {
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        acc += (double)g[i] * (double)g[i];
+    for (int o = 1; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
+    __shared__ double red[16];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+        atomicAdd(out, t);
+    }
+}
+
+__global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
+                            float *__restrict__ m, float *__restrict__ v, int64_t n,
+                            rlp_adam_cfg c, const double *clip_sqnorm) {
+    float scale = 1.f;
+    if (clip_sqnorm) {  // clip_grad_norm_: coef = max_norm / (norm + 1e-6), clamped to <= 1
+        const float norm = (float)sqrt(*clip_sqnorm);
+        scale = fminf(c.max_norm / (norm + 1e-6f), 1.f);
+    }
+    const float bc1 = 1.f - powf(c.beta1, (float)c.step);
+    const float bc2 = 1.f - powf(c.beta2, (float)c.step);
+    const float step_size = c.lr / bc1, bc2_sqrt = sqrtf(bc2);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float gi = clip_sqnorm ? g[i] * scale : g[i];
+        float mi = m[i];
+        mi = mi + (1.f - c.beta1) * (gi - mi);           // exp_avg.lerp_(grad, 1 - beta1)
+        const float vi = v[i] * c.beta2 + (1.f - c.beta2) * gi * gi;  // mul_(b2).addcmul_(g, g, 1-b2)
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + c.eps;
+        p[i] = p[i] + (-step_size) * (mi / denom);       // addcdiv_(exp_avg, denom, -step_size)
+    }
+}
+
+static int ppo2_grid() {  // one persistent block per CU (cached: device properties are slow)
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            cus = n;
+        else
+            cus = 256;
+    }
+    return cus;
+}
+
+}  // namespace rlp
+
+using namespace rlp;
+
+extern "C" {
+
+int64_t rlp_ppo2_workspace_floats(const rlp_mlp_desc *desc, int64_t rows) {
+    MfmaNet net;
+    if (!desc || !mfma_net_from_desc(*desc, &net) || net.H != kUpdH || rows < 0) return RLP_EINVAL;
+    const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
+    const int64_t grid = ppo2_grid();
+    return 2 * tiles * kUpdTileFloats + grid * (kUpdH * kUpdH + kUpdH * net.S + 2 * kUpdH) +
+           grid * 4 * (net.A * kUpdH + net.A);
+}
+
+int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_loss_cfg *cfg,
+                  const float *s, const float *a, const float *a_logprob, const float *adv,
+                  const float *v_target, const int64_t *index, int64_t rows, float *grad,
+                  double *loss_sum, float *workspace, rlp_stream_t stream) {
+    RLP_REQUIRE(desc && packed && cfg && s && grad && workspace, "rlp_ppo2_grad: null argument");
+    MfmaNet net;
+    if (!mfma_net_from_desc(*desc, &net) || net.H != kUpdH)
+        return fail(RLP_EUNSUPPORTED, "rlp_ppo2_grad: need a [S->256->256->A] tanh net");
+    const bool actor = cfg->kind == RLP_LOSS_ACTOR;
+    RLP_REQUIRE(actor || cfg->kind == RLP_LOSS_CRITIC, "rlp_ppo2_grad: loss kind %d", cfg->kind);
+    if (actor) {
+        RLP_REQUIRE(a && a_logprob && adv, "rlp_ppo2_grad: actor loss needs a, a_logprob, adv");
+        RLP_REQUIRE(net.out_tanh, "rlp_ppo2_grad: actor net needs a tanh output layer");
+    } else {
+        RLP_REQUIRE(v_target && net.A == 1 && !net.out_tanh,
+                    "rlp_ppo2_grad: critic loss needs v_target and a linear [..->1] net");
+    }
+    RLP_REQUIRE(rows > 0, "rlp_ppo2_grad: rows=%lld", (long long)rows);
+    hipStream_t st = as_stream(stream);
+    const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
+    const int grid = (int)(tiles < ppo2_grid() ? tiles : ppo2_grid());
+    const int gfull = ppo2_grid();
+    Ppo2Args g{};
+    g.packed = packed; g.net = net;
+    g.s = s; g.a = a; g.lp = a_logprob; g.adv = adv; g.vt = v_target; g.index = index;
+    g.rows = rows; g.inv_rows = 1.f / (float)rows; g.eps_clip = cfg->eps_clip;
+    float ent = 0.f;
+    for (int k = 0; k < net.A && actor; ++k) {
+        g.std_[k] = cfg->std[k];
+        g.off[k] = (cfg->a_min[k] + cfg->a_max[k]) / 2.0f;
+        g.gain[k] = cfg->a_max[k] - g.off[k];
+        ent += 0.5f + 0.91893853320467274178f + logf(cfg->std[k]);  // Normal.entropy()
+    }
+    g.ent_row = cfg->entropy_coef * ent;
+    g.g2t = workspace;
+    g.g1t = workspace + tiles * kUpdTileFloats;
+    float *partw = workspace + 2 * tiles * kUpdTileFloats;
+    g.part3 = partw + (int64_t)gfull * (kUpdH * kUpdH + kUpdH * net.S + 2 * kUpdH);
+    g.loss_sum = loss_sum;
+#define RLP_FD(KS1, A_, L) ppo2_fd_kernel<KS1, A_, L><<<grid, 256, 0, st>>>(g)
+    if (actor) {
+        if (net.ks1 == 1) {
+            if (net.A == 1) RLP_FD(1, 1, 0); else if (net.A == 2) RLP_FD(1, 2, 0); else if (net.A == 3) RLP_FD(1, 3, 0); else RLP_FD(1, 4, 0);
+        } else {
+            if (net.A == 1) RLP_FD(2, 1, 0); else if (net.A == 2) RLP_FD(2, 2, 0); else if (net.A == 3) RLP_FD(2, 3, 0); else RLP_FD(2, 4, 0);
+        }
+    } else {
+        if (net.ks1 == 1) RLP_FD(1, 1, 1); else RLP_FD(2, 1, 1);
+    }
+#undef RLP_FD
+    RLP_CHECK_LAUNCH("rlp_ppo2_grad (fd)");
+    WArgs w{};
+    w.packed = packed; w.net = net; w.s = s; w.index = index; w.rows = rows;
+    w.g2t = g.g2t; w.g1t = g.g1t; w.part = partw;
+    if (net.ks1 == 1) ppo2_wgrad_kernel<1><<<grid, 256, 0, st>>>(w);
+    else ppo2_wgrad_kernel<2><<<grid, 256, 0, st>>>(w);
+    RLP_CHECK_LAUNCH("rlp_ppo2_grad (wgrad)");
+    const int64_t total = (int64_t)net.H * net.S + net.H + (int64_t)net.H * net.H + net.H +
+                          (int64_t)net.A * net.H + net.A;
+    ppo2_reduce_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(net, partw, grid, g.part3,
+                                                                    grid * 4, grad);
+    RLP_CHECK_LAUNCH("rlp_ppo2_grad (reduce)");
+    return RLP_OK;
+}
+
+int rlp_grad_sqnorm(const float *grad, int64_t n, double *out, rlp_stream_t stream) {
+    RLP_REQUIRE(grad && out && n >= 0, "rlp_grad_sqnorm: bad argument");
+    if (n == 0) return RLP_OK;
+    int64_t blocks = (n + 1023) / 1024;
+    if (blocks > 1024) blocks = 1024;
+    sqnorm_kernel<<<(int)blocks, 1024, 0, as_stream(stream)>>>(grad, n, out);
+    RLP_CHECK_LAUNCH("rlp_grad_sqnorm");
+    return RLP_OK;
+}
+
+int rlp_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                  const rlp_adam_cfg *cfg, const double *clip_sqnorm, rlp_stream_t stream) {
+    RLP_REQUIRE(param && grad && exp_avg && exp_avg_sq && cfg && n >= 0 && cfg->step >= 1,
+                "rlp_adam_step: bad argument");
+    if (n == 0) return RLP_OK;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    adam_kernel<<<(int)blocks, 256, 0, as_stream(stream)>>>(param, grad, exp_avg, exp_avg_sq, n,
+                                                            *cfg, clip_sqnorm);
+    RLP_CHECK_LAUNCH("rlp_adam_step");
+    return RLP_OK;
+}
+
+}  // extern "C"

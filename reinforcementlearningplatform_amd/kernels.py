@@ -167,3 +167,51 @@ def adv_normalize(adv, stats):
     check(lib().rlp_adv_normalize(ptr(adv), adv.numel(), ptr(stats), stream_ptr()),
           "rlp_adv_normalize")
     return adv
+
+
+# ---------------------------------------------------------------------------------------------
+# PPO2 update (include/rlp.h: rlp_ppo2_grad, rlp_grad_sqnorm, rlp_adam_step)
+# ---------------------------------------------------------------------------------------------
+def ppo2_loss_cfg(kind, eps_clip=0.2, entropy_coef=0.01, std=(), a_min=(), a_max=()):
+    c = _abi.PPO2LossCfg()
+    c.kind, c.eps_clip, c.entropy_coef = int(kind), float(eps_clip), float(entropy_coef)
+    for i, (sd, lo, hi) in enumerate(zip(std, a_min, a_max)):
+        c.std[i], c.a_min[i], c.a_max[i] = float(sd), float(lo), float(hi)
+    return c
+
+
+def ppo2_workspace(desc, rows, device=None):
+    n = lib().rlp_ppo2_workspace_floats(C.byref(desc), int(rows))
+    check(n if n < 0 else 0, "rlp_ppo2_workspace_floats")
+    return torch.empty(int(n), dtype=torch.float32, device=_dev(device))
+
+
+def ppo2_grad(desc, packed, cfg, s, a=None, a_logprob=None, adv=None, v_target=None, index=None,
+              grad=None, loss_sum=None, workspace=None):
+    """Gradient of one PPO2 optimiser step's loss (flat torch parameter order) over the rows of
+    s (or s[index]); loss_sum (float64 [1], +=) receives the summed per-row loss."""
+    rows = int(index.shape[0]) if index is not None else int(s.shape[0])
+    dev = s.device
+    grad = grad if grad is not None else torch.empty(desc.param_count(), dtype=torch.float32,
+                                                     device=dev)
+    if workspace is None:
+        workspace = ppo2_workspace(desc, rows, dev)
+    f = lambda t: None if t is None else t.contiguous()
+    check(lib().rlp_ppo2_grad(C.byref(desc), ptr(packed), C.byref(cfg), ptr(f(s)), ptr(f(a)),
+                              ptr(f(a_logprob)), ptr(f(adv)), ptr(f(v_target)), ptr(f(index)),
+                              rows, ptr(grad), ptr(loss_sum), ptr(workspace), stream_ptr()),
+          "rlp_ppo2_grad")
+    return grad
+
+
+def grad_sqnorm(grad, out):
+    check(lib().rlp_grad_sqnorm(ptr(grad), grad.numel(), ptr(out), stream_ptr()), "rlp_grad_sqnorm")
+    return out
+
+
+def adam_step(param, grad, exp_avg, exp_avg_sq, lr, step, beta1=0.9, beta2=0.999, eps=1e-8,
+              clip_sqnorm=None, max_norm=0.5):
+    c = _abi.AdamCfg()
+    c.lr, c.beta1, c.beta2, c.eps, c.max_norm, c.step = lr, beta1, beta2, eps, max_norm, int(step)
+    check(lib().rlp_adam_step(ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(),
+                              C.byref(c), ptr(clip_sqnorm), stream_ptr()), "rlp_adam_step")
