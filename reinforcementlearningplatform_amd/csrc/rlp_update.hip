@@ -8,11 +8,14 @@
 //                     z2 = W2 h1 (f16x3 through the block's W2 chunk ring), h2, z3, the loss's
 //                     gradient g3 = dL/dz3 per row, dW3/db3 partials (registers), g2 = W3^T g3 *
 //                     (1 - h2^2), backward dh1 = W2^T g2 (f16x3 over the W2^T chunks, per-row
-//                     power-of-two scaling of g2), g1 = dh1 * (1 - h1^2); G2, G1 -> HBM in a
-//                     [tile][neuron][64 rows] layout (rows contiguous: the reduction operand of
-//                     the next kernel).
-//   ppo2_wgrad_kernel dW2 = sum_r g2 h1^T (exact f32 MFMA, h1 recomputed bit-identically from s),
-//                     dW1 | db1 = sum_r g1 [s | 1]^T, db2 = sum_r g2; per-block partials.
+//                     power-of-two scaling of g2), g1 = dh1 * (1 - h1^2), dW1/db1 partials (the
+//                     g1 tile transposed through LDS); G2 -> HBM in a [tile][neuron][64 rows]
+//                     layout (rows contiguous: the reduction operand of the next kernel) and
+//                     max|g2| (atomicMax) for its power-of-two scale.
+//   ppo2_wgrad_kernel dW2 = sum_r g2 h1^T and db2 = sum_r g2 on f16x3 MFMA with K = 32 rows per
+//                     instruction (g2 split under one power-of-two scale from max|g2|; h1
+//                     recomputed bit-identically from s, once per block, as LDS fragments);
+//                     per-block partials.
 // A deterministic reduce assembles the flat gradient (torch parameter order).
 #include "rlp_mfma_x3.hpp"
 
@@ -30,8 +33,9 @@ struct Ppo2Args {
     int64_t rows;
     float inv_rows, eps_clip, ent_row;  // ent_row = entropy_coef * sum_a entropy_a (constant)
     float std_[4], gain[4], off[4];
-    float *g2t, *g1t;   // [tiles][256][64]
-    float *part3;       // [grid * 4][A * 256 + A]: per-wave dW3 | db3 partials
+    float *g2t;         // [tiles][256][64]
+    unsigned *g2max;    // bits of max|g2| (atomicMax)
+    float *part3;       // [grid * 4][A*256 + A + 256*S + 256]: per-wave dW3 | db3 | dW1 | db1
     double *loss_sum;
 };
 
@@ -97,10 +101,12 @@ template <int KS1, int A, int LOSS>
 __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
     constexpr int H = kUpdH, SMALL = mlp_small_floats<H, KS1, A>();
     constexpr int STG = 20;  // staging row pitch: conflict-free b32 writes, 16-B aligned b128 reads
-    __shared__ __attribute__((aligned(16))) float lds[SMALL + kX3RingFloats + 4 * H * STG + 4 * 16 * 4];
+    __shared__ __attribute__((aligned(16))) float lds[SMALL + kX3RingFloats + 4 * H * STG + 4 * 16 * 4 +
+                                                      4 * 16 * 8];
     float *small = lds, *ring = lds + SMALL;
     float *const stg = lds + SMALL + kX3RingFloats + (threadIdx.x >> 6) * H * STG;
     float *const g3s = lds + SMALL + kX3RingFloats + 4 * H * STG + (threadIdx.x >> 6) * 64;  // [16][4]
+    float *const srw = lds + SMALL + kX3RingFloats + 4 * H * STG + 4 * 64 + (threadIdx.x >> 6) * 128;  // [16][8]
     const MfmaNet &net = g.net;
     mlp_small_to_lds(g.packed, net, small);
     __syncthreads();
@@ -133,6 +139,14 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
         for (int c = 0; c < 4; ++c) dW3p[a][c] = 0.f;
     }
     double lsum = 0.0;
+    float dW1p[4][8], db1p[4];  // neurons 64 c + lane
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        db1p[c] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dW1p[c][k] = 0.f;
+    }
+    float g2max = 0.f;
 
     const int64_t ntiles = (g.rows + kUpdRows - 1) / kUpdRows;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -141,8 +155,8 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
         asm volatile("" : "+s"(Pg));
         const gptr<float> Xf = as_global(Pg) + net.off_x3 + wv * 4 * 256 + lane * 4;
         const gptr<float> Xb = as_global(Pg) + net.off_x3t + wv * 4 * 256 + lane * 4;
-        float *g2base = g.g2t, *g1base = g.g1t;
-        asm volatile("" : "+s"(g2base), "+s"(g1base));
+        float *g2base = g.g2t;
+        asm volatile("" : "+s"(g2base));
         // the small weights are re-read from LDS per use, not hoisted into ~300 registers
         const float *sm = small;
         asm volatile("" : "+s"(sm));
@@ -159,6 +173,7 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
         for (int kk = 0; kk < KS1; ++kk) {
             const int k = 4 * kk + gq;
             bobs[kk] = (valid && k < S) ? g.s[src * S + k] : 0.f;
+            srw[e * 8 + k] = bobs[kk];  // this wave's s rows, for dW1
         }
         auto layer1 = [&](int t) {
             float w1[KS1];
@@ -306,6 +321,7 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
             for (int q = 0; q < 4; ++q) m = fmaxf(m, fabsf(acc[j][q]));
         m = fmaxf(m, __shfl_xor(m, 16));
         m = fmaxf(m, __shfl_xor(m, 32));
+        g2max = fmaxf(g2max, m);
         const int ex = m > 0.f ? __builtin_amdgcn_frexp_expf(m) : 0;  // m in [2^(ex-1), 2^ex)
         const float sc = __builtin_amdgcn_ldexpf(1.f, 14 - ex);
         const float unscale = __builtin_amdgcn_ldexpf(1.f, ex - 14) / sw;  // exact powers of two
@@ -334,11 +350,37 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
                 stg[(16 * t + 4 * gq + q) * STG + e] = dh1[t][q] * unscale * (1.f - h1 * h1);
             }
         }
-        store_tile(g1base + tile * kUpdTileFloats);
+        // ---- dW1 | db1 = sum_rows g1 [s | 1]^T through the staged g1 tile
+        wave_sync_lds();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float *grow = stg + (64 * c + lane) * STG;
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const floatx4 gv = *reinterpret_cast<const floatx4 *>(grow + 4 * q4);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    db1p[c] += gv[u];
+#pragma unroll
+                    for (int k = 0; k < 4 * KS1; ++k)
+                        dW1p[c][k] = __builtin_fmaf(gv[u], srw[(4 * q4 + u) * 8 + k], dW1p[c][k]);
+                }
+            }
+        }
+        wave_sync_lds();
     }
 
-    // ---- per-wave partials: dW3 (lane's neurons) | db3 summed over the 16 row lanes; loss
-    float *out = g.part3 + (size_t)(blockIdx.x * 4 + wv) * (A * H + A);
+    // ---- per-wave partials: dW3 (lane's neurons) | db3 summed over the 16 row lanes | dW1 | db1
+    float *out = g.part3 + (size_t)(blockIdx.x * 4 + wv) * (A * H + A + H * S + H);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int n = 64 * c + lane;
+        for (int k = 0; k < S; ++k) out[A * H + A + n * S + k] = dW1p[c][k];
+        out[A * H + A + H * S + n] = db1p[c];
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) g2max = fmaxf(g2max, __shfl_xor(g2max, o));
+    if (lane == 0) atomicMax(g.g2max, __float_as_uint(g2max));  // non-negative: uint order
 #pragma unroll
     for (int a = 0; a < A; ++a) {
 #pragma unroll
@@ -361,16 +403,20 @@ struct WArgs {
     const float *s;
     const int64_t *index;
     int64_t rows;
-    const float *g2t, *g1t;
-    float *part;  // [grid][H*H + H*S + 2H]: dW2 | dW1 | db1 | db2
+    const float *g2t;
+    const unsigned *g2max;
+    float *part;  // [grid][H*H + H]: dW2 | db2
 };
 
+// B fragments of h1 for one 64-row tile: [ks 2][nt 16][hi, lo][64 lanes][8 halfs] (64 KiB):
+// lane (g, e) of MFMA step ks holds h1(rows 32 ks + 8 g + i, neuron 16 nt + e) * 2^SH
 template <int KS1>
 __global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
     constexpr int H = kUpdH, SP = 4 * KS1;
     __shared__ float srow[kUpdRows][SP];
     __shared__ float w1s[H][SP + 1];
     __shared__ float b1s[H];
+    __shared__ __attribute__((aligned(16))) _Float16 hfrag[2 * 16 * 2 * 64 * 8];
     const MfmaNet &net = w.net;
     const int S = net.S;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, gq = lane >> 4, e = lane & 15;
@@ -379,16 +425,28 @@ __global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
         for (int i = threadIdx.x; i < H * SP; i += blockDim.x) w1s[i / SP][i % SP] = W1c[i];
         for (int i = threadIdx.x; i < H; i += blockDim.x) b1s[i] = B1c[i];
     }
-    floatx4 acc2[4][16], acc1[4], accb[4];
+    // g2 scale: max|g2| * 2^sg in [2^13, 2^14)
+    const float gm = __uint_as_float(*w.g2max);
+    const int gex = gm > 0.f ? __builtin_amdgcn_frexp_expf(gm) : 0;
+    const float sg = __builtin_amdgcn_ldexpf(1.f, 14 - gex);
+    const float un2 = __builtin_amdgcn_ldexpf(1.f, gex - 14) / kX3HScale;  // 1 / (2^sg 2^SH)
+    const float unb = __builtin_amdgcn_ldexpf(1.f, gex - 14);
+    half8 ones, zeros;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        ones[i] = (_Float16)1.0f;
+        zeros[i] = (_Float16)0.0f;
+    }
+    floatx4 acc2[4][16], accb[4];
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt) {
-        acc1[jt] = accb[jt] = floatx4{0.f, 0.f, 0.f, 0.f};
+        accb[jt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int nt = 0; nt < 16; ++nt) acc2[jt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
     const int64_t ntiles = (w.rows + kUpdRows - 1) / kUpdRows;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        __syncthreads();
+        __syncthreads();  // previous tile's fragments are consumed
         for (int i = threadIdx.x; i < kUpdRows * SP; i += blockDim.x) {
             const int rr = i / SP, k = i % SP;
             const int64_t r = tile * kUpdRows + rr;
@@ -397,101 +455,94 @@ __global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
             srow[rr][k] = v;
         }
         __syncthreads();
-        // A operands: G[tile][j][16 gq + q], j = 64 wv + 16 jt + e (MFMA step q <-> row 16 gq + q)
-        float a2[4][16];
-        const float *g2base = w.g2t, *g1base = w.g1t;
-        asm volatile("" : "+s"(g2base), "+s"(g1base));
-        const float *G2 = g2base + tile * kUpdTileFloats + 16 * gq;
+        // h1 fragments: 2048 items (ks, nt, lane) of 8 rows, 8 per thread; the k-ordered f32 fma
+        // chain of the forward's layer-1 MFMA, so h1 is bit-identical
+#pragma unroll 1
+        for (int it = threadIdx.x; it < 2048; it += blockDim.x) {
+            const int ln = it & 63, nt = (it >> 6) & 15, ks = it >> 10;
+            const int n = 16 * nt + (ln & 15), r0 = 32 * ks + 8 * (ln >> 4);
+            float x[8];
 #pragma unroll
-        for (int jt = 0; jt < 4; ++jt) {
-            const gptr<float> src = as_global(G2 + (64 * wv + 16 * jt + e) * kUpdRows);
+            for (int i = 0; i < 8; ++i) {
+                float pre = b1s[n];
 #pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-                const floatx4 v = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 4 * q4);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) a2[jt][4 * q4 + u] = v[u];
+                for (int k = 0; k < SP; ++k) pre = __builtin_fmaf(w1s[n][k], srow[r0 + i][k], pre);
+                x[i] = kX3HScale * tanh_fast(pre);
             }
+            half8 hh, hl;
+            split8(x, hh, hl);
+            *reinterpret_cast<half8 *>(hfrag + (((ks * 16 + nt) * 2 + 0) * 64 + ln) * 8) = hh;
+            *reinterpret_cast<half8 *>(hfrag + (((ks * 16 + nt) * 2 + 1) * 64 + ln) * 8) = hl;
         }
+        __syncthreads();
+        const float *g2base = w.g2t;
+        asm volatile("" : "+s"(g2base));
 #pragma unroll
-        for (int nt = 0; nt < 16; ++nt) {
-            const int n = 16 * nt + e;
-            float w1[SP];
+        for (int ks = 0; ks < 2; ++ks) {
+            // A operands: g2(rows 32 ks + 8 gq + i, j = 64 wv + 16 jt + e) * 2^sg, split
+            half8 ah[4], al[4];
 #pragma unroll
-            for (int k = 0; k < SP; ++k) w1[k] = w1s[n][k];
-            const float b1 = b1s[n];
+            for (int jt = 0; jt < 4; ++jt) {
+                const gptr<float> src = as_global(g2base + tile * kUpdTileFloats +
+                                                  (64 * wv + 16 * jt + e) * kUpdRows + 32 * ks + 8 * gq);
+                const floatx4 v0 = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src);
+                const floatx4 v1 = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 4);
+                float x[8];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                // h1 of row 16 gq + q, neuron n: the k-ordered f32 fma chain of the forward's MFMA
-                float pre = b1;
-#pragma unroll
-                for (int k = 0; k < SP; ++k) pre = __builtin_fmaf(w1[k], srow[16 * gq + q][k], pre);
-                const float h1 = tanh_fast(pre);
-#pragma unroll
-                for (int jt = 0; jt < 4; ++jt)
-                    acc2[jt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[jt][q], h1, acc2[jt][nt], 0, 0, 0);
+                for (int u = 0; u < 4; ++u) {
+                    x[u] = v0[u] * sg;
+                    x[u + 4] = v1[u] * sg;
+                }
+                split8(x, ah[jt], al[jt]);
             }
-        }
-        // [s | 1] operand: column e < S -> s, e == S -> 1 (db), else 0
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const float bs = e < S ? srow[16 * gq + q][e < SP ? e : 0] : (e == S ? 1.f : 0.f);
+            for (int nt = 0; nt < 16; ++nt) {
+                const half8 bh = *reinterpret_cast<const half8 *>(hfrag + (((ks * 16 + nt) * 2 + 0) * 64 + lane) * 8);
+                const half8 bl = *reinterpret_cast<const half8 *>(hfrag + (((ks * 16 + nt) * 2 + 1) * 64 + lane) * 8);
 #pragma unroll
-            for (int jt = 0; jt < 4; ++jt)
-                accb[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[jt][q], bs, accb[jt], 0, 0, 0);
-        }
-        const float *G1 = g1base + tile * kUpdTileFloats + 16 * gq;
-#pragma unroll
-        for (int jt = 0; jt < 4; ++jt) {
-            const gptr<float> src = as_global(G1 + (64 * wv + 16 * jt + e) * kUpdRows);
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-                const floatx4 v = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 4 * q4);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) a2[jt][4 * q4 + u] = v[u];
+                for (int jt = 0; jt < 4; ++jt) {
+                    floatx4 v = acc2[jt][nt];
+                    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jt], bh, v, 0, 0, 0);
+                    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jt], bl, v, 0, 0, 0);
+                    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jt], bh, v, 0, 0, 0);
+                    acc2[jt][nt] = v;
+                }
             }
-        }
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const float bs = e < S ? srow[16 * gq + q][e < SP ? e : 0] : (e == S ? 1.f : 0.f);
-#pragma unroll
-            for (int jt = 0; jt < 4; ++jt)
-                acc1[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[jt][q], bs, acc1[jt], 0, 0, 0);
+            for (int jt = 0; jt < 4; ++jt) {  // db2: g2 against a ones column
+                accb[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jt], ones, accb[jt], 0, 0, 0);
+                accb[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jt], ones, accb[jt], 0, 0, 0);
+            }
         }
     }
-    // C layout: lane holds rows m = 4 gq + q (j = 64 wv + 16 jt + m), column e
-    float *out = w.part + (size_t)blockIdx.x * (H * H + H * S + 2 * H);
-    float *dW1 = out + H * H, *db1 = dW1 + H * S, *db2 = db1 + H;
+    (void)zeros;
+    // C layout: lane holds rows m = 4 gq + q (j = 64 wv + 16 jt + m), column e (n = 16 nt + e)
+    float *out = w.part + (size_t)blockIdx.x * (H * H + H);
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int j = 64 * wv + 16 * jt + 4 * gq + q;
 #pragma unroll
-            for (int nt = 0; nt < 16; ++nt) out[j * H + 16 * nt + e] = acc2[jt][nt][q];
-            if (e < S) dW1[j * S + e] = acc1[jt][q];
-            if (e == S) {
-                db1[j] = acc1[jt][q];
-                db2[j] = accb[jt][q];
-            }
+            for (int nt = 0; nt < 16; ++nt) out[j * H + 16 * nt + e] = acc2[jt][nt][q] * un2;
+            if (e == 0) out[H * H + j] = accb[jt][q] * unb;
         }
 }
 
-// grad (torch order W1 b1 W2 b2 W3 b3) = sum over blocks of the partials, in block order
+// grad (torch order W1 b1 W2 b2 W3 b3) = sum over blocks / waves of the partials, in order
 __global__ void ppo2_reduce_kernel(MfmaNet net, const float *__restrict__ part, int nw,
                                    const float *__restrict__ part3, int n3, float *grad) {
     const int H = net.H, S = net.S, A = net.A;
     const int64_t total = (int64_t)H * S + H + (int64_t)H * H + H + (int64_t)A * H + A;
-    const int pw = H * H + H * S + 2 * H, p3 = A * H + A;
+    const int pw = H * H + H, p3 = A * H + A + H * S + H;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
         const float *src;
         int stride, cnt;
         int64_t off;
-        if (i < H * S) { src = part; off = H * H + i; stride = pw; cnt = nw; }                     // W1
-        else if (i < H * S + H) { src = part; off = H * H + H * S + (i - H * S); stride = pw; cnt = nw; }  // b1
-        else if (i < H * S + H + H * H) { src = part; off = i - (H * S + H); stride = pw; cnt = nw; }     // W2
-        else if (i < H * S + 2 * H + H * H) { src = part; off = H * H + H * S + H + (i - (H * S + H + H * H)); stride = pw; cnt = nw; }  // b2
-        else { src = part3; off = i - (H * S + 2 * H + H * H); stride = p3; cnt = n3; }              // W3, b3
+        if (i < H * S + H) { src = part3; off = A * H + A + i; stride = p3; cnt = n3; }       // W1, b1
+        else if (i < H * S + H + H * H + H) { src = part; off = i - (H * S + H); stride = pw; cnt = nw; }  // W2, b2
+        else { src = part3; off = i - (H * S + 2 * H + H * H); stride = p3; cnt = n3; }        // W3, b3
         float acc = 0.f;
         for (int b = 0; b < cnt; ++b) acc += src[(size_t)b * stride + off];
         grad[i] = acc;
@@ -562,8 +613,8 @@ int64_t rlp_ppo2_workspace_floats(const rlp_mlp_desc *desc, int64_t rows) {
     if (!desc || !mfma_net_from_desc(*desc, &net) || net.H != kUpdH || rows < 0) return RLP_EINVAL;
     const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
     const int64_t grid = ppo2_grid();
-    return 2 * tiles * kUpdTileFloats + grid * (kUpdH * kUpdH + kUpdH * net.S + 2 * kUpdH) +
-           grid * 4 * (net.A * kUpdH + net.A);
+    return tiles * kUpdTileFloats + grid * (kUpdH * kUpdH + kUpdH) +
+           grid * 4 * (net.A * kUpdH + net.A + kUpdH * net.S + kUpdH) + 16;
 }
 
 int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_loss_cfg *cfg,
@@ -601,9 +652,12 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     }
     g.ent_row = cfg->entropy_coef * ent;
     g.g2t = workspace;
-    g.g1t = workspace + tiles * kUpdTileFloats;
-    float *partw = workspace + 2 * tiles * kUpdTileFloats;
-    g.part3 = partw + (int64_t)gfull * (kUpdH * kUpdH + kUpdH * net.S + 2 * kUpdH);
+    float *partw = workspace + tiles * kUpdTileFloats;
+    g.part3 = partw + (int64_t)gfull * (kUpdH * kUpdH + kUpdH);
+    g.g2max = reinterpret_cast<unsigned *>(g.part3 + (int64_t)gfull * 4 *
+                                           (net.A * kUpdH + net.A + kUpdH * net.S + kUpdH));
+    if (hipMemsetAsync(g.g2max, 0, sizeof(unsigned), st) != hipSuccess)
+        return fail(RLP_EINVAL, "rlp_ppo2_grad: memset");
     g.loss_sum = loss_sum;
 #define RLP_FD(KS1, A_, L) ppo2_fd_kernel<KS1, A_, L><<<grid, 256, 0, st>>>(g)
     if (actor) {
@@ -619,7 +673,7 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (fd)");
     WArgs w{};
     w.packed = packed; w.net = net; w.s = s; w.index = index; w.rows = rows;
-    w.g2t = g.g2t; w.g1t = g.g1t; w.part = partw;
+    w.g2t = g.g2t; w.g2max = g.g2max; w.part = partw;
     if (net.ks1 == 1) ppo2_wgrad_kernel<1><<<grid, 256, 0, st>>>(w);
     else ppo2_wgrad_kernel<2><<<grid, 256, 0, st>>>(w);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (wgrad)");
