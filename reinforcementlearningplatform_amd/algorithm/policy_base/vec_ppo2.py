@@ -7,9 +7,11 @@ One iteration:
   advantages  rlp_value_fixup (V(s') of time-outs), rlp_reward_norm (Normalization, per rank as
               each DPPO2 worker keeps its own), rlp_gae + rlp_adv_normalize
   update      K epochs of the PPO2 clipped objective (Proximal_Policy_Optimization2.py:102-160)
-              in torch autograd on the GPU; under torch.distributed the actor+critic gradients are
-              averaged in ONE flat all-reduce per step (RCCL over xGMI) — synchronous data
-              parallelism instead of the reference's Hogwild shared-memory updates.
+              on librlp's kernels (NativePPO2Learner: rlp_ppo2_grad + rlp_adam_step; learner=
+              "torch" selects the torch-autograd PPO2Learner below, the parity reference); under
+              torch.distributed the actor+critic gradients are averaged in ONE flat all-reduce per
+              step (RCCL over xGMI) — synchronous data parallelism instead of the reference's
+              Hogwild shared-memory updates.
 """
 import numpy as np
 import torch
@@ -126,7 +128,7 @@ class PPO2Learner:
 
 class VecPPO2:
     def __init__(self, env, actor, critic, ppo_msg=None, T=128, success_rule=None, seed=None,
-                 process_group=None, device=None):
+                 process_group=None, device=None, learner="native"):
         self.env = env
         self.kind, self.params = env.KIND, env.params
         self.n, self.T = env.n_envs, int(T)
@@ -134,7 +136,11 @@ class VecPPO2:
         self.msg = dict(DEFAULT_PPO_MSG, **(ppo_msg or {}))
         if 'k_epo' in self.msg:                       # DPPO2 drivers name it k_epo
             self.msg['K_epochs'] = self.msg['k_epo']
-        self.learner = PPO2Learner(actor, critic, self.msg, process_group, self.device)
+        if learner not in ("native", "torch"):
+            raise ValueError(f"VecPPO2: learner {learner!r} (native | torch)")
+        from .native_ppo2 import NativePPO2Learner
+        cls = NativePPO2Learner if learner == "native" else PPO2Learner
+        self.learner = cls(actor, critic, self.msg, process_group, self.device)
         self.actor, self.critic = self.learner.actor, self.learner.critic
         self.world = self.learner.world
         self.gpu_actor = GPUNet(self.actor, True, self.device)

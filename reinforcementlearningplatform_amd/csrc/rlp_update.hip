@@ -40,7 +40,9 @@ struct Ppo2Args {
 };
 
 // wave-level 256x256 GEMM of 16 rows through the block's chunk ring (all 4 waves call it in step):
-// acc[j] += A-chunks(Xw) x B(P), B(P) = bop(P) as f16 hi/lo (rlp_mfma_x3.hpp layout)
+// acc[j] += A-chunks(Xw) x B(P), B(P) = bop(P) as f16 hi/lo (rlp_mfma_x3.hpp layout). One wave
+// per SIMD here, so latency is hidden inside the wave: a chunk's 16 A fragments are read up front
+// and the next phase's B operands are prepared inside the second chunk's MFMA region.
 template <class BOp>
 __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, float *my_part,
                                           floatx4 (&acc)[16], BOp &&bop) {
@@ -55,10 +57,11 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
     block_barrier_raw();  // every wave is done reading the ring
     issue(0);
     issue(1);
+    half8 bh, bl;
+    bop(0, bh, bl);
 #pragma unroll 1
     for (int P = 0; P < 8; ++P) {
-        half8 bh, bl;
-        bop(P, bh, bl);
+        half8 nbh, nbl;
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             const int c = 2 * P + hf;
@@ -67,17 +70,28 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
             block_barrier_raw();
             if (c + 2 < NC) issue(c + 2);
             const float *slot = ring + (c % kX3Ring) * kX3ChunkFloats + lane * 4;
+            half8 ah[8], al[8];
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
-                const half8 ah = *reinterpret_cast<const half8 *>(slot + (2 * jj) * 256);
-                const half8 al = *reinterpret_cast<const half8 *>(slot + (2 * jj + 1) * 256);
+                ah[jj] = *reinterpret_cast<const half8 *>(slot + (2 * jj) * 256);
+                al[jj] = *reinterpret_cast<const half8 *>(slot + (2 * jj + 1) * 256);
+            }
+            if (hf == 1) bop(P + 1 < 8 ? P + 1 : 7, nbh, nbl);
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
                 floatx4 v = acc[8 * hf + jj];
-                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, v, 0, 0, 0);
-                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, v, 0, 0, 0);
-                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, v, 0, 0, 0);
+                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jj], bh, v, 0, 0, 0);
+                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jj], bl, v, 0, 0, 0);
+                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jj], bh, v, 0, 0, 0);
                 acc[8 * hf + jj] = v;
             }
+            // the 16 fragment reads first, then the 24 MFMAs (the default schedule sinks each
+            // read next to its MFMA: one exposed LDS latency per 3 MFMAs at one wave per SIMD)
+            __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 24, 0);
         }
+        bh = nbh;
+        bl = nbl;
     }
 }
 

@@ -122,3 +122,50 @@ def test_native_update_tracks_torch_learner(clip, mini):
             assert torch.allclose(pn, pt, rtol=1e-5, atol=2e-6), float((pn - pt).abs().max())
     assert abs(float(ln[0]) - float(lt[0])) <= 1e-4 * (abs(float(lt[0])) + 1)
     assert abs(float(ln[1]) - float(lt[1])) <= 1e-4 * (abs(float(lt[1])) + 1)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, out):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    # gloo on one card: both ranks share cuda:0 (the N-GPU runs use RCCL, one GPU per rank)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    msg = dict(DEFAULT_PPO_MSG, K_epochs=3, use_grad_clip=True)
+    actor, critic, s, a, lp, adv, vt = make_case(4, 1, 2048, seed=21)
+    if rank == 1:  # a different init: rank 0's replica is broadcast
+        with torch.no_grad():
+            for p in list(actor.parameters()) + list(critic.parameters()):
+                p.add_(0.05)
+    nl = NativePPO2Learner(actor, critic, msg, device="cuda")
+    sl = slice(rank * 1024, (rank + 1) * 1024)
+    dev = lambda t: t[sl].cuda().contiguous()
+    nl.update(dev(s), dev(a), dev(lp), dev(adv), dev(vt))
+    out[rank] = torch.cat([nl.net_a.flat, nl.net_c.flat]).cpu().numpy().copy()
+    torch.distributed.destroy_process_group()
+
+
+def test_native_update_data_parallel_two_ranks():
+    """Synchronous DP (one flat gradient all-reduce per step) of the native learner == a single
+    learner on the concatenated batch (equal halves: mean of means == mean)."""
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_dp_worker, args=(2, _free_port(), out), nprocs=2, start_method="spawn")
+    r0, r1 = np.asarray(out[0]), np.asarray(out[1])
+    np.testing.assert_allclose(r0, r1, rtol=0, atol=1e-7)
+    msg = dict(DEFAULT_PPO_MSG, K_epochs=3, use_grad_clip=True)
+    actor, critic, s, a, lp, adv, vt = make_case(4, 1, 2048, seed=21)
+    nl = NativePPO2Learner(actor, critic, msg, device="cuda")
+    dev = lambda t: t.cuda().contiguous()
+    nl.update(dev(s), dev(a), dev(lp), dev(adv), dev(vt))
+    ref = torch.cat([nl.net_a.flat, nl.net_c.flat]).cpu().numpy()
+    np.testing.assert_allclose(r0, ref, rtol=1e-5, atol=2e-6)
