@@ -28,6 +28,25 @@
 namespace rlp {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+// scale * tanh(x) for two values on the packed FP32 pipe (v_pk_mul/add/fma_f32 around the two
+// transcendentals): bit-identical per element to scale * tanh_fast(x) (exact power-of-two scale)
+__device__ __forceinline__ float2v tanh2_scaled(float2v x, float k, float scale) {
+    const float2v t = x * k;
+    const float2v e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+    const float2v d = e + 1.0f;
+    const float2v r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    return __builtin_elementwise_fma(r, (float2v){-2.0f * scale, -2.0f * scale},
+                                     (float2v){scale, scale});
+}
+
+// f16 hi + lo of two values (packed RNE converts)
+__device__ __forceinline__ void split2(float2v x, half2v &hi, half2v &lo) {
+    hi = __builtin_convertvector(x, half2v);
+    lo = __builtin_convertvector(x - __builtin_convertvector(hi, float2v), half2v);
+}
 
 constexpr int kX3Waves = 4;             // waves per block sharing the W2 ring
 constexpr int kX3Ring = 3;              // chunks resident in the ring
@@ -105,15 +124,21 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
 #pragma unroll
         for (int sb = 0; sb < SUB; ++sb)
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float pre = i < 4 ? hp0[sb][i] : hp1[sb][i - 4];
+            for (int i = 0; i < 8; i += 2) {
+                const float2v pre = i < 4 ? (float2v){hp0[sb][i], hp0[sb][i + 1]}
+                                          : (float2v){hp1[sb][i - 4], hp1[sb][i - 3]};
+#if RLP_EXPERIMENT == 4  // timing experiment only: no hidden tanh
+                const float2v x = pre * kX3HScale;
+#else
                 // 2^SH tanh(pre), bit-identical to kX3HScale * tanh_fast(pre)
-                const float ex = __builtin_amdgcn_exp2f(pre * 2.8853900817779268f);
-                const float x = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + ex),
-                                               kX3HScale);
-                const _Float16 hi = (_Float16)x;
-                bh[sb][i] = hi;
-                bl[sb][i] = (_Float16)(x - (float)hi);
+                const float2v x = tanh2_scaled(pre, 2.8853900817779268f, kX3HScale);
+#endif
+                half2v hi, lo;
+                split2(x, hi, lo);
+                bh[sb][i] = hi.x;
+                bh[sb][i + 1] = hi.y;
+                bl[sb][i] = lo.x;
+                bl[sb][i + 1] = lo.y;
             }
         if (P + 1 < NPH) {  // next phase's layer-1 tiles, under this phase's MFMAs
             layer1(2 * P + 2, hp0);
@@ -143,12 +168,13 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
         }
     }
 
-    // ---- layer 3: out[a][env] = sum_n W3[a][n] tanh(H2^T[n][env]) + b3[a]
-    float part[SUB][NOUT];
+    // ---- layer 3: out[a][env] = sum_n W3[a][n] tanh(H2^T[n][env]) + b3[a] (pairs of neurons on
+    // the packed FP32 pipe: two partial sums per output)
+    float2v part[SUB][NOUT];
 #pragma unroll
     for (int sb = 0; sb < SUB; ++sb)
 #pragma unroll
-        for (int a = 0; a < NOUT; ++a) part[sb][a] = 0.f;
+        for (int a = 0; a < NOUT; ++a) part[sb][a] = (float2v){0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         floatx4 w3[NOUT];
@@ -159,18 +185,23 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
 #pragma unroll
         for (int sb = 0; sb < SUB; ++sb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float ex = __builtin_amdgcn_exp2f(acc[sb][j][r] * k_out);
-                const float h = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + ex), 1.0f);
+            for (int r = 0; r < 4; r += 2) {
+#if RLP_EXPERIMENT == 3  // timing experiment only: no output-layer tanh
+                const float2v h = (float2v){acc[sb][j][r], acc[sb][j][r + 1]} * k_out;
+#else
+                const float2v h = tanh2_scaled((float2v){acc[sb][j][r], acc[sb][j][r + 1]}, k_out, 1.0f);
+#endif
 #pragma unroll
-                for (int a = 0; a < NOUT; ++a) part[sb][a] = __builtin_fmaf(w3[a][r], h, part[sb][a]);
+                for (int a = 0; a < NOUT; ++a)
+                    part[sb][a] = __builtin_elementwise_fma((float2v){w3[a][r], w3[a][r + 1]}, h,
+                                                            part[sb][a]);
             }
     }
 #pragma unroll
     for (int sb = 0; sb < SUB; ++sb)
 #pragma unroll
         for (int a = 0; a < NOUT; ++a) {
-            float v = part[sb][a];
+            float v = part[sb][a].x + part[sb][a].y;
             v += __shfl_xor(v, 16);
             v += __shfl_xor(v, 32);
             out[sb][a] = v + (a < nout ? b3c[a] : 0.f);

@@ -39,12 +39,15 @@ struct RolloutArgs {
 // share a SIMD (MI355X_MICROARCH.md "Two waves per SIMD"); one block per CU, per-wave W2 rings.
 // f16x3 path: 4-wave blocks sharing one W2 ring, two blocks per CU (2 waves per SIMD).
 template <int SUB, bool X3> constexpr int rollout_block() { return X3 ? 256 : (SUB == 4 ? 256 : 512); }
-template <bool X3> constexpr int rollout_min_blocks() { return X3 ? 2 : 1; }
+// f16x3: SUB == 2 -> two 4-wave blocks per CU (2 waves per SIMD, 256 registers each); SUB == 4 ->
+// one block per CU (1 wave per SIMD, 512 registers: the SUB x 64 accumulators live in AGPRs) with
+// all 64 lanes doing f64 physics
+template <int SUB, bool X3> constexpr int rollout_min_blocks() { return X3 && SUB == 2 ? 2 : 1; }
 
 constexpr int RING = 3;  // fp32 path: W2 k-phases in flight per wave
 
 template <int KIND, int H, int SUB, bool X3>
-__global__ void __launch_bounds__((rollout_block<SUB, X3>()), (rollout_min_blocks<X3>()))
+__global__ void __launch_bounds__((rollout_block<SUB, X3>()), (rollout_min_blocks<SUB, X3>()))
 rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__restrict__ need_reset,
                const float *__restrict__ actor, MfmaNet an, const float *__restrict__ critic,
                MfmaNet cn, RolloutArgs ra, rlp_rollout_bufs b) {
@@ -306,9 +309,13 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
                     an.S, an.A, cn.S, cn.A, E::S, E::A);
     if (an.H != 256 || cn.H != 256)
         return fail(RLP_EUNSUPPORTED, "rlp_rollout: hidden width %d/%d (built for 256)", an.H, cn.H);
-    if (prec == RLP_MLP_F16X3)
+    if (prec == RLP_MLP_F16X3) {
+        if (sub == 4)
+            return launch_rollout<KIND, 256, 4, true>(params, state, need_reset, actor, an, critic,
+                                                      cn, ra, b, stream);
         return launch_rollout<KIND, 256, 2, true>(params, state, need_reset, actor, an, critic, cn,
                                                   ra, b, stream);
+    }
     if (sub == 2)
         return launch_rollout<KIND, 256, 2, false>(params, state, need_reset, actor, an, critic, cn,
                                                    ra, b, stream);
