@@ -351,7 +351,9 @@ int rlp_abi_version(void);
  * 4 uav, 5 mlp_desc, 6 rollout_cfg, 7 rollout_bufs, 8 ppo2_loss_cfg, 9 adam_cfg): FFI bindings
  * verify their mirrors with it. */
 int64_t rlp_struct_size(int which);
-/* Tuning knob of rlp_rollout: 16-env sub-blocks per wave (2 or 4; default 2). */
+/* Tuning knob of rlp_rollout: 16-env sub-blocks per wave: 0 = auto (default; the f16x3 path
+ * takes 1 when 2 would leave fewer than two blocks per CU, e.g. 32 768 UAV envs), 1 (f16x3 only),
+ * 2 or 4. */
 int rlp_set_rollout_sub(int sub);
 /* Arithmetic of rlp_rollout's hidden layer (the [256 x 256] GEMM, 99 % of its FLOPs):
  *   RLP_MLP_F16X3 (default): error-compensated split, w*x = wh*xh + wh*xl + wl*xh on f16 MFMA with

@@ -42,7 +42,7 @@ template <int SUB, bool X3> constexpr int rollout_block() { return X3 ? 256 : (S
 // f16x3: SUB == 2 -> two 4-wave blocks per CU (2 waves per SIMD, 256 registers each); SUB == 4 ->
 // one block per CU (1 wave per SIMD, 512 registers: the SUB x 64 accumulators live in AGPRs) with
 // all 64 lanes doing f64 physics
-template <int SUB, bool X3> constexpr int rollout_min_blocks() { return X3 && SUB == 2 ? 2 : 1; }
+template <int SUB, bool X3> constexpr int rollout_min_blocks() { return X3 && SUB <= 2 ? 2 : 1; }
 
 constexpr int RING = 3;  // fp32 path: W2 k-phases in flight per wave
 
@@ -310,20 +310,34 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
     if (an.H != 256 || cn.H != 256)
         return fail(RLP_EUNSUPPORTED, "rlp_rollout: hidden width %d/%d (built for 256)", an.H, cn.H);
     if (prec == RLP_MLP_F16X3) {
+        if (sub == 0) {  // auto: 32-env waves unless that leaves fewer than 2 blocks per CU
+            static int cus = 0;
+            if (cus == 0) {
+                int dev = 0;
+                if (hipGetDevice(&dev) != hipSuccess ||
+                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                        hipSuccess || cus <= 0)
+                    cus = 256;
+            }
+            sub = (ra.n + 127) / 128 < 2 * cus ? 1 : 2;
+        }
+        if (sub == 1)
+            return launch_rollout<KIND, 256, 1, true>(params, state, need_reset, actor, an, critic,
+                                                      cn, ra, b, stream);
         if (sub == 4)
             return launch_rollout<KIND, 256, 4, true>(params, state, need_reset, actor, an, critic,
                                                       cn, ra, b, stream);
         return launch_rollout<KIND, 256, 2, true>(params, state, need_reset, actor, an, critic, cn,
                                                   ra, b, stream);
     }
-    if (sub == 2)
+    if (sub <= 2)
         return launch_rollout<KIND, 256, 2, false>(params, state, need_reset, actor, an, critic, cn,
                                                    ra, b, stream);
     return launch_rollout<KIND, 256, 4, false>(params, state, need_reset, actor, an, critic, cn, ra,
                                                b, stream);
 }
 
-static int g_rollout_sub = 2;
+static int g_rollout_sub = 0;  // 0: auto
 static int g_mlp_precision = RLP_MLP_F16X3;
 
 }  // namespace rlp
@@ -341,10 +355,11 @@ int rlp_set_mlp_precision(int mode) {
 
 int rlp_get_mlp_precision(void) { return g_mlp_precision; }
 
-// tuning knob of the fp32 path (envs per wave = 16 * sub); sub in {2, 4}
+// tuning knob (envs per wave = 16 * sub): 0 = auto (f16x3: 1 when 32-env waves would leave fewer
+// than 2 blocks per CU, else 2; f32: 2), 1 (f16x3 only), 2, 4
 
 int rlp_set_rollout_sub(int sub) {
-    if (sub != 2 && sub != 4) return fail(RLP_EINVAL, "rlp_set_rollout_sub: %d", sub);
+    if (sub < 0 || sub > 4 || sub == 3) return fail(RLP_EINVAL, "rlp_set_rollout_sub: %d", sub);
     g_rollout_sub = sub;
     return RLP_OK;
 }
