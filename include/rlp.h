@@ -345,10 +345,39 @@ int rlp_adam_step(float *param, const float *grad, float *exp_avg, float *exp_av
                   const rlp_adam_cfg *cfg, const double *clip_sqnorm, rlp_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
+/* Replay buffer resident in HBM (utils/classes.py:189-247 ReplayBuffer; DDPG.learn
+ * algorithm/actor_critic/DDPG.py:72-109). Device columns of `capacity` rows, fp32:
+ * s [cap][S], a [cap][A], r [cap], s_next [cap][S], end [cap] (= 1 - done, :209). */
+typedef struct rlp_replay {
+    float *s, *a, *r, *s_next, *end;
+    int64_t capacity;
+    int32_t S, A;
+} rlp_replay;
+/* store_transition (:201-210) of n transitions in order: row (counter + i) % capacity (the
+ * caller advances its mem_counter by n). reward is the env's f64 reward. */
+int rlp_replay_store(const rlp_replay *rb, int64_t counter, const float *s, const float *a,
+                     const double *reward, const float *s_next, const uint8_t *done, int64_t n,
+                     rlp_stream_t stream);
+/* sample_buffer(is_reward_ascent=False) (:236-237): `batch` row indices uniform in
+ * [0, max_mem) with replacement, Philox-keyed by (seed, counter). */
+int rlp_replay_sample_uniform(int64_t max_mem, int64_t batch, uint64_t seed, uint64_t counter,
+                              int64_t *index, rlp_stream_t stream);
+/* sample_buffer(is_reward_ascent=True) (:212-235): rows sorted by reward ascending (stable),
+ * pool = the top int(0.25 * max_mem), *n_out = min(pool, batch) rows drawn without replacement
+ * in random order. Device workspace of rlp_replay_workspace_bytes(max_mem) bytes. */
+int64_t rlp_replay_workspace_bytes(int64_t capacity);
+int rlp_replay_sample_reward_top(const rlp_replay *rb, int64_t max_mem, int64_t batch,
+                                 uint64_t seed, uint64_t counter, int64_t *index, int64_t *n_out,
+                                 void *workspace, int64_t workspace_bytes, rlp_stream_t stream);
+/* rows index[0..batch) of every column into dense [batch][..] tensors */
+int rlp_replay_gather(const rlp_replay *rb, const int64_t *index, int64_t batch, float *s,
+                      float *a, float *r, float *s_next, float *end, rlp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------ */
 const char *rlp_last_error_string(void);
 int rlp_abi_version(void);
 /* sizeof of the ABI structs as compiled into the library (0 cartpole, 1 angleonly, 2 soi, 3 ugv,
- * 4 uav, 5 mlp_desc, 6 rollout_cfg, 7 rollout_bufs, 8 ppo2_loss_cfg, 9 adam_cfg): FFI bindings
+ * 4 uav, 5 mlp_desc, 6 rollout_cfg, 7 rollout_bufs, 8 ppo2_loss_cfg, 9 adam_cfg, 10 replay): FFI bindings
  * verify their mirrors with it. */
 int64_t rlp_struct_size(int which);
 /* Tuning knob of rlp_rollout: 16-env sub-blocks per wave: 0 = auto (default; the f16x3 path

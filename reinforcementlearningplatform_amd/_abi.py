@@ -136,6 +136,11 @@ class AdamCfg(C.Structure):
                 ("max_norm", C.c_float), ("step", C.c_int32)]
 
 
+class Replay(C.Structure):
+    _fields_ = [("s", C.c_void_p), ("a", C.c_void_p), ("r", C.c_void_p), ("s_next", C.c_void_p),
+                ("end", C.c_void_p), ("capacity", C.c_int64), ("S", C.c_int32), ("A", C.c_int32)]
+
+
 PARAM_TYPES = {
     RLP_ENV_CARTPOLE: CartPoleParams,
     RLP_ENV_CARTPOLE_ANGLEONLY: AngleOnlyParams,
@@ -311,7 +316,8 @@ def check_struct_sizes():
             "soi": C.sizeof(SOIParams), "ugv": C.sizeof(UGVParams),
             "uav": C.sizeof(UAVHoverParams), "mlp_desc": C.sizeof(MLPDesc),
             "rollout_cfg": C.sizeof(RolloutCfg), "rollout_bufs": C.sizeof(RolloutBufs),
-            "ppo2_loss_cfg": C.sizeof(PPO2LossCfg), "adam_cfg": C.sizeof(AdamCfg)}
+            "ppo2_loss_cfg": C.sizeof(PPO2LossCfg), "adam_cfg": C.sizeof(AdamCfg),
+            "replay": C.sizeof(Replay)}
 
 
 _ = math  # keep import for callers doing deg arithmetic

@@ -51,6 +51,11 @@ def _declare(lib):
         "rlp_ppo2_grad": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp]),
         "rlp_grad_sqnorm": (i32, [vp, i64, vp, vp]),
         "rlp_adam_step": (i32, [vp, vp, vp, vp, i64, vp, vp, vp]),
+        "rlp_replay_store": (i32, [vp, i64, vp, vp, vp, vp, vp, i64, vp]),
+        "rlp_replay_sample_uniform": (i32, [i64, i64, u64, u64, vp, vp]),
+        "rlp_replay_workspace_bytes": (i64, [i64]),
+        "rlp_replay_sample_reward_top": (i32, [vp, i64, i64, u64, u64, vp, vp, vp, i64, vp]),
+        "rlp_replay_gather": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -147,6 +147,7 @@ int64_t rlp_struct_size(int which) {
     case 7: return sizeof(rlp_rollout_bufs);
     case 8: return sizeof(rlp_ppo2_loss_cfg);
     case 9: return sizeof(rlp_adam_cfg);
+    case 10: return sizeof(rlp_replay);
     }
     return -1;
 }

@@ -88,22 +88,20 @@ template <> struct Env<RLP_ENV_CARTPOLE> {
         const double tt = time + p.dt;
         double xx[4] = {s[0], s[1], s[2], s[3]};
         while (time < tt) {  // fp64 time accumulation => 10 or 11 sub-steps
-            double K1[4], K2[4], K3[4], K4[4], tmp[4], d[4];
+            // (K1 + 2*K2 + 2*K3 + K4) / 6 evaluates left to right: a running sum is bit-identical
+            double sum[4], tmp[4], d[4];
             ode(p, force, xx, d);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { K1[i] = h * d[i]; tmp[i] = xx[i] + K1[i] / 2; }
+            for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = k; tmp[i] = xx[i] + k / 2; }
             ode(p, force, tmp, d);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { K2[i] = h * d[i]; tmp[i] = xx[i] + K2[i] / 2; }
+            for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k / 2; }
             ode(p, force, tmp, d);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { K3[i] = h * d[i]; tmp[i] = xx[i] + K3[i]; }
+            for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k; }
             ode(p, force, tmp, d);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                K4[i] = h * d[i];
-                xx[i] = xx[i] + (K1[i] + 2 * K2[i] + 2 * K3[i] + K4[i]) / 6;
-            }
+            for (int i = 0; i < 4; ++i) xx[i] = xx[i] + (sum[i] + h * d[i]) / 6;
             time += h;
         }
         s[0] = xx[0]; s[1] = xx[1]; s[2] = xx[2]; s[3] = xx[3]; s[4] = time;
@@ -171,21 +169,20 @@ template <> struct Env<RLP_ENV_CARTPOLE_ANGLEONLY> {
         const float af = a[0];
         const double force = (double)af, dt = p.dt;
         double xx[4] = {s[0], s[1], s[2], s[3]};
-        double K1[4], K2[4], K3[4], K4[4], tmp[4], d[4];
+        double sum[4], tmp[4], d[4];  // running RK4 sum (bit-identical, see CartPole)
         ode(p, force, xx, d);  // rk44 :218-229 (one RK4 step of dt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { K1[i] = dt * d[i]; tmp[i] = xx[i] + K1[i] / 2; }
+        for (int i = 0; i < 4; ++i) { const double k = dt * d[i]; sum[i] = k; tmp[i] = xx[i] + k / 2; }
         ode(p, force, tmp, d);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { K2[i] = dt * d[i]; tmp[i] = xx[i] + K2[i] / 2; }
+        for (int i = 0; i < 4; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k / 2; }
         ode(p, force, tmp, d);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { K3[i] = dt * d[i]; tmp[i] = xx[i] + K3[i]; }
+        for (int i = 0; i < 4; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k; }
         ode(p, force, tmp, d);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            K4[i] = dt * d[i];
-            xx[i] = xx[i] + (K1[i] + 2 * K2[i] + 2 * K3[i] + K4[i]) / 6;
+            xx[i] = xx[i] + (sum[i] + dt * d[i]) / 6;
         }
         const double time = s[4] + dt;
         s[0] = xx[0]; s[1] = xx[1]; s[2] = xx[2]; s[3] = xx[3]; s[4] = time;
@@ -355,21 +352,20 @@ template <bool BIDIR> struct UGV {
                                                 double &reward, int &flag, bool &done) {
         const double al = (double)a[0], aa = (double)a[1], dt = p.dt;
         double xx[5] = {s[0], s[1], s[2], s[3], s[4]};
-        double K1[5], K2[5], K3[5], K4[5], t[5], d[5];
+        double sum[5], t[5], d[5];  // running RK4 sum (bit-identical, see CartPole)
         ode(p, al, aa, xx, d);  // rk44 :294-313
 #pragma unroll
-        for (int i = 0; i < 5; ++i) { K1[i] = dt * d[i]; t[i] = xx[i] + K1[i] / 2; }
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = k; t[i] = xx[i] + k / 2; }
         ode(p, al, aa, t, d);
 #pragma unroll
-        for (int i = 0; i < 5; ++i) { K2[i] = dt * d[i]; t[i] = xx[i] + K2[i] / 2; }
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; t[i] = xx[i] + k / 2; }
         ode(p, al, aa, t, d);
 #pragma unroll
-        for (int i = 0; i < 5; ++i) { K3[i] = dt * d[i]; t[i] = xx[i] + K3[i]; }
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; t[i] = xx[i] + k; }
         ode(p, al, aa, t, d);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-            K4[i] = dt * d[i];
-            s[i] = xx[i] + (K1[i] + 2 * K2[i] + 2 * K3[i] + K4[i]) / 6;
+            s[i] = xx[i] + (sum[i] + dt * d[i]) / 6;
         }
         if (!BIDIR && s[2] < 0.) s[2] = 0.;
         const double time = s[5] + dt;
@@ -530,22 +526,21 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
         }
         // update -> rk44(n=1) uav.py:462-483
         const double h = p.dt / 1;
-        double xx[12], K1[12], K2[12], K3[12], t[12], d[12];
+        // s[0..11] is the RK4 base point (unchanged until the end); running sum of
+        // (K1 + 2*K2 + 2*K3 + K4), bit-identical to the left-to-right expression
+        double sum[12], t[12], d[12];
+        ode(p, uf, tq, s, d);
 #pragma unroll
-        for (int i = 0; i < 12; ++i) xx[i] = s[i];
-        ode(p, uf, tq, xx, d);
-#pragma unroll
-        for (int i = 0; i < 12; ++i) { K1[i] = h * d[i]; t[i] = xx[i] + K1[i] / 2; }
+        for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = k; t[i] = s[i] + k / 2; }
         ode(p, uf, tq, t, d);
 #pragma unroll
-        for (int i = 0; i < 12; ++i) { K2[i] = h * d[i]; t[i] = xx[i] + K2[i] / 2; }
+        for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; t[i] = s[i] + k / 2; }
         ode(p, uf, tq, t, d);
 #pragma unroll
-        for (int i = 0; i < 12; ++i) { K3[i] = h * d[i]; t[i] = xx[i] + K3[i]; }
+        for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; t[i] = s[i] + k; }
         ode(p, uf, tq, t, d);
 #pragma unroll
-        for (int i = 0; i < 12; ++i)
-            s[i] = xx[i] + (K1[i] + 2 * K2[i] + 2 * K3[i] + h * d[i]) / 6;
+        for (int i = 0; i < 12; ++i) s[i] = s[i] + (sum[i] + h * d[i]) / 6;
         s[T] += p.dt;
         if (s[PSI] > kPi) s[PSI] -= 2 * kPi;
         if (s[PSI] < -kPi) s[PSI] += 2 * kPi;

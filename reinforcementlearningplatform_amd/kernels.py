@@ -215,3 +215,68 @@ def adam_step(param, grad, exp_avg, exp_avg_sq, lr, step, beta1=0.9, beta2=0.999
     c.lr, c.beta1, c.beta2, c.eps, c.max_norm, c.step = lr, beta1, beta2, eps, max_norm, int(step)
     check(lib().rlp_adam_step(ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(),
                               C.byref(c), ptr(clip_sqnorm), stream_ptr()), "rlp_adam_step")
+
+
+# ---------------------------------------------------------------------------------------------
+# Replay buffer in HBM (include/rlp.h: rlp_replay_*)
+# ---------------------------------------------------------------------------------------------
+def replay_alloc(capacity, S, A, device=None):
+    """Device columns of a replay buffer and the rlp_replay struct pointing at them."""
+    dev = _dev(device)
+    f32 = dict(dtype=torch.float32, device=dev)
+    cols = {"s": torch.zeros((capacity, S), **f32), "a": torch.zeros((capacity, A), **f32),
+            "r": torch.zeros(capacity, **f32), "s_next": torch.zeros((capacity, S), **f32),
+            "end": torch.zeros(capacity, **f32)}
+    rb = _abi.Replay()
+    for k, t in cols.items():
+        setattr(rb, k, t.data_ptr())
+    rb.capacity, rb.S, rb.A = int(capacity), int(S), int(A)
+    return cols, rb
+
+
+def replay_store(rb, counter, s, a, reward, s_next, done):
+    n = int(s.shape[0])
+    f = lambda t, dt: t.to(dtype=dt).contiguous()
+    check(lib().rlp_replay_store(C.byref(rb), int(counter), ptr(f(s, torch.float32)),
+                                 ptr(f(a, torch.float32)), ptr(f(reward, torch.float64)),
+                                 ptr(f(s_next, torch.float32)), ptr(f(done, torch.uint8)), n,
+                                 stream_ptr()), "rlp_replay_store")
+    return n
+
+
+def replay_sample_uniform(max_mem, batch, seed, counter, out=None, device=None):
+    out = out if out is not None else torch.empty(int(batch), dtype=torch.int64, device=_dev(device))
+    check(lib().rlp_replay_sample_uniform(int(max_mem), int(batch), int(seed), int(counter),
+                                          ptr(out), stream_ptr()), "rlp_replay_sample_uniform")
+    return out
+
+
+def replay_workspace(max_mem, device=None):
+    nb = lib().rlp_replay_workspace_bytes(int(max_mem))
+    check(nb if nb < 0 else 0, "rlp_replay_workspace_bytes")
+    return torch.empty(int(nb), dtype=torch.uint8, device=_dev(device))
+
+
+def replay_sample_reward_top(rb, max_mem, batch, seed, counter, workspace=None, out=None):
+    dev = torch.device("cuda")
+    out = out if out is not None else torch.empty(int(batch), dtype=torch.int64, device=dev)
+    ws = workspace if workspace is not None else replay_workspace(max_mem, dev)
+    n_out = C.c_int64(0)
+    check(lib().rlp_replay_sample_reward_top(C.byref(rb), int(max_mem), int(batch), int(seed),
+                                             int(counter), ptr(out), C.byref(n_out), ptr(ws),
+                                             ws.numel(), stream_ptr()),
+          "rlp_replay_sample_reward_top")
+    return out[:n_out.value]
+
+
+def replay_gather(rb, index, out=None):
+    B = int(index.shape[0])
+    dev = index.device
+    f32 = dict(dtype=torch.float32, device=dev)
+    out = out if out is not None else (
+        torch.empty((B, rb.S), **f32), torch.empty((B, rb.A), **f32), torch.empty(B, **f32),
+        torch.empty((B, rb.S), **f32), torch.empty(B, **f32))
+    s, a, r, s2, e = out
+    check(lib().rlp_replay_gather(C.byref(rb), ptr(index.contiguous()), B, ptr(s), ptr(a), ptr(r),
+                                  ptr(s2), ptr(e), stream_ptr()), "rlp_replay_gather")
+    return out

@@ -64,6 +64,80 @@ class RewardScaling:
 # the reference (a single env appends one row per step), to_tensor() hands fp32 tensors to the
 # learner's device.
 # ---------------------------------------------------------------------------------------------
+class ReplayBuffer:
+    """utils/classes.py:189-247 ReplayBuffer with the columns resident in HBM (rlp_replay_*).
+
+    Same constructor and methods; store_transition also takes a batch (leading axis n: the n
+    envs of one step, stored in env order as n sequential store_transition calls would), and
+    sample_buffer returns device fp32 tensors (s, a, r, s_, end[, log_probs]) — what DDPG.learn
+    turns the reference's numpy arrays into. Sampling draws from a Philox stream keyed by
+    (seed, sample count) instead of numpy's / random's global generators."""
+
+    def __init__(self, max_size: int, batch_size: int, state_dim: int, action_dim: int,
+                 device=None, seed=None):
+        self.mem_size = int(max_size)
+        self.mem_counter = 0
+        self.batch_size = int(batch_size)
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.cols, self.rb = K.replay_alloc(self.mem_size, state_dim, action_dim, self.device)
+        self.s_mem, self.a_mem, self.r_mem = self.cols["s"], self.cols["a"], self.cols["r"]
+        self._s_mem, self.end_mem = self.cols["s_next"], self.cols["end"]
+        self.log_prob_mem = torch.zeros(self.mem_size, dtype=torch.float32, device=self.device)
+        self.sorted_index = []
+        self.resort_count = 0
+        self.seed = int(seed) if seed is not None else int(np.random.randint(0, 2 ** 31 - 1))
+        self.sample_count = 0
+        self._ws = None
+
+    def _dev(self, x, dtype, cols=None):
+        t = torch.as_tensor(np.asarray(x) if not torch.is_tensor(x) else x, device=self.device)
+        t = t.to(dtype)
+        return t.reshape(-1, cols) if cols else t.reshape(-1)
+
+    def store_transition(self, state, action, reward, state_, done, log_p=0.,
+                         has_log_prob: bool = False):
+        S, A = self.rb.S, self.rb.A
+        s = self._dev(state, torch.float32, S)
+        n = s.shape[0]
+        if has_log_prob:
+            rows = (self.mem_counter + torch.arange(n, device=self.device)) % self.mem_size
+            self.log_prob_mem[rows] = self._dev(log_p, torch.float32).expand(n)
+        K.replay_store(self.rb, self.mem_counter, s, self._dev(action, torch.float32, A),
+                       self._dev(reward, torch.float64), self._dev(state_, torch.float32, S),
+                       self._dev(np.asarray(done) if not torch.is_tensor(done) else done,
+                                 torch.uint8))
+        self.mem_counter += n
+
+    def get_reward_sort(self):
+        """Indices of the stored rows sorted by reward, ascending (stable) — :212-217."""
+        m = min(self.mem_counter, self.mem_size)
+        self.sorted_index = torch.sort(self.r_mem[:m], stable=True).indices
+
+    def store_transition_per_episode(self, states, actions, rewards, states_, dones, log_ps=None,
+                                     has_log_prob: bool = False):
+        self.resort_count += 1
+        self.store_transition(states, actions, rewards, states_, dones,
+                              0. if log_ps is None else log_ps, has_log_prob)
+
+    def sample_index(self, is_reward_ascent: bool = True):
+        max_mem = min(self.mem_counter, self.mem_size)
+        self.sample_count += 1
+        if is_reward_ascent:
+            if self._ws is None:
+                self._ws = K.replay_workspace(self.mem_size, self.device)
+            return K.replay_sample_reward_top(self.rb, max_mem, self.batch_size, self.seed,
+                                              self.sample_count, self._ws)
+        return K.replay_sample_uniform(max_mem, self.batch_size, self.seed, self.sample_count,
+                                       device=self.device)
+
+    def sample_buffer(self, is_reward_ascent: bool = True, has_log_prob: bool = False):
+        idx = self.sample_index(is_reward_ascent)
+        s, a, r, s_, end = K.replay_gather(self.rb, idx)
+        if has_log_prob:
+            return s, a, r, s_, end, self.log_prob_mem[idx]
+        return s, a, r, s_, end
+
+
 class RolloutBuffer:
     FIELDS = ("s", "a", "a_lp", "r", "s_", "done", "success")
 
@@ -215,11 +289,12 @@ class PPOCritic(nn.Module):
 # ---------------------------------------------------------------------------------------------
 class GPUNet:
     """Runs `module`'s forward through librlp: the Linear layers (registration order) become an
-    rlp_mlp_desc with tanh hidden activations; an actor with `gain`/`off` gets tanh * gain + off on
-    the last layer, a critic the identity. The mapping is verified against module(x) on a probe
-    batch when built; an architecture that does not match raises instead of silently diverging."""
+    rlp_mlp_desc with tanh (PPO drivers) or ReLU (DDPG drivers) hidden activations — found by
+    checking the module's own forward on a probe batch; an actor with `gain`/`off` gets
+    tanh * gain + off on the last layer, a critic the identity. An architecture that matches
+    neither raises instead of silently diverging."""
 
-    def __init__(self, module: nn.Module, is_actor: bool, device="cuda"):
+    def __init__(self, module: nn.Module, is_actor: bool, device="cuda", hidden_act=None):
         self.module = module
         self.is_actor = is_actor
         self.device = torch.device(device)
@@ -230,13 +305,20 @@ class GPUNet:
         for a, b in zip(self.linears[:-1], self.linears[1:]):
             if a.out_features != b.in_features:
                 raise ValueError("GPUNet: Linear layers do not chain")
-        acts = [_abi.RLP_ACT_TANH] * (len(self.linears) - 1)
-        acts.append(_abi.RLP_ACT_TANH if is_actor else _abi.RLP_ACT_NONE)
-        self.desc = _abi.MLPDesc.make(dims, acts)
-        self.packed = None
-        self.flat = None
-        self.refresh()
-        self._verify()
+        last = _abi.RLP_ACT_TANH if is_actor else _abi.RLP_ACT_NONE
+        cands = [hidden_act] if hidden_act is not None else [_abi.RLP_ACT_TANH, _abi.RLP_ACT_RELU]
+        err = None
+        for act in cands:
+            self.desc = _abi.MLPDesc.make(dims, [act] * (len(self.linears) - 1) + [last])
+            self.packed = None
+            self.flat = None
+            self.refresh()
+            err = self._mismatch()
+            if err is None:
+                break
+        if err is not None:
+            raise ValueError("GPUNet: module forward is not a Linear/Tanh or Linear/ReLU stack this "
+                             f"adapter maps (max diff {err:.3g})")
 
     @property
     def mfma_ok(self):
@@ -265,13 +347,14 @@ class GPUNet:
             y = y * gain + off
         return y
 
-    def _verify(self):
+    def _mismatch(self):
+        """None if the mapping reproduces module(x) on a probe batch, else the max difference."""
         g = torch.Generator().manual_seed(0)
         x = torch.rand(64, self.desc.dims[0], generator=g) * 4 - 2
         with torch.no_grad():
             p = next(self.module.parameters())
             ref = self.module(x.to(p.device, p.dtype)).float().to(self.device)
         got = self(x.to(self.device))
-        if not torch.allclose(got, ref, rtol=1e-4, atol=1e-4):
-            raise ValueError("GPUNet: module forward is not a Linear/Tanh stack this adapter maps "
-                             f"(max diff {float((got - ref).abs().max()):.3g})")
+        if torch.allclose(got, ref, rtol=1e-4, atol=1e-4):
+            return None
+        return float((got - ref).abs().max())

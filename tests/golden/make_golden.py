@@ -505,6 +505,64 @@ def gen_reward_norm():
     print("reward_norm", out[:3])
 
 
+def gen_replay():
+    """ReplayBuffer (utils/classes.py:189-247): ring overwrite, end = 1 - done, stable ascending
+    reward sort (ties included)."""
+    rb = cls_mod.ReplayBuffer(10, 4, 2, 1)
+    n = 23
+    s = rng.normal(size=(n, 2))
+    a = rng.uniform(-3, 3, size=(n, 1))
+    r = np.round(rng.normal(size=n), 1)        # rounded: equal rewards exercise the stable sort
+    s2 = rng.normal(size=(n, 2))
+    d = (rng.uniform(size=n) < 0.3).astype(float)
+    for i in range(n):
+        rb.store_transition(s[i], a[i], r[i], s2[i], d[i])
+    with quiet():
+        rb.get_reward_sort()
+    np.savez(os.path.join(OUT, "replay.npz"), s=s, a=a, r=r, s2=s2, d=d, s_mem=rb.s_mem,
+             a_mem=rb.a_mem, r_mem=rb.r_mem, s2_mem=rb._s_mem, end_mem=rb.end_mem,
+             mem_counter=rb.mem_counter, sorted_index=np.asarray(rb.sorted_index))
+    print("replay", rb.mem_counter, rb.sorted_index[:5])
+
+
+def gen_ddpg():
+    """One DDPG.learn step (algorithm/actor_critic/DDPG.py:72-109) with the DDPG-SOI driver's nets
+    (demonstration/DDPG/DDPG-4-SecondOrderIntegration/train.py:26-100) on a fixed batch."""
+    with quiet():
+        drv_d = load("demonstration/DDPG/DDPG-4-SecondOrderIntegration/train.py", "ref_ddpg_soi_train")
+        ddpg_mod = load("algorithm/actor_critic/DDPG.py", "ref_ddpg")
+    torch.manual_seed(11)
+    lo, hi = np.array([-3., -3.]), np.array([3., 3.])
+    nets = [drv_d.Actor(1e-4, 4, 2, lo, hi), drv_d.Actor(1e-4, 4, 2, lo, hi),
+            drv_d.Critic(3e-4, 4, 2), drv_d.Critic(3e-4, 4, 2)]
+    env_msg = {'state_dim': 4, 'action_dim': 2, 'action_range': np.stack([lo, hi], 1), 'name': 'SOI'}
+    agent = ddpg_mod.DDPG(env_msg=env_msg, gamma=0.99, actor_soft_update=0.005,
+                          critic_soft_update=0.005, memory_capacity=10000, batch_size=64,
+                          actor=nets[0], target_actor=nets[1], critic=nets[2], target_critic=nets[3])
+    flat = lambda m: torch.cat([p.detach().reshape(-1) for p in m.parameters()]).numpy().copy()
+    before = {k: flat(m) for k, m in zip(("actor", "target_actor", "critic", "target_critic"),
+                                         (agent.actor, agent.target_actor, agent.critic,
+                                          agent.target_critic))}
+    B = 64
+    batch = (rng.uniform(-2, 2, (B, 4)), rng.uniform(-3, 3, (B, 2)), rng.normal(size=B),
+             rng.uniform(-2, 2, (B, 4)), (rng.uniform(size=B) > 0.1).astype(np.float32))
+    agent.memory.mem_counter = 10000
+    agent.memory.sample_buffer = lambda is_reward_ascent=True, has_log_prob=False: batch
+    agent.learn(is_reward_ascent=False, iter=1)
+    after = {k: flat(m) for k, m in zip(("actor", "target_actor", "critic", "target_critic"),
+                                        (agent.actor, agent.target_actor, agent.critic,
+                                         agent.target_critic))}
+    np.savez(os.path.join(OUT, "ddpg_soi_learn.npz"), s=batch[0], a=batch[1], r=batch[2],
+             s2=batch[3], end=batch[4], **{f"before_{k}": v for k, v in before.items()},
+             **{f"after_{k}": v for k, v in after.items()})
+    print("ddpg", {k: float(np.abs(after[k] - before[k]).max()) for k in after})
+
+
+if __name__ == "__main__" and len(sys.argv) > 2:   # selected generators only
+    for name in sys.argv[2:]:
+        globals()["gen_" + name]()
+    sys.exit(0)
+
 if __name__ == "__main__":
     gen_cartpole("cartpole_ppo2", mods["cp_ppo2"])
     gen_cartpole("cartpole_dppo2", mods["cp_dppo2"], n=100)
@@ -520,6 +578,8 @@ if __name__ == "__main__":
     gen_nets()
     gen_gae()
     gen_reward_norm()
+    gen_replay()
+    gen_ddpg()
     with open(os.path.join(OUT, "VERSIONS.txt"), "w") as f:
         f.write(f"numpy {np.__version__}\ntorch {torch.__version__}\npython {sys.version.split()[0]}\n"
                 f"reference {REF} (HKPolyU-UAV/ReinforcementLearningPlatform @ 2025-02-28)\n")

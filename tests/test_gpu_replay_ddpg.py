@@ -1,0 +1,173 @@
+"""GPU parity of the HBM replay buffer (rlp_replay_*) and the DDPG agent / VecDDPG loop against the
+reference ReplayBuffer (utils/classes.py:189-247) and DDPG.learn (algorithm/actor_critic/
+DDPG.py:72-109), pinned by tests/golden/replay.npz and ddpg_soi_learn.npz (made by running the
+reference, tests/golden/make_golden.py)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as func
+
+from reinforcementlearningplatform_amd import kernels as K
+from reinforcementlearningplatform_amd.algorithm.actor_critic.DDPG import DDPG
+from reinforcementlearningplatform_amd.algorithm.actor_critic.vec_ddpg import VecDDPG
+from reinforcementlearningplatform_amd.environment.SecondOrderIntegration.SecondOrderIntegration \
+    import SecondOrderIntegration
+from reinforcementlearningplatform_amd.utils.classes import GPUNet, ReplayBuffer
+
+pytestmark = pytest.mark.gpu
+
+
+def test_replay_store_and_sort_match_reference(golden):
+    g = golden("replay")
+    for batched in (False, True):
+        rb = ReplayBuffer(10, 4, 2, 1, device="cuda", seed=1)
+        if batched:   # n = 23 > capacity in one call: only the last 10 can survive, as sequentially
+            rb.store_transition(g["s"], g["a"], g["r"], g["s2"], g["d"])
+        else:
+            for i in range(len(g["r"])):
+                rb.store_transition(g["s"][i], g["a"][i], g["r"][i], g["s2"][i], g["d"][i])
+        assert rb.mem_counter == int(g["mem_counter"])
+        for ours, ref in ((rb.s_mem, g["s_mem"]), (rb.a_mem, g["a_mem"]), (rb.r_mem, g["r_mem"]),
+                          (rb._s_mem, g["s2_mem"]), (rb.end_mem, g["end_mem"])):
+            np.testing.assert_array_equal(ours.cpu().numpy(), np.asarray(ref, np.float32))
+        rb.get_reward_sort()
+        np.testing.assert_array_equal(rb.sorted_index.cpu().numpy(), g["sorted_index"])
+        # sample_buffer(is_reward_ascent=True): random.sample(sorted_index[-q:], min(q, batch))
+        q = int(0.25 * 10)
+        idx = rb.sample_index(is_reward_ascent=True).cpu().numpy()
+        assert len(idx) == min(q, 4) and set(idx) == set(g["sorted_index"][-q:])
+
+
+def test_replay_uniform_sampling():
+    max_mem, B = 1000, 200_000
+    i1 = K.replay_sample_uniform(max_mem, B, seed=5, counter=1).cpu().numpy()
+    i2 = K.replay_sample_uniform(max_mem, B, seed=5, counter=1).cpu().numpy()
+    i3 = K.replay_sample_uniform(max_mem, B, seed=5, counter=2).cpu().numpy()
+    assert i1.min() >= 0 and i1.max() < max_mem
+    np.testing.assert_array_equal(i1, i2)
+    assert (i1 != i3).mean() > 0.99
+    counts = np.bincount(i1, minlength=max_mem)
+    exp = B / max_mem
+    chi2 = ((counts - exp) ** 2 / exp).sum()
+    assert chi2 < max_mem + 6 * np.sqrt(2 * max_mem)     # ~6 sigma of a chi2(999)
+
+
+def test_replay_reward_top_large():
+    cap = 100_000
+    rng = np.random.default_rng(0)
+    rb = ReplayBuffer(cap, 20_000, 3, 2, device="cuda", seed=3)
+    n = 77_777   # partially filled
+    r = np.round(rng.normal(size=n), 2)
+    rb.store_transition(rng.normal(size=(n, 3)), rng.normal(size=(n, 2)), r,
+                        rng.normal(size=(n, 3)), np.zeros(n))
+    idx = rb.sample_index(is_reward_ascent=True).cpu().numpy()
+    q = int(0.25 * n)
+    order = np.argsort(r.astype(np.float32), kind="stable")
+    assert len(idx) == min(q, 20_000) and len(set(idx)) == len(idx)
+    assert set(idx) <= set(order[-q:])
+    s, a, rr, s2, end = rb.sample_buffer(is_reward_ascent=False)
+    assert s.shape == (20_000, 3) and a.shape == (20_000, 2) and (end == 1).all()
+
+
+# the DDPG-SOI driver's nets (demonstration/DDPG/DDPG-4-SecondOrderIntegration/train.py:26-100)
+class Critic(nn.Module):
+    def __init__(self, beta, state_dim, action_dim):
+        super().__init__()
+        self.fc1 = nn.Linear(state_dim + action_dim, 256)
+        self.fc2 = nn.Linear(256, 256)
+        self.action_value = nn.Linear(action_dim, 256)
+        self.q = nn.Linear(256, 1)
+        self.optimizer = torch.optim.Adam(self.parameters(), lr=beta)
+
+    def forward(self, s, a):
+        sav = func.relu(self.fc1(torch.cat([s, a], 1)))
+        sav = func.relu(self.fc2(sav))
+        return self.q(sav)
+
+
+class Actor(nn.Module):
+    def __init__(self, alpha, state_dim, action_dim, a_min, a_max):
+        super().__init__()
+        self.a_min = torch.tensor(a_min, dtype=torch.float)
+        self.a_max = torch.tensor(a_max, dtype=torch.float)
+        self.off = (self.a_min + self.a_max) / 2.0
+        self.gain = self.a_max - self.off
+        self.fc1 = nn.Linear(state_dim, 256)
+        self.fc2 = nn.Linear(256, 256)
+        self.mu = nn.Linear(256, action_dim)
+        self.optimizer = torch.optim.Adam(self.parameters(), lr=alpha)
+
+    def forward(self, s):
+        s = func.relu(self.fc1(s))
+        s = func.relu(self.fc2(s))
+        return self.gain * torch.tanh(self.mu(s)) + self.off
+
+
+def load_flat(m, flat):
+    off = 0
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.from_numpy(np.asarray(flat[off:off + p.numel()])).view_as(p))
+            off += p.numel()
+
+
+def make_agent(g=None, memory=10000, batch=64, seed=0):
+    lo, hi = np.array([-3., -3.]), np.array([3., 3.])
+    nets = [Actor(1e-4, 4, 2, lo, hi), Actor(1e-4, 4, 2, lo, hi), Critic(3e-4, 4, 2),
+            Critic(3e-4, 4, 2)]
+    if g is not None:
+        for m, k in zip(nets, ("actor", "target_actor", "critic", "target_critic")):
+            load_flat(m, g[f"before_{k}"])
+    env_msg = {'state_dim': 4, 'action_dim': 2, 'action_range': np.stack([lo, hi], 1),
+               'name': 'SecondOrderIntegration'}
+    return DDPG(env_msg, gamma=0.99, actor_soft_update=0.005, critic_soft_update=0.005,
+                memory_capacity=memory, batch_size=batch, actor=nets[0], target_actor=nets[1],
+                critic=nets[2], target_critic=nets[3], device="cuda", seed=seed)
+
+
+def test_ddpg_update_matches_reference(golden):
+    g = golden("ddpg_soi_learn")
+    agent = make_agent(g)
+    dev = lambda k: torch.as_tensor(np.asarray(g[k]), dtype=torch.float32, device="cuda")
+    agent.update(dev("s"), dev("a"), dev("r"), dev("s2"), dev("end"))
+    for k, m in (("actor", agent.actor), ("target_actor", agent.target_actor),
+                 ("critic", agent.critic), ("target_critic", agent.target_critic)):
+        got = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+        np.testing.assert_allclose(got, g[f"after_{k}"], rtol=1e-5, atol=1e-7, err_msg=k)
+
+
+def test_batched_actor_and_noise():
+    agent = make_agent()
+    s = torch.rand(5000, 4, device="cuda") * 4 - 2
+    a0 = agent.choose_action(s, is_optimal=True)
+    with torch.no_grad():
+        ref = agent.actor(s)
+    torch.testing.assert_close(a0, ref, rtol=1e-5, atol=2e-6)   # ReLU net through librlp
+    sig = np.array([0.5, 0.5], np.float32)
+    a1 = agent.choose_action(s, sigma=sig)
+    z = ((a1 - ref) / 0.5)[(a1.abs() < 2.9).all(1)]             # unclipped rows
+    assert abs(float(z.mean())) < 0.05 and abs(float(z.std()) - 1) < 0.05
+    assert float(a1.abs().max()) <= 3.0
+
+
+def test_vecddpg_loop_fills_replay_and_learns():
+    n = 4096
+    env = SecondOrderIntegration(n_envs=n, variant="ddpg", seed=2)
+    env.reset(random=True)
+    agent = make_agent(memory=200_000, batch=512, seed=4)
+    loop = VecDDPG(env, agent, learn_iters=1)
+    p0 = torch.cat([p.detach().reshape(-1) for p in agent.actor.parameters()]).clone()
+    dones = 0
+    for t in range(30):
+        r, d, out = loop.step()
+        dones += int(d.sum())
+        assert torch.isfinite(r).all()
+    assert agent.memory.mem_counter == 30 * n
+    p1 = torch.cat([p.detach().reshape(-1) for p in agent.actor.parameters()])
+    assert torch.isfinite(p1).all() and not torch.equal(p0, p1)
+    assert out is not None and all(torch.isfinite(x) for x in out)
+    # the ring holds what the envs produced: end = 1 - done and obs bounded by the DDPG copy
+    m = agent.memory
+    assert set(torch.unique(m.end_mem[:30 * n]).tolist()) <= {0.0, 1.0}
+    assert float(m.s_mem[:30 * n].abs().max()) < 10
