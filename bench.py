@@ -165,6 +165,65 @@ def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
     return seg.n * seg.T * iters / dt, dt / iters
 
 
+def soi_ddpg_leg(rank, n=65536, steps=20, warmup=3, batch=4096, capacity=1 << 20, seed=11):
+    """BASELINE config 3: SecondOrderIntegration DDPG (DDPG copy), n envs, replay buffer in HBM.
+    One step = actor forward (librlp MLP, ReLU) + exploration noise + env step + n transitions
+    into the replay ring + auto-reset, then one DDPG update on `batch` rows sampled from HBM
+    (the driver's one learn() per env step, train.py:240, with the batch scaled from 64)."""
+    import torch.nn as nn
+    import torch.nn.functional as func
+    from reinforcementlearningplatform_amd.algorithm.actor_critic.DDPG import DDPG
+    from reinforcementlearningplatform_amd.algorithm.actor_critic.vec_ddpg import VecDDPG
+    from reinforcementlearningplatform_amd.environment.SecondOrderIntegration.SecondOrderIntegration \
+        import SecondOrderIntegration
+
+    class Critic(nn.Module):   # train.py:26-60
+        def __init__(self, beta, S, A):
+            super().__init__()
+            self.fc1, self.fc2 = nn.Linear(S + A, 256), nn.Linear(256, 256)
+            self.action_value, self.q = nn.Linear(A, 256), nn.Linear(256, 1)
+            self.optimizer = torch.optim.Adam(self.parameters(), lr=beta)
+
+        def forward(self, s, a):
+            return self.q(func.relu(self.fc2(func.relu(self.fc1(torch.cat([s, a], 1))))))
+
+    class Actor(nn.Module):    # train.py:63-100
+        def __init__(self, alpha, S, A, lo, hi):
+            super().__init__()
+            self.a_min, self.a_max = torch.tensor(lo, dtype=torch.float), torch.tensor(hi, dtype=torch.float)
+            self.off = (self.a_min + self.a_max) / 2.0
+            self.gain = self.a_max - self.off
+            self.fc1, self.fc2, self.mu = nn.Linear(S, 256), nn.Linear(256, 256), nn.Linear(256, A)
+            self.optimizer = torch.optim.Adam(self.parameters(), lr=alpha)
+
+        def forward(self, s):
+            return self.gain * torch.tanh(self.mu(func.relu(self.fc2(func.relu(self.fc1(s)))))) + self.off
+
+    torch.manual_seed(seed)
+    env = SecondOrderIntegration(n_envs=n, variant="ddpg", seed=seed, env_id0=rank * n)
+    env.reset(random=True)
+    lo, hi = env.action_range[:, 0], env.action_range[:, 1]
+    nets = [Actor(1e-4, 4, 2, lo, hi), Actor(1e-4, 4, 2, lo, hi), Critic(3e-4, 4, 2), Critic(3e-4, 4, 2)]
+    msg = {'state_dim': 4, 'action_dim': 2, 'action_range': env.action_range, 'name': env.name}
+    agent = DDPG(msg, 0.99, 0.005, 0.005, capacity, batch, *nets, device="cuda", seed=seed)
+    loop = VecDDPG(env, agent, learn_iters=1)
+    out = {}
+    for learn in (False, True):
+        for _ in range(warmup):
+            loop.step(learn=learn)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loop.step(learn=learn)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        out["with_learn" if learn else "env_only"] = n * steps / dt
+    return {"value": out["with_learn"], "unit": "env-steps/s", "env_only": out["env_only"],
+            "envs_per_gpu": n, "replay_capacity": capacity, "batch": batch, "learn_iters_per_step": 1,
+            "config": "SecondOrderIntegration (DDPG copy) DDPG, replay in HBM, nets [4,256,256,2] "
+                      "relu / Q [6,256,256,1] relu; DDPG update in torch on the device"}
+
+
 def cpu_baseline(env, seconds=10.0):
     """Oracle (plain-C port of the reference loop, 1 thread) on a bounded sample of the same
     workload: actor + critic forward, sampling and env step per env-step."""
@@ -212,6 +271,7 @@ def main():
     ap.add_argument("--e2e", type=int, default=2, help="PPO2 iterations incl. the K-epoch update to time (0: skip)")
     ap.add_argument("--uav", type=int, default=1, help="also time the UavRobust rollout (32768 envs/GPU)")
     ap.add_argument("--fp32-leg", type=int, default=1, help="also time the exact-f32 MLP path")
+    ap.add_argument("--ddpg", type=int, default=1, help="also time SOI DDPG with the HBM replay (config 3)")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
@@ -327,6 +387,13 @@ def main():
                                    "envs_per_gpu": 32768, "global_envs": 32768 * world, "T": 64,
                                    "config": "UavRobust hover outer loop (6-DoF + FNTSMC), PPO2 [6,256,256,3]"}
         del useg
+    if args.ddpg and args.env == "cartpole":
+        d = soi_ddpg_leg(rank)
+        if dist is not None:
+            t = torch.tensor([d["value"], d["env_only"]], device="cuda", dtype=torch.float64)
+            dist.all_reduce(t)   # independent replicas: sum of the ranks' rates
+            d["value"], d["env_only"] = float(t[0]), float(t[1])
+        out["soi_ddpg"] = d
     if args.e2e:
         v, it_s = e2e_iterations(seg, args.e2e, learner=args.learner)
         v_all = v * world
