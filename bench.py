@@ -224,6 +224,50 @@ def soi_ddpg_leg(rank, n=65536, steps=20, warmup=3, batch=4096, capacity=1 << 20
                       "relu / Q [6,256,256,1] relu; DDPG update in torch on the device"}
 
 
+def ugvoa_leg(rank, n=16384, steps=30, warmup=3, seed=5):
+    """SURVEY §8(f) f3 / BASELINE config 5 shard: UGVForwardObstacleAvoidance (env-dir copy) env
+    steps at n envs per GPU (131 072 / 8): f64 RK4 + the 37-beam fake lidar against the env's
+    obstacles + reward/terminal + auto-reset of finished envs (map generator on the GPU), actions
+    uniform over the action box. One lidar scan per env-step (obs_cur of a step is the previous
+    obs_next, as in the drivers)."""
+    from reinforcementlearningplatform_amd.environment.UGVForwardObstacleAvoidance import \
+        UGVForwardObstacleAvoidance
+    env = UGVForwardObstacleAvoidance(n_envs=n, seed=seed, env_id0=rank * n)
+    kind, p = env.KIND, env.params
+    lo = torch.tensor(env.action_range[:, 0], device="cuda", dtype=torch.float32)
+    hi = torch.tensor(env.action_range[:, 1], device="cuda", dtype=torch.float32)
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    acts = [lo + (hi - lo) * torch.rand(n, 2, device="cuda", generator=g) for _ in range(8)]
+    counter = [1]
+
+    def one(i, ev=None):
+        if ev is not None:
+            ev[0].record()
+        _, on, r, f, d = K.env_step(kind, p, env.state, acts[i % 8], want_obs_cur=False)
+        if ev is not None:
+            ev[1].record()
+        K.env_reset(kind, p, env.state, mask=d, seed=seed, counter=counter[0], env_id0=rank * n)
+        counter[0] += 1
+        return d
+
+    for i in range(warmup):
+        one(i)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    dsum = torch.zeros((), device="cuda", dtype=torch.int64)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        dsum += one(i, evs[i]).sum()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    step_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    return {"value": n * steps / dt, "unit": "env-steps/s", "envs_per_gpu": n,
+            "env_step_kernel_ms": step_ms, "resets_per_step": float(dsum) / steps,
+            "config": "UGVForwardObstacleAvoidance env-dir copy: f64 RK4 + 37-beam lidar vs 10 "
+                      "circles + GPU map generator on reset, random actions"}
+
+
 def cpu_baseline(env, seconds=10.0):
     """Oracle (plain-C port of the reference loop, 1 thread) on a bounded sample of the same
     workload: actor + critic forward, sampling and env step per env-step."""
@@ -272,6 +316,7 @@ def main():
     ap.add_argument("--uav", type=int, default=1, help="also time the UavRobust rollout (32768 envs/GPU)")
     ap.add_argument("--fp32-leg", type=int, default=1, help="also time the exact-f32 MLP path")
     ap.add_argument("--ddpg", type=int, default=1, help="also time SOI DDPG with the HBM replay (config 3)")
+    ap.add_argument("--oa", type=int, default=1, help="also time UGVForwardObstacleAvoidance env steps (lidar)")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
@@ -394,6 +439,13 @@ def main():
             dist.all_reduce(t)   # independent replicas: sum of the ranks' rates
             d["value"], d["env_only"] = float(t[0]), float(t[1])
         out["soi_ddpg"] = d
+    if args.oa and args.env == "cartpole":
+        d = ugvoa_leg(rank)
+        if dist is not None:
+            t = torch.tensor([d["value"]], device="cuda", dtype=torch.float64)
+            dist.all_reduce(t)
+            d["value"] = float(t[0])
+        out["ugvoa_lidar"] = d
     if args.e2e:
         v, it_s = e2e_iterations(seg, args.e2e, learner=args.learner)
         v_all = v * world

@@ -56,6 +56,9 @@ enum rlp_env_kind {
     /* environment/UavRobust/UavHoverOuterLoop.py: 6-DoF rigid body (uav.py) + FNTSMC attitude
        loop (FNTSMC.py) driven by an RL virtual-acceleration command. */
     RLP_ENV_UAV_HOVER_OUTER_LOOP = 6,
+    /* environment/UGVForwardObstacleAvoidance/UGVForwardObstacleAvoidance.py: unicycle + 37-beam
+       fake lidar against up to 15 circular obstacles per env (map.py generate_circle_obs_training). */
+    RLP_ENV_UGV_OBSTACLE_AVOIDANCE = 7,
 };
 
 /* Physics-state dimension D, observation dim S and action dim A per kind (also queryable). */
@@ -64,6 +67,10 @@ enum rlp_env_kind {
 #define RLP_SOI_D 7       /* x, y, vx, vy, time, target_x, target_y */
 #define RLP_UGV_D 8       /* x, y, vel, phi, omega, time, target_x, target_y */
 #define RLP_UAV_D 22      /* x y z vx vy vz phi theta psi p q r | time | pos_ref[3] | s1[3] | att_ref[3] */
+#define RLP_UGVOA_NOBS 15   /* obstacle slots per env: obsNum 10 (env dir, PPO2 demo) or 15 (DPPO2 demo,
+                               DPPO2-4-UGVForwardObstacleAvoidance/UGVForwardObstacleAvoidance.py:543) */
+#define RLP_UGVOA_NLASER 37 /* beams: int(2 * laserRange / laserStep) + 1 = 180/5 + 1 */
+#define RLP_UGVOA_D (8 + 3 * RLP_UGVOA_NOBS) /* x y vel phi omega time tx ty | (cx cy r) x NOBS */
 
 /* CartPole.py:27-46 (physical constants), :187-217 get_reward literals, :273-274 reset law. */
 typedef struct rlp_cartpole_params {
@@ -152,6 +159,32 @@ typedef struct rlp_uav_hover_params {
     double target_offset; /* generate_random_point(offset=1.0) */
     double Qx, Qv, R;     /* 1, 0.1, 0.02 */
 } rlp_uav_hover_params;
+
+/* UGVForwardObstacleAvoidance.py:12-104 (constants), get_fake_laser :274-397, get_state :399-411,
+   is_Terminal :433-450, get_reward :452-469, ode/rk44 :471-502, reset :520-557 with
+   map.py:152-174 generate_circle_obs_training(5, 5, 4 r_vehicle, 4 r_vehicle, 0.2, 0.5, n_obs).
+   shaped = 1 selects the PPO2/DPPO2 demo copies (demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/
+   UGVForwardObstacleAvoidance.py): dt 0.05, success ignores omega (:421-427), the r1..r4 shaped
+   reward (:449-473) and rk44's gate on the pre-step velocity (:488-500). */
+typedef struct rlp_ugv_oa_params {
+    double map_size[2];   /* 5, 5 */
+    double dt, time_max;  /* 0.1, 15 */
+    double kf, kt;        /* 0.1, 0.1 */
+    double v_max, e_phi_max, omega_max;   /* 3, pi, 2 pi */
+    double a_linear_max, a_angular_max;   /* 3, 2 pi */
+    double r_vehicle;     /* 0.15 */
+    double laser_dis, laser_blind, laser_range; /* 2, 0, deg2rad(90) */
+    double static_gain;   /* 1 */
+    double Q_pos, Q_vel, Q_phi, Q_omega;  /* 2, 0, 2, 1 */
+    double safety_dis_obs, safety_dis_st; /* 4 r_vehicle, 4 r_vehicle */
+    double r_min, r_max;  /* 0.2, 0.5 */
+    double st_margin;     /* 0.3: start/target ~ U(margin, map - margin) */
+    int32_t n_obs;        /* obstacles placed by reset, <= RLP_UGVOA_NOBS; unused slots are parked
+                             outside the map, where they can neither collide nor be seen */
+    int32_t max_tries;    /* rejection-sampling bound per draw (an unplaceable obstacle is parked) */
+    int32_t shaped;       /* 0: env-dir copy, 1: PPO2/DPPO2 demo copy */
+    int32_t reserved;
+} rlp_ugv_oa_params;
 
 /* Dimensions of a kind. Returns RLP_EINVAL for an unknown kind. Host-only, no device work. */
 int rlp_env_dims(int kind, int *D, int *S, int *A);
@@ -377,7 +410,8 @@ int rlp_replay_gather(const rlp_replay *rb, const int64_t *index, int64_t batch,
 const char *rlp_last_error_string(void);
 int rlp_abi_version(void);
 /* sizeof of the ABI structs as compiled into the library (0 cartpole, 1 angleonly, 2 soi, 3 ugv,
- * 4 uav, 5 mlp_desc, 6 rollout_cfg, 7 rollout_bufs, 8 ppo2_loss_cfg, 9 adam_cfg, 10 replay): FFI bindings
+ * 4 uav, 5 mlp_desc, 6 rollout_cfg, 7 rollout_bufs, 8 ppo2_loss_cfg, 9 adam_cfg, 10 replay,
+ * 11 ugv_oa): FFI bindings
  * verify their mirrors with it. */
 int64_t rlp_struct_size(int which);
 /* Tuning knob of rlp_rollout: 16-env sub-blocks per wave: 0 = auto (default; the f16x3 path

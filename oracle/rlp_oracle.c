@@ -570,6 +570,230 @@ static void uav_step(const rlp_uav_hover_params *p, double *s, const float *a, f
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* UGV forward obstacle avoidance — environment/UGVForwardObstacleAvoidance/                  */
+/* UGVForwardObstacleAvoidance.py. s = {x y vel phi omega time tx ty | (cx cy r) x NOBS}       */
+/* ------------------------------------------------------------------------------------------ */
+#define OA_NOBS RLP_UGVOA_NOBS
+#define OA_NL RLP_UGVOA_NLASER
+
+static double oa_vec_rad(double x1, double y1, double x2, double y2) { /* functions.py:35-46 */
+    double n1 = sqrt(x1 * x1 + y1 * y1), n2 = sqrt(x2 * x2 + y2 * y2);
+    if (n2 < 1e-4 || n1 < 1e-4) return 0;
+    double c = (x1 * x2 + y1 * y2) / (n1 * n2);
+    return acos(fmin(fmax(c, -1.0), 1.0));
+}
+
+static double oa_dis(double x1, double y1, double x2, double y2) { /* dis_two_points */
+    double dx = x1 - x2, dy = y1 - y2;
+    return sqrt(dx * dx + dy * dy);
+}
+
+static int oa_collision(const rlp_ugv_oa_params *p, const double *s) { /* :261-272 */
+    for (int k = 0; k < OA_NOBS; ++k)
+        if (oa_dis(s[0], s[1], s[8 + 3 * k], s[9 + 3 * k]) <= s[10 + 3 * k] + p->r_vehicle) return 1;
+    return 0;
+}
+
+/* get_fake_laser :274-397, literally: obstacles visited in argsort(ref_dis) order, first hit wins */
+static void oa_laser(const rlp_ugv_oa_params *p, const double *s, double *laser) {
+    double x = s[0], y = s[1], xm = p->map_size[0], ym = p->map_size[1], L = p->laser_dis;
+    if (oa_collision(p, s)) {
+        for (int i = 0; i < OA_NL; ++i) laser[i] = p->laser_blind;
+        return;
+    }
+    double ref[OA_NOBS];
+    int order[OA_NOBS];
+    for (int k = 0; k < OA_NOBS; ++k) {
+        ref[k] = oa_dis(x, y, s[8 + 3 * k], s[9 + 3 * k]);
+        order[k] = k;
+    }
+    for (int k = 1; k < OA_NOBS; ++k) { /* stable ascending sort */
+        int v = order[k], j = k - 1;
+        while (j >= 0 && ref[order[j]] > ref[v]) { order[j + 1] = order[j]; --j; }
+        order[j + 1] = v;
+    }
+    double start = s[3] - p->laser_range, stop = s[3] + p->laser_range;
+    double step = (stop - start) / (OA_NL - 1); /* np.linspace */
+    double th1 = oa_vec_rad(1, 0, xm - x, ym - y);
+    double th2 = oa_vec_rad(1, 0, 0 - x, ym - y);
+    double th3 = -oa_vec_rad(1, 0, 0 - x, 0 - y);
+    double th4 = -oa_vec_rad(1, 0, xm - x, 0 - y);
+    for (int i = 0; i < OA_NL; ++i) {
+        double ph = i == OA_NL - 1 ? stop : (double)i * step + start;
+        if (ph > PI) ph -= 2 * PI;
+        if (ph < -PI) ph += 2 * PI;
+        double m = tan(ph), b = y - m * x;
+        double cosT = fabs(m) / sqrt(1 + m * m), sinT = 1 / sqrt(1 + m * m);
+        double tx, ty;
+        if (th4 < ph && ph <= th1) {
+            tx = xm; ty = m * xm + b;
+            if (x + L / sqrt(1 + m * m) < xm) {
+                tx = x + L / sqrt(1 + m * m);
+                ty = m >= 0 ? y + cosT * L : y - cosT * L;
+            }
+        } else if (th1 < ph && ph <= th2) {
+            if (fabs(m) < 1e8) { tx = (ym - b) / m; ty = ym; } else { tx = x; ty = ym; }
+            if (y + fabs(m) * L / sqrt(1 + m * m) < ym) {
+                tx = m >= 0 ? x + L * sinT : x - L * sinT;
+                ty = y + fabs(m) * L / sqrt(1 + m * m);
+            }
+        } else if (th3 < ph && ph <= th4) {
+            if (fabs(m) < 1e8) { tx = -b / m; ty = 0; } else { tx = x; ty = 0; }
+            if (y - fabs(m) * L / sqrt(1 + m * m) > 0) {
+                tx = m >= 0 ? x - L * sinT : x + L * sinT;
+                ty = y - fabs(m) * L / sqrt(1 + m * m);
+            }
+        } else {
+            tx = 0; ty = b;
+            if (x - L / sqrt(1 + m * m) > 0) {
+                tx = x - L / sqrt(1 + m * m);
+                ty = m >= 0 ? y - cosT * L : y + cosT * L;
+            }
+        }
+        int found = 0;
+        for (int kk = 0; kk < OA_NOBS; ++kk) {
+            int k = order[kk];
+            double x0 = s[8 + 3 * k], y0 = s[9 + 3 * k], r0 = s[10 + 3 * k];
+            if (ref[k] > L + r0) continue;
+            if (fabs(m * x0 - y0 + b) / sqrt(1 + m * m) > r0) continue;
+            if (oa_vec_rad(tx - x, ty - y, x0 - x, y0 - y) > PI / 2) continue;
+            double fx = (x0 + m * y0 - m * b) / (m * m + 1);
+            double fy = (m * x0 + m * m * y0 + b) / (m * m + 1);
+            double rd = oa_dis(fx, fy, x0, y0);
+            double dd = tx - x, sg = dd > 0 ? 1.0 : (dd < 0 ? -1.0 : 0.0);
+            double cx = fx - sg * sqrt(r0 * r0 - rd * rd) / sqrt(m * m + 1);
+            if (fmin(x, tx) <= cx && cx <= fmax(x, tx)) {
+                found = 1;
+                double dis = fabs(cx - x) * sqrt(m * m + 1);
+                laser[i] = dis < p->laser_blind ? p->laser_blind : dis;
+                break;
+            }
+        }
+        if (!found) {
+            double dis = oa_dis(x, y, tx, ty);
+            if (dis > L) laser[i] = L;
+            else if (p->laser_blind < dis && dis <= L) laser[i] = dis;
+            else laser[i] = p->laser_blind;
+        }
+    }
+}
+
+static double oa_e(const double *s) { return oa_dis(s[6], s[7], s[0], s[1]); } /* :512-513 */
+
+static double oa_ephi(const double *s) { /* get_e_phi -> cal_vector_rad_oriented */
+    double x1 = cos(s[3]), y1 = sin(s[3]), x2 = s[6] - s[0], y2 = s[7] - s[1];
+    if (sqrt(x2 * x2 + y2 * y2) < 1e-4 || sqrt(x1 * x1 + y1 * y1) < 1e-4) return 0;
+    return atan2(x1 * y2 - y1 * x2, x1 * x2 + y1 * y2);
+}
+
+static void oa_obs(const rlp_ugv_oa_params *p, const double *s, float *o) { /* get_state :399-411 */
+    double e_max = sqrt(p->map_size[0] * p->map_size[0] + p->map_size[1] * p->map_size[1]) / 2;
+    double lz[OA_NL];
+    o[0] = (float)((2 / e_max * oa_e(s) - 1) * p->static_gain);
+    o[1] = (float)((2 / p->v_max * s[2] - 1) * p->static_gain);
+    o[2] = (float)((oa_ephi(s) / p->e_phi_max) * p->static_gain);
+    o[3] = (float)((s[4] / p->omega_max) * p->static_gain);
+    oa_laser(p, s, lz);
+    for (int i = 0; i < OA_NL; ++i) o[4 + i] = (float)((2 * lz[i] / p->laser_dis - 1) * p->static_gain);
+}
+
+static void oa_ode(const rlp_ugv_oa_params *p, double al, double aa, const double *x, double *d) {
+    d[0] = x[2] * cos(x[3]);
+    d[1] = x[2] * sin(x[3]);
+    d[2] = al - p->kf * x[2];
+    d[3] = x[4];
+    d[4] = aa - p->kt * x[4];
+}
+
+static void oa_step(const rlp_ugv_oa_params *p, double *s, const float *a, float *obs_cur,
+                    float *obs_next, double *reward, int32_t *flag, uint8_t *done) {
+    double e_max = sqrt(p->map_size[0] * p->map_size[0] + p->map_size[1] * p->map_size[1]) / 2;
+    double c0 = (2 / e_max * oa_e(s) - 1) * p->static_gain; /* current_state[0], [1] (f64) */
+    double c1 = (2 / p->v_max * s[2] - 1) * p->static_gain;
+    if (obs_cur) oa_obs(p, s, obs_cur);
+    double al = (double)a[0], aa = (double)a[1], dt = p->dt; /* rk44 :484-502 */
+    double xx[5] = {s[0], s[1], s[2], s[3], s[4]};
+    double K1[5], K2[5], K3[5], K4[5], t[5], d[5];
+    oa_ode(p, al, aa, xx, d);
+    for (int i = 0; i < 5; ++i) { K1[i] = dt * d[i]; t[i] = xx[i] + K1[i] / 2; }
+    oa_ode(p, al, aa, t, d);
+    for (int i = 0; i < 5; ++i) { K2[i] = dt * d[i]; t[i] = xx[i] + K2[i] / 2; }
+    oa_ode(p, al, aa, t, d);
+    for (int i = 0; i < 5; ++i) { K3[i] = dt * d[i]; t[i] = xx[i] + K3[i]; }
+    oa_ode(p, al, aa, t, d);
+    for (int i = 0; i < 5; ++i) { K4[i] = dt * d[i]; xx[i] = xx[i] + (K1[i] + 2 * K2[i] + 2 * K3[i] + K4[i]) / 6; }
+    if (p->shaped) { /* demo copy rk44 :496-500 tests the pre-step vel */
+        if (s[2] < 0.) { s[3] = xx[3]; s[4] = xx[4]; s[2] = 0.; }
+        else { for (int i = 0; i < 5; ++i) s[i] = xx[i]; }
+    } else {
+        for (int i = 0; i < 5; ++i) s[i] = xx[i];
+        if (s[2] < 0.) s[2] = 0.;
+    }
+    s[5] = s[5] + dt;
+    if (s[3] > PI) s[3] -= 2 * PI;
+    if (s[3] < -PI) s[3] += 2 * PI;
+    double e = oa_e(s), eph = oa_ephi(s);
+    int f = 0; /* is_Terminal :433-450 */
+    if (s[0] > p->map_size[0] || s[0] < 0 || s[1] > p->map_size[1] || s[1] < 0) f = 1;
+    if (s[5] > p->time_max) f = 2;
+    int success = fabs(e) <= 0.05 && (p->shaped ? 1 : fabs(s[4]) < 0.01) && fabs(s[2]) < 0.01;
+    if (success) f = 3;
+    if (oa_collision(p, s)) f = 4;
+    oa_obs(p, s, obs_next);
+    *flag = f;
+    *done = f != 0;
+    if (p->shaped) { /* demo copy get_reward :449-473 */
+        double n0 = (2 / e_max * e - 1) * p->static_gain, n1 = (2 / p->v_max * s[2] - 1) * p->static_gain;
+        double r1 = -1 - fabs(s[4]) * 0.1, r2, r3, r4;
+        if (c0 > n0 + 1e-3) r2 = 5; else if (1e-3 + c0 < n0) r2 = -5; else r2 = 0;
+        if (fabs(c1) > fabs(n1) + 1e-2) r3 = 2; else if (1e-2 + fabs(c1) < fabs(n1)) r3 = -2; else r3 = 0;
+        if (success) r4 = 500; else if (f == 4) r4 = -300; else r4 = 0;
+        *reward = r1 + r2 + r3 + r4;
+        return;
+    }
+    double u_pos = -fabs(e) * p->Q_pos; /* get_reward :452-469 */
+    double u_vel = -fabs(s[2]) * p->Q_vel;
+    double u_phi = e > 0.1 ? -fabs(eph) * p->Q_phi : 0.0;
+    double u_om = -fabs(s[4]) * p->Q_omega;
+    double u_psi = 0.;
+    if (f == 1) u_psi = (p->time_max - s[5]) / p->dt * (u_pos + u_vel + u_phi + u_om);
+    *reward = u_pos + u_vel + u_phi + u_om + u_psi;
+}
+
+/* reset(random=True) :520-557 + map.py generate_circle_obs_training, Philox tag 0x400 + draw */
+static void oa_reset(const rlp_ugv_oa_params *p, double *s, uint64_t seed, uint64_t counter,
+                     uint64_t env_id) {
+    uint32_t draw = 0;
+    double u[2], v[2], xm = p->map_size[0], ym = p->map_size[1], mg = p->st_margin;
+    philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, u);
+    double sx = mg + ((xm - mg) - mg) * u[0], sy = mg + ((ym - mg) - mg) * u[1];
+    double tx = sx, ty = sy;
+    for (int k = 0; k < p->max_tries && oa_dis(tx, ty, sx, sy) < p->safety_dis_st; ++k) {
+        philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, u);
+        tx = mg + ((xm - mg) - mg) * u[0];
+        ty = mg + ((ym - mg) - mg) * u[1];
+    }
+    for (int k = 0; k < OA_NOBS; ++k) {
+        double cx = -1000.0 - 10.0 * k, cy = -1000.0, r = p->r_min;
+        for (int tr = 0; k < p->n_obs && tr < p->max_tries; ++tr) {
+            philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, u);
+            philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, v);
+            double ccx = 0 + (xm - 0) * u[0], ccy = 0 + (ym - 0) * u[1];
+            double rr = p->r_min + (p->r_max - p->r_min) * v[0];
+            int ok = oa_dis(sx, sy, ccx, ccy) > rr + p->safety_dis_st &&
+                     oa_dis(tx, ty, ccx, ccy) > rr + p->safety_dis_st;
+            for (int j = 0; j < k && ok; ++j)
+                if (oa_dis(s[8 + 3 * j], s[9 + 3 * j], ccx, ccy) <= s[10 + 3 * j] + rr + p->safety_dis_obs) ok = 0;
+            if (ok) { cx = ccx; cy = ccy; r = rr; break; }
+        }
+        s[8 + 3 * k] = cx; s[9 + 3 * k] = cy; s[10 + 3 * k] = r;
+    }
+    philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, u);
+    s[0] = sx; s[1] = sy; s[2] = 0.; s[3] = -PI + (PI - -PI) * u[0]; s[4] = 0.; s[5] = 0.;
+    s[6] = tx; s[7] = ty;
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* Generic entry points (kind dispatch), SoA state [D][n]                                      */
 /* ------------------------------------------------------------------------------------------ */
 int oracle_env_dims(int kind, int *D, int *S, int *A) {
@@ -580,6 +804,7 @@ int oracle_env_dims(int kind, int *D, int *S, int *A) {
     case RLP_ENV_UGV_FORWARD:
     case RLP_ENV_UGV_BIDIRECTIONAL: *D = RLP_UGV_D; *S = 4; *A = 2; return 0;
     case RLP_ENV_UAV_HOVER_OUTER_LOOP: *D = RLP_UAV_D; *S = 6; *A = 3; return 0;
+    case RLP_ENV_UGV_OBSTACLE_AVOIDANCE: *D = RLP_UGVOA_D; *S = 4 + OA_NL; *A = 2; return 0;
     }
     return -1;
 }
@@ -600,6 +825,7 @@ static void env_step1(int kind, const void *params, double *s, const float *a, f
     case RLP_ENV_UGV_FORWARD: ugv_step((const rlp_ugv_params *)params, 0, s, a, oc, on, r, f, dn); break;
     case RLP_ENV_UGV_BIDIRECTIONAL: ugv_step((const rlp_ugv_params *)params, 1, s, a, oc, on, r, f, dn); break;
     case RLP_ENV_UAV_HOVER_OUTER_LOOP: uav_step((const rlp_uav_hover_params *)params, s, a, oc, on, r, f, dn); break;
+    case RLP_ENV_UGV_OBSTACLE_AVOIDANCE: oa_step((const rlp_ugv_oa_params *)params, s, a, oc, on, r, f, dn); break;
     }
 }
 
@@ -611,6 +837,7 @@ static void env_obs1(int kind, const void *params, const double *s, float *o) {
     case RLP_ENV_UGV_FORWARD: ugv_obs((const rlp_ugv_params *)params, 0, s, o); break;
     case RLP_ENV_UGV_BIDIRECTIONAL: ugv_obs((const rlp_ugv_params *)params, 1, s, o); break;
     case RLP_ENV_UAV_HOVER_OUTER_LOOP: uav_obs((const rlp_uav_hover_params *)params, s, o); break;
+    case RLP_ENV_UGV_OBSTACLE_AVOIDANCE: oa_obs((const rlp_ugv_oa_params *)params, s, o); break;
     }
 }
 
@@ -618,7 +845,7 @@ int oracle_env_step(int kind, const void *params, double *state, int n, const fl
                     float *obs_cur, float *obs_next, double *reward, int32_t *flag, uint8_t *done) {
     int D, S, A;
     if (oracle_env_dims(kind, &D, &S, &A)) return -1;
-    double s[32];
+    double s[64];
     for (int i = 0; i < n; ++i) {
         gather(state, D, n, i, s);
         env_step1(kind, params, s, action + (size_t)i * A, obs_cur ? obs_cur + (size_t)i * S : NULL,
@@ -631,7 +858,7 @@ int oracle_env_step(int kind, const void *params, double *state, int n, const fl
 int oracle_env_observe(int kind, const void *params, const double *state, int n, float *obs) {
     int D, S, A;
     if (oracle_env_dims(kind, &D, &S, &A)) return -1;
-    double s[32];
+    double s[64];
     for (int i = 0; i < n; ++i) {
         gather(state, D, n, i, s);
         env_obs1(kind, params, s, obs + (size_t)i * S);
@@ -703,6 +930,9 @@ static void env_reset1(int kind, const void *params, double *s, uint64_t seed, u
         /* s1 and att_ref are NOT reset (carried over, as in the reference) */
         break;
     }
+    case RLP_ENV_UGV_OBSTACLE_AVOIDANCE:
+        oa_reset((const rlp_ugv_oa_params *)params, s, seed, counter, env_id);
+        break;
     }
 }
 
@@ -710,7 +940,7 @@ int oracle_env_reset(int kind, const void *params, double *state, int n, const u
                      const double *init_state, uint64_t seed, uint64_t counter, uint64_t env_id0) {
     int D, S, A;
     if (oracle_env_dims(kind, &D, &S, &A)) return -1;
-    double s[32];
+    double s[64];
     for (int i = 0; i < n; ++i) {
         if (mask && !mask[i]) continue;
         if (init_state) {
@@ -861,8 +1091,8 @@ int oracle_rollout(int kind, const void *env_params, double *state, uint8_t *nee
     int D, S, A;
     if (oracle_env_dims(kind, &D, &S, &A)) return -1;
     int n = cfg->n;
-    double s[32];
-    float o[16], on[16], mean[8], eps[8], act[8], lp[8], v;
+    double s[64];
+    float o[64], on[64], mean[8], eps[8], act[8], lp[8], v;
     float gain[4], off[4];
     for (int j = 0; j < A; ++j) {
         off[j] = (cfg->a_min[j] + cfg->a_max[j]) / 2.0f;

@@ -19,6 +19,11 @@ RLP_ENV_SOI = 3
 RLP_ENV_UGV_FORWARD = 4
 RLP_ENV_UGV_BIDIRECTIONAL = 5
 RLP_ENV_UAV_HOVER_OUTER_LOOP = 6
+RLP_ENV_UGV_OBSTACLE_AVOIDANCE = 7
+
+RLP_UGVOA_NOBS = 15     # obstacle slots per env (obsNum 10 or 15 by copy)
+RLP_UGVOA_NLASER = 37   # int(2 * laserRange / laserStep) + 1
+RLP_UGVOA_D = 8 + 3 * RLP_UGVOA_NOBS
 
 # (D physics-state dim, S observation dim, A action dim)
 ENV_DIMS = {
@@ -28,6 +33,7 @@ ENV_DIMS = {
     RLP_ENV_UGV_FORWARD: (8, 4, 2),
     RLP_ENV_UGV_BIDIRECTIONAL: (8, 4, 2),
     RLP_ENV_UAV_HOVER_OUTER_LOOP: (22, 6, 3),
+    RLP_ENV_UGV_OBSTACLE_AVOIDANCE: (RLP_UGVOA_D, 4 + RLP_UGVOA_NLASER, 2),
 }
 
 RLP_ACT_NONE, RLP_ACT_TANH, RLP_ACT_RELU = 0, 1, 2
@@ -136,6 +142,14 @@ class AdamCfg(C.Structure):
                 ("max_norm", C.c_float), ("step", C.c_int32)]
 
 
+class UGVOAParams(C.Structure):
+    _fields_ = [("map_size", C.c_double * 2)] + [(n, C.c_double) for n in (
+        "dt", "time_max", "kf", "kt", "v_max", "e_phi_max", "omega_max", "a_linear_max",
+        "a_angular_max", "r_vehicle", "laser_dis", "laser_blind", "laser_range", "static_gain",
+        "Q_pos", "Q_vel", "Q_phi", "Q_omega", "safety_dis_obs", "safety_dis_st", "r_min", "r_max",
+        "st_margin")] + [(n, C.c_int32) for n in ("n_obs", "max_tries", "shaped", "reserved")]
+
+
 class Replay(C.Structure):
     _fields_ = [("s", C.c_void_p), ("a", C.c_void_p), ("r", C.c_void_p), ("s_next", C.c_void_p),
                 ("end", C.c_void_p), ("capacity", C.c_int64), ("S", C.c_int32), ("A", C.c_int32)]
@@ -148,6 +162,7 @@ PARAM_TYPES = {
     RLP_ENV_UGV_FORWARD: UGVParams,
     RLP_ENV_UGV_BIDIRECTIONAL: UGVParams,
     RLP_ENV_UAV_HOVER_OUTER_LOOP: UAVHoverParams,
+    RLP_ENV_UGV_OBSTACLE_AVOIDANCE: UGVOAParams,
 }
 
 
@@ -273,6 +288,36 @@ def uav_hover_params():
     return p
 
 
+def ugv_oa_params(variant="env"):
+    """environment/UGVForwardObstacleAvoidance/UGVForwardObstacleAvoidance.py:12-104 (constants),
+    :452-469 (Q literals), :527-537 (generate_circle_obs_training arguments: safety distances
+    4 * r_vehicle, r in [0.2, 0.5], obsNum 10), map.py:66-73 (start/target margin 0.3).
+    variant 'ppo2': demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/UGVForwardObstacleAvoidance.py
+    (dt 0.05 :40, success ignores omega :421-427, shaped reward :449-473, rk44 pre-step vel gate
+    :488-500); 'dppo2': the DPPO2 copy, identical to 'ppo2' but obsNum=15 (:543)."""
+    p = UGVOAParams()
+    p.map_size[0], p.map_size[1] = 5.0, 5.0
+    p.dt, p.time_max = 0.1, 15.0
+    p.kf, p.kt = 0.1, 0.1
+    p.v_max, p.e_phi_max, p.omega_max = 3, np.pi, 2 * np.pi
+    p.a_linear_max, p.a_angular_max = 3, 2 * np.pi
+    p.r_vehicle = 0.15
+    p.laser_dis, p.laser_blind, p.laser_range = 2.0, 0.0, deg2rad(90)
+    p.static_gain = 1.
+    p.Q_pos, p.Q_vel, p.Q_phi, p.Q_omega = 2., 0.0, 2., 1.0
+    p.safety_dis_obs = p.safety_dis_st = 4 * p.r_vehicle
+    p.r_min, p.r_max = 0.2, 0.5
+    p.st_margin = 0.3
+    p.n_obs, p.max_tries, p.shaped = 10, 4096, 0
+    if variant in ("ppo2", "dppo2"):
+        p.dt, p.shaped = 0.05, 1
+        if variant == "dppo2":
+            p.n_obs = 15
+    elif variant != "env":
+        raise ValueError(variant)
+    return p
+
+
 def default_params(kind, variant=None):
     if kind == RLP_ENV_CARTPOLE:
         return cartpole_params(variant or "ppo2")
@@ -284,6 +329,8 @@ def default_params(kind, variant=None):
         return ugv_params(kind, variant or "env")
     if kind == RLP_ENV_UAV_HOVER_OUTER_LOOP:
         return uav_hover_params()
+    if kind == RLP_ENV_UGV_OBSTACLE_AVOIDANCE:
+        return ugv_oa_params(variant or "env")
     raise ValueError(f"unknown env kind {kind}")
 
 
@@ -295,7 +342,7 @@ def action_bounds(kind, params):
         return [-params.fm], [params.fm]
     if kind == RLP_ENV_SOI:
         return [-params.f_max] * 2, [params.f_max] * 2
-    if kind in (RLP_ENV_UGV_FORWARD, RLP_ENV_UGV_BIDIRECTIONAL):
+    if kind in (RLP_ENV_UGV_FORWARD, RLP_ENV_UGV_BIDIRECTIONAL, RLP_ENV_UGV_OBSTACLE_AVOIDANCE):
         return ([-params.a_linear_max, -params.a_angular_max],
                 [params.a_linear_max, params.a_angular_max])
     if kind == RLP_ENV_UAV_HOVER_OUTER_LOOP:
@@ -307,7 +354,7 @@ def timeout_flag(kind):
     """terminal_flag value meaning 'time out' per kind (the PPO2 drivers' success rule excludes it)."""
     return {RLP_ENV_CARTPOLE: 3, RLP_ENV_CARTPOLE_ANGLEONLY: 3, RLP_ENV_SOI: 2,
             RLP_ENV_UGV_FORWARD: 2, RLP_ENV_UGV_BIDIRECTIONAL: 2,
-            RLP_ENV_UAV_HOVER_OUTER_LOOP: 1}[kind]
+            RLP_ENV_UAV_HOVER_OUTER_LOOP: 1, RLP_ENV_UGV_OBSTACLE_AVOIDANCE: 2}[kind]
 
 
 def check_struct_sizes():
@@ -317,7 +364,7 @@ def check_struct_sizes():
             "uav": C.sizeof(UAVHoverParams), "mlp_desc": C.sizeof(MLPDesc),
             "rollout_cfg": C.sizeof(RolloutCfg), "rollout_bufs": C.sizeof(RolloutBufs),
             "ppo2_loss_cfg": C.sizeof(PPO2LossCfg), "adam_cfg": C.sizeof(AdamCfg),
-            "replay": C.sizeof(Replay)}
+            "replay": C.sizeof(Replay), "ugv_oa": C.sizeof(UGVOAParams)}
 
 
 _ = math  # keep import for callers doing deg arithmetic

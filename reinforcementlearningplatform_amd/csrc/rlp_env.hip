@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(256) env_step_kernel(typename Env<KIND>::P p, 
     bool dn;
     E::step(p, s, a, on, r, f, dn);
 #pragma unroll
-    for (int d = 0; d < E::D; ++d) state[(size_t)d * n + i] = s[d];
+    for (int d = 0; d < EnvDW<E>::value; ++d) state[(size_t)d * n + i] = s[d];
 #pragma unroll
     for (int j = 0; j < E::S; ++j) obs_next[(size_t)i * E::S + j] = on[j];
     reward[i] = r;
@@ -111,6 +111,7 @@ int dispatch_kind(int kind, F &&f) {
     case RLP_ENV_UGV_FORWARD: return f(std::integral_constant<int, RLP_ENV_UGV_FORWARD>());
     case RLP_ENV_UGV_BIDIRECTIONAL: return f(std::integral_constant<int, RLP_ENV_UGV_BIDIRECTIONAL>());
     case RLP_ENV_UAV_HOVER_OUTER_LOOP: return f(std::integral_constant<int, RLP_ENV_UAV_HOVER_OUTER_LOOP>());
+    case RLP_ENV_UGV_OBSTACLE_AVOIDANCE: return f(std::integral_constant<int, RLP_ENV_UGV_OBSTACLE_AVOIDANCE>());
     }
     return fail(RLP_EINVAL, "unknown env kind %d", kind);
 }
@@ -148,6 +149,7 @@ int64_t rlp_struct_size(int which) {
     case 8: return sizeof(rlp_ppo2_loss_cfg);
     case 9: return sizeof(rlp_adam_cfg);
     case 10: return sizeof(rlp_replay);
+    case 11: return sizeof(rlp_ugv_oa_params);
     }
     return -1;
 }

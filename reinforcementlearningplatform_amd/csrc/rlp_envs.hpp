@@ -49,6 +49,11 @@ __device__ __forceinline__ void sincos_fast(double x, double *sp, double *cp) {
 
 template <int KIND> struct Env;
 
+// components of the physics state step() may change (E::DW when the kind declares it, else D):
+// the step kernel writes back only those
+template <class E, class = void> struct EnvDW { static constexpr int value = E::D; };
+template <class E> struct EnvDW<E, std::void_t<decltype(E::DW)>> { static constexpr int value = E::DW; };
+
 // ==========================================================================================
 // CartPole — environment/CartPole/CartPole.py (PPO2 and DPPO2 demo copies via params)
 // state: theta, dtheta, x, dx, time
@@ -593,6 +598,257 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
             const double lo = p.pos_zone[i][0] + p.target_offset, hi = p.pos_zone[i][1] - p.target_offset;
             s[REF + i] = lo + (hi - lo) * uu[i];
         }
+    }
+};
+
+// ==========================================================================================
+// UGV forward obstacle avoidance — environment/UGVForwardObstacleAvoidance/
+// UGVForwardObstacleAvoidance.py. state: x y vel phi omega time tx ty | (cx cy r) x NOBS.
+// The fake lidar (get_fake_laser :274-397) is restated in the reference's f64 expression order,
+// branch for branch, one env per lane: 37 beams, each against the obstacles in order of distance.
+// ==========================================================================================
+template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
+    using P = rlp_ugv_oa_params;
+    static constexpr int NOBS = RLP_UGVOA_NOBS, NL = RLP_UGVOA_NLASER;
+    static constexpr int D = RLP_UGVOA_D, S = 4 + NL, A = 2;
+    static constexpr int DW = 8;  // step() changes only x..ty (the obstacles are fixed per episode)
+    enum { X = 0, Y = 1, V = 2, PHI = 3, OM = 4, T = 5, TX = 6, TY = 7, OB = 8 };
+
+    // utils/functions.py:35-46 cal_vector_rad
+    __device__ static __forceinline__ double vec_rad(double x1, double y1, double x2, double y2) {
+        const double n1 = sqrt(x1 * x1 + y1 * y1), n2 = sqrt(x2 * x2 + y2 * y2);
+        if (n2 < 1e-4 || n1 < 1e-4) return 0;
+        double c = (x1 * x2 + y1 * y2) / (n1 * n2);
+        c = c > -1 ? c : -1;
+        c = c < 1 ? c : 1;
+        return acos(c);
+    }
+    // utils/functions.py:49-60 cal_vector_rad_oriented(v1 = [cos phi, sin phi], v2 = target - pos)
+    __device__ static __forceinline__ double e_phi(const double *s) {
+        const double c = cos(s[PHI]), sn = sin(s[PHI]);
+        const double x2 = s[TX] - s[X], y2 = s[TY] - s[Y];
+        if (sqrt(x2 * x2 + y2 * y2) < 1e-4 || sqrt(c * c + sn * sn) < 1e-4) return 0;
+        return atan2(c * y2 - sn * x2, c * x2 + sn * y2);
+    }
+    __device__ static __forceinline__ double get_e(const double *s) {  // :512-513
+        const double ex = s[TX] - s[X], ey = s[TY] - s[Y];
+        return sqrt(ex * ex + ey * ey);
+    }
+    __device__ static __forceinline__ bool collision(const P &p, const double *s) {  // :261-272
+#pragma unroll
+        for (int k = 0; k < NOBS; ++k) {
+            const double dx = s[X] - s[OB + 3 * k], dy = s[Y] - s[OB + 3 * k + 1];
+            if (sqrt(dx * dx + dy * dy) <= s[OB + 3 * k + 2] + p.r_vehicle) return true;
+        }
+        return false;
+    }
+    // writes get_state's normalised beams (2 * laser / laserDis - 1) * gain into o[0..NL)
+    __device__ static void laser(const P &p, const double *s, float *o) {  // :274-397
+        const double x = s[X], y = s[Y], xm = p.map_size[0], ym = p.map_size[1];
+        if (collision(p, s)) {
+            const float v = (float)((2 * p.laser_blind / p.laser_dis - 1) * p.static_gain);
+            for (int i = 0; i < NL; ++i) o[i] = v;
+            return;
+        }
+        // The reference walks the obstacles in argsort(ref_dis) order (stable for 10 values) and
+        // stops at the first hit; the same result is the hit with the smallest (ref_dis, index),
+        // which a fixed, unrolled obstacle loop finds without sorting or dynamic indexing.
+        double ref[NOBS];
+#pragma unroll
+        for (int k = 0; k < NOBS; ++k) {
+            const double dx = x - s[OB + 3 * k], dy = y - s[OB + 3 * k + 1];
+            ref[k] = sqrt(dx * dx + dy * dy);
+        }
+        // np.linspace(phi - R, phi + R, NL): i * step + start, last element = stop
+        const double start = s[PHI] - p.laser_range, stop = s[PHI] + p.laser_range;
+        const double step = (stop - start) / (NL - 1);
+        const double theta1 = vec_rad(1, 0, xm - x, ym - y);
+        const double theta2 = vec_rad(1, 0, 0 - x, ym - y);
+        const double theta3 = -vec_rad(1, 0, 0 - x, 0 - y);
+        const double theta4 = -vec_rad(1, 0, xm - x, 0 - y);
+        const double L = p.laser_dis;
+        for (int i = 0; i < NL; ++i) {
+            double ph = i == NL - 1 ? stop : (double)i * step + start;
+            if (ph > kPi) ph -= 2 * kPi;
+            if (ph < -kPi) ph += 2 * kPi;
+            const double m = tan(ph), b = y - m * x;
+            const double sq = sqrt(1 + m * m);
+            const double cosT = fabs(m) / sq, sinT = 1 / sq;
+            double tx, ty;
+            if (theta4 < ph && ph <= theta1) {
+                tx = xm; ty = m * xm + b;
+                const double t = x + L / sq;
+                if (t < xm) { tx = t; ty = m >= 0 ? y + cosT * L : y - cosT * L; }
+            } else if (theta1 < ph && ph <= theta2) {
+                if (fabs(m) < 1e8) { tx = (ym - b) / m; ty = ym; } else { tx = x; ty = ym; }
+                const double t = y + fabs(m) * L / sq;
+                if (t < ym) { tx = m >= 0 ? x + L * sinT : x - L * sinT; ty = t; }
+            } else if (theta3 < ph && ph <= theta4) {
+                if (fabs(m) < 1e8) { tx = -b / m; ty = 0; } else { tx = x; ty = 0; }
+                const double t = y - fabs(m) * L / sq;
+                if (t > 0) { tx = m >= 0 ? x - L * sinT : x + L * sinT; ty = t; }
+            } else {
+                tx = 0; ty = b;
+                const double t = x - L / sq;
+                if (t > 0) { tx = t; ty = m >= 0 ? y - cosT * L : y + cosT * L; }
+            }
+            bool found = false;
+            double val = 0, best = 0;
+#pragma unroll
+            for (int k = 0; k < NOBS; ++k) {
+                const double x0 = s[OB + 3 * k], y0 = s[OB + 3 * k + 1], r0 = s[OB + 3 * k + 2];
+                if (found && !(ref[k] < best)) continue;
+                if (ref[k] > L + r0) continue;
+                if (fabs(m * x0 - y0 + b) / sqrt(1 + m * m) > r0) continue;
+                if (vec_rad(tx - x, ty - y, x0 - x, y0 - y) > kPi / 2) continue;
+                const double m2 = m * m;
+                const double fx = (x0 + m * y0 - m * b) / (m2 + 1);
+                const double fy = (m * x0 + m2 * y0 + b) / (m2 + 1);
+                const double ddx = fx - x0, ddy = fy - y0;
+                const double rd = sqrt(ddx * ddx + ddy * ddy);
+                const double dir = tx - x;
+                const double sg = dir > 0 ? 1.0 : (dir < 0 ? -1.0 : 0.0);
+                const double cross = fx - sg * sqrt(r0 * r0 - rd * rd) / sqrt(m2 + 1);
+                const double lo = x < tx ? x : tx, hi = x < tx ? tx : x;  // min/max(start, term)
+                if (lo <= cross && cross <= hi) {
+                    found = true;
+                    best = ref[k];
+                    const double dis = fabs(cross - x) * sqrt(m2 + 1);
+                    val = dis < p.laser_blind ? p.laser_blind : dis;
+                }
+            }
+            if (!found) {
+                const double dx = x - tx, dy = y - ty;
+                const double dis = sqrt(dx * dx + dy * dy);
+                if (dis > L) val = L;
+                else if (p.laser_blind < dis && dis <= L) val = dis;
+                else val = p.laser_blind;
+            }
+            o[i] = (float)((2 * val / L - 1) * p.static_gain);
+        }
+    }
+    __device__ static __forceinline__ void obs_from(const P &p, const double *s, double e,
+                                                    double eph, float *o) {  // get_state :399-411
+        const double e_max = sqrt(p.map_size[0] * p.map_size[0] + p.map_size[1] * p.map_size[1]) / 2;
+        o[0] = (float)((2 / e_max * e - 1) * p.static_gain);
+        o[1] = (float)((2 / p.v_max * s[V] - 1) * p.static_gain);
+        o[2] = (float)((eph / p.e_phi_max) * p.static_gain);
+        o[3] = (float)((s[OM] / p.omega_max) * p.static_gain);
+        laser(p, s, o + 4);
+    }
+    __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
+        obs_from(p, s, get_e(s), e_phi(s), o);
+    }
+    __device__ static __forceinline__ void ode(const P &p, double al, double aa, const double *x,
+                                               double *d) {  // ode :471-482
+        d[0] = x[2] * cos(x[3]);
+        d[1] = x[2] * sin(x[3]);
+        d[2] = al - p.kf * x[2];
+        d[3] = x[4];
+        d[4] = aa - p.kt * x[4];
+    }
+    __device__ static void step(const P &p, double *s, const float *a, float *on, double &reward,
+                                int &flag, bool &done) {
+        const double al = (double)a[0], aa = (double)a[1], dt = p.dt;
+        const double e_max = sqrt(p.map_size[0] * p.map_size[0] + p.map_size[1] * p.map_size[1]) / 2;
+        // current_state[0..1] in f64 (the shaped reward compares them with next_state's)
+        const double c0 = (2 / e_max * get_e(s) - 1) * p.static_gain;
+        const double c1 = (2 / p.v_max * s[V] - 1) * p.static_gain;
+        double sum[5], t[5], d[5];  // rk44 :484-502, running RK4 sum (bit-identical, see CartPole)
+        ode(p, al, aa, s, d);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = k; t[i] = s[i] + k / 2; }
+        ode(p, al, aa, t, d);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; t[i] = s[i] + k / 2; }
+        ode(p, al, aa, t, d);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; t[i] = s[i] + k; }
+        ode(p, al, aa, t, d);
+        if (p.shaped && s[V] < 0.) {  // demo copy rk44 :496-500: gate on the pre-step velocity
+            s[PHI] = s[PHI] + (sum[PHI] + dt * d[PHI]) / 6;
+            s[OM] = s[OM] + (sum[OM] + dt * d[OM]) / 6;
+            s[V] = 0.;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) s[i] = s[i] + (sum[i] + dt * d[i]) / 6;
+            if (!p.shaped && s[V] < 0.) s[V] = 0.;
+        }
+        s[T] = s[T] + dt;
+        if (s[PHI] > kPi) s[PHI] -= 2 * kPi;
+        if (s[PHI] < -kPi) s[PHI] += 2 * kPi;
+        const double e = get_e(s), eph = e_phi(s);
+        int f = 0;  // is_Terminal :433-450 (later conditions override)
+        if (s[X] > p.map_size[0] || s[X] < 0 || s[Y] > p.map_size[1] || s[Y] < 0) f = 1;
+        if (s[T] > p.time_max) f = 2;
+        const bool success = fabs(e) <= 0.05 && (p.shaped || fabs(s[OM]) < 0.01) && fabs(s[V]) < 0.01;
+        if (success) f = 3;
+        if (collision(p, s)) f = 4;
+        obs_from(p, s, e, eph, on);
+        flag = f;
+        done = f != 0;
+        if (p.shaped) {  // demo copy get_reward :449-473
+            const double n0 = (2 / e_max * e - 1) * p.static_gain;
+            const double n1 = (2 / p.v_max * s[V] - 1) * p.static_gain;
+            const double r1 = -1 - fabs(s[OM]) * 0.1;
+            const double r2 = c0 > n0 + 1e-3 ? 5.0 : (1e-3 + c0 < n0 ? -5.0 : 0.0);
+            const double r3 = fabs(c1) > fabs(n1) + 1e-2 ? 2.0 : (1e-2 + fabs(c1) < fabs(n1) ? -2.0 : 0.0);
+            const double r4 = success ? 500.0 : (f == 4 ? -300.0 : 0.0);
+            reward = r1 + r2 + r3 + r4;
+            return;
+        }
+        const double u_pos = -fabs(e) * p.Q_pos;  // get_reward :452-469
+        const double u_vel = -fabs(s[V]) * p.Q_vel;
+        const double u_phi = e > 0.1 ? -fabs(eph) * p.Q_phi : 0.0;
+        const double u_om = -fabs(s[OM]) * p.Q_omega;
+        double u_psi = 0.;
+        if (f == 1) {
+            const double n_ = (p.time_max - s[T]) / p.dt;
+            u_psi = n_ * (u_pos + u_vel + u_phi + u_om);
+        }
+        reward = u_pos + u_vel + u_phi + u_om + u_psi;
+    }
+    // reset(random=True) :520-557 + map.py:66-174 (generate_circle_obs_training): start/target,
+    // then NOBS circles by rejection sampling, Philox-keyed (seed, counter, env_id, draw)
+    __device__ static void reset(const P &p, double *s, uint64_t seed, uint64_t counter,
+                                 uint64_t env_id) {
+        uint32_t draw = 0;
+        auto u2 = [&](double u[2]) { philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, u); };
+        const double xm = p.map_size[0], ym = p.map_size[1], mg = p.st_margin;
+        double u[2], v[2];
+        u2(u);
+        const double sx = mg + ((xm - mg) - mg) * u[0], sy = mg + ((ym - mg) - mg) * u[1];
+        double tx = sx, ty = sy;
+        for (int k = 0; k < p.max_tries; ++k) {
+            const double dx = tx - sx, dy = ty - sy;
+            if (sqrt(dx * dx + dy * dy) >= p.safety_dis_st) break;
+            u2(u);
+            tx = mg + ((xm - mg) - mg) * u[0];
+            ty = mg + ((ym - mg) - mg) * u[1];
+        }
+        for (int k = 0; k < NOBS; ++k) {
+            double cx = -1000.0 - 10.0 * k, cy = -1000.0, r = p.r_min;  // parked if unplaceable
+            for (int tr = 0; k < p.n_obs && tr < p.max_tries; ++tr) {
+                u2(u);
+                u2(v);
+                const double ccx = 0 + (xm - 0) * u[0], ccy = 0 + (ym - 0) * u[1];
+                const double rr = p.r_min + (p.r_max - p.r_min) * v[0];
+                bool ok = true;
+                double dx = sx - ccx, dy = sy - ccy;
+                if (sqrt(dx * dx + dy * dy) <= rr + p.safety_dis_st) ok = false;
+                dx = tx - ccx; dy = ty - ccy;
+                if (sqrt(dx * dx + dy * dy) <= rr + p.safety_dis_st) ok = false;
+                for (int j = 0; j < k && ok; ++j) {
+                    dx = s[OB + 3 * j] - ccx; dy = s[OB + 3 * j + 1] - ccy;
+                    if (sqrt(dx * dx + dy * dy) <= s[OB + 3 * j + 2] + rr + p.safety_dis_obs) ok = false;
+                }
+                if (ok) { cx = ccx; cy = ccy; r = rr; break; }
+            }
+            s[OB + 3 * k] = cx; s[OB + 3 * k + 1] = cy; s[OB + 3 * k + 2] = r;
+        }
+        u2(u);
+        s[X] = sx; s[Y] = sy; s[V] = 0.; s[PHI] = -kPi + (kPi - -kPi) * u[0]; s[OM] = 0.;
+        s[T] = 0.; s[TX] = tx; s[TY] = ty;
     }
 };
 

@@ -48,6 +48,15 @@ class VecEnv(rl_base):
     def initial_physics(self) -> np.ndarray:
         raise NotImplementedError
 
+    # -- subclass hooks for reset(random=False): the [D][n] device state it restores, and what a
+    # random reset records (the obstacle-avoidance env replays its last random episode start)
+    def _initial_state_tensor(self):
+        init = np.repeat(self.initial_physics().reshape(self._D, 1), self.n_envs, axis=1)
+        return torch.from_numpy(np.ascontiguousarray(init)).to(self.device)
+
+    def _after_random_reset(self, mask):
+        pass
+
     # -- helpers
     def _squeeze(self, x):
         x = x.detach().cpu().numpy()
@@ -85,10 +94,10 @@ class VecEnv(rl_base):
             K.env_reset(self.KIND, self.params, self.state, mask=m, seed=self.seed,
                         counter=self.reset_counter, env_id0=self.env_id0)
             self.reset_counter += 1
+            self._after_random_reset(m)
         else:
-            init = np.repeat(self.initial_physics().reshape(self._D, 1), self.n_envs, axis=1)
             K.env_reset(self.KIND, self.params, self.state, mask=m,
-                        init_state=torch.from_numpy(np.ascontiguousarray(init)).to(self.device))
+                        init_state=self._initial_state_tensor())
         obs = self.get_state()
         self.current_state = obs.copy()
         self.next_state = obs.copy()

@@ -16,6 +16,7 @@ cv2 is absent here and only used for drawing: it is replaced by a no-op module.
 """
 import importlib.util
 import os
+import signal
 import sys
 import types
 
@@ -86,6 +87,12 @@ with quiet():
     mods["ugvb_env"] = load("environment/UGV/UGVBidirectional.py", "ref_ugvb")
     mods["ugvb_ppo2"] = load("demonstration/PPO2/PPO2-4-UGVBidirectional/UGVBidirectional.py",
                              "ref_ugvb_ppo2")
+    mods["ugvoa_env"] = load("environment/UGVForwardObstacleAvoidance/UGVForwardObstacleAvoidance.py",
+                             "ref_ugvoa")
+    mods["ugvoa_ppo2"] = load("demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/"
+                              "UGVForwardObstacleAvoidance.py", "ref_ugvoa_ppo2")
+    mods["ugvoa_dppo2"] = load("demonstration/DPPO2/DPPO2-4-UGVForwardObstacleAvoidance/"
+                               "UGVForwardObstacleAvoidance.py", "ref_ugvoa_dppo2")
     import environment.UavRobust.UavHoverOuterLoop as uav_mod  # noqa: E402
     from environment.UavRobust.uav import uav_param  # noqa: E402
     from environment.UavRobust.FNTSMC import fntsmc_param  # noqa: E402
@@ -558,9 +565,109 @@ def gen_ddpg():
     print("ddpg", {k: float(np.abs(after[k] - before[k]).max()) for k in after})
 
 
+# ---------------------------------------------------------------------------------------------
+# UGV forward obstacle avoidance: maps from the reference's own generator (reset(True)), then
+# teacher-forced states (near obstacles, walls, the target, the time limit, axis-aligned beams)
+# ---------------------------------------------------------------------------------------------
+OA_NOBS = 15
+
+
+def oa_full_state(env):
+    st = [env.pos[0], env.pos[1], env.vel, env.phi, env.omega, env.time, env.target[0],
+          env.target[1]]
+    obs = [[o[1][0], o[1][1], o[2][0]] for o in env.obs]
+    for k in range(len(obs), OA_NOBS):
+        obs.append([-1000.0 - 10.0 * k, -1000.0, 0.2])   # parked slot (never seen, never hit)
+    return st + [v for o in obs for v in o]
+
+
+def _alarm(signum, frame):
+    raise TimeoutError
+
+
+def gen_ugvoa(key, n=400):
+    signal.signal(signal.SIGALRM, _alarm)
+    cls = mods[key].UGVForwardObstacleAvoidance
+    env = None
+    while env is None:
+        try:
+            signal.alarm(2)
+            with quiet():
+                env = cls()
+        except TimeoutError:
+            pass
+        finally:
+            signal.alarm(0)
+    rows = {k: [] for k in ("state", "action", "state_next", "obs_cur", "obs_next", "reward",
+                            "flag", "done")}
+    maps = []
+    for i in range(n):
+        while True:    # the reference's rejection sampler can loop forever (obsNum 15): retry
+            try:
+                signal.alarm(2)
+                with quiet():
+                    env.reset(True)
+                break
+            except TimeoutError:
+                continue
+            finally:
+                signal.alarm(0)
+        obs = env.obs
+        maps.append([[o[1][0], o[1][1], o[2][0]] for o in obs])
+        k = int(rng.integers(0, int(env.time_max / env.dt) + 2))
+        tm = 0.
+        for _ in range(k):
+            tm += env.dt
+        pos = rng.uniform(-0.05, 5.05, 2)
+        vel = rng.uniform(-0.5, 3)
+        phi = rng.uniform(-np.pi, np.pi)
+        om = rng.uniform(-3, 3)
+        j = i % 8
+        if j == 1:     # next to (or just inside) an obstacle: collision / blind beams
+            c = obs[int(rng.integers(0, len(obs)))]
+            ang = rng.uniform(-np.pi, np.pi)
+            d = c[2][0] + env.r_vehicle + rng.uniform(-0.03, 0.05)
+            pos = np.array(c[1]) + d * np.array([np.cos(ang), np.sin(ang)])
+        elif j == 2:   # at the target, slow: success
+            pos = env.target + rng.uniform(-0.04, 0.04, 2); vel = rng.uniform(-0.02, 0.02)
+            om = rng.uniform(-0.02, 0.02)
+        elif j == 3:   # beams exactly axis-aligned (tan of +-pi/2: the |m| >= 1e8 branches)
+            phi = float(rng.choice([0.0, np.pi / 2, -np.pi / 2, np.pi, -np.pi]))
+        elif j == 4:   # near a wall / corner, heading out
+            pos = rng.choice([0.02, 4.98], 2) + rng.uniform(-0.02, 0.02, 2)
+        elif j == 5:   # time limit
+            k = int(rng.integers(int(env.time_max / env.dt) - 3, int(env.time_max / env.dt) + 2))
+            tm = 0.
+            for _ in range(k):
+                tm += env.dt
+        elif j == 6:   # inside the lidar range of several obstacles
+            c = obs[int(rng.integers(0, len(obs)))]
+            pos = np.array(c[1]) + rng.uniform(-1.2, 1.2, 2)
+        a = f32([rng.uniform(-3, 3), rng.uniform(-2 * np.pi, 2 * np.pi)])
+        with quiet():
+            env.pos = pos.copy(); env.vel = vel; env.phi = phi; env.omega = om; env.time = tm
+            rows["state"].append(oa_full_state(env))
+            env.step_update(a)
+        rows["action"].append(a)
+        rows["state_next"].append(oa_full_state(env))
+        rows["obs_cur"].append(env.current_state)
+        rows["obs_next"].append(env.next_state)
+        rows["reward"].append(float(env.reward))
+        rows["flag"].append(env.terminal_flag)
+        rows["done"].append(int(env.is_terminal))
+    out = {k: np.array(v) for k, v in rows.items()}
+    out["action"] = out["action"].astype(np.float32)
+    out["maps"] = np.array(maps)
+    np.savez_compressed(os.path.join(OUT, f"{key}.npz"), **out)
+    print(key, "flags", np.bincount(out["flag"]))
+
+
 if __name__ == "__main__" and len(sys.argv) > 2:   # selected generators only
     for name in sys.argv[2:]:
-        globals()["gen_" + name]()
+        if name.startswith("ugvoa_"):
+            gen_ugvoa(name, n=400 if name == "ugvoa_env" else 300)
+        else:
+            globals()["gen_" + name]()
     sys.exit(0)
 
 if __name__ == "__main__":
@@ -575,6 +682,9 @@ if __name__ == "__main__":
     gen_ugv("ugvb_env", mods["ugvb_env"].UGVBidirectional)
     gen_ugv("ugvb_ppo2", mods["ugvb_ppo2"].UGVBidirectional, n=200)
     gen_uav("uav_hover")
+    gen_ugvoa("ugvoa_env")
+    gen_ugvoa("ugvoa_ppo2", n=300)
+    gen_ugvoa("ugvoa_dppo2", n=300)
     gen_nets()
     gen_gae()
     gen_reward_norm()

@@ -66,6 +66,11 @@ def _random_states(kind, n, rng):
         st[0:2] = rng.uniform(-0.1, 5.1, (2, n)); st[2] = rng.uniform(-0.5, 3, n)
         st[3] = rng.uniform(-np.pi, np.pi, n); st[4] = rng.uniform(-3, 3, n)
         st[5] = rng.integers(0, 500, n) * 0.02
+    elif kind == A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE:   # the reset maps, any pose in/near them
+        st[0:2] = rng.uniform(-0.1, 5.1, (2, n)); st[2] = rng.uniform(-0.5, 3, n)
+        st[3] = rng.uniform(-np.pi, np.pi, n); st[4] = rng.uniform(-3, 3, n)
+        st[5] = rng.integers(0, 152, n) * 0.1
+        st[3, ::7] = rng.choice([0.0, np.pi / 2, -np.pi / 2, np.pi, -np.pi], st[3, ::7].shape)
     else:
         st[0:3] = rng.uniform(-4.9, 4.9, (3, n)); st[2] = rng.uniform(0.05, 4.9, n)
         st[3:6] = rng.uniform(-2, 2, (3, n)); st[6:9] = rng.uniform(-0.6, 0.6, (3, n))

@@ -21,6 +21,9 @@ ENV_CASES = [
     ("ugvb_ppo2", A.RLP_ENV_UGV_BIDIRECTIONAL,
      lambda: A.ugv_params(A.RLP_ENV_UGV_BIDIRECTIONAL, "ppo2")),
     ("uav_hover", A.RLP_ENV_UAV_HOVER_OUTER_LOOP, A.uav_hover_params),
+    ("ugvoa_env", A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE, lambda: A.ugv_oa_params("env")),
+    ("ugvoa_ppo2", A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE, lambda: A.ugv_oa_params("ppo2")),
+    ("ugvoa_dppo2", A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE, lambda: A.ugv_oa_params("dppo2")),
 ]
 
 
@@ -167,3 +170,46 @@ def test_reward_norm_batched_equals_merged_stats():
     assert rms[0] == allr.size
     np.testing.assert_allclose(rms[1], allr.mean(), rtol=1e-12)
     np.testing.assert_allclose(rms[3], allr.std(), rtol=1e-10)
+
+
+def check_oa_maps(state, p):
+    """Structural properties of UGVForwardObstacleAvoidance reset maps ([D][n] physics state)
+    against map.py:66-174's legality rules (shared with the GPU reset test)."""
+    n = state.shape[1]
+    S, T = state[0:2], state[6:8]
+    m = p.st_margin
+    assert (S >= m).all() and (S[0] <= p.map_size[0] - m).all() and (S[1] <= p.map_size[1] - m).all()
+    assert (np.hypot(*(T - S)) >= p.safety_dis_st).all()
+    assert (np.abs(state[3]) <= np.pi).all() and (state[[2, 4, 5]] == 0).all()
+    C = state[8:].reshape(A.RLP_UGVOA_NOBS, 3, n)
+    placed = C[:, 0] > -500
+    assert not placed[p.n_obs:].any()
+    for k in range(p.n_obs):
+        ok = placed[k]
+        c, r = C[k, :2][:, ok], C[k, 2][ok]
+        assert ((r >= p.r_min) & (r <= p.r_max)).all()
+        assert (c >= 0).all() and (c[0] <= p.map_size[0]).all() and (c[1] <= p.map_size[1]).all()
+        assert (np.hypot(*(S[:, ok] - c)) > r + p.safety_dis_st).all()
+        assert (np.hypot(*(T[:, ok] - c)) > r + p.safety_dis_st).all()
+        for j in range(k):
+            both = ok & placed[j]
+            d = np.hypot(*(C[j, :2][:, both] - C[k, :2][:, both]))
+            assert (d > C[j, 2][both] + C[k, 2][both] + p.safety_dis_obs).all()
+    return placed
+
+
+@pytest.mark.parametrize("variant", ["env", "dppo2"])
+def test_ugvoa_reset_maps_legal(golden, variant):
+    """The Philox rejection sampler obeys the reference generator's legality rules; with the
+    default bound every obstacle of a 10-obstacle map is placed, and the radius distribution
+    matches the reference's own maps (golden 'maps', drawn by map.py)."""
+    p = A.ugv_oa_params(variant)
+    n = 400
+    st = np.zeros((A.RLP_UGVOA_D, n))
+    oracle.env_reset(A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE, p, st, seed=7, counter=3)
+    placed = check_oa_maps(st, p)
+    frac = placed[:p.n_obs].mean()
+    assert frac == 1.0 if variant == "env" else frac > 0.97
+    ref_r = golden("ugvoa_" + variant)["maps"][..., 2].ravel()
+    ours = st[10::3][:p.n_obs][placed[:p.n_obs]].ravel()
+    assert abs(ours.mean() - ref_r.mean()) < 0.02
