@@ -588,8 +588,9 @@ static double oa_dis(double x1, double y1, double x2, double y2) { /* dis_two_po
     return sqrt(dx * dx + dy * dy);
 }
 
+/* obstacle slots >= n_obs are not part of the map (reset parks them outside it) */
 static int oa_collision(const rlp_ugv_oa_params *p, const double *s) { /* :261-272 */
-    for (int k = 0; k < OA_NOBS; ++k)
+    for (int k = 0; k < p->n_obs; ++k)
         if (oa_dis(s[0], s[1], s[8 + 3 * k], s[9 + 3 * k]) <= s[10 + 3 * k] + p->r_vehicle) return 1;
     return 0;
 }
@@ -603,11 +604,12 @@ static void oa_laser(const rlp_ugv_oa_params *p, const double *s, double *laser)
     }
     double ref[OA_NOBS];
     int order[OA_NOBS];
-    for (int k = 0; k < OA_NOBS; ++k) {
+    int nob = p->n_obs;
+    for (int k = 0; k < nob; ++k) {
         ref[k] = oa_dis(x, y, s[8 + 3 * k], s[9 + 3 * k]);
         order[k] = k;
     }
-    for (int k = 1; k < OA_NOBS; ++k) { /* stable ascending sort */
+    for (int k = 1; k < nob; ++k) { /* stable ascending sort */
         int v = order[k], j = k - 1;
         while (j >= 0 && ref[order[j]] > ref[v]) { order[j + 1] = order[j]; --j; }
         order[j + 1] = v;
@@ -651,7 +653,7 @@ static void oa_laser(const rlp_ugv_oa_params *p, const double *s, double *laser)
             }
         }
         int found = 0;
-        for (int kk = 0; kk < OA_NOBS; ++kk) {
+        for (int kk = 0; kk < nob; ++kk) {
             int k = order[kk];
             double x0 = s[8 + 3 * k], y0 = s[9 + 3 * k], r0 = s[10 + 3 * k];
             if (ref[k] > L + r0) continue;
@@ -760,35 +762,41 @@ static void oa_step(const rlp_ugv_oa_params *p, double *s, const float *a, float
     *reward = u_pos + u_vel + u_phi + u_om + u_psi;
 }
 
-/* reset(random=True) :520-557 + map.py generate_circle_obs_training, Philox tag 0x400 + draw */
+/* reset(random=True) :520-557 + map.py:66-174 generate_circle_obs_training: sequential rejection
+ * sampling. Each draw is Philox-keyed by what it is: start 0x40000000, target try t 0x41000000 + t,
+ * obstacle k try t 0x42000000 / 0x42800000 + (k << 16) + t, heading 0x43000000. */
+static void oa_draw_point(const rlp_ugv_oa_params *p, uint64_t seed, uint64_t counter,
+                          uint64_t id, uint32_t tag, double *x, double *y) { /* map.py:66-74 */
+    double u[2], mg = p->st_margin;
+    philox_u01_f64x2(seed, counter, id, tag, u);
+    *x = mg + ((p->map_size[0] - mg) - mg) * u[0];
+    *y = mg + ((p->map_size[1] - mg) - mg) * u[1];
+}
+
 static void oa_reset(const rlp_ugv_oa_params *p, double *s, uint64_t seed, uint64_t counter,
                      uint64_t env_id) {
-    uint32_t draw = 0;
-    double u[2], v[2], xm = p->map_size[0], ym = p->map_size[1], mg = p->st_margin;
-    philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, u);
-    double sx = mg + ((xm - mg) - mg) * u[0], sy = mg + ((ym - mg) - mg) * u[1];
-    double tx = sx, ty = sy;
-    for (int k = 0; k < p->max_tries && oa_dis(tx, ty, sx, sy) < p->safety_dis_st; ++k) {
-        philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, u);
-        tx = mg + ((xm - mg) - mg) * u[0];
-        ty = mg + ((ym - mg) - mg) * u[1];
-    }
+    double sx, sy, tx, ty, u[2], v[2];
+    oa_draw_point(p, seed, counter, env_id, 0x40000000u, &sx, &sy);
+    tx = sx; ty = sy;
+    for (int t = 0; t < p->max_tries && oa_dis(tx, ty, sx, sy) < p->safety_dis_st; ++t)
+        oa_draw_point(p, seed, counter, env_id, 0x41000000u + (uint32_t)t, &tx, &ty);
     for (int k = 0; k < OA_NOBS; ++k) {
-        double cx = -1000.0 - 10.0 * k, cy = -1000.0, r = p->r_min;
-        for (int tr = 0; k < p->n_obs && tr < p->max_tries; ++tr) {
-            philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, u);
-            philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, v);
-            double ccx = 0 + (xm - 0) * u[0], ccy = 0 + (ym - 0) * u[1];
+        double cx = -1000.0 - 10.0 * k, cy = -1000.0, r = p->r_min; /* parked */
+        for (int t = 0; k < p->n_obs && t < p->max_tries; ++t) {
+            uint32_t kt = ((uint32_t)k << 16) + (uint32_t)t;
+            philox_u01_f64x2(seed, counter, env_id, 0x42000000u + kt, u);
+            philox_u01_f64x2(seed, counter, env_id, 0x42800000u + kt, v);
+            double ccx = 0 + (p->map_size[0] - 0) * u[0], ccy = 0 + (p->map_size[1] - 0) * u[1];
             double rr = p->r_min + (p->r_max - p->r_min) * v[0];
             int ok = oa_dis(sx, sy, ccx, ccy) > rr + p->safety_dis_st &&
                      oa_dis(tx, ty, ccx, ccy) > rr + p->safety_dis_st;
-            for (int j = 0; j < k && ok; ++j)
+            for (int j = 0; j < k && ok; ++j) /* __is_new_obs_in_obs: r_existing + r_new + safety */
                 if (oa_dis(s[8 + 3 * j], s[9 + 3 * j], ccx, ccy) <= s[10 + 3 * j] + rr + p->safety_dis_obs) ok = 0;
             if (ok) { cx = ccx; cy = ccy; r = rr; break; }
         }
         s[8 + 3 * k] = cx; s[9 + 3 * k] = cy; s[10 + 3 * k] = r;
     }
-    philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, u);
+    philox_u01_f64x2(seed, counter, env_id, 0x43000000u, u);
     s[0] = sx; s[1] = sy; s[2] = 0.; s[3] = -PI + (PI - -PI) * u[0]; s[4] = 0.; s[5] = 0.;
     s[6] = tx; s[7] = ty;
 }

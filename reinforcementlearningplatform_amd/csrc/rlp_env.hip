@@ -101,6 +101,16 @@ __global__ void __launch_bounds__(256) env_reset_kernel(typename Env<KIND>::P p,
     for (int d = 0; d < E::D; ++d) state[(size_t)d * n + i] = s[d];
 }
 
+// UGVForwardObstacleAvoidance step / observe: rlp_lidar.hip
+int launch_ugvoa_step(const rlp_ugv_oa_params &p, double *state, int n, const float *action,
+                      float *obs_cur, float *obs_next, double *reward, int32_t *flag,
+                      uint8_t *done, hipStream_t st);
+int launch_ugvoa_observe(const rlp_ugv_oa_params &p, const double *state, int n, float *obs,
+                         hipStream_t st);
+int launch_ugvoa_reset(const rlp_ugv_oa_params &p, double *state, int n, const uint8_t *mask,
+                       const double *init, uint64_t seed, uint64_t counter, uint64_t env_id0,
+                       hipStream_t st);
+
 // kind -> template dispatch
 template <typename F>
 int dispatch_kind(int kind, F &&f) {
@@ -164,10 +174,15 @@ int rlp_env_step(int kind, const void *params, double *state, int n, const float
     return dispatch_kind(kind, [&](auto k) {
         constexpr int K = decltype(k)::value;
         const auto &p = *static_cast<const typename Env<K>::P *>(params);
-        env_step_kernel<K><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
-            p, state, n, action, obs_cur, obs_next, reward, flag, done);
-        RLP_CHECK_LAUNCH("rlp_env_step");
-        return RLP_OK;
+        if constexpr (K == RLP_ENV_UGV_OBSTACLE_AVOIDANCE) {  // beam-per-lane lidar kernel
+            return launch_ugvoa_step(p, state, n, action, obs_cur, obs_next, reward, flag, done,
+                                     as_stream(stream));
+        } else {
+            env_step_kernel<K><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
+                p, state, n, action, obs_cur, obs_next, reward, flag, done);
+            RLP_CHECK_LAUNCH("rlp_env_step");
+            return RLP_OK;
+        }
     });
 }
 
@@ -179,9 +194,13 @@ int rlp_env_observe(int kind, const void *params, const double *state, int n, fl
     return dispatch_kind(kind, [&](auto k) {
         constexpr int K = decltype(k)::value;
         const auto &p = *static_cast<const typename Env<K>::P *>(params);
-        env_observe_kernel<K><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(p, state, n, obs);
-        RLP_CHECK_LAUNCH("rlp_env_observe");
-        return RLP_OK;
+        if constexpr (K == RLP_ENV_UGV_OBSTACLE_AVOIDANCE) {
+            return launch_ugvoa_observe(p, state, n, obs, as_stream(stream));
+        } else {
+            env_observe_kernel<K><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(p, state, n, obs);
+            RLP_CHECK_LAUNCH("rlp_env_observe");
+            return RLP_OK;
+        }
     });
 }
 
@@ -194,10 +213,15 @@ int rlp_env_reset(int kind, const void *params, double *state, int n, const uint
     return dispatch_kind(kind, [&](auto k) {
         constexpr int K = decltype(k)::value;
         const auto &p = *static_cast<const typename Env<K>::P *>(params);
-        env_reset_kernel<K><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
-            p, state, n, mask, init_state, seed, counter, env_id0);
-        RLP_CHECK_LAUNCH("rlp_env_reset");
-        return RLP_OK;
+        if constexpr (K == RLP_ENV_UGV_OBSTACLE_AVOIDANCE) {  // wave-per-env map generator
+            return launch_ugvoa_reset(p, state, n, mask, init_state, seed, counter, env_id0,
+                                      as_stream(stream));
+        } else {
+            env_reset_kernel<K><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
+                p, state, n, mask, init_state, seed, counter, env_id0);
+            RLP_CHECK_LAUNCH("rlp_env_reset");
+            return RLP_OK;
+        }
     });
 }
 

@@ -634,98 +634,132 @@ template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
         const double ex = s[TX] - s[X], ey = s[TY] - s[Y];
         return sqrt(ex * ex + ey * ey);
     }
-    __device__ static __forceinline__ bool collision(const P &p, const double *s) {  // :261-272
+    // collision_check :261-272 over the first n_obs slots; ob(k, x0, y0, r0) fetches obstacle k
+    template <class Ob>
+    __device__ static __forceinline__ bool collision_at(const P &p, double x, double y, Ob &&ob) {
 #pragma unroll
         for (int k = 0; k < NOBS; ++k) {
-            const double dx = s[X] - s[OB + 3 * k], dy = s[Y] - s[OB + 3 * k + 1];
-            if (sqrt(dx * dx + dy * dy) <= s[OB + 3 * k + 2] + p.r_vehicle) return true;
+            if (k >= p.n_obs) continue;
+            double x0, y0, r0;
+            ob(k, x0, y0, r0);
+            const double dx = x - x0, dy = y - y0;
+            if (sqrt(dx * dx + dy * dy) <= r0 + p.r_vehicle) return true;
         }
         return false;
     }
-    // writes get_state's normalised beams (2 * laser / laserDis - 1) * gain into o[0..NL)
+    __device__ static __forceinline__ bool collision(const P &p, const double *s) {
+        return collision_at(p, s[X], s[Y], [&](int k, double &x0, double &y0, double &r0) {
+            x0 = s[OB + 3 * k]; y0 = s[OB + 3 * k + 1]; r0 = s[OB + 3 * k + 2];
+        });
+    }
+    // per-pose part of get_fake_laser: beam angles (np.linspace(phi - R, phi + R, NL): i * step +
+    // start, last element = stop) and the four corner angles that pick a beam's wall
+    struct Pose {
+        double x, y, start, stop, step, th1, th2, th3, th4;
+    };
+    __device__ static __forceinline__ Pose pose(const P &p, double x, double y, double phi) {
+        const double xm = p.map_size[0], ym = p.map_size[1];
+        Pose q;
+        q.x = x; q.y = y;
+        q.start = phi - p.laser_range;
+        q.stop = phi + p.laser_range;
+        q.step = (q.stop - q.start) / (NL - 1);
+        q.th1 = vec_rad(1, 0, xm - x, ym - y);
+        q.th2 = vec_rad(1, 0, 0 - x, ym - y);
+        q.th3 = -vec_rad(1, 0, 0 - x, 0 - y);
+        q.th4 = -vec_rad(1, 0, xm - x, 0 - y);
+        return q;
+    }
+    // beam i of get_fake_laser :283-397 (no collision): distance to the first circle hit, else
+    // to the wall / range end. The reference walks the obstacles in argsort(ref_dis) order
+    // (stable for <= 16 values) and stops at the first hit; the same result is the hit with the
+    // smallest (ref_dis, index), found here without sorting. ob(k, x0, y0, r0, ref) fetches
+    // obstacle k and its distance to the vehicle.
+    template <class Ob>
+    __device__ static __forceinline__ double beam(const P &p, const Pose &q, int i, Ob &&ob) {
+        const double x = q.x, y = q.y, xm = p.map_size[0], ym = p.map_size[1], L = p.laser_dis;
+        double ph = i == NL - 1 ? q.stop : (double)i * q.step + q.start;
+        if (ph > kPi) ph -= 2 * kPi;
+        if (ph < -kPi) ph += 2 * kPi;
+        const double m = tan(ph), b = y - m * x;
+        const double sq = sqrt(1 + m * m);
+        const double cosT = fabs(m) / sq, sinT = 1 / sq;
+        double tx, ty;
+        if (q.th4 < ph && ph <= q.th1) {
+            tx = xm; ty = m * xm + b;
+            const double t = x + L / sq;
+            if (t < xm) { tx = t; ty = m >= 0 ? y + cosT * L : y - cosT * L; }
+        } else if (q.th1 < ph && ph <= q.th2) {
+            if (fabs(m) < 1e8) { tx = (ym - b) / m; ty = ym; } else { tx = x; ty = ym; }
+            const double t = y + fabs(m) * L / sq;
+            if (t < ym) { tx = m >= 0 ? x + L * sinT : x - L * sinT; ty = t; }
+        } else if (q.th3 < ph && ph <= q.th4) {
+            if (fabs(m) < 1e8) { tx = -b / m; ty = 0; } else { tx = x; ty = 0; }
+            const double t = y - fabs(m) * L / sq;
+            if (t > 0) { tx = m >= 0 ? x - L * sinT : x + L * sinT; ty = t; }
+        } else {
+            tx = 0; ty = b;
+            const double t = x - L / sq;
+            if (t > 0) { tx = t; ty = m >= 0 ? y - cosT * L : y + cosT * L; }
+        }
+        const double m2 = m * m;
+        const double dir = tx - x;
+        const double sg = dir > 0 ? 1.0 : (dir < 0 ? -1.0 : 0.0);
+        const double lo = x < tx ? x : tx, hi = x < tx ? tx : x;  // min/max(start, terminal)
+        bool found = false;
+        double val = 0, best = 0;
+#pragma unroll
+        for (int k = 0; k < NOBS; ++k) {
+            if (k >= p.n_obs) continue;
+            double x0, y0, r0, ref;
+            ob(k, x0, y0, r0, ref);
+            if (found && !(ref < best)) continue;
+            if (ref > L + r0) continue;
+            if (fabs(m * x0 - y0 + b) / sq > r0) continue;
+            if (vec_rad(tx - x, ty - y, x0 - x, y0 - y) > kPi / 2) continue;
+            const double fx = (x0 + m * y0 - m * b) / (m2 + 1);
+            const double fy = (m * x0 + m2 * y0 + b) / (m2 + 1);
+            const double ddx = fx - x0, ddy = fy - y0;
+            const double rd = sqrt(ddx * ddx + ddy * ddy);
+            const double cross = fx - sg * sqrt(r0 * r0 - rd * rd) / sqrt(m2 + 1);
+            if (lo <= cross && cross <= hi) {
+                found = true;
+                best = ref;
+                const double dis = fabs(cross - x) * sqrt(m2 + 1);
+                val = dis < p.laser_blind ? p.laser_blind : dis;
+            }
+        }
+        if (!found) {
+            const double dx = x - tx, dy = y - ty;
+            const double dis = sqrt(dx * dx + dy * dy);
+            if (dis > L) val = L;
+            else if (p.laser_blind < dis && dis <= L) val = dis;
+            else val = p.laser_blind;
+        }
+        return val;
+    }
+    // get_state's normalised beam value
+    __device__ static __forceinline__ float beam_obs(const P &p, double dis) {
+        return (float)((2 * dis / p.laser_dis - 1) * p.static_gain);
+    }
+    // all beams from the register-resident state (generic env kernels); o[0..NL)
     __device__ static void laser(const P &p, const double *s, float *o) {  // :274-397
-        const double x = s[X], y = s[Y], xm = p.map_size[0], ym = p.map_size[1];
         if (collision(p, s)) {
-            const float v = (float)((2 * p.laser_blind / p.laser_dis - 1) * p.static_gain);
+            const float v = beam_obs(p, p.laser_blind);
             for (int i = 0; i < NL; ++i) o[i] = v;
             return;
         }
-        // The reference walks the obstacles in argsort(ref_dis) order (stable for 10 values) and
-        // stops at the first hit; the same result is the hit with the smallest (ref_dis, index),
-        // which a fixed, unrolled obstacle loop finds without sorting or dynamic indexing.
         double ref[NOBS];
 #pragma unroll
         for (int k = 0; k < NOBS; ++k) {
-            const double dx = x - s[OB + 3 * k], dy = y - s[OB + 3 * k + 1];
+            const double dx = s[X] - s[OB + 3 * k], dy = s[Y] - s[OB + 3 * k + 1];
             ref[k] = sqrt(dx * dx + dy * dy);
         }
-        // np.linspace(phi - R, phi + R, NL): i * step + start, last element = stop
-        const double start = s[PHI] - p.laser_range, stop = s[PHI] + p.laser_range;
-        const double step = (stop - start) / (NL - 1);
-        const double theta1 = vec_rad(1, 0, xm - x, ym - y);
-        const double theta2 = vec_rad(1, 0, 0 - x, ym - y);
-        const double theta3 = -vec_rad(1, 0, 0 - x, 0 - y);
-        const double theta4 = -vec_rad(1, 0, xm - x, 0 - y);
-        const double L = p.laser_dis;
-        for (int i = 0; i < NL; ++i) {
-            double ph = i == NL - 1 ? stop : (double)i * step + start;
-            if (ph > kPi) ph -= 2 * kPi;
-            if (ph < -kPi) ph += 2 * kPi;
-            const double m = tan(ph), b = y - m * x;
-            const double sq = sqrt(1 + m * m);
-            const double cosT = fabs(m) / sq, sinT = 1 / sq;
-            double tx, ty;
-            if (theta4 < ph && ph <= theta1) {
-                tx = xm; ty = m * xm + b;
-                const double t = x + L / sq;
-                if (t < xm) { tx = t; ty = m >= 0 ? y + cosT * L : y - cosT * L; }
-            } else if (theta1 < ph && ph <= theta2) {
-                if (fabs(m) < 1e8) { tx = (ym - b) / m; ty = ym; } else { tx = x; ty = ym; }
-                const double t = y + fabs(m) * L / sq;
-                if (t < ym) { tx = m >= 0 ? x + L * sinT : x - L * sinT; ty = t; }
-            } else if (theta3 < ph && ph <= theta4) {
-                if (fabs(m) < 1e8) { tx = -b / m; ty = 0; } else { tx = x; ty = 0; }
-                const double t = y - fabs(m) * L / sq;
-                if (t > 0) { tx = m >= 0 ? x - L * sinT : x + L * sinT; ty = t; }
-            } else {
-                tx = 0; ty = b;
-                const double t = x - L / sq;
-                if (t > 0) { tx = t; ty = m >= 0 ? y - cosT * L : y + cosT * L; }
-            }
-            bool found = false;
-            double val = 0, best = 0;
-#pragma unroll
-            for (int k = 0; k < NOBS; ++k) {
-                const double x0 = s[OB + 3 * k], y0 = s[OB + 3 * k + 1], r0 = s[OB + 3 * k + 2];
-                if (found && !(ref[k] < best)) continue;
-                if (ref[k] > L + r0) continue;
-                if (fabs(m * x0 - y0 + b) / sqrt(1 + m * m) > r0) continue;
-                if (vec_rad(tx - x, ty - y, x0 - x, y0 - y) > kPi / 2) continue;
-                const double m2 = m * m;
-                const double fx = (x0 + m * y0 - m * b) / (m2 + 1);
-                const double fy = (m * x0 + m2 * y0 + b) / (m2 + 1);
-                const double ddx = fx - x0, ddy = fy - y0;
-                const double rd = sqrt(ddx * ddx + ddy * ddy);
-                const double dir = tx - x;
-                const double sg = dir > 0 ? 1.0 : (dir < 0 ? -1.0 : 0.0);
-                const double cross = fx - sg * sqrt(r0 * r0 - rd * rd) / sqrt(m2 + 1);
-                const double lo = x < tx ? x : tx, hi = x < tx ? tx : x;  // min/max(start, term)
-                if (lo <= cross && cross <= hi) {
-                    found = true;
-                    best = ref[k];
-                    const double dis = fabs(cross - x) * sqrt(m2 + 1);
-                    val = dis < p.laser_blind ? p.laser_blind : dis;
-                }
-            }
-            if (!found) {
-                const double dx = x - tx, dy = y - ty;
-                const double dis = sqrt(dx * dx + dy * dy);
-                if (dis > L) val = L;
-                else if (p.laser_blind < dis && dis <= L) val = dis;
-                else val = p.laser_blind;
-            }
-            o[i] = (float)((2 * val / L - 1) * p.static_gain);
-        }
+        const Pose q = pose(p, s[X], s[Y], s[PHI]);
+        for (int i = 0; i < NL; ++i)
+            o[i] = beam_obs(p, beam(p, q, i, [&](int k, double &x0, double &y0, double &r0, double &rf) {
+                x0 = s[OB + 3 * k]; y0 = s[OB + 3 * k + 1]; r0 = s[OB + 3 * k + 2]; rf = ref[k];
+            }));
     }
     __device__ static __forceinline__ void obs_from(const P &p, const double *s, double e,
                                                     double eph, float *o) {  // get_state :399-411
@@ -735,6 +769,15 @@ template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
         o[2] = (float)((eph / p.e_phi_max) * p.static_gain);
         o[3] = (float)((s[OM] / p.omega_max) * p.static_gain);
         laser(p, s, o + 4);
+    }
+    // get_state's first four components (e, vel, e_phi, omega)
+    __device__ static __forceinline__ void obs_head(const P &p, const double *s, double e,
+                                                    double eph, float *o) {
+        const double e_max = sqrt(p.map_size[0] * p.map_size[0] + p.map_size[1] * p.map_size[1]) / 2;
+        o[0] = (float)((2 / e_max * e - 1) * p.static_gain);
+        o[1] = (float)((2 / p.v_max * s[V] - 1) * p.static_gain);
+        o[2] = (float)((eph / p.e_phi_max) * p.static_gain);
+        o[3] = (float)((s[OM] / p.omega_max) * p.static_gain);
     }
     __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
         obs_from(p, s, get_e(s), e_phi(s), o);
@@ -747,8 +790,12 @@ template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
         d[3] = x[4];
         d[4] = aa - p.kt * x[4];
     }
-    __device__ static void step(const P &p, double *s, const float *a, float *on, double &reward,
-                                int &flag, bool &done) {
+    // dynamics, terminal flag and reward of step_update (rk44 -> is_Terminal -> get_reward) on
+    // s[0..8); coll(x, y) is collision_check at the new pose. Returns e and e_phi for get_state.
+    template <class Coll>
+    __device__ static __forceinline__ void step_core(const P &p, double *s, const float *a,
+                                                     Coll &&coll, double &reward, int &flag,
+                                                     bool &done, double &e_out, double &eph_out) {
         const double al = (double)a[0], aa = (double)a[1], dt = p.dt;
         const double e_max = sqrt(p.map_size[0] * p.map_size[0] + p.map_size[1] * p.map_size[1]) / 2;
         // current_state[0..1] in f64 (the shaped reward compares them with next_state's)
@@ -783,8 +830,9 @@ template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
         if (s[T] > p.time_max) f = 2;
         const bool success = fabs(e) <= 0.05 && (p.shaped || fabs(s[OM]) < 0.01) && fabs(s[V]) < 0.01;
         if (success) f = 3;
-        if (collision(p, s)) f = 4;
-        obs_from(p, s, e, eph, on);
+        if (coll(s[X], s[Y])) f = 4;
+        e_out = e;
+        eph_out = eph;
         flag = f;
         done = f != 0;
         if (p.shaped) {  // demo copy get_reward :449-473
@@ -808,45 +856,93 @@ template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
         }
         reward = u_pos + u_vel + u_phi + u_om + u_psi;
     }
-    // reset(random=True) :520-557 + map.py:66-174 (generate_circle_obs_training): start/target,
-    // then NOBS circles by rejection sampling, Philox-keyed (seed, counter, env_id, draw)
+    __device__ static void step(const P &p, double *s, const float *a, float *on, double &reward,
+                                int &flag, bool &done) {
+        double e, eph;
+        step_core(p, s, a, [&](double x, double y) {
+            return collision_at(p, x, y, [&](int k, double &x0, double &y0, double &r0) {
+                x0 = s[OB + 3 * k]; y0 = s[OB + 3 * k + 1]; r0 = s[OB + 3 * k + 2];
+            });
+        }, reward, flag, done, e, eph);
+        obs_from(p, s, e, eph, on);
+    }
+    // reset(random=True) :520-557 + map.py:66-174 (generate_circle_obs_training). Every draw is
+    // Philox-keyed by what it is — (seed, counter, env_id, tag(obstacle k, try t)) — not by how
+    // many draws came before, so a wave can test 64 tries of one obstacle at once and keep the
+    // first legal one (rlp_lidar.hip oa_reset_kernel) with the same result as this sequential
+    // rejection sampler. Requires max_tries <= 65535.
+    static constexpr uint32_t kTagStart = 0x40000000u, kTagTarget = 0x41000000u,
+                              kTagObs = 0x42000000u, kTagObsR = 0x42800000u, kTagPhi = 0x43000000u;
+    // map.py:66-74: U([0.3, 0.3], [xMax - 0.3, yMax - 0.3])
+    __device__ static __forceinline__ void draw_point(const P &p, uint64_t seed, uint64_t counter,
+                                                      uint64_t id, uint32_t tag, double &x,
+                                                      double &y) {
+        const double mg = p.st_margin;
+        double u[2];
+        philox_u01_f64x2(seed, counter, id, tag, u);
+        x = mg + ((p.map_size[0] - mg) - mg) * u[0];
+        y = mg + ((p.map_size[1] - mg) - mg) * u[1];
+    }
+    // map.py:76-80: center ~ U([0, 0], [xMax, yMax]), r ~ U(rMin, rMax)
+    __device__ static __forceinline__ void draw_obstacle(const P &p, uint64_t seed,
+                                                         uint64_t counter, uint64_t id, int k,
+                                                         int t, double &cx, double &cy,
+                                                         double &r) {
+        const uint32_t kt = ((uint32_t)k << 16) + (uint32_t)t;
+        double u[2], v[2];
+        philox_u01_f64x2(seed, counter, id, kTagObs + kt, u);
+        philox_u01_f64x2(seed, counter, id, kTagObsR + kt, v);
+        cx = 0 + (p.map_size[0] - 0) * u[0];
+        cy = 0 + (p.map_size[1] - 0) * u[1];
+        r = p.r_min + (p.r_max - p.r_min) * v[0];
+    }
+    // map.py:113-127 __is_obs_legal / __is_new_obs_in_obs for a circle against start, target and
+    // the k obstacles placed before it (ob(j, x0, y0, r0))
+    template <class Ob>
+    __device__ static __forceinline__ bool legal(const P &p, double sx, double sy, double tx,
+                                                 double ty, double cx, double cy, double r, int k,
+                                                 Ob &&ob) {
+        double dx = sx - cx, dy = sy - cy;
+        if (sqrt(dx * dx + dy * dy) <= r + p.safety_dis_st) return false;
+        dx = tx - cx; dy = ty - cy;
+        if (sqrt(dx * dx + dy * dy) <= r + p.safety_dis_st) return false;
+        for (int j = 0; j < k; ++j) {
+            double x0, y0, r0;
+            ob(j, x0, y0, r0);
+            dx = x0 - cx; dy = y0 - cy;
+            if (sqrt(dx * dx + dy * dy) <= r0 + r + p.safety_dis_obs) return false;
+        }
+        return true;
+    }
+    __device__ static __forceinline__ double parked_x(int k) { return -1000.0 - 10.0 * k; }
+    static constexpr double kParkedY = -1000.0;
     __device__ static void reset(const P &p, double *s, uint64_t seed, uint64_t counter,
                                  uint64_t env_id) {
-        uint32_t draw = 0;
-        auto u2 = [&](double u[2]) { philox_u01_f64x2(seed, counter, env_id, 0x400u + draw++, u); };
-        const double xm = p.map_size[0], ym = p.map_size[1], mg = p.st_margin;
-        double u[2], v[2];
-        u2(u);
-        const double sx = mg + ((xm - mg) - mg) * u[0], sy = mg + ((ym - mg) - mg) * u[1];
-        double tx = sx, ty = sy;
-        for (int k = 0; k < p.max_tries; ++k) {
+        double sx, sy;
+        draw_point(p, seed, counter, env_id, kTagStart, sx, sy);
+        double tx = sx, ty = sy;  // map.py:68-73: terminal = start; redraw while too close
+        for (int t = 0; t < p.max_tries; ++t) {
             const double dx = tx - sx, dy = ty - sy;
             if (sqrt(dx * dx + dy * dy) >= p.safety_dis_st) break;
-            u2(u);
-            tx = mg + ((xm - mg) - mg) * u[0];
-            ty = mg + ((ym - mg) - mg) * u[1];
+            draw_point(p, seed, counter, env_id, kTagTarget + (uint32_t)t, tx, ty);
         }
         for (int k = 0; k < NOBS; ++k) {
-            double cx = -1000.0 - 10.0 * k, cy = -1000.0, r = p.r_min;  // parked if unplaceable
-            for (int tr = 0; k < p.n_obs && tr < p.max_tries; ++tr) {
-                u2(u);
-                u2(v);
-                const double ccx = 0 + (xm - 0) * u[0], ccy = 0 + (ym - 0) * u[1];
-                const double rr = p.r_min + (p.r_max - p.r_min) * v[0];
-                bool ok = true;
-                double dx = sx - ccx, dy = sy - ccy;
-                if (sqrt(dx * dx + dy * dy) <= rr + p.safety_dis_st) ok = false;
-                dx = tx - ccx; dy = ty - ccy;
-                if (sqrt(dx * dx + dy * dy) <= rr + p.safety_dis_st) ok = false;
-                for (int j = 0; j < k && ok; ++j) {
-                    dx = s[OB + 3 * j] - ccx; dy = s[OB + 3 * j + 1] - ccy;
-                    if (sqrt(dx * dx + dy * dy) <= s[OB + 3 * j + 2] + rr + p.safety_dis_obs) ok = false;
+            double cx = parked_x(k), cy = kParkedY, r = p.r_min;  // parked if unplaceable
+            for (int t = 0; k < p.n_obs && t < p.max_tries; ++t) {
+                double ccx, ccy, rr;
+                draw_obstacle(p, seed, counter, env_id, k, t, ccx, ccy, rr);
+                if (legal(p, sx, sy, tx, ty, ccx, ccy, rr, k,
+                          [&](int j, double &x0, double &y0, double &r0) {
+                              x0 = s[OB + 3 * j]; y0 = s[OB + 3 * j + 1]; r0 = s[OB + 3 * j + 2];
+                          })) {
+                    cx = ccx; cy = ccy; r = rr;
+                    break;
                 }
-                if (ok) { cx = ccx; cy = ccy; r = rr; break; }
             }
             s[OB + 3 * k] = cx; s[OB + 3 * k + 1] = cy; s[OB + 3 * k + 2] = r;
         }
-        u2(u);
+        double u[2];
+        philox_u01_f64x2(seed, counter, env_id, kTagPhi, u);
         s[X] = sx; s[Y] = sy; s[V] = 0.; s[PHI] = -kPi + (kPi - -kPi) * u[0]; s[OM] = 0.;
         s[T] = 0.; s[TX] = tx; s[TY] = ty;
     }

@@ -1,0 +1,260 @@
+// rlp_lidar.hip — UGVForwardObstacleAvoidance step / observe with the fake lidar cast one beam per
+// lane (get_fake_laser environment/UGVForwardObstacleAvoidance/
+// UGVForwardObstacleAvoidance.py:274-397).
+//
+// A block owns EB envs. Phase 1 (one lane per env): f64 RK4 step, terminal flag, reward, the
+// per-pose lidar setup (beam angles, the four corner angles, collision, each obstacle's distance)
+// into LDS. Phase 2 (every lane): the EB x 37 (env, beam) pairs are spread over the block; a beam
+// reads its env's pose and obstacles from LDS (lanes of one env read the same words: broadcast)
+// and writes one float of obs[env][4 + beam]. One env per lane would hold 45 obstacle doubles in
+// VGPRs (1 wave / SIMD, scratch spills) and leave most of the chip idle at 16 K envs; a beam per
+// lane keeps ~40 VGPRs of live state and launches 37x the lanes. The arithmetic of each beam is
+// Env<7>::beam — the same code the generic kernels run, restating the reference line by line.
+#include "rlp_envs.hpp"
+
+namespace rlp {
+
+using OA = Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE>;
+constexpr int kOaThreads = 256;
+
+struct alignas(16) OaObstacle {
+    double x0, y0, r0, ref;  // ref = distance from the pose being scanned
+};
+
+template <int EB>
+struct OaLds {
+    OaObstacle ob[EB][OA::NOBS];
+    OA::Pose q[EB];
+    int coll[EB];
+};
+
+// per-pose setup by the env's lane: obstacle distances, collision and the beam geometry
+template <int EB>
+__device__ __forceinline__ void oa_setup(const OA::P &p, OaLds<EB> &L, int t, const double *s) {
+    const double x = s[OA::X], y = s[OA::Y];
+    for (int k = 0; k < p.n_obs; ++k) {
+        const double dx = x - L.ob[t][k].x0, dy = y - L.ob[t][k].y0;
+        L.ob[t][k].ref = sqrt(dx * dx + dy * dy);
+    }
+    L.coll[t] = OA::collision_at(p, x, y, [&](int k, double &x0, double &y0, double &r0) {
+        x0 = L.ob[t][k].x0; y0 = L.ob[t][k].y0; r0 = L.ob[t][k].r0;
+    });
+    L.q[t] = OA::pose(p, x, y, s[OA::PHI]);
+}
+
+template <int EB>
+__device__ __forceinline__ void oa_scan(const OA::P &p, const OaLds<EB> &L, int e0, int ne,
+                                        float *__restrict__ obs) {
+    const float blind = OA::beam_obs(p, p.laser_blind);
+    for (int it = threadIdx.x; it < ne * OA::NL; it += kOaThreads) {
+        const int e = it / OA::NL, i = it - e * OA::NL;
+        float v = blind;
+        if (!L.coll[e]) {
+            const OA::Pose q = L.q[e];
+            v = OA::beam_obs(p, OA::beam(p, q, i, [&](int k, double &x0, double &y0, double &r0,
+                                                      double &rf) {
+                const OaObstacle o = L.ob[e][k];
+                x0 = o.x0; y0 = o.y0; r0 = o.r0; rf = o.ref;
+            }));
+        }
+        obs[(size_t)(e0 + e) * OA::S + 4 + i] = v;
+    }
+}
+
+// STEP: step_update (+ obs_cur if requested); !STEP: get_state only
+template <int EB, bool STEP>
+__global__ void __launch_bounds__(kOaThreads) oa_kernel(OA::P p, double *state, int n,
+                                                        const float *__restrict__ action,
+                                                        float *obs_cur, float *obs_next,
+                                                        double *reward, int32_t *flag,
+                                                        uint8_t *done) {
+    __shared__ OaLds<EB> L;
+    const int t = threadIdx.x;
+    const int e0 = blockIdx.x * EB;
+    const int ne = n - e0 < EB ? n - e0 : EB;
+    const bool own = t < ne;
+    const size_t i = (size_t)e0 + t;
+    double s[OA::DW];
+    if (own) {
+#pragma unroll
+        for (int d = 0; d < OA::DW; ++d) s[d] = state[(size_t)d * n + i];
+        for (int k = 0; k < p.n_obs; ++k) {
+            L.ob[t][k].x0 = state[(size_t)(OA::OB + 3 * k) * n + i];
+            L.ob[t][k].y0 = state[(size_t)(OA::OB + 3 * k + 1) * n + i];
+            L.ob[t][k].r0 = state[(size_t)(OA::OB + 3 * k + 2) * n + i];
+        }
+    }
+    float *first = STEP ? obs_cur : obs_next;
+    if (first) {  // scan at the current pose (get_state / step's current_state)
+        if (own) {
+            oa_setup(p, L, t, s);
+            float h[4];
+            OA::obs_head(p, s, OA::get_e(s), OA::e_phi(s), h);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) first[i * OA::S + j] = h[j];
+        }
+        __syncthreads();
+        oa_scan(p, L, e0, ne, first);
+        if (!STEP) return;
+        __syncthreads();
+    }
+    if (STEP) {
+        if (own) {
+            const float a[2] = {action[i * 2], action[i * 2 + 1]};
+            double r, e, eph;
+            int f;
+            bool dn;
+            OA::step_core(p, s, a, [&](double x, double y) {
+                return OA::collision_at(p, x, y, [&](int k, double &x0, double &y0, double &r0) {
+                    x0 = L.ob[t][k].x0; y0 = L.ob[t][k].y0; r0 = L.ob[t][k].r0;
+                });
+            }, r, f, dn, e, eph);
+#pragma unroll
+            for (int d = 0; d < OA::DW; ++d) state[(size_t)d * n + i] = s[d];
+            reward[i] = r;
+            flag[i] = f;
+            done[i] = dn ? 1 : 0;
+            oa_setup(p, L, t, s);
+            float h[4];
+            OA::obs_head(p, s, e, eph, h);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) obs_next[i * OA::S + j] = h[j];
+        }
+        __syncthreads();
+        oa_scan(p, L, e0, ne, obs_next);
+    }
+}
+
+static int g_oa_cus = 0;
+
+template <bool STEP>
+static int launch_oa(const OA::P &p, double *state, int n, const float *action, float *obs_cur,
+                     float *obs_next, double *reward, int32_t *flag, uint8_t *done, hipStream_t st) {
+    if (p.n_obs < 0 || p.n_obs > OA::NOBS)
+        return fail(RLP_EINVAL, "UGVForwardObstacleAvoidance: n_obs=%d (0..%d)", p.n_obs, OA::NOBS);
+    if (!g_oa_cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&g_oa_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            g_oa_cus = 256;
+    }
+    // fewer envs per block when the batch is small, so every CU gets several blocks
+    if ((n + 63) / 64 >= 4 * g_oa_cus)
+        oa_kernel<64, STEP><<<(n + 63) / 64, kOaThreads, 0, st>>>(p, state, n, action, obs_cur,
+                                                                 obs_next, reward, flag, done);
+    else
+        oa_kernel<16, STEP><<<(n + 15) / 16, kOaThreads, 0, st>>>(p, state, n, action, obs_cur,
+                                                                 obs_next, reward, flag, done);
+    RLP_CHECK_LAUNCH("UGVForwardObstacleAvoidance lidar");
+    return RLP_OK;
+}
+
+int launch_ugvoa_step(const rlp_ugv_oa_params &p, double *state, int n, const float *action,
+                      float *obs_cur, float *obs_next, double *reward, int32_t *flag,
+                      uint8_t *done, hipStream_t st) {
+    return launch_oa<true>(p, state, n, action, obs_cur, obs_next, reward, flag, done, st);
+}
+
+int launch_ugvoa_observe(const rlp_ugv_oa_params &p, const double *state, int n, float *obs,
+                         hipStream_t st) {
+    return launch_oa<false>(p, const_cast<double *>(state), n, nullptr, nullptr, obs, nullptr,
+                            nullptr, nullptr, st);
+}
+
+// reset(random=True) with one wave per env: each round, lane l tests try (round * 64 + l) of the
+// target / of obstacle k, and the lowest legal try wins — the sequential sampler's result
+// (Env<7>::reset) at ~1 round per draw instead of the wave waiting on its unluckiest lane.
+constexpr int kOaResetWaves = 4;
+
+__global__ void __launch_bounds__(64 * kOaResetWaves) oa_reset_kernel(
+    OA::P p, double *state, int n, const uint8_t *mask, const double *init, uint64_t seed,
+    uint64_t counter, uint64_t env_id0) {
+    __shared__ double obl[kOaResetWaves][OA::NOBS * 3];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int e = blockIdx.x * kOaResetWaves + w;
+    if (e >= n || (mask && !mask[e])) return;  // uniform per wave
+    const size_t i = (size_t)e;
+    if (init) {
+        for (int d = lane; d < OA::D; d += 64) state[(size_t)d * n + i] = init[(size_t)d * n + i];
+        return;
+    }
+    const uint64_t id = env_id0 + (uint64_t)e;
+    double sx, sy;
+    OA::draw_point(p, seed, counter, id, OA::kTagStart, sx, sy);
+    double tx = sx, ty = sy;
+    if (!(0.0 >= p.safety_dis_st)) {  // terminal = start fails the distance test: redraw
+        for (int t0 = 0; t0 < p.max_tries; t0 += 64) {
+            const int t = t0 + lane;
+            double cx = 0, cy = 0;
+            bool ok = false;
+            if (t < p.max_tries) {
+                OA::draw_point(p, seed, counter, id, OA::kTagTarget + (uint32_t)t, cx, cy);
+                const double dx = cx - sx, dy = cy - sy;
+                ok = sqrt(dx * dx + dy * dy) >= p.safety_dis_st;
+            }
+            const uint64_t b = __ballot(ok);
+            const bool last = t0 + 64 >= p.max_tries;
+            if (b || last) {  // first legal try, else the last try drawn
+                const int src = b ? __ffsll((unsigned long long)b) - 1 : (p.max_tries - 1 - t0);
+                tx = __shfl(cx, src);
+                ty = __shfl(cy, src);
+                break;
+            }
+        }
+    }
+    for (int k = 0; k < OA::NOBS; ++k) {
+        double cx = OA::parked_x(k), cy = OA::kParkedY, r = p.r_min;
+        for (int t0 = 0; k < p.n_obs && t0 < p.max_tries; t0 += 64) {
+            const int t = t0 + lane;
+            double ccx = 0, ccy = 0, rr = 0;
+            bool ok = false;
+            if (t < p.max_tries) {
+                OA::draw_obstacle(p, seed, counter, id, k, t, ccx, ccy, rr);
+                ok = OA::legal(p, sx, sy, tx, ty, ccx, ccy, rr, k,
+                               [&](int j, double &x0, double &y0, double &r0) {
+                                   x0 = obl[w][3 * j]; y0 = obl[w][3 * j + 1]; r0 = obl[w][3 * j + 2];
+                               });
+            }
+            const uint64_t b = __ballot(ok);
+            if (b) {
+                const int src = __ffsll((unsigned long long)b) - 1;
+                cx = __shfl(ccx, src);
+                cy = __shfl(ccy, src);
+                r = __shfl(rr, src);
+                break;
+            }
+        }
+        if (lane == 0) {
+            obl[w][3 * k] = cx;
+            obl[w][3 * k + 1] = cy;
+            obl[w][3 * k + 2] = r;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    double u[2];
+    philox_u01_f64x2(seed, counter, id, OA::kTagPhi, u);
+    const double head[OA::DW] = {sx, sy, 0., -kPi + (kPi - -kPi) * u[0], 0., 0., tx, ty};
+    if (lane < OA::DW) {
+        double v = head[0];
+#pragma unroll
+        for (int d = 1; d < OA::DW; ++d) v = lane == d ? head[d] : v;
+        state[(size_t)lane * n + i] = v;
+    }
+    if (lane < OA::NOBS * 3) state[(size_t)(OA::OB + lane) * n + i] = obl[w][lane];
+}
+
+int launch_ugvoa_reset(const rlp_ugv_oa_params &p, double *state, int n, const uint8_t *mask,
+                       const double *init, uint64_t seed, uint64_t counter, uint64_t env_id0,
+                       hipStream_t st) {
+    if (p.n_obs < 0 || p.n_obs > OA::NOBS || p.max_tries < 0 || p.max_tries > 65535)
+        return fail(RLP_EINVAL, "rlp_env_reset: n_obs=%d (0..%d) max_tries=%d (0..65535)", p.n_obs,
+                    OA::NOBS, p.max_tries);
+    oa_reset_kernel<<<(n + kOaResetWaves - 1) / kOaResetWaves, 64 * kOaResetWaves, 0, st>>>(
+        p, state, n, mask, init, seed, counter, env_id0);
+    RLP_CHECK_LAUNCH("rlp_env_reset (UGVForwardObstacleAvoidance)");
+    return RLP_OK;
+}
+
+}  // namespace rlp
