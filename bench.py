@@ -269,6 +269,44 @@ def ugvoa_leg(rank, n=16384, steps=30, warmup=3, seed=5):
                       "circles + GPU map generator on reset, random actions"}
 
 
+def ugvoa_sac_leg(rank, n=16384, steps=20, warmup=3, batch=4096, capacity=1 << 20, seed=13):
+    """BASELINE config 5 shard: UGVForwardObstacleAvoidance SAC, n envs per GPU (131 072 / 8),
+    replay in HBM. One step = actor trunk + squashed-Gaussian sample (librlp) + env step with the
+    lidar kernel + n transitions into the replay ring + auto-reset (GPU map generator), then one
+    SAC update on `batch` rows sampled from HBM (the driver's learn() per env step, batch scaled
+    from 256). Nets: the SAC demo drivers' SACActor [41,128,64,2+2] / twin SACCritic [43,128,64,1]."""
+    from reinforcementlearningplatform_amd.algorithm.actor_critic.Soft_Actor_Critic import SAC
+    from reinforcementlearningplatform_amd.algorithm.actor_critic.vec_sac import VecSAC
+    from reinforcementlearningplatform_amd.environment.UGVForwardObstacleAvoidance import \
+        UGVForwardObstacleAvoidance
+    from reinforcementlearningplatform_amd.utils.classes import SACActor, SACCritic
+    torch.manual_seed(seed)
+    env = UGVForwardObstacleAvoidance(n_envs=n, seed=seed, env_id0=rank * n)
+    S, Ad = env.state_dim, env.action_dim
+    lo, hi = env.action_range[:, 0], env.action_range[:, 1]
+    msg = {'state_dim': S, 'action_dim': Ad, 'action_range': env.action_range, 'name': env.name}
+    agent = SAC(msg, 0.99, 0.005, capacity, batch, SACActor(S, Ad, lo, hi, std_min=0.05, std_scale=1.),
+                SACCritic(S, Ad), SACCritic(S, Ad), 1e-4, 1e-4, 1e-4, True, device="cuda", seed=seed,
+                graph=True)
+    loop = VecSAC(env, agent)
+    out = {}
+    for learn in (False, True):
+        for _ in range(warmup):
+            loop.step(learn=learn)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loop.step(learn=learn)
+        torch.cuda.synchronize()
+        out["with_learn" if learn else "env_only"] = n * steps / (time.perf_counter() - t0)
+    return {"value": out["with_learn"], "unit": "env-steps/s", "env_only": out["env_only"],
+            "envs_per_gpu": n, "replay_capacity": capacity, "batch": batch,
+            "learn_iters_per_step": 1,
+            "config": "UGVForwardObstacleAvoidance (env-dir copy, 37-beam lidar, 10 circles) SAC, "
+                      "replay in HBM, demo nets; SAC update in torch on the device, one HIP graph "
+                      "per update (sample, gather, update, soft update, actor refresh)"}
+
+
 def cpu_baseline(env, seconds=10.0):
     """Oracle (plain-C port of the reference loop, 1 thread) on a bounded sample of the same
     workload: actor + critic forward, sampling and env step per env-step."""
@@ -318,6 +356,7 @@ def main():
     ap.add_argument("--fp32-leg", type=int, default=1, help="also time the exact-f32 MLP path")
     ap.add_argument("--ddpg", type=int, default=1, help="also time SOI DDPG with the HBM replay (config 3)")
     ap.add_argument("--oa", type=int, default=1, help="also time UGVForwardObstacleAvoidance env steps (lidar)")
+    ap.add_argument("--sac", type=int, default=1, help="also time UGVForwardObstacleAvoidance SAC (config 5 shard)")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
@@ -447,6 +486,13 @@ def main():
             dist.all_reduce(t)
             d["value"] = float(t[0])
         out["ugvoa_lidar"] = d
+    if args.sac and args.env == "cartpole":
+        d = ugvoa_sac_leg(rank)
+        if dist is not None:
+            t = torch.tensor([d["value"], d["env_only"]], device="cuda", dtype=torch.float64)
+            dist.all_reduce(t)   # independent env shards / replicas: sum of the ranks' rates
+            d["value"], d["env_only"] = float(t[0]), float(t[1])
+        out["ugvoa_sac"] = d
     if args.e2e:
         v, it_s = e2e_iterations(seg, args.e2e, learner=args.learner)
         v_all = v * world

@@ -243,6 +243,22 @@ int rlp_mlp_forward(const rlp_mlp_desc *desc, const float *params, const float *
 int64_t rlp_mfma_packed_count(const rlp_mlp_desc *desc);
 int rlp_mfma_pack(const rlp_mlp_desc *desc, const float *params, float *packed, rlp_stream_t stream);
 
+/* SAC squashed-Gaussian policy head: SACActor.forward (utils/classes.py:464-486, and the demo
+ * drivers' copy with a per-dim log_std clamp, demonstration/SAC/SAC-4-UGVForward/train.py:68-88)
+ * after the trunk, plus SAC.choose_action's clamp (Soft_Actor_Critic.py:63-67). Per row i, dim j:
+ *   ls = clamp(head[i][A + j], ls_lo[j], ls_hi[j]);  std = exp(ls)
+ *   u  = deterministic ? head[i][j] : head[i][j] + std * eps        (Normal.rsample)
+ *   log_pi[i] = sum_j Normal(mean, std).log_prob(u) - sum_j 2 (log 2 - u - softplus(-2 u))
+ *   action = tanh(u) * gain[j] + off[j], then clamped to [a_min, a_max] when a_min != NULL.
+ * head: [n][2A] device (mean | log_std, i.e. the two Linear heads concatenated); eps from
+ * `noise` [n][A] when non-NULL, else Philox normals keyed (seed, counter, env_id0 + i) as in
+ * rlp_policy_sample. ls_lo, ls_hi, gain, off, a_min, a_max: HOST arrays of A floats (a_min, a_max
+ * nullable together); log_pi nullable. fp32 throughout, as torch. */
+int rlp_sac_sample(const float *head, int n, int A, const float *ls_lo, const float *ls_hi,
+                   const float *gain, const float *off, const float *a_min, const float *a_max,
+                   int deterministic, const float *noise, uint64_t seed, uint64_t counter,
+                   uint64_t env_id0, float *action, float *log_pi, rlp_stream_t stream);
+
 /* Proximal_Policy_Optimization2.choose_action (Proximal_Policy_Optimization2.py:69-76):
  *   a = clamp(mean + std*eps, a_min, a_max);  logp = Normal(mean, std).log_prob(a)  (per dim)
  * eps from `noise` [n][A] if non-NULL, else Philox normals keyed (seed, counter, env_id0+i).

@@ -38,6 +38,8 @@ def _declare(lib):
         "rlp_mfma_packed_count": (i64, [vp]),
         "rlp_mfma_pack": (i32, [vp, vp, vp, vp]),
         "rlp_policy_sample": (i32, [vp, i32, i32, vp, vp, vp, vp, u64, u64, u64, vp, vp, vp]),
+        "rlp_sac_sample": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, vp, i32, vp, u64, u64, u64, vp, vp,
+                                 vp]),
         "rlp_rollout": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "rlp_mfma_forward": (i32, [vp, vp, vp, vp, i64, vp]),
         "rlp_value_fixup": (i32, [vp, vp, vp, vp, vp, vp, i64, vp]),

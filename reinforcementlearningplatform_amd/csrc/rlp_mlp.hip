@@ -193,6 +193,55 @@ __global__ void __launch_bounds__(256) policy_sample_kernel(const float *__restr
     }
 }
 
+struct SacArgs {
+    float ls_lo[4], ls_hi[4], gain[4], off[4], a_min[4], a_max[4];
+    int clamp_action, deterministic;
+};
+
+// softplus with torch's default threshold (beta 1, threshold 20)
+__device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+
+template <int A>
+__global__ void __launch_bounds__(256) sac_sample_kernel(const float *__restrict__ head, int n,
+                                                         SacArgs sa, const float *noise,
+                                                         uint64_t seed, uint64_t counter,
+                                                         uint64_t env_id0, float *action,
+                                                         float *log_pi) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float eps[A];
+    if (sa.deterministic) {
+#pragma unroll
+        for (int j = 0; j < A; ++j) eps[j] = 0.f;
+    } else if (noise) {
+#pragma unroll
+        for (int j = 0; j < A; ++j) eps[j] = noise[(size_t)i * A + j];
+    } else {
+        philox_normal_f32<A>(seed, counter, env_id0 + (uint64_t)i, eps);
+    }
+    float lp = 0.f, corr = 0.f;
+    const float kHalfLog2Pi = 0.918938533204672742f;  // math.log(math.sqrt(2 * math.pi)) in f32
+    const float kLog2 = 0.693147180559945309f;         // np.log(2) in f32
+#pragma unroll
+    for (int j = 0; j < A; ++j) {
+        const float mean = head[(size_t)i * 2 * A + j];
+        float ls = head[(size_t)i * 2 * A + A + j];
+        ls = fminf(fmaxf(ls, sa.ls_lo[j]), sa.ls_hi[j]);  // torch.clamp
+        const float sd = expf(ls);
+        const float u = sa.deterministic ? mean : mean + eps[j] * sd;  // loc + eps * scale
+        // Normal.log_prob: -((u - loc) ** 2) / (2 * var) - log(scale) - log(sqrt(2 pi))
+        const float d = u - mean;
+        const float lpj = -(d * d) / (2.f * (sd * sd)) - logf(sd) - kHalfLog2Pi;
+        lp = j == 0 ? lpj : lp + lpj;
+        const float cj = 2.f * ((kLog2 - u) - softplus_f(-2.f * u));
+        corr = j == 0 ? cj : corr + cj;
+        float a = tanhf(u) * sa.gain[j] + sa.off[j];
+        if (sa.clamp_action) a = fmaxf(fminf(a, sa.a_max[j]), sa.a_min[j]);
+        action[(size_t)i * A + j] = a;
+    }
+    if (log_pi) log_pi[i] = lp - corr;
+}
+
 }  // namespace rlp
 
 using namespace rlp;
@@ -274,4 +323,37 @@ int rlp_policy_sample(const float *mean, int n, int A, const float *std, const f
     return RLP_OK;
 }
 
+int rlp_sac_sample(const float *head, int n, int A, const float *ls_lo, const float *ls_hi,
+                   const float *gain, const float *off, const float *a_min, const float *a_max,
+                   int deterministic, const float *noise, uint64_t seed, uint64_t counter,
+                   uint64_t env_id0, float *action, float *log_pi, rlp_stream_t stream) {
+    RLP_REQUIRE(head && ls_lo && ls_hi && gain && off && action, "rlp_sac_sample: null argument");
+    RLP_REQUIRE((a_min == nullptr) == (a_max == nullptr), "rlp_sac_sample: a_min/a_max both or neither");
+    RLP_REQUIRE(A >= 1 && A <= 4, "rlp_sac_sample: A = %d not in [1, 4]", A);
+    if (n <= 0) return n == 0 ? RLP_OK : RLP_EINVAL;
+    SacArgs sa;
+    for (int j = 0; j < 4; ++j) {
+        const bool on = j < A;
+        sa.ls_lo[j] = on ? ls_lo[j] : 0.f;
+        sa.ls_hi[j] = on ? ls_hi[j] : 0.f;
+        sa.gain[j] = on ? gain[j] : 0.f;
+        sa.off[j] = on ? off[j] : 0.f;
+        sa.a_min[j] = on && a_min ? a_min[j] : 0.f;
+        sa.a_max[j] = on && a_max ? a_max[j] : 0.f;
+    }
+    sa.clamp_action = a_min != nullptr;
+    sa.deterministic = deterministic != 0;
+    const dim3 grid((n + 255) / 256), block(256);
+    hipStream_t s = as_stream(stream);
+    switch (A) {
+    case 1: sac_sample_kernel<1><<<grid, block, 0, s>>>(head, n, sa, noise, seed, counter, env_id0, action, log_pi); break;
+    case 2: sac_sample_kernel<2><<<grid, block, 0, s>>>(head, n, sa, noise, seed, counter, env_id0, action, log_pi); break;
+    case 3: sac_sample_kernel<3><<<grid, block, 0, s>>>(head, n, sa, noise, seed, counter, env_id0, action, log_pi); break;
+    case 4: sac_sample_kernel<4><<<grid, block, 0, s>>>(head, n, sa, noise, seed, counter, env_id0, action, log_pi); break;
+    }
+    RLP_CHECK_LAUNCH("rlp_sac_sample");
+    return RLP_OK;
+}
+
 }  // extern "C"
+

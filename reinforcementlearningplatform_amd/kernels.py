@@ -109,6 +109,23 @@ def policy_sample(mean, std, a_min, a_max, noise=None, seed=0, counter=0, env_id
     return a, lp
 
 
+def sac_sample(head, ls_lo, ls_hi, gain, off, a_min=None, a_max=None, deterministic=False,
+               noise=None, seed=0, counter=0, env_id0=0, with_logprob=True):
+    """rlp_sac_sample: the SAC squashed-Gaussian head on head = [n][2A] (mean | log_std)."""
+    n, A2 = head.shape
+    A = A2 // 2
+    a = torch.empty((n, A), dtype=torch.float32, device=head.device)
+    lp = torch.empty(n, dtype=torch.float32, device=head.device) if with_logprob else None
+    clamp = a_min is not None
+    check(lib().rlp_sac_sample(ptr(head.contiguous()), n, A, _host_f32(ls_lo, A),
+                               _host_f32(ls_hi, A), _host_f32(gain, A), _host_f32(off, A),
+                               _host_f32(a_min, A) if clamp else None,
+                               _host_f32(a_max, A) if clamp else None, int(bool(deterministic)),
+                               ptr(noise), seed, counter, env_id0, ptr(a), ptr(lp), stream_ptr()),
+          "rlp_sac_sample")
+    return a, lp
+
+
 def rollout_buffers(kind, T, n, device=None):
     _, S, A = dims(kind)
     dev = _dev(device)

@@ -358,3 +358,139 @@ class GPUNet:
         if torch.allclose(got, ref, rtol=1e-4, atol=1e-4):
             return None
         return float((got - ref).abs().max())
+
+
+# ---------------------------------------------------------------------------------------------
+# SAC networks: utils/classes.py:438-527 (SACActor / SACCritic). With std_min / std_scale given,
+# SACActor is the SAC demo drivers' copy (demonstration/SAC/SAC-4-UGVForward/train.py:33-88),
+# whose log_std clamp is per action dim instead of (-20, 2). Parameter names match the
+# reference so state_dicts load unchanged.
+# ---------------------------------------------------------------------------------------------
+class SACActor(nn.Module):
+    def __init__(self, state_dim: int = 3, action_dim: int = 3, a_min=np.zeros(3), a_max=np.ones(3),
+                 use_orthogonal_init: bool = True, std_min=None, std_scale=None):
+        super().__init__()
+        self.fc1 = nn.Linear(state_dim, 128)
+        self.fc2 = nn.Linear(128, 64)
+        self.mean_layer = nn.Linear(64, action_dim)
+        self.log_std_layer = nn.Linear(64, action_dim)
+        self.a_min = torch.tensor(a_min, dtype=torch.float)
+        self.a_max = torch.tensor(a_max, dtype=torch.float)
+        self.off = (self.a_min + self.a_max) / 2.0
+        self.gain = self.a_max - self.off
+        self.std_min, self.std_scale = std_min, std_scale
+        if use_orthogonal_init:
+            self.orthogonal_init_all()
+
+    def orthogonal_init_all(self):
+        _orthogonal(self.fc1)
+        _orthogonal(self.fc2)
+        _orthogonal(self.mean_layer, gain=0.01)
+        _orthogonal(self.log_std_layer, gain=0.01)
+
+    def _apply(self, fn, *args, **kwargs):
+        super()._apply(fn, *args, **kwargs)
+        self.a_min, self.a_max = fn(self.a_min), fn(self.a_max)
+        self.off, self.gain = fn(self.off), fn(self.gain)
+        return self
+
+    def log_std_bounds(self):
+        """(lo, hi) of the log_std clamp, per action dim, float32 — as forward() computes them."""
+        A = self.mean_layer.out_features
+        if self.std_min is None:
+            return torch.full((A,), -20.0), torch.full((A,), 2.0)
+        lo = torch.log(self.std_min * (self.a_max - self.a_min) / 2)
+        hi = (self.a_max - self.a_min) / 2 / self.std_scale
+        return lo.cpu(), hi.cpu()
+
+    def forward(self, x, deterministic=False, with_logprob=True):
+        x = torch.relu(self.fc1(x))
+        x = torch.relu(self.fc2(x))
+        mean = self.mean_layer(x)
+        log_std = self.log_std_layer(x)
+        if self.std_min is None:
+            log_std = torch.clamp(log_std, -20, 2)
+        else:
+            log_std = torch.clamp(log_std, torch.log(self.std_min * (self.a_max - self.a_min) / 2),
+                                  (self.a_max - self.a_min) / 2 / self.std_scale)
+        std = torch.exp(log_std)
+        dist = torch.distributions.Normal(mean, std)
+        a = mean if deterministic else dist.rsample()
+        if with_logprob:  # Spinning Up's tanh-squash correction
+            log_pi = dist.log_prob(a).sum(dim=1, keepdim=True)
+            log_pi -= (2 * (np.log(2) - a - torch.nn.functional.softplus(-2 * a))).sum(dim=1, keepdim=True)
+        else:
+            log_pi = None
+        a = torch.tanh(a) * self.gain + self.off
+        return a, log_pi
+
+
+class SACCritic(nn.Module):
+    def __init__(self, state_dim: int = 3, action_dim: int = 1, use_orthogonal_init: bool = True):
+        super().__init__()
+        self.fc1 = nn.Linear(state_dim + action_dim, 128)
+        self.fc2 = nn.Linear(128, 64)
+        self.fc3 = nn.Linear(64, 1)
+        self.fc4 = nn.Linear(state_dim + action_dim, 128)
+        self.fc5 = nn.Linear(128, 64)
+        self.fc6 = nn.Linear(64, 1)
+        if use_orthogonal_init:
+            self.orthogonal_init_all()
+
+    def orthogonal_init_all(self):
+        for m in (self.fc1, self.fc2, self.fc3, self.fc4, self.fc5, self.fc6):
+            _orthogonal(m)
+
+    def forward(self, s, a):
+        s_a = torch.cat([s, a], 1)
+        q1 = self.fc3(torch.relu(self.fc2(torch.relu(self.fc1(s_a)))))
+        q2 = self.fc6(torch.relu(self.fc5(torch.relu(self.fc4(s_a)))))
+        return q1, q2
+
+
+class GPUSACActor:
+    """SACActor.forward for a batch on librlp: the ReLU trunk + both heads as one
+    [S -> 128 -> 64 -> 2A] MLP (rlp_mlp_forward) and the squashed-Gaussian sample, log-prob and
+    action clamp in rlp_sac_sample (Philox noise)."""
+
+    def __init__(self, actor: SACActor, device="cuda"):
+        self.actor = actor
+        self.device = torch.device(device)
+        S, A = actor.fc1.in_features, actor.mean_layer.out_features
+        self.A = A
+        self.desc = _abi.MLPDesc.make([S, 128, 64, 2 * A], [_abi.RLP_ACT_RELU, _abi.RLP_ACT_RELU,
+                                                             _abi.RLP_ACT_NONE])
+        self.refresh()
+
+    def refresh(self):
+        a = self.actor
+        with torch.no_grad():
+            parts = [a.fc1.weight, a.fc1.bias, a.fc2.weight, a.fc2.bias,
+                     torch.cat([a.mean_layer.weight, a.log_std_layer.weight], 0),
+                     torch.cat([a.mean_layer.bias, a.log_std_layer.bias], 0)]
+            self.flat = torch.cat([t.detach().reshape(-1).to(self.device, torch.float32)
+                                   for t in parts]).contiguous()
+        lo, hi = a.log_std_bounds()
+        self.ls_lo, self.ls_hi = lo.tolist(), hi.tolist()
+        self.gain, self.off = a.gain.cpu().tolist(), a.off.cpu().tolist()
+
+    def copy_from_actor(self):
+        """refresh() of the weights in place (graph-capturable: no new tensors)."""
+        a = self.actor
+        with torch.no_grad():
+            off = 0
+            for t in (a.fc1.weight, a.fc1.bias, a.fc2.weight, a.fc2.bias):
+                self.flat[off:off + t.numel()].copy_(t.reshape(-1))
+                off += t.numel()
+            for t in (a.mean_layer.weight, a.log_std_layer.weight, a.mean_layer.bias,
+                      a.log_std_layer.bias):
+                self.flat[off:off + t.numel()].copy_(t.reshape(-1))
+                off += t.numel()
+
+    def head(self, s):
+        return K.mlp_forward(self.desc, self.flat, s.to(self.device, torch.float32).contiguous())
+
+    def __call__(self, s, deterministic=False, with_logprob=True, a_min=None, a_max=None,
+                 seed=0, counter=0, env_id0=0, noise=None):
+        return K.sac_sample(self.head(s), self.ls_lo, self.ls_hi, self.gain, self.off, a_min, a_max,
+                            deterministic, noise, seed, counter, env_id0, with_logprob)

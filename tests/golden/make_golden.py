@@ -662,6 +662,84 @@ def gen_ugvoa(key, n=400):
     print(key, "flags", np.bincount(out["flag"]))
 
 
+# ---------------------------------------------------------------------------------------------
+# SAC: the squashed-Gaussian actor head (utils/classes.py SACActor and the SAC demo copy) and two
+# SAC.learn updates (algorithm/actor_critic/Soft_Actor_Critic.py:70-124), Normal.rsample's noise
+# recorded so the device code can replay it
+# ---------------------------------------------------------------------------------------------
+class _EpsTape:
+    def __init__(self, replay=None):
+        self.tape, self.replay = [], replay
+        self.orig = torch.distributions.Normal.rsample
+
+    def __enter__(self):
+        tape = self
+
+        def rsample(dist, sample_shape=torch.Size()):
+            shape = dist._extended_shape(sample_shape)
+            eps = tape.replay.pop(0) if tape.replay is not None else torch.randn(shape)
+            tape.tape.append(eps.clone())
+            return dist.loc + eps * dist.scale
+        torch.distributions.Normal.rsample = rsample
+        return self
+
+    def __exit__(self, *a):
+        torch.distributions.Normal.rsample = self.orig
+
+
+def gen_sac():
+    with quiet():
+        drv_s = load("demonstration/SAC/SAC-4-UGVForward/train.py", "ref_sac_ugvf_train")
+        sac_mod = load("algorithm/actor_critic/Soft_Actor_Critic.py", "ref_sac")
+    torch.manual_seed(13)
+    S, A, B = 41, 2, 64
+    lo, hi = np.array([-3., -2 * np.pi]), np.array([3., 2 * np.pi])
+    out = {}
+    # actor heads: utils.classes.SACActor (clamp -20, 2) and the demo copy (per-dim clamp)
+    for key, actor in (("utils", cls_mod.SACActor(S, A, lo, hi)),
+                       ("demo", drv_s.SACActor(S, A, lo, hi, std_scale=1.))):
+        with torch.no_grad():   # spread log_std over both clamp bounds
+            actor.log_std_layer.weight.mul_(4000.0)
+            actor.mean_layer.weight.mul_(100.0)
+        x = torch.tensor(rng.uniform(-1, 1, (512, S)), dtype=torch.float)
+        with torch.no_grad(), _EpsTape() as tp:
+            a, lp = actor(x)
+            a_det, _ = actor(x, deterministic=True, with_logprob=False)
+        out[f"{key}_params"] = torch.cat([p.detach().reshape(-1) for p in actor.parameters()]).numpy()
+        out[f"{key}_x"], out[f"{key}_eps"] = x.numpy(), tp.tape[0].numpy()
+        out[f"{key}_a"], out[f"{key}_logpi"], out[f"{key}_a_det"] = a.numpy(), lp.numpy(), a_det.numpy()
+    # two learn() iterations with the demo nets
+    actor = drv_s.SACActor(S, A, lo, hi, std_scale=1.)
+    critic, target = drv_s.SACCritic(S, A), drv_s.SACCritic(S, A)
+    env_msg = {'state_dim': S, 'action_dim': A, 'action_range': np.stack([lo, hi], 1), 'name': 'OA'}
+    agent = sac_mod.SAC(env_msg=env_msg, gamma=0.99, critic_tau=0.005, memory_capacity=10000,
+                        batch_size=B, actor=actor, critic=critic, target_critic=target, a_lr=1e-4,
+                        c_lr=1e-4, alpha_lr=1e-4, adaptive_alpha=True)
+    flat = lambda m: torch.cat([p.detach().reshape(-1) for p in m.parameters()]).numpy().copy()
+    for k, m in (("actor", agent.actor), ("critic", agent.critic), ("target_critic", agent.target_critic)):
+        out[f"before_{k}"] = flat(m)
+    batches = []
+    for it in range(2):
+        batches.append((rng.uniform(-1, 1, (B, S)), rng.uniform(lo, hi, (B, A)), rng.normal(size=B),
+                        rng.uniform(-1, 1, (B, S)), (rng.uniform(size=B) < 0.1).astype(np.float32)))
+    agent.memory.mem_counter = 10000
+    agent.memory.sample_buffer = lambda is_reward_ascent=True, has_log_prob=False: batches.pop(0)
+    keep = [tuple(np.array(x) for x in b) for b in batches]
+    with _EpsTape() as tp:
+        agent.learn(is_reward_ascent=False, iter=2)
+    for k, m in (("actor", agent.actor), ("critic", agent.critic), ("target_critic", agent.target_critic)):
+        out[f"after_{k}"] = flat(m)
+    out["after_log_alpha"] = agent.log_alpha.detach().numpy().copy()
+    out["learn_eps"] = np.stack([e.numpy() for e in tp.tape])
+    for i, b in enumerate(keep):
+        for name, v in zip(("s", "a", "r", "s2", "dw"), b):
+            out[f"b{i}_{name}"] = v
+    np.savez_compressed(os.path.join(OUT, "sac.npz"), **out)
+    print("sac", len(tp.tape), float(out["after_log_alpha"][0]),
+          {k: float(np.abs(out[f"after_{k}"] - out[f"before_{k}"]).max())
+           for k in ("actor", "critic", "target_critic")})
+
+
 if __name__ == "__main__" and len(sys.argv) > 2:   # selected generators only
     for name in sys.argv[2:]:
         if name.startswith("ugvoa_"):
@@ -690,6 +768,7 @@ if __name__ == "__main__":
     gen_reward_norm()
     gen_replay()
     gen_ddpg()
+    gen_sac()
     with open(os.path.join(OUT, "VERSIONS.txt"), "w") as f:
         f.write(f"numpy {np.__version__}\ntorch {torch.__version__}\npython {sys.version.split()[0]}\n"
                 f"reference {REF} (HKPolyU-UAV/ReinforcementLearningPlatform @ 2025-02-28)\n")
