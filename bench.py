@@ -205,7 +205,8 @@ def soi_ddpg_leg(rank, n=65536, steps=20, warmup=3, batch=4096, capacity=1 << 20
     lo, hi = env.action_range[:, 0], env.action_range[:, 1]
     nets = [Actor(1e-4, 4, 2, lo, hi), Actor(1e-4, 4, 2, lo, hi), Critic(3e-4, 4, 2), Critic(3e-4, 4, 2)]
     msg = {'state_dim': 4, 'action_dim': 2, 'action_range': env.action_range, 'name': env.name}
-    agent = DDPG(msg, 0.99, 0.005, 0.005, capacity, batch, *nets, device="cuda", seed=seed)
+    agent = DDPG(msg, 0.99, 0.005, 0.005, capacity, batch, *nets, device="cuda", seed=seed,
+                 graph=True)
     loop = VecDDPG(env, agent, learn_iters=1)
     out = {}
     for learn in (False, True):
@@ -221,7 +222,7 @@ def soi_ddpg_leg(rank, n=65536, steps=20, warmup=3, batch=4096, capacity=1 << 20
     return {"value": out["with_learn"], "unit": "env-steps/s", "env_only": out["env_only"],
             "envs_per_gpu": n, "replay_capacity": capacity, "batch": batch, "learn_iters_per_step": 1,
             "config": "SecondOrderIntegration (DDPG copy) DDPG, replay in HBM, nets [4,256,256,2] "
-                      "relu / Q [6,256,256,1] relu; DDPG update in torch on the device"}
+                      "relu / Q [6,256,256,1] relu; DDPG update in torch on the device, one HIP graph per update"}
 
 
 def ugvoa_leg(rank, n=16384, steps=30, warmup=3, seed=5):

@@ -8,7 +8,10 @@ Same constructor, attributes and methods as the reference. Differences that matt
     kernel) and the N(0, sigma^2) exploration noise + clip through rlp_policy_sample (Philox),
     returning a device tensor;
   * the update itself is the reference's torch code on the device (critic MSE to the target
-    r + gamma * (1 - done) * Q'(s', mu'(s')), actor loss -Q(s, mu(s)), soft target updates).
+    r + gamma * (1 - done) * Q'(s', mu'(s')), actor loss -Q(s, mu(s)), soft target updates);
+  * graph=True captures one whole learn iteration (uniform batch indices from torch's generator,
+    the replay gather, the update with the nets' Adam switched to capturable, the soft updates
+    and the GPU actor's weight refresh) in a HIP graph and replays it.
 """
 import numpy as np
 import torch
@@ -22,7 +25,7 @@ class DDPG:
     def __init__(self, env_msg: dict, gamma: float = 0.99, actor_soft_update: float = 1e-2,
                  critic_soft_update: float = 1e-2, memory_capacity: int = 5000,
                  batch_size: int = 512, actor=None, target_actor=None, critic=None,
-                 target_critic=None, device=None, seed=None):
+                 target_critic=None, device=None, seed=None, graph=False):
         if actor is None or target_actor is None or critic is None or target_critic is None:
             raise ValueError("DDPG: pass the driver's actor/target_actor/critic/target_critic "
                              "(the reference's default-argument placeholder nets have no forward)")
@@ -49,6 +52,8 @@ class DDPG:
         self.reward = 0
         self.gpu_actor = None
         self.noise_counter = 0
+        self.graph = bool(graph)
+        self._graph = None
 
     def choose_action_random(self, n=None):
         if n is None:
@@ -88,14 +93,57 @@ class DDPG:
     def learn(self, is_reward_ascent=True, iter=1):
         if self.memory.mem_counter < self.memory.batch_size:
             return None
+        if self.graph and not is_reward_ascent:
+            return self._learn_graphed(iter)
         critic_loss = actor_loss = None
         for _ in range(iter):
             s, a, r, s_, done = self.memory.sample_buffer(is_reward_ascent=is_reward_ascent)
             critic_loss, actor_loss = self.update(s, a, r, s_, done)
         return critic_loss, actor_loss
 
+    # -- HIP-graph learn (see the module docstring)
+    def _graph_body(self):
+        mem = self.memory
+        idx = (torch.rand(mem.batch_size, device=self.device) * self._gmax).long()
+        idx.clamp_(max=mem.mem_size - 1)
+        s, a, r, s_, done = K.replay_gather(mem.rb, idx, out=self._gbuf)
+        c, al = self._update_core(s, a, r, s_, done)
+        self._gloss[0].copy_(c)
+        self._gloss[1].copy_(al)
+        self.gpu_actor.copy_from_module()
+
+    def _learn_graphed(self, iters):
+        from .Soft_Actor_Critic import _capture
+        mem = self.memory
+        if self._graph is None:
+            if self.gpu_actor is None:
+                self.gpu_actor = GPUNet(self.actor, True, self.device)
+            for opt in (self.critic.optimizer, self.actor.optimizer):
+                for grp in opt.param_groups:
+                    grp["capturable"] = True
+            B, S, A = mem.batch_size, mem.rb.S, mem.rb.A
+            f32 = dict(dtype=torch.float32, device=self.device)
+            self._gbuf = (torch.empty((B, S), **f32), torch.empty((B, A), **f32),
+                          torch.empty(B, **f32), torch.empty((B, S), **f32), torch.empty(B, **f32))
+            self._gmax = torch.zeros((), **f32)
+            self._gloss = torch.zeros(2, **f32)
+            self._gmax.fill_(float(min(mem.mem_counter, mem.mem_size)))
+            self._graph = _capture(self._graph_body, self.device,
+                                   [self.actor, self.target_actor, self.critic, self.target_critic],
+                                   [self.critic.optimizer, self.actor.optimizer])
+        for _ in range(iters):
+            self._gmax.fill_(float(min(mem.mem_counter, mem.mem_size)))
+            self._graph.replay()
+        return self._gloss[0], self._gloss[1]
+
     def update(self, s, a, r, s_, done):
         """One DDPG update on a sampled batch (done = the buffer's 1 - done column), :83-109."""
+        out = self._update_core(s, a, r, s_, done)
+        if self.gpu_actor is not None:
+            self.gpu_actor.refresh()
+        return out
+
+    def _update_core(self, s, a, r, s_, done):
         with torch.no_grad():
             Q_ = self.target_critic(s_, self.target_actor(s_))
             target_Q = r.unsqueeze(1) + self.gamma * done.unsqueeze(1) * Q_
@@ -113,8 +161,6 @@ class DDPG:
         for params in self.critic.parameters():
             params.requires_grad = True
         self.update_network_parameters()
-        if self.gpu_actor is not None:
-            self.gpu_actor.refresh()
         return critic_loss.detach(), actor_loss.detach()
 
     def update_network_parameters(self):

@@ -24,17 +24,13 @@ from ...utils.classes import GPUSACActor, ReplayBuffer
 
 
 class _Snapshot:
-    """Values of an agent's parameters and optimizer states, to undo graph warm-up updates
-    in place (the tensors themselves must stay the ones the graph captures)."""
+    """Values of parameters and optimizer states, to undo graph warm-up updates in place (the
+    tensors themselves must stay the ones the graph captures)."""
 
-    def __init__(self, agent):
-        self.params = [p for m in (agent.actor, agent.critic, agent.target_critic)
-                       for p in m.parameters()]
-        if agent.adaptive_alpha:
-            self.params.append(agent.log_alpha)
+    def __init__(self, params, opts):
+        self.params = list(params)
         self.saved = [p.detach().clone() for p in self.params]
-        self.opts = [agent.actor_optimizer, agent.critic_optimizer] + (
-            [agent.alpha_optimizer] if agent.adaptive_alpha else [])
+        self.opts = list(opts)
         self.state = {id(t): t.detach().clone() for o in self.opts for st in o.state.values()
                       for t in st.values() if torch.is_tensor(t)}
 
@@ -50,6 +46,31 @@ class _Snapshot:
                                 t.copy_(self.state[id(t)])
                             else:   # state created by the warm-up: back to a fresh Adam
                                 t.zero_()
+
+
+def _capture(body, device, modules, opts, extra_params=()):
+    """Warm `body` up on a side stream (optimizer states, library workspaces), undo the warm-up
+    updates, then capture one call of it in a HIP graph (torch.cuda.CUDAGraph)."""
+    params = [p for m in modules for p in m.parameters()] + list(extra_params)
+    snap = _Snapshot(params, opts)
+    # torch.distributions' argument checks read values back to the host, which a stream under
+    # capture cannot do: off while warming up and capturing
+    validate = torch.distributions.Distribution._validate_args
+    torch.distributions.Distribution.set_default_validate_args(False)
+    try:
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                body()
+        torch.cuda.current_stream(device).wait_stream(side)
+        snap.restore()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            body()
+    finally:
+        torch.distributions.Distribution.set_default_validate_args(validate)
+    return graph
 
 
 class SAC:
@@ -156,24 +177,11 @@ class SAC:
             self._gmax = torch.zeros((), **f32)
             self._gloss = torch.zeros(2, **f32)
             self._gmax.fill_(float(min(mem.mem_counter, mem.mem_size)))
-            snap = _Snapshot(self)
-            # torch.distributions' argument checks read values back to the host, which a stream
-            # under capture cannot do: off while warming up and capturing
-            validate = torch.distributions.Distribution._validate_args
-            torch.distributions.Distribution.set_default_validate_args(False)
-            try:
-                side = torch.cuda.Stream(self.device)
-                side.wait_stream(torch.cuda.current_stream(self.device))
-                with torch.cuda.stream(side):   # warm-up: optimizer states, library workspaces
-                    for _ in range(3):
-                        self._graph_body()
-                torch.cuda.current_stream(self.device).wait_stream(side)
-                snap.restore()   # the warm-up updates are undone
-                self._graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._graph):
-                    self._graph_body()
-            finally:
-                torch.distributions.Distribution.set_default_validate_args(validate)
+            opts = [self.actor_optimizer, self.critic_optimizer] + (
+                [self.alpha_optimizer] if self.adaptive_alpha else [])
+            self._graph = _capture(self._graph_body, self.device,
+                                   [self.actor, self.critic, self.target_critic], opts,
+                                   [self.log_alpha] if self.adaptive_alpha else [])
         for _ in range(iters):
             self._gmax.fill_(float(min(mem.mem_counter, mem.mem_size)))
             self._graph.replay()

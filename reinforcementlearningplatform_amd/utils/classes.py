@@ -332,6 +332,17 @@ class GPUNet:
             cnt = K.lib().rlp_mfma_packed_count(__import__("ctypes").byref(self.desc))
             self.packed = K.mfma_pack(self.desc, self.flat, out=self.packed) if cnt > 0 else None
 
+    def copy_from_module(self):
+        """refresh() in place (graph-capturable: the same flat / packed tensors)."""
+        with torch.no_grad():
+            off = 0
+            for l in self.linears:
+                for t in (l.weight, l.bias):
+                    self.flat[off:off + t.numel()].copy_(t.reshape(-1))
+                    off += t.numel()
+            if self.packed is not None:
+                K.mfma_pack(self.desc, self.flat, out=self.packed)
+
     def raw(self, x):
         """Last-layer output (tanh already applied for an actor, before gain/off)."""
         x = x.to(self.device, torch.float32).contiguous()

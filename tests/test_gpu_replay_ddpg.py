@@ -112,7 +112,7 @@ def load_flat(m, flat):
             off += p.numel()
 
 
-def make_agent(g=None, memory=10000, batch=64, seed=0):
+def make_agent(g=None, memory=10000, batch=64, seed=0, graph=False):
     lo, hi = np.array([-3., -3.]), np.array([3., 3.])
     nets = [Actor(1e-4, 4, 2, lo, hi), Actor(1e-4, 4, 2, lo, hi), Critic(3e-4, 4, 2),
             Critic(3e-4, 4, 2)]
@@ -123,7 +123,7 @@ def make_agent(g=None, memory=10000, batch=64, seed=0):
                'name': 'SecondOrderIntegration'}
     return DDPG(env_msg, gamma=0.99, actor_soft_update=0.005, critic_soft_update=0.005,
                 memory_capacity=memory, batch_size=batch, actor=nets[0], target_actor=nets[1],
-                critic=nets[2], target_critic=nets[3], device="cuda", seed=seed)
+                critic=nets[2], target_critic=nets[3], device="cuda", seed=seed, graph=graph)
 
 
 def test_ddpg_update_matches_reference(golden):
@@ -151,11 +151,12 @@ def test_batched_actor_and_noise():
     assert float(a1.abs().max()) <= 3.0
 
 
-def test_vecddpg_loop_fills_replay_and_learns():
+@pytest.mark.parametrize("graph", [False, True])
+def test_vecddpg_loop_fills_replay_and_learns(graph):
     n = 4096
     env = SecondOrderIntegration(n_envs=n, variant="ddpg", seed=2)
     env.reset(random=True)
-    agent = make_agent(memory=200_000, batch=512, seed=4)
+    agent = make_agent(memory=200_000, batch=512, seed=4, graph=graph)
     loop = VecDDPG(env, agent, learn_iters=1)
     p0 = torch.cat([p.detach().reshape(-1) for p in agent.actor.parameters()]).clone()
     dones = 0
@@ -171,3 +172,32 @@ def test_vecddpg_loop_fills_replay_and_learns():
     m = agent.memory
     assert set(torch.unique(m.end_mem[:30 * n]).tolist()) <= {0.0, 1.0}
     assert float(m.s_mem[:30 * n].abs().max()) < 10
+
+
+def test_ddpg_graphed_update_is_one_adam_step():
+    """graph=True: the captured learn moves every parameter by one Adam step (<= ~lr) from the
+    same start as an eager agent, and the GPU actor is refreshed inside the graph."""
+    e_agent, g_agent = make_agent(seed=1), make_agent(seed=1, graph=True)
+    for m_e, m_g in ((e_agent.actor, g_agent.actor), (e_agent.critic, g_agent.critic),
+                     (e_agent.target_actor, g_agent.target_actor),
+                     (e_agent.target_critic, g_agent.target_critic)):
+        m_g.load_state_dict(m_e.state_dict())
+    rng = np.random.default_rng(0)
+    n = 5000
+    g_agent.memory.store_transition(rng.uniform(-2, 2, (n, 4)), rng.uniform(-3, 3, (n, 2)),
+                                    rng.normal(size=n), rng.uniform(-2, 2, (n, 4)),
+                                    (rng.uniform(size=n) < 0.1).astype(float))
+    g_agent.choose_action(torch.zeros(8, 4, device="cuda"), True)   # builds the GPU actor
+    g_agent.learn(is_reward_ascent=False)
+    torch.cuda.synchronize()
+    for lr, m_e, m_g in ((1e-4, e_agent.actor, g_agent.actor), (3e-4, e_agent.critic, g_agent.critic)):
+        pe = torch.cat([p.detach().reshape(-1) for p in m_e.parameters()])
+        pg = torch.cat([p.detach().reshape(-1) for p in m_g.parameters()])
+        assert torch.isfinite(pg).all() and not torch.equal(pe, pg)
+        assert float((pe - pg).abs().max()) <= 1.5 * lr
+    flat = g_agent.gpu_actor.flat.clone()
+    g_agent.gpu_actor.refresh()
+    torch.testing.assert_close(flat, g_agent.gpu_actor.flat, rtol=0, atol=0)
+    for _ in range(5):
+        g_agent.learn(is_reward_ascent=False, iter=2)
+    assert all(torch.isfinite(p).all() for p in g_agent.actor.parameters())
