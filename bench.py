@@ -156,12 +156,21 @@ def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
             K.mfma_pack(seg.ad, seg.actor, out=seg.apk)
             K.mfma_pack(seg.cd, seg.critic, out=seg.cpk)
     one()
+    dist_on = torch.distributed.is_available() and torch.distributed.is_initialized()
+    if dist_on:
+        torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(iters):
         one()
+    if dist_on:
+        torch.distributed.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if dist_on:   # the slowest rank's clock
+        t = torch.tensor([dt], device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
     return seg.n * seg.T * iters / dt, dt / iters
 
 

@@ -281,7 +281,9 @@ int rlp_mlp_forward(const rlp_mlp_desc *desc, const float *params, const float *
 
 int64_t rlp_mfma_packed_count(const rlp_mlp_desc *desc) {
     MfmaNet net;
-    if (!desc || !mfma_net_from_desc(*desc, &net)) return RLP_EUNSUPPORTED;
+    if (!desc || !mfma_net_from_desc(*desc, &net))
+        return fail(RLP_EUNSUPPORTED,
+                    "rlp_mfma_packed_count: need [S<=8 -> H -> H -> A<=4], H in {64,128,256}");
     return net.count;
 }
 

@@ -69,7 +69,7 @@ def run_both(kind, n, T, seed=3407, sub=None, params=None, success=None):
     return {k: host(v) for k, v in bufs.items()}, ob, host(st), ost, host(need), oneed, (ad, ap, cd, cp)
 
 
-@pytest.mark.parametrize("kind", sorted(A.ENV_DIMS))
+@pytest.mark.parametrize("kind", sorted(A.ROLLOUT_KINDS))
 @pytest.mark.parametrize("sub", [1, 2, 4])
 def test_rollout_closed_loop_vs_oracle(kind, sub):
     T = 12
@@ -89,6 +89,15 @@ def test_rollout_closed_loop_vs_oracle(kind, sub):
     vn_ok = g["done"][:, same] == 0
     a, b = g["value_next"][:, same][vn_ok], o["value_next"][:, same][vn_ok]
     assert (np.abs(a - b) <= 1e-4 + 1e-4 * np.abs(b)).mean() > 0.999
+
+
+def test_rollout_rejects_lidar_env():
+    """The 41-input lidar env is outside the fused kernel's net shapes: a clean error, no launch."""
+    kind = A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE
+    D, S, Ad = A.ENV_DIMS[kind]
+    ad, ap, cd, cp = nets(S, Ad, seed=1)
+    with pytest.raises(_native.RLPError, match="S<=8"):
+        K.mfma_pack(ad, dev(ap))
 
 
 def test_rollout_invariants_at_bench_size():
