@@ -47,6 +47,26 @@ __device__ __forceinline__ void sincos_fast(double x, double *sp, double *cp) {
     *cp = ((q + 1) & 2) ? -c0 : c0;
 }
 
+// x / 6 (the RK4 average): x * (1/6) plus one FMA residual correction (Markstein) — the correctly
+// rounded quotient but for rare ties, <= 1 ulp always; 3 VALU ops instead of the ~12 of the
+// general f64 division (scale / rcp / Newton / fmas / fixup)
+__device__ __forceinline__ double div6(double x) {
+    constexpr double r6 = 1.0 / 6.0;
+    const double q = x * r6;
+    return fma(fma(-6.0, q, x), r6, q);
+}
+
+// num / den for a finite, normal den (every physics denominator here: masses, inertias,
+// M + m - 3/4 m cos^2, cos(theta) away from 0): v_rcp_f64 + two Newton steps + a residual
+// correction, <= 1 ulp (no scaling / special-value path: 8 VALU ops instead of ~12)
+__device__ __forceinline__ double div_nr(double num, double den) {
+    double y = __builtin_amdgcn_rcp(den);
+    y = fma(y, fma(-den, y, 1.0), y);
+    y = fma(y, fma(-den, y, 1.0), y);
+    const double q = num * y;
+    return fma(fma(-den, q, num), y, q);
+}
+
 template <int KIND> struct Env;
 
 // components of the physics state step() may change (E::DW when the kind declares it, else D):
@@ -72,7 +92,7 @@ template <> struct Env<RLP_ENV_CARTPOLE> {
         num = num - p.kf * dx;
         num = num - 3.0 / 4.0 * p.m * p.g * Sv * Cv;
         double den = p.M + p.m - 3.0 / 4.0 * p.m * (Cv * Cv);
-        double ddx = num / den;
+        double ddx = div_nr(num, den);
         double ddth = 3.0 / 4.0 / p.m / p.ell * (p.m * p.g * Sv - p.m * ddx * Cv);
         d[0] = dth; d[1] = ddth; d[2] = dx; d[3] = ddx;
     }
@@ -106,7 +126,7 @@ template <> struct Env<RLP_ENV_CARTPOLE> {
             for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k; }
             ode(p, force, tmp, d);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) xx[i] = xx[i] + (sum[i] + h * d[i]) / 6;
+            for (int i = 0; i < 4; ++i) xx[i] = xx[i] + div6(sum[i] + h * d[i]);
             time += h;
         }
         s[0] = xx[0]; s[1] = xx[1]; s[2] = xx[2]; s[3] = xx[3]; s[4] = time;
@@ -161,7 +181,7 @@ template <> struct Env<RLP_ENV_CARTPOLE_ANGLEONLY> {
         num = num - p.kf * dx;
         num = num - 3.0 / 4.0 * p.m * p.g * Sv * Cv;
         double den = p.M + p.m - 3.0 / 4.0 * p.m * (Cv * Cv);
-        double ddx = num / den;
+        double ddx = div_nr(num, den);
         double ddth = 3.0 / 4.0 / p.m / p.ell * (p.m * p.g * Sv - p.m * ddx * Cv);
         d[0] = dth; d[1] = ddth; d[2] = dx; d[3] = ddx;
     }
@@ -187,7 +207,7 @@ template <> struct Env<RLP_ENV_CARTPOLE_ANGLEONLY> {
         ode(p, force, tmp, d);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            xx[i] = xx[i] + (sum[i] + dt * d[i]) / 6;
+            xx[i] = xx[i] + div6(sum[i] + dt * d[i]);
         }
         const double time = s[4] + dt;
         s[0] = xx[0]; s[1] = xx[1]; s[2] = xx[2]; s[3] = xx[3]; s[4] = time;
@@ -249,10 +269,10 @@ template <> struct Env<RLP_ENV_SOI> {
             K3[0] = h * t2; K3[1] = h * t3; K3[2] = h * (f0 - p.k * t2); K3[3] = h * (f1 - p.k * t3);
             t2 = x2 + K3[2]; t3 = x3 + K3[3];
             K4[0] = h * t2; K4[1] = h * t3; K4[2] = h * (f0 - p.k * t2); K4[3] = h * (f1 - p.k * t3);
-            s[0] = x0 + (K1[0] + 2 * K2[0] + 2 * K3[0] + K4[0]) / 6;
-            s[1] = x1 + (K1[1] + 2 * K2[1] + 2 * K3[1] + K4[1]) / 6;
-            s[2] = x2 + (K1[2] + 2 * K2[2] + 2 * K3[2] + K4[2]) / 6;
-            s[3] = x3 + (K1[3] + 2 * K2[3] + 2 * K3[3] + K4[3]) / 6;
+            s[0] = x0 + div6(K1[0] + 2 * K2[0] + 2 * K3[0] + K4[0]);
+            s[1] = x1 + div6(K1[1] + 2 * K2[1] + 2 * K3[1] + K4[1]);
+            s[2] = x2 + div6(K1[2] + 2 * K2[2] + 2 * K3[2] + K4[2]);
+            s[3] = x3 + div6(K1[3] + 2 * K2[3] + 2 * K3[3] + K4[3]);
             time += h;
         }
         s[4] = time;
@@ -370,7 +390,7 @@ template <bool BIDIR> struct UGV {
         ode(p, al, aa, t, d);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-            s[i] = xx[i] + (sum[i] + dt * d[i]) / 6;
+            s[i] = xx[i] + div6(sum[i] + dt * d[i]);
         }
         if (!BIDIR && s[2] < 0.) s[2] = 0.;
         const double time = s[5] + dt;
@@ -429,23 +449,23 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
                                                const double *x, double *d) {
         const double vx = x[3], vy = x[4], vz = x[5], phi = x[6], th = x[7], psi = x[8];
         const double pp = x[9], q = x[10], r = x[11];
-        const double dp = (-p.kr * pp - q * r * (p.J[2] - p.J[1]) + tq[0]) / p.J[0];
-        const double dq = (-p.kr * q - pp * r * (p.J[0] - p.J[2]) + tq[1]) / p.J[1];
-        const double dr = (-p.kr * r - pp * q * (p.J[1] - p.J[0]) + tq[2]) / p.J[2];
+        const double dp = div_nr(-p.kr * pp - q * r * (p.J[2] - p.J[1]) + tq[0], p.J[0]);
+        const double dq = div_nr(-p.kr * q - pp * r * (p.J[0] - p.J[2]) + tq[1], p.J[1]);
+        const double dr = div_nr(-p.kr * r - pp * q * (p.J[1] - p.J[0]) + tq[2], p.J[2]);
         double sphi, cphi, sth, cth, spsi, cpsi;
         sincos_fast(phi, &sphi, &cphi);
         sincos_fast(th, &sth, &cth);
         sincos_fast(psi, &spsi, &cpsi);
-        const double tth = sth / cth;
+        const double tth = div_nr(sth, cth);
         const double R01 = tth * sphi, R02 = tth * cphi, R11 = cphi, R12 = -sphi;
-        const double R21 = sphi / cth, R22 = cphi / cth;
+        const double R21 = div_nr(sphi, cth), R22 = div_nr(cphi, cth);
         d[6] = 1 * pp + R01 * q + R02 * r;
         d[7] = 0 * pp + R11 * q + R12 * r;
         d[8] = 0 * pp + R21 * q + R22 * r;
         d[0] = vx; d[1] = vy; d[2] = vz;
-        d[3] = (thr * (cpsi * sth * cphi + spsi * sphi) - p.kt * vx + 0.0) / p.m;
-        d[4] = (thr * (spsi * sth * cphi - cpsi * sphi) - p.kt * vy + 0.0) / p.m;
-        d[5] = -p.g + (thr * cphi * cth - p.kt * vz + 0.0) / p.m;
+        d[3] = div_nr(thr * (cpsi * sth * cphi + spsi * sphi) - p.kt * vx + 0.0, p.m);
+        d[4] = div_nr(thr * (spsi * sth * cphi - cpsi * sphi) - p.kt * vy + 0.0, p.m);
+        d[5] = -p.g + div_nr(thr * cphi * cth - p.kt * vz + 0.0, p.m);
         d[9] = dp; d[10] = dq; d[11] = dr;
     }
     __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
@@ -481,7 +501,7 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
             aref[i] = daref[i] * p.dt + old;
         }
         // att_control uav_pos_ctrl.py:46-65 -> fntsmc_att.control_update FNTSMC.py:80-106
-        const double tth = sth / cth;
+        const double tth = div_nr(sth, cth);
         const double f1[3][3] = {{1., sphi * tth, cphi * tth}, {0., cphi, -sphi},
                                  {0., sphi / cth, cphi / cth}};
         const double rho2[3] = {pp, q, r};
@@ -545,7 +565,7 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
         for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; t[i] = s[i] + k; }
         ode(p, uf, tq, t, d);
 #pragma unroll
-        for (int i = 0; i < 12; ++i) s[i] = s[i] + (sum[i] + h * d[i]) / 6;
+        for (int i = 0; i < 12; ++i) s[i] = s[i] + div6(sum[i] + h * d[i]);
         s[T] += p.dt;
         if (s[PSI] > kPi) s[PSI] -= 2 * kPi;
         if (s[PSI] < -kPi) s[PSI] += 2 * kPi;
@@ -813,12 +833,12 @@ template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
         for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; t[i] = s[i] + k; }
         ode(p, al, aa, t, d);
         if (p.shaped && s[V] < 0.) {  // demo copy rk44 :496-500: gate on the pre-step velocity
-            s[PHI] = s[PHI] + (sum[PHI] + dt * d[PHI]) / 6;
-            s[OM] = s[OM] + (sum[OM] + dt * d[OM]) / 6;
+            s[PHI] = s[PHI] + div6(sum[PHI] + dt * d[PHI]);
+            s[OM] = s[OM] + div6(sum[OM] + dt * d[OM]);
             s[V] = 0.;
         } else {
 #pragma unroll
-            for (int i = 0; i < 5; ++i) s[i] = s[i] + (sum[i] + dt * d[i]) / 6;
+            for (int i = 0; i < 5; ++i) s[i] = s[i] + div6(sum[i] + dt * d[i]);
             if (!p.shaped && s[V] < 0.) s[V] = 0.;
         }
         s[T] = s[T] + dt;

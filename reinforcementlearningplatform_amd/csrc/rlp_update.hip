@@ -102,6 +102,12 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// block barrier for LDS hand-offs only: drains this wave's LDS ops, not its global loads (HIP's
+// __syncthreads also waits for vmcnt(0), which would expose prefetched loads)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ void split8(const float (&x)[8], half8 &bh, half8 &bl) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -460,15 +466,36 @@ __global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
     }
     const int64_t ntiles = (w.rows + kUpdRows - 1) / kUpdRows;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        __syncthreads();  // previous tile's fragments are consumed
-        for (int i = threadIdx.x; i < kUpdRows * SP; i += blockDim.x) {
-            const int rr = i / SP, k = i % SP;
+        // this thread's s values for the tile, then the wave's G2 operands of both k-steps: the
+        // G2 loads stay in flight under the h1 fragment build (LDS-only barriers below do not
+        // drain vmcnt), instead of one exposed HBM round trip per k-step
+        float sv[(kUpdRows * SP + 255) / 256];
+#pragma unroll
+        for (int u = 0; u < (kUpdRows * SP + 255) / 256; ++u) {
+            const int i = threadIdx.x + 256 * u, rr = i / SP, k = i % SP;
             const int64_t r = tile * kUpdRows + rr;
-            float v = 0.f;
-            if (r < w.rows && k < S) v = w.s[(w.index ? w.index[r] : r) * S + k];
-            srow[rr][k] = v;
+            sv[u] = (i < kUpdRows * SP && r < w.rows && k < S) ? w.s[(w.index ? w.index[r] : r) * S + k] : 0.f;
         }
-        __syncthreads();
+        const float *g2base = w.g2t;
+        asm volatile("" : "+s"(g2base));
+        floatx4 gv[2][4][2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int jt = 0; jt < 4; ++jt) {
+                // A operands: g2(rows 32 ks + 8 gq + i, j = 64 wv + 16 jt + e)
+                const gptr<float> src = as_global(g2base + tile * kUpdTileFloats +
+                                                  (64 * wv + 16 * jt + e) * kUpdRows + 32 * ks + 8 * gq);
+                gv[ks][jt][0] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src);
+                gv[ks][jt][1] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 4);
+            }
+        lds_barrier();  // previous tile's fragments are consumed
+#pragma unroll
+        for (int u = 0; u < (kUpdRows * SP + 255) / 256; ++u) {
+            const int i = threadIdx.x + 256 * u;
+            if (i < kUpdRows * SP) srow[i / SP][i % SP] = sv[u];
+        }
+        lds_barrier();
         // h1 fragments: 2048 items (ks, nt, lane) of 8 rows, 8 per thread; the k-ordered f32 fma
         // chain of the forward's layer-1 MFMA, so h1 is bit-identical
 #pragma unroll 1
@@ -488,24 +515,18 @@ __global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
             *reinterpret_cast<half8 *>(hfrag + (((ks * 16 + nt) * 2 + 0) * 64 + ln) * 8) = hh;
             *reinterpret_cast<half8 *>(hfrag + (((ks * 16 + nt) * 2 + 1) * 64 + ln) * 8) = hl;
         }
-        __syncthreads();
-        const float *g2base = w.g2t;
-        asm volatile("" : "+s"(g2base));
+        lds_barrier();
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            // A operands: g2(rows 32 ks + 8 gq + i, j = 64 wv + 16 jt + e) * 2^sg, split
+            // A operands scaled by 2^sg and split
             half8 ah[4], al[4];
 #pragma unroll
             for (int jt = 0; jt < 4; ++jt) {
-                const gptr<float> src = as_global(g2base + tile * kUpdTileFloats +
-                                                  (64 * wv + 16 * jt + e) * kUpdRows + 32 * ks + 8 * gq);
-                const floatx4 v0 = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src);
-                const floatx4 v1 = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 4);
                 float x[8];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    x[u] = v0[u] * sg;
-                    x[u + 4] = v1[u] * sg;
+                    x[u] = gv[ks][jt][0][u] * sg;
+                    x[u + 4] = gv[ks][jt][1][u] * sg;
                 }
                 split8(x, ah[jt], al[jt]);
             }
