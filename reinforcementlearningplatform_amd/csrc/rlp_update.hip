@@ -39,10 +39,16 @@ struct Ppo2Args {
     double *loss_sum;
 };
 
+// block barrier for LDS hand-offs only: drains this wave's LDS ops, not its global loads (HIP's
+// __syncthreads also waits for vmcnt(0), which would expose prefetched loads)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // wave-level 256x256 GEMM of 16 rows through the block's chunk ring (all 4 waves call it in step):
-// acc[j] += A-chunks(Xw) x B(P), B(P) = bop(P) as f16 hi/lo (rlp_mfma_x3.hpp layout). One wave
-// per SIMD here, so latency is hidden inside the wave: a chunk's 16 A fragments are read up front
-// and the next phase's B operands are prepared inside the second chunk's MFMA region.
+// acc[j] += A-chunks(Xw) x B(P), B(P) = bop(P) as f16 hi/lo (rlp_mfma_x3.hpp layout). The phase
+// loop is fully unrolled, so bop may read register arrays at compile-time indices; the next
+// phase's B operands are prepared inside the second chunk's MFMA region.
 template <class BOp>
 __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, float *my_part,
                                           floatx4 (&acc)[16], BOp &&bop) {
@@ -50,16 +56,18 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
     const int lane = threadIdx.x & 63;
     auto issue = [&](int c) {
         float *slot = my_part + (c % kX3Ring) * kX3ChunkFloats;
-        const gptr<float> src = Xw + c * kX3ChunkFloats;
+        gptr<float> src = Xw + c * kX3ChunkFloats;
+        // opaque: the unrolled loop would otherwise materialise all 64 piece addresses up front
+        asm volatile("" : "+v"(src));
 #pragma unroll
         for (int q = 0; q < 4; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
     };
-    block_barrier_raw();  // every wave is done reading the ring
+    lds_barrier();  // every wave is done with the ring (and the staging tiles aliasing it)
     issue(0);
     issue(1);
     half8 bh, bl;
     bop(0, bh, bl);
-#pragma unroll 1
+#pragma unroll
     for (int P = 0; P < 8; ++P) {
         half8 nbh, nbl;
 #pragma unroll
@@ -70,28 +78,31 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
             block_barrier_raw();
             if (c + 2 < NC) issue(c + 2);
             const float *slot = ring + (c % kX3Ring) * kX3ChunkFloats + lane * 4;
-            half8 ah[8], al[8];
+            if (hf == 1 && P + 1 < 8) bop(P + 1, nbh, nbl);
+            // the chunk's 8 output tiles in two groups of 4 (8 fragment reads, then 12 MFMAs):
+            // 32 fragment registers instead of 64 keep two waves per SIMD within 256 registers
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj) {
-                ah[jj] = *reinterpret_cast<const half8 *>(slot + (2 * jj) * 256);
-                al[jj] = *reinterpret_cast<const half8 *>(slot + (2 * jj + 1) * 256);
-            }
-            if (hf == 1) bop(P + 1 < 8 ? P + 1 : 7, nbh, nbl);
+            for (int g4 = 0; g4 < 2; ++g4) {
+                half8 ah[4], al[4];
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj) {
-                floatx4 v = acc[8 * hf + jj];
-                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jj], bh, v, 0, 0, 0);
-                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jj], bl, v, 0, 0, 0);
-                v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jj], bh, v, 0, 0, 0);
-                acc[8 * hf + jj] = v;
+                for (int u = 0; u < 4; ++u) {
+                    ah[u] = *reinterpret_cast<const half8 *>(slot + (2 * (4 * g4 + u)) * 256);
+                    al[u] = *reinterpret_cast<const half8 *>(slot + (2 * (4 * g4 + u) + 1) * 256);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    floatx4 v = acc[8 * hf + 4 * g4 + u];
+                    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[u], bh, v, 0, 0, 0);
+                    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[u], bl, v, 0, 0, 0);
+                    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[u], bh, v, 0, 0, 0);
+                    acc[8 * hf + 4 * g4 + u] = v;
+                }
             }
-            // the 16 fragment reads first, then the 24 MFMAs (the default schedule sinks each
-            // read next to its MFMA: one exposed LDS latency per 3 MFMAs at one wave per SIMD)
-            __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 24, 0);
         }
-        bh = nbh;
-        bl = nbl;
+        if (P + 1 < 8) {
+            bh = nbh;
+            bl = nbl;
+        }
     }
 }
 
@@ -100,12 +111,6 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// block barrier for LDS hand-offs only: drains this wave's LDS ops, not its global loads (HIP's
-// __syncthreads also waits for vmcnt(0), which would expose prefetched loads)
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 __device__ __forceinline__ void split8(const float (&x)[8], half8 &bh, half8 &bl) {
@@ -117,16 +122,22 @@ __device__ __forceinline__ void split8(const float (&x)[8], half8 &bh, half8 &bl
     }
 }
 
+// LDS of one FD block (floats): [ ring (3 x 16 KiB) aliased by the 4 waves' half-tile staging
+// buffers | small weights | g3s | srw ]. The staging buffers are only used between the two GEMMs
+// and after the second, each window opened and closed by a block barrier, so two blocks fit a CU.
+constexpr int kFdStg = 20;  // staging row pitch: conflict-free b32 writes, 16-B aligned b128 reads
+constexpr int kFdStgFloats = 128 * kFdStg;  // [128 neurons][16 rows] (half of the 256 neurons)
+constexpr int kFdRegion = kX3RingFloats > 4 * kFdStgFloats ? kX3RingFloats : 4 * kFdStgFloats;
+
 template <int KS1, int A, int LOSS>
-__global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
+__global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
     constexpr int H = kUpdH, SMALL = mlp_small_floats<H, KS1, A>();
-    constexpr int STG = 20;  // staging row pitch: conflict-free b32 writes, 16-B aligned b128 reads
-    __shared__ __attribute__((aligned(16))) float lds[SMALL + kX3RingFloats + 4 * H * STG + 4 * 16 * 4 +
-                                                      4 * 16 * 8];
-    float *small = lds, *ring = lds + SMALL;
-    float *const stg = lds + SMALL + kX3RingFloats + (threadIdx.x >> 6) * H * STG;
-    float *const g3s = lds + SMALL + kX3RingFloats + 4 * H * STG + (threadIdx.x >> 6) * 64;  // [16][4]
-    float *const srw = lds + SMALL + kX3RingFloats + 4 * H * STG + 4 * 64 + (threadIdx.x >> 6) * 128;  // [16][8]
+    constexpr int STG = kFdStg;
+    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + 4 * 16 * 4 + 4 * 16 * 8];
+    float *ring = lds, *small = lds + kFdRegion;
+    float *const stg = lds + (threadIdx.x >> 6) * kFdStgFloats;  // aliases the ring
+    float *const g3s = lds + kFdRegion + SMALL + (threadIdx.x >> 6) * 64;            // [16][4]
+    float *const srw = lds + kFdRegion + SMALL + 4 * 64 + (threadIdx.x >> 6) * 128;  // [16][8]
     const MfmaNet &net = g.net;
     mlp_small_to_lds(g.packed, net, small);
     __syncthreads();
@@ -137,17 +148,28 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
     const float sw = info[0], acc_scale = info[1];
     const float k_out = 2.8853900817779268f * info[2];
     float *const my_part = ring + wv * 4 * 256;
-    // this wave's [256 neurons][16 rows] tile (staged in LDS) -> G[tile][n][64 rows] columns
-    // 16 wv .. 16 wv + 15, as 16 coalesced float4 stores per lane
-    auto store_tile = [&](float *Gt) {
-        wave_sync_lds();
+    // stage neurons [128 h, 128 h + 128) of the wave's [256 neurons][16 rows] register tile
+    // (the staging addresses are made opaque per use: otherwise the compiler hoists dozens of
+    // lane-dependent LDS addresses out of the tile loop and spills them)
+    auto stage_half = [&](const floatx4 (&t)[16], int h) {
+        float *b = stg + (4 * gq) * STG + e;
+        asm volatile("" : "+v"(b));
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int f = i * 64 + lane, n = f >> 2, c = f & 3;
-            const floatx4 v = *reinterpret_cast<const floatx4 *>(stg + n * STG + 4 * c);
-            *reinterpret_cast<floatx4 *>(Gt + n * kUpdRows + 16 * wv + 4 * c) = v;
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[(16 * j + q) * STG] = t[8 * h + j][q];
+    };
+    // the staged half -> G[tile][n][64 rows] columns 16 wv .. 16 wv + 15 (8 coalesced float4 stores)
+    auto store_half = [&](float *Gt, int h) {
+        const float *b = stg + (lane >> 2) * STG + 4 * (lane & 3);
+        asm volatile("" : "+v"(b));
+        float *o = Gt + (128 * h + (lane >> 2)) * kUpdRows + 16 * wv + 4 * (lane & 3);
+        asm volatile("" : "+v"(o));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {  // n = 16 i + lane / 4, columns 4 (lane % 4) ..
+            const floatx4 v = *reinterpret_cast<const floatx4 *>(b + 16 * i * STG);
+            *reinterpret_cast<floatx4 *>(o + 16 * i * kUpdRows) = v;
         }
-        wave_sync_lds();
     };
 
     float dW3p[A][4];  // neurons 64 c + lane
@@ -159,12 +181,12 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
         for (int c = 0; c < 4; ++c) dW3p[a][c] = 0.f;
     }
     double lsum = 0.0;
-    float dW1p[4][8], db1p[4];  // neurons 64 c + lane
+    float dW1p[4][4 * KS1], db1p[4];  // neurons 64 c + lane
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         db1p[c] = 0.f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) dW1p[c][k] = 0.f;
+        for (int k = 0; k < 4 * KS1; ++k) dW1p[c][k] = 0.f;
     }
     float g2max = 0.f;
 
@@ -177,7 +199,7 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
         const gptr<float> Xb = as_global(Pg) + net.off_x3t + wv * 4 * 256 + lane * 4;
         float *g2base = g.g2t;
         asm volatile("" : "+s"(g2base));
-        // the small weights are re-read from LDS per use, not hoisted into ~300 registers
+        // the small weights are re-read from LDS per use, not hoisted into registers
         const float *sm = small;
         asm volatile("" : "+s"(sm));
         const float *W1c = sm;
@@ -288,34 +310,37 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
         if (gq == 0) {
             lsum += (double)lrow;
 #pragma unroll
-            for (int a = 0; a < A; ++a) db3p[a] += g3[a];
-        }
-        // ---- dW3 = sum_rows g3 h2^T through the staging tile (transpose: lane owns neurons
-        // 64 c + lane and sums over the wave's 16 rows); g2 = (W3^T g3) * (1 - h2^2) in place
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) stg[(16 * j + 4 * gq + q) * STG + e] = acc[j][q];
-        if (gq == 0) {
-#pragma unroll
-            for (int a = 0; a < A; ++a) g3s[e * 4 + a] = g3[a];
-        }
-        wave_sync_lds();
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const float *hrow = stg + (64 * c + lane) * STG;
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-                const floatx4 h = *reinterpret_cast<const floatx4 *>(hrow + 4 * q4);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const floatx4 gr = *reinterpret_cast<const floatx4 *>(g3s + (4 * q4 + u) * 4);
-#pragma unroll
-                    for (int a = 0; a < A; ++a) dW3p[a][c] = __builtin_fmaf(gr[a], h[u], dW3p[a][c]);
-                }
+            for (int a = 0; a < A; ++a) {
+                db3p[a] += g3[a];
+                g3s[e * 4 + a] = g3[a];
             }
         }
-        wave_sync_lds();
+        lds_barrier();  // every wave is done reading the ring: the staging tiles may overwrite it
+        // ---- dW3 = sum_rows g3 h2^T through the staging tile, one half of the neurons at a time
+        // (transpose: lane owns neurons 64 c + lane and sums over the wave's 16 rows)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            stage_half(acc, h);
+            wave_sync_lds();
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                const float *hrow = stg + (64 * cc + lane) * STG;
+                asm volatile("" : "+v"(hrow));
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const floatx4 hv = *reinterpret_cast<const floatx4 *>(hrow + 4 * q4);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const floatx4 gr = *reinterpret_cast<const floatx4 *>(g3s + (4 * q4 + u) * 4);
+#pragma unroll
+                        for (int a = 0; a < A; ++a)
+                            dW3p[a][2 * h + cc] = __builtin_fmaf(gr[a], hv[u], dW3p[a][2 * h + cc]);
+                    }
+                }
+            }
+            wave_sync_lds();
+        }
+        // ---- g2 = (W3^T g3) * (1 - h2^2) in place, to HBM through the staging tile
 #pragma unroll
         for (int j = 0; j < 16; ++j)
 #pragma unroll
@@ -328,12 +353,15 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
                 acc[j][q] = dh * (1.f - h * h);
             }
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) stg[(16 * j + 4 * gq + q) * STG + e] = acc[j][q];
-        store_tile(g2base + tile * kUpdTileFloats);
+        for (int h = 0; h < 2; ++h) {
+            stage_half(acc, h);
+            wave_sync_lds();
+            store_half(g2base + tile * kUpdTileFloats, h);
+            wave_sync_lds();
+        }
 
-        // ---- backward: dh1 = W2^T g2, with g2 scaled per row into f16 range
+        // ---- backward: dh1 = W2^T g2, with g2 scaled per row into f16 range; B operands of phase
+        // P straight from the g2 registers (neurons 32 P + 4 gq + i and 32 P + 16 + 4 gq + i)
         float m = 0.f;
 #pragma unroll
         for (int j = 0; j < 16; ++j)
@@ -348,18 +376,16 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
         floatx4 dh1[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) dh1[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-        // B operands from the staged g2 tile (still in stg after store_tile): row e, neurons
-        // 32P + 4gq + i and 32P + 16 + 4gq + i
         x3_gemm16(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                x[i] = stg[(32 * P + 4 * gq + i) * STG + e] * sc;
-                x[i + 4] = stg[(32 * P + 16 + 4 * gq + i) * STG + e] * sc;
+                x[i] = acc[2 * P][i] * sc;
+                x[i + 4] = acc[2 * P + 1][i] * sc;
             }
             split8(x, bh, bl);
         });
-        wave_sync_lds();  // stg is rewritten with g1 below
+        lds_barrier();  // the ring is free again: g1 goes through the staging tiles
         // ---- g1 = dh1 * (1 - h1^2), h1 recomputed (bit-identical to the forward's)
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
@@ -367,27 +393,33 @@ __global__ void __launch_bounds__(256, 1) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float h1 = tanh_fast(pre[q]);
-                stg[(16 * t + 4 * gq + q) * STG + e] = dh1[t][q] * unscale * (1.f - h1 * h1);
+                dh1[t][q] = dh1[t][q] * unscale * (1.f - h1 * h1);
             }
         }
-        // ---- dW1 | db1 = sum_rows g1 [s | 1]^T through the staged g1 tile
-        wave_sync_lds();
+        // ---- dW1 | db1 = sum_rows g1 [s | 1]^T through the staging tile, by halves
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const float *grow = stg + (64 * c + lane) * STG;
+        for (int h = 0; h < 2; ++h) {
+            stage_half(dh1, h);
+            wave_sync_lds();
 #pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-                const floatx4 gv = *reinterpret_cast<const floatx4 *>(grow + 4 * q4);
+            for (int cc = 0; cc < 2; ++cc) {
+                const float *grow = stg + (64 * cc + lane) * STG;
+                asm volatile("" : "+v"(grow));
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    db1p[c] += gv[u];
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const floatx4 gv = *reinterpret_cast<const floatx4 *>(grow + 4 * q4);
 #pragma unroll
-                    for (int k = 0; k < 4 * KS1; ++k)
-                        dW1p[c][k] = __builtin_fmaf(gv[u], srw[(4 * q4 + u) * 8 + k], dW1p[c][k]);
+                    for (int u = 0; u < 4; ++u) {
+                        db1p[2 * h + cc] += gv[u];
+#pragma unroll
+                        for (int k = 0; k < 4 * KS1; ++k)
+                            dW1p[2 * h + cc][k] = __builtin_fmaf(gv[u], srw[(4 * q4 + u) * 8 + k],
+                                                                 dW1p[2 * h + cc][k]);
+                    }
                 }
             }
+            wave_sync_lds();
         }
-        wave_sync_lds();
     }
 
     // ---- per-wave partials: dW3 (lane's neurons) | db3 summed over the 16 row lanes | dW1 | db1
@@ -624,7 +656,7 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
     }
 }
 
-static int ppo2_grid() {  // one persistent block per CU (cached: device properties are slow)
+static int ppo2_grid() {  // CUs of the device (cached: device properties are slow)
     static int cus = 0;
     if (cus == 0) {
         int dev = 0, n = 0;
@@ -647,9 +679,9 @@ int64_t rlp_ppo2_workspace_floats(const rlp_mlp_desc *desc, int64_t rows) {
     MfmaNet net;
     if (!desc || !mfma_net_from_desc(*desc, &net) || net.H != kUpdH || rows < 0) return RLP_EINVAL;
     const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
-    const int64_t grid = ppo2_grid();
+    const int64_t grid = ppo2_grid();  // wgrad: one block per CU; FD: two
     return tiles * kUpdTileFloats + grid * (kUpdH * kUpdH + kUpdH) +
-           grid * 4 * (net.A * kUpdH + net.A + kUpdH * net.S + kUpdH) + 16;
+           2 * grid * 4 * (net.A * kUpdH + net.A + kUpdH * net.S + kUpdH) + 16;
 }
 
 int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_loss_cfg *cfg,
@@ -672,7 +704,8 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     RLP_REQUIRE(rows > 0, "rlp_ppo2_grad: rows=%lld", (long long)rows);
     hipStream_t st = as_stream(stream);
     const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
-    const int grid = (int)(tiles < ppo2_grid() ? tiles : ppo2_grid());
+    const int grid = (int)(tiles < ppo2_grid() ? tiles : ppo2_grid());         // wgrad: 1 per CU
+    const int gfd = (int)(tiles < 2 * ppo2_grid() ? tiles : 2 * ppo2_grid());  // FD: 2 per CU
     const int gfull = ppo2_grid();
     Ppo2Args g{};
     g.packed = packed; g.net = net;
@@ -689,12 +722,12 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     g.g2t = workspace;
     float *partw = workspace + tiles * kUpdTileFloats;
     g.part3 = partw + (int64_t)gfull * (kUpdH * kUpdH + kUpdH);
-    g.g2max = reinterpret_cast<unsigned *>(g.part3 + (int64_t)gfull * 4 *
+    g.g2max = reinterpret_cast<unsigned *>(g.part3 + (int64_t)2 * gfull * 4 *
                                            (net.A * kUpdH + net.A + kUpdH * net.S + kUpdH));
     if (hipMemsetAsync(g.g2max, 0, sizeof(unsigned), st) != hipSuccess)
         return fail(RLP_EINVAL, "rlp_ppo2_grad: memset");
     g.loss_sum = loss_sum;
-#define RLP_FD(KS1, A_, L) ppo2_fd_kernel<KS1, A_, L><<<grid, 256, 0, st>>>(g)
+#define RLP_FD(KS1, A_, L) ppo2_fd_kernel<KS1, A_, L><<<gfd, 256, 0, st>>>(g)
     if (actor) {
         if (net.ks1 == 1) {
             if (net.A == 1) RLP_FD(1, 1, 0); else if (net.A == 2) RLP_FD(1, 2, 0); else if (net.A == 3) RLP_FD(1, 3, 0); else RLP_FD(1, 4, 0);
@@ -715,7 +748,7 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     const int64_t total = (int64_t)net.H * net.S + net.H + (int64_t)net.H * net.H + net.H +
                           (int64_t)net.A * net.H + net.A;
     ppo2_reduce_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(net, partw, grid, g.part3,
-                                                                    grid * 4, grad);
+                                                                    gfd * 4, grad);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (reduce)");
     return RLP_OK;
 }

@@ -8,9 +8,9 @@ export TMPDIR=/tmp
 ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline"}
 (cd /tmp && timeout -k 10 120 rocprofv3 -L > "$OUT/$TAG/counters_list.txt" 2>&1) || true
 i=0
-for group in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
-             "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY" \
-             "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_VMEM" "TCC_HIT_sum TCC_MISS_sum"; do
+DEFAULT_GROUPS='FETCH_SIZE;WRITE_SIZE;SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES;SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY;SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_VMEM;TCC_HIT_sum TCC_MISS_sum'
+IFS=';' read -ra PGROUPS <<< "${PMC_GROUPS:-$DEFAULT_GROUPS}"
+for group in "${PGROUPS[@]}"; do
   i=$((i+1))
   (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $group --output-format csv -d "$OUT/$TAG/p$i" -o run \
       -- python3 "$ROOT/bench.py" $ARGS) > "$OUT/$TAG/p$i.log" 2>&1
