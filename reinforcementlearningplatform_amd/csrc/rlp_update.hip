@@ -461,10 +461,14 @@ struct WArgs {
 };
 
 // B fragments of h1 for one 64-row tile: [ks 2][nt 16][hi, lo][64 lanes][8 halfs] (64 KiB):
-// lane (g, e) of MFMA step ks holds h1(rows 32 ks + 8 g + i, neuron 16 nt + e) * 2^SH
+// lane (g, e) of MFMA step ks holds h1(rows 32 ks + 8 g + i, neuron 16 nt + e) * 2^SH.
+// 8 waves (2 per SIMD): wave wv owns output rows j in [32 wv, 32 wv + 32) of dW2 (128 accumulator
+// registers), all waves share the tile's h1 fragments.
+constexpr int kWgWaves = 8;
 template <int KS1>
-__global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
-    constexpr int H = kUpdH, SP = 4 * KS1;
+__global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
+    constexpr int H = kUpdH, SP = 4 * KS1, NT = 64 * kWgWaves;
+    constexpr int SV = (kUpdRows * SP + NT - 1) / NT;
     __shared__ float srow[kUpdRows][SP];
     __shared__ float w1s[H][SP + 1];
     __shared__ float b1s[H];
@@ -483,15 +487,12 @@ __global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
     const float sg = __builtin_amdgcn_ldexpf(1.f, 14 - gex);
     const float un2 = __builtin_amdgcn_ldexpf(1.f, gex - 14) / kX3HScale;  // 1 / (2^sg 2^SH)
     const float unb = __builtin_amdgcn_ldexpf(1.f, gex - 14);
-    half8 ones, zeros;
+    half8 ones;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        ones[i] = (_Float16)1.0f;
-        zeros[i] = (_Float16)0.0f;
-    }
-    floatx4 acc2[4][16], accb[4];
+    for (int i = 0; i < 8; ++i) ones[i] = (_Float16)1.0f;
+    floatx4 acc2[2][16], accb[2];
 #pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
+    for (int jt = 0; jt < 2; ++jt) {
         accb[jt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int nt = 0; nt < 16; ++nt) acc2[jt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -501,37 +502,37 @@ __global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
         // this thread's s values for the tile, then the wave's G2 operands of both k-steps: the
         // G2 loads stay in flight under the h1 fragment build (LDS-only barriers below do not
         // drain vmcnt), instead of one exposed HBM round trip per k-step
-        float sv[(kUpdRows * SP + 255) / 256];
+        float sv[SV];
 #pragma unroll
-        for (int u = 0; u < (kUpdRows * SP + 255) / 256; ++u) {
-            const int i = threadIdx.x + 256 * u, rr = i / SP, k = i % SP;
+        for (int u = 0; u < SV; ++u) {
+            const int i = threadIdx.x + NT * u, rr = i / SP, k = i % SP;
             const int64_t r = tile * kUpdRows + rr;
             sv[u] = (i < kUpdRows * SP && r < w.rows && k < S) ? w.s[(w.index ? w.index[r] : r) * S + k] : 0.f;
         }
         const float *g2base = w.g2t;
         asm volatile("" : "+s"(g2base));
-        floatx4 gv[2][4][2];
+        floatx4 gv[2][2][2];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-            for (int jt = 0; jt < 4; ++jt) {
-                // A operands: g2(rows 32 ks + 8 gq + i, j = 64 wv + 16 jt + e)
+            for (int jt = 0; jt < 2; ++jt) {
+                // A operands: g2(rows 32 ks + 8 gq + i, j = 32 wv + 16 jt + e)
                 const gptr<float> src = as_global(g2base + tile * kUpdTileFloats +
-                                                  (64 * wv + 16 * jt + e) * kUpdRows + 32 * ks + 8 * gq);
+                                                  (32 * wv + 16 * jt + e) * kUpdRows + 32 * ks + 8 * gq);
                 gv[ks][jt][0] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src);
                 gv[ks][jt][1] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 4);
             }
         lds_barrier();  // previous tile's fragments are consumed
 #pragma unroll
-        for (int u = 0; u < (kUpdRows * SP + 255) / 256; ++u) {
-            const int i = threadIdx.x + 256 * u;
+        for (int u = 0; u < SV; ++u) {
+            const int i = threadIdx.x + NT * u;
             if (i < kUpdRows * SP) srow[i / SP][i % SP] = sv[u];
         }
         lds_barrier();
-        // h1 fragments: 2048 items (ks, nt, lane) of 8 rows, 8 per thread; the k-ordered f32 fma
+        // h1 fragments: 2048 items (ks, nt, lane) of 8 rows, 4 per thread; the k-ordered f32 fma
         // chain of the forward's layer-1 MFMA, so h1 is bit-identical
 #pragma unroll 1
-        for (int it = threadIdx.x; it < 2048; it += blockDim.x) {
+        for (int it = threadIdx.x; it < 2048; it += NT) {
             const int ln = it & 63, nt = (it >> 6) & 15, ks = it >> 10;
             const int n = 16 * nt + (ln & 15), r0 = 32 * ks + 8 * (ln >> 4);
             float x[8];
@@ -551,9 +552,9 @@ __global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             // A operands scaled by 2^sg and split
-            half8 ah[4], al[4];
+            half8 ah[2], al[2];
 #pragma unroll
-            for (int jt = 0; jt < 4; ++jt) {
+            for (int jt = 0; jt < 2; ++jt) {
                 float x[8];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
@@ -567,7 +568,7 @@ __global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
                 const half8 bh = *reinterpret_cast<const half8 *>(hfrag + (((ks * 16 + nt) * 2 + 0) * 64 + lane) * 8);
                 const half8 bl = *reinterpret_cast<const half8 *>(hfrag + (((ks * 16 + nt) * 2 + 1) * 64 + lane) * 8);
 #pragma unroll
-                for (int jt = 0; jt < 4; ++jt) {
+                for (int jt = 0; jt < 2; ++jt) {
                     floatx4 v = acc2[jt][nt];
                     v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jt], bh, v, 0, 0, 0);
                     v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jt], bl, v, 0, 0, 0);
@@ -576,20 +577,19 @@ __global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
                 }
             }
 #pragma unroll
-            for (int jt = 0; jt < 4; ++jt) {  // db2: g2 against a ones column
+            for (int jt = 0; jt < 2; ++jt) {  // db2: g2 against a ones column
                 accb[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jt], ones, accb[jt], 0, 0, 0);
                 accb[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jt], ones, accb[jt], 0, 0, 0);
             }
         }
     }
-    (void)zeros;
-    // C layout: lane holds rows m = 4 gq + q (j = 64 wv + 16 jt + m), column e (n = 16 nt + e)
+    // C layout: lane holds rows m = 4 gq + q (j = 32 wv + 16 jt + m), column e (n = 16 nt + e)
     float *out = w.part + (size_t)blockIdx.x * (H * H + H);
 #pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
+    for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int j = 64 * wv + 16 * jt + 4 * gq + q;
+            const int j = 32 * wv + 16 * jt + 4 * gq + q;
 #pragma unroll
             for (int nt = 0; nt < 16; ++nt) out[j * H + 16 * nt + e] = acc2[jt][nt][q] * un2;
             if (e == 0) out[H * H + j] = accb[jt][q] * unb;
@@ -597,22 +597,36 @@ __global__ void __launch_bounds__(256, 1) ppo2_wgrad_kernel(WArgs w) {
 }
 
 // grad (torch order W1 b1 W2 b2 W3 b3) = sum over blocks / waves of the partials, in order
-__global__ void ppo2_reduce_kernel(MfmaNet net, const float *__restrict__ part, int nw,
-                                   const float *__restrict__ part3, int n3, float *grad) {
+// 64 consecutive outputs per block x kRedSplit partial-slices: each thread sums every
+// kRedSplit-th partial of its output (loads coalesced across the 64 outputs), then a fixed-order
+// LDS combine — deterministic, and no thread walks all 2 x 4 x CUs FD partials serially
+constexpr int kRedSplit = 16;
+__global__ void __launch_bounds__(64 * kRedSplit)
+ppo2_reduce_kernel(MfmaNet net, const float *__restrict__ part, int nw,
+                   const float *__restrict__ part3, int n3, float *grad) {
     const int H = net.H, S = net.S, A = net.A;
     const int64_t total = (int64_t)H * S + H + (int64_t)H * H + H + (int64_t)A * H + A;
     const int pw = H * H + H, p3 = A * H + A + H * S + H;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
+    const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 64 + o;
+    float acc = 0.f;
+    if (i < total) {
         const float *src;
         int stride, cnt;
         int64_t off;
         if (i < H * S + H) { src = part3; off = A * H + A + i; stride = p3; cnt = n3; }       // W1, b1
         else if (i < H * S + H + H * H + H) { src = part; off = i - (H * S + H); stride = pw; cnt = nw; }  // W2, b2
         else { src = part3; off = i - (H * S + 2 * H + H * H); stride = p3; cnt = n3; }        // W3, b3
-        float acc = 0.f;
-        for (int b = 0; b < cnt; ++b) acc += src[(size_t)b * stride + off];
-        grad[i] = acc;
+        for (int b = sl; b < cnt; b += kRedSplit) acc += src[(size_t)b * stride + off];
+    }
+    __shared__ float red[kRedSplit][64];
+    red[sl][o] = acc;
+    __syncthreads();
+    if (sl == 0 && i < total) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < kRedSplit; ++k) t += red[k][o];
+        grad[i] = t;
     }
 }
 
@@ -742,13 +756,13 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     WArgs w{};
     w.packed = packed; w.net = net; w.s = s; w.index = index; w.rows = rows;
     w.g2t = g.g2t; w.g2max = g.g2max; w.part = partw;
-    if (net.ks1 == 1) ppo2_wgrad_kernel<1><<<grid, 256, 0, st>>>(w);
-    else ppo2_wgrad_kernel<2><<<grid, 256, 0, st>>>(w);
+    if (net.ks1 == 1) ppo2_wgrad_kernel<1><<<grid, 64 * kWgWaves, 0, st>>>(w);
+    else ppo2_wgrad_kernel<2><<<grid, 64 * kWgWaves, 0, st>>>(w);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (wgrad)");
     const int64_t total = (int64_t)net.H * net.S + net.H + (int64_t)net.H * net.H + net.H +
                           (int64_t)net.A * net.H + net.A;
-    ppo2_reduce_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(net, partw, grid, g.part3,
-                                                                    gfd * 4, grad);
+    ppo2_reduce_kernel<<<(int)((total + 63) / 64), 64 * kRedSplit, 0, st>>>(net, partw, grid,
+                                                                          g.part3, gfd * 4, grad);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (reduce)");
     return RLP_OK;
 }
