@@ -434,6 +434,10 @@ int64_t rlp_struct_size(int which);
  * takes 1 when 2 would leave fewer than two blocks per CU, e.g. 32 768 UAV envs), 1 (f16x3 only),
  * 2 or 4. */
 int rlp_set_rollout_sub(int sub);
+/* Tuning knob of rlp_rollout (f16x3 path): 1 = shared-physics kernel (default where its LDS fits:
+ * the block's env state in LDS, each step's f64 physics on full 64-lane waves), 0 = the
+ * register-resident kernel (physics on the 16*sub lanes of each env's own wave). Same results. */
+int rlp_set_rollout_physics(int shared);
 /* Arithmetic of rlp_rollout's hidden layer (the [256 x 256] GEMM, 99 % of its FLOPs):
  *   RLP_MLP_F16X3 (default): error-compensated split, w*x = wh*xh + wh*xl + wl*xh on f16 MFMA with
  *     f32 accumulation — fp32-class accuracy (see tests/test_gpu_rollout.py) at 16/3 x the f32

@@ -44,6 +44,7 @@ def _declare(lib):
         "rlp_mfma_forward": (i32, [vp, vp, vp, vp, i64, vp]),
         "rlp_value_fixup": (i32, [vp, vp, vp, vp, vp, vp, i64, vp]),
         "rlp_set_rollout_sub": (i32, [i32]),
+        "rlp_set_rollout_physics": (i32, [i32]),
         "rlp_set_mlp_precision": (i32, [i32]),
         "rlp_get_mlp_precision": (i32, []),
         "rlp_reward_norm": (i32, [vp, i32, i32, vp, vp, vp, vp]),
@@ -119,3 +120,8 @@ def get_mlp_precision():
 
 def set_rollout_sub(sub):
     check(lib().rlp_set_rollout_sub(int(sub)), "rlp_set_rollout_sub")
+
+
+def set_rollout_physics(shared):
+    """1: shared-physics rollout kernel (default where it fits), 0: register-resident kernel."""
+    check(lib().rlp_set_rollout_physics(int(shared)), "rlp_set_rollout_physics")

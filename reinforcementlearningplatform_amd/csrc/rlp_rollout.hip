@@ -206,6 +206,189 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
 }
 
 // ------------------------------------------------------------------------------------------
+// Shared-physics variant of the f16x3 rollout (rollout_sp_kernel): the block's envs keep their
+// f64 state in LDS instead of one wave's registers, and each step's physics (sampling, RK4,
+// reward/terminal, buffer stores, auto-reset) runs on FULL 64-lane waves — EB/64 of the block's
+// waves per step, the role rotating over the waves so every SIMD gets the same share. In the
+// register-resident kernel a 32-env wave runs the f64 physics on 32 of its 64 lanes: half of the
+// VALU issue the physics costs (the kernel's binding resource) is idle lanes.
+// Per step: [all waves] obs from LDS -> actor + critic (shared W2 chunk ring) -> (mean, V) to LDS
+// | block barrier | [physics waves] sample, step, stores, reset, next obs to LDS | block barrier.
+// Same arithmetic, same Philox counters and the same reset points as rollout_kernel: a finished
+// env is reset right after its terminal step with the next step's counter (rollout_kernel does it
+// at the start of that step), except after the segment's last step, where need_reset carries it.
+// ------------------------------------------------------------------------------------------
+template <int KIND, int SUB>
+constexpr int rollout_sp_lds_bytes() {
+    using E = Env<KIND>;
+    constexpr int KS1 = (E::S + 3) / 4, EB = 4 * 16 * SUB;
+    return 4 * (2 * mlp_small_floats<256, KS1, E::A>() + EB * 8 + EB * (E::A + 1) + kX3RingFloats) +
+           8 * E::D * EB + 2 * EB;
+}
+// two blocks per CU must fit the CU's 160 KiB
+template <int KIND, int SUB>
+constexpr bool rollout_sp_fits() { return SUB <= 2 && rollout_sp_lds_bytes<KIND, SUB>() <= 80 * 1024; }
+
+template <int KIND, int H, int SUB>
+__global__ void __launch_bounds__(256, 2)
+rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__restrict__ need_reset,
+                  const float *__restrict__ actor, MfmaNet an, const float *__restrict__ critic,
+                  MfmaNet cn, RolloutArgs ra, rlp_rollout_bufs b) {
+    using E = Env<KIND>;
+    constexpr int S = E::S, A = E::A, D = E::D, KS1 = (S + 3) / 4, WENV = 16 * SUB;
+    constexpr int WAVES = 4, EB = WAVES * WENV, PW = EB / 64, ROT = WAVES / PW;
+    static_assert(EB % 64 == 0, "physics waves are full: EB must be a multiple of 64");
+    constexpr int SMALL = mlp_small_floats<H, KS1, A>();
+    __shared__ __attribute__((aligned(16))) float lds[2 * SMALL + EB * 8 + EB * (A + 1) + kX3RingFloats];
+    __shared__ double st[D][EB];
+    __shared__ uint8_t s_need[EB], s_pdone[EB];
+    float *small_a = lds, *small_c = lds + SMALL;
+    float(*sob)[8] = reinterpret_cast<float(*)[8]>(lds + 2 * SMALL);
+    float(*mv)[A + 1] = reinterpret_cast<float(*)[A + 1]>(lds + 2 * SMALL + EB * 8);
+    float *ring = lds + 2 * SMALL + EB * 8 + EB * (A + 1);
+    mlp_small_to_lds(actor, an, small_a);
+    mlp_small_to_lds(critic, cn, small_c);
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, e = lane & 15;
+    const int n = ra.n;
+    const int base = blockIdx.x * EB;
+
+    // state -> LDS; the first step's resets and observations (threads 0..EB-1, one env each)
+    for (int i = threadIdx.x; i < D * EB; i += blockDim.x) {
+        const int d = i / EB, le = i % EB;
+        st[d][le] = base + le < n ? state[(size_t)d * n + base + le] : 0.0;
+    }
+    __syncthreads();
+    if (threadIdx.x < EB) {
+        const int le = threadIdx.x, env = base + le;
+        double s[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) s[d] = st[d][le];
+        float o[S];
+        if (env < n && need_reset[env]) {
+            E::reset(p, s, ra.seed, ra.step0, ra.env_id0 + (uint64_t)env);
+#pragma unroll
+            for (int d = 0; d < D; ++d) st[d][le] = s[d];
+        }
+        E::observe(p, s, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sob[le][j] = (env < n && j < S) ? o[j] : 0.f;
+        s_need[le] = 0;
+        s_pdone[le] = 1;  // no value_next write before step 0
+    }
+    __syncthreads();
+
+    auto mlp_pass = [&](bool both) {
+        float bobs[SUB][KS1];
+#pragma unroll
+        for (int sb = 0; sb < SUB; ++sb)
+#pragma unroll
+            for (int kk = 0; kk < KS1; ++kk) bobs[sb][kk] = sob[WENV * wave + 16 * sb + e][4 * kk + g];
+#pragma unroll 1
+        for (int which = both ? 0 : 1; which < 2; ++which) {
+            float out[SUB][A];
+            mlp_x3_forward<H, SUB, KS1, A>(which ? critic : actor, which ? small_c : small_a, ring,
+                                           which ? cn : an, which ? 1 : A, bobs, out);
+            // lane (sub-block g, env e) owns out[g]
+            float sel[A];
+#pragma unroll
+            for (int a = 0; a < A; ++a) sel[a] = out[0][a];
+#pragma unroll
+            for (int sb = 1; sb < SUB; ++sb)
+                if (g == sb) {
+#pragma unroll
+                    for (int a = 0; a < A; ++a) sel[a] = out[sb][a];
+                }
+            if (lane < WENV) {
+                if (which) {
+                    mv[WENV * wave + lane][A] = sel[0];
+                } else {
+#pragma unroll
+                    for (int a = 0; a < A; ++a) mv[WENV * wave + lane][a] = sel[a];
+                }
+            }
+        }
+    };
+
+    for (int t = 0; t < ra.T; ++t) {
+        const uint64_t gstep = ra.step0 + (uint64_t)t;
+        mlp_pass(true);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // (mean, V) of every env
+        if (wave / PW == t % ROT) {  // this step's physics waves
+            const int le = 64 * (wave % PW) + lane, env = base + le;
+            if (env < n) {
+                const uint64_t eid = ra.env_id0 + (uint64_t)env;
+                const size_t k = (size_t)t * n + env;
+                double s[D];
+#pragma unroll
+                for (int d = 0; d < D; ++d) s[d] = st[d][le];
+                float o[S], eps[A], act[A], lp[A];
+#pragma unroll
+                for (int j = 0; j < S; ++j) o[j] = sob[le][j];
+                const float v = mv[le][A];
+                philox_normal_f32<A>(ra.seed, gstep, eid, eps);
+#pragma unroll
+                for (int a = 0; a < A; ++a) {
+                    const float mr = mv[le][a];
+                    const float m = (an.out_tanh ? tanhf(mr) : mr) * ra.gain[a] + ra.off[a];
+                    float x = m + ra.std_[a] * eps[a];
+                    x = fmaxf(fminf(x, ra.a_max[a]), ra.a_min[a]);
+                    act[a] = x;
+                    lp[a] = normal_logp(x, m, ra.std_[a]);
+                }
+                float on[S];
+                double r;
+                int f;
+                bool dn;
+                E::step(p, s, act, on, r, f, dn);
+#pragma unroll
+                for (int j = 0; j < S; ++j) {
+                    b.obs[k * S + j] = o[j];
+                    b.obs_next[k * S + j] = on[j];
+                }
+#pragma unroll
+                for (int a = 0; a < A; ++a) {
+                    b.action[k * A + a] = act[a];
+                    b.logp[k * A + a] = lp[a];
+                }
+                b.reward[k] = (float)r;
+                b.value[k] = v;
+                b.done[k] = dn;
+                b.success[k] = success_of(ra.success_rule, ra.success_flag, dn, f);
+                b.flag[k] = (int8_t)f;
+                if (!s_pdone[le]) b.value_next[k - n] = v;  // V(s'_{t-1}) == V(s_t) when no reset
+                s_pdone[le] = dn;
+                if (dn && t + 1 < ra.T) {  // the next step's reset (rollout_kernel: at its start)
+                    E::reset(p, s, ra.seed, gstep + 1, eid);
+                    E::observe(p, s, on);
+                } else {
+                    s_need[le] = dn;
+                }
+#pragma unroll
+                for (int d = 0; d < D; ++d) st[d][le] = s[d];
+#pragma unroll
+                for (int j = 0; j < S; ++j) sob[le][j] = on[j];
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // next observations
+    }
+
+    // bootstrap V(s'_{T-1}) for envs that did not terminate on the last step
+    mlp_pass(false);
+    __syncthreads();
+    if (threadIdx.x < EB) {
+        const int le = threadIdx.x, env = base + le;
+        if (env < n) {
+            if (!s_pdone[le]) b.value_next[(size_t)(ra.T - 1) * n + env] = mv[le][A];
+#pragma unroll
+            for (int d = 0; d < D; ++d) state[(size_t)d * n + env] = st[d][le];
+            need_reset[env] = s_need[le];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Packed-net forward over rows (evaluate(), learn()'s V(s) / V(s'), the value fix-up).
 // Each wave walks 16*SUB-row groups (grid-stride); with a row predicate, groups without an
 // active row are skipped wave-uniformly.
@@ -283,6 +466,8 @@ static int launch_packed_forward(const MfmaNet &net, const float *P, const float
     return RLP_OK;
 }
 
+static int g_rollout_shared_physics = 1;  // rlp_set_rollout_physics
+
 template <int KIND, int H, int SUB, bool X3>
 static int launch_rollout(const void *params, double *state, uint8_t *need_reset,
                           const float *actor, const MfmaNet &an, const float *critic,
@@ -292,8 +477,17 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     constexpr int threads = rollout_block<SUB, X3>();
     constexpr int envs_per_block = threads / 64 * 16 * SUB;
     const int blocks = (ra.n + envs_per_block - 1) / envs_per_block;
-    rollout_kernel<KIND, H, SUB, X3><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor, an,
-                                                                 critic, cn, ra, b);
+    if constexpr (X3 && rollout_sp_fits<KIND, SUB>()) {
+        if (g_rollout_shared_physics)
+            rollout_sp_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor,
+                                                                          an, critic, cn, ra, b);
+        else
+            rollout_kernel<KIND, H, SUB, X3><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor,
+                                                                         an, critic, cn, ra, b);
+    } else {
+        rollout_kernel<KIND, H, SUB, X3><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor,
+                                                                     an, critic, cn, ra, b);
+    }
     RLP_CHECK_LAUNCH("rlp_rollout");
     return RLP_OK;
 }
@@ -357,6 +551,14 @@ int rlp_get_mlp_precision(void) { return g_mlp_precision; }
 
 // tuning knob (envs per wave = 16 * sub): 0 = auto (f16x3: 1 when 32-env waves would leave fewer
 // than 2 blocks per CU, else 2; f32: 2), 1 (f16x3 only), 2, 4
+
+// tuning knob: 1 (default) = the shared-physics f16x3 kernel where its LDS fits (full-lane
+// physics), 0 = the register-resident kernel
+int rlp_set_rollout_physics(int shared) {
+    if (shared != 0 && shared != 1) return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
+    g_rollout_shared_physics = shared;
+    return RLP_OK;
+}
 
 int rlp_set_rollout_sub(int sub) {
     if (sub < 0 || sub > 4 || sub == 3) return fail(RLP_EINVAL, "rlp_set_rollout_sub: %d", sub);

@@ -133,6 +133,41 @@ def test_rollout_invariants_at_bench_size():
     assert th0.abs().max() <= np.pi / 8 + 1e-6 and obs0[:, 1].abs().max() == 0
 
 
+@pytest.mark.parametrize("kind", [A.RLP_ENV_CARTPOLE, A.RLP_ENV_CARTPOLE_ANGLEONLY, A.RLP_ENV_SOI,
+                                  A.RLP_ENV_UGV_FORWARD])
+def test_shared_physics_kernel_equals_register_kernel(kind):
+    """rlp_rollout's shared-physics kernel (state in LDS, full-lane physics waves, resets right
+    after the terminal step) and the register-resident kernel give identical buffers, state and
+    need_reset flags, including envs that terminate and reset inside the segment."""
+    D, S, Ad = A.ENV_DIMS[kind]
+    p = A.default_params(kind)
+    ad, ap, cd, cp = nets(S, Ad, seed=kind + 20)
+    lo, hi = A.action_bounds(kind, p)
+    std = [(h - l) / 3 for l, h in zip(lo, hi)]
+    n, T = 16384 + 37, 96
+    cfg = K.make_rollout_cfg(T, n, 99, 5, 0, std, lo, hi, A.RLP_SUCCESS_DONE_AND_FLAG_NE,
+                             A.timeout_flag(kind))
+    apk, cpk = K.mfma_pack(ad, dev(ap)), K.mfma_pack(cd, dev(cp))
+    runs = []
+    try:
+        for phys in (1, 0):
+            _native.set_rollout_physics(phys)
+            st = K.new_state(kind, n)
+            need = torch.ones(n, dtype=torch.uint8, device="cuda")
+            bufs = K.rollout_buffers(kind, T, n)
+            for seg in range(2):  # a second segment starts from the first's state / need_reset
+                K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs)
+            runs.append(({k: v.clone() for k, v in bufs.items()}, st.clone(), need.clone()))
+    finally:
+        _native.set_rollout_physics(1)
+    (b1, s1, n1), (b0, s0, n0) = runs
+    assert b1["done"][:-1].any(), "no env terminated inside the segment"
+    for key in b1:
+        assert torch.equal(b1[key], b0[key]), key
+    assert torch.equal(s1, s0)
+    assert torch.equal(n1, n0)
+
+
 def test_rollout_segments_chain():
     """Two T/2 segments == one T segment (state, need_reset and Philox counters carry over)."""
     kind = A.RLP_ENV_UAV_HOVER_OUTER_LOOP
