@@ -147,15 +147,25 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             const int c = 2 * P + hf;
+#if RLP_EXPERIMENT < 7  // 7, 8: timing experiments only, no DMA waits (8: no DMA at all)
             if (c + 1 < NC) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // own part of c landed
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+#if RLP_EXPERIMENT != 5 && RLP_EXPERIMENT < 7  // 5: no block barriers (chunks may be stale)
             block_barrier_raw();  // all parts of c landed; everyone is done with chunk c - 1
+#endif
+#if RLP_EXPERIMENT != 8
             if (c + 2 < NC) issue(c + 2);  // into chunk c - 1's slot
+#endif
             const float *slot = ring + (c % kX3Ring) * kX3ChunkFloats + lane * 4;
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
+#if RLP_EXPERIMENT == 6  // timing experiment only: no fragment reads (B operands as A)
+                const half8 ah = bh[0], al = bl[0];
+#else
                 const half8 ah = *reinterpret_cast<const half8 *>(slot + (2 * jj) * 256);
                 const half8 al = *reinterpret_cast<const half8 *>(slot + (2 * jj + 1) * 256);
+#endif
 #pragma unroll
                 for (int sb = 0; sb < SUB; ++sb) {
                     floatx4 a = acc[sb][8 * hf + jj];

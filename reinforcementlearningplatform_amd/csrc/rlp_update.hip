@@ -152,23 +152,23 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
     // (the staging addresses are made opaque per use: otherwise the compiler hoists dozens of
     // lane-dependent LDS addresses out of the tile loop and spills them)
     auto stage_half = [&](const floatx4 (&t)[16], int h) {
-        float *b = stg + (4 * gq) * STG + e;
-        asm volatile("" : "+v"(b));
+        int ob = (4 * gq) * STG + e;
+        asm volatile("" : "+v"(ob));
 #pragma unroll
         for (int j = 0; j < 8; ++j)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) b[(16 * j + q) * STG] = t[8 * h + j][q];
+            for (int q = 0; q < 4; ++q) stg[ob + (16 * j + q) * STG] = t[8 * h + j][q];
     };
     // the staged half -> G[tile][n][64 rows] columns 16 wv .. 16 wv + 15 (8 coalesced float4 stores)
-    auto store_half = [&](float *Gt, int h) {
-        const float *b = stg + (lane >> 2) * STG + 4 * (lane & 3);
-        asm volatile("" : "+v"(b));
-        float *o = Gt + (128 * h + (lane >> 2)) * kUpdRows + 16 * wv + 4 * (lane & 3);
-        asm volatile("" : "+v"(o));
+    auto store_half = [&](__attribute__((address_space(1))) float *Gt, int h) {
+        int ob = (lane >> 2) * STG + 4 * (lane & 3);
+        asm volatile("" : "+v"(ob));
+        int oo = (128 * h + (lane >> 2)) * kUpdRows + 16 * wv + 4 * (lane & 3);
+        asm volatile("" : "+v"(oo));
 #pragma unroll
         for (int i = 0; i < 8; ++i) {  // n = 16 i + lane / 4, columns 4 (lane % 4) ..
-            const floatx4 v = *reinterpret_cast<const floatx4 *>(b + 16 * i * STG);
-            *reinterpret_cast<floatx4 *>(o + 16 * i * kUpdRows) = v;
+            const floatx4 v = *reinterpret_cast<const floatx4 *>(stg + ob + 16 * i * STG);
+            *reinterpret_cast<__attribute__((address_space(1))) floatx4 *>(Gt + oo + 16 * i * kUpdRows) = v;
         }
     };
 
@@ -197,11 +197,12 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
         asm volatile("" : "+s"(Pg));
         const gptr<float> Xf = as_global(Pg) + net.off_x3 + wv * 4 * 256 + lane * 4;
         const gptr<float> Xb = as_global(Pg) + net.off_x3t + wv * 4 * 256 + lane * 4;
-        float *g2base = g.g2t;
+        auto *g2base = (__attribute__((address_space(1))) float *)g.g2t;
         asm volatile("" : "+s"(g2base));
         // the small weights are re-read from LDS per use, not hoisted into registers
-        const float *sm = small;
-        asm volatile("" : "+s"(sm));
+        int smo = 0;  // (an opaque offset keeps the LDS address space; a pointer would go FLAT)
+        asm volatile("" : "+s"(smo));
+        const float *sm = small + smo;
         const float *W1c = sm;
         const float *B1c = sm + (net.off_b1 - net.off_w1);
         const float *B2c = sm + (net.off_b2 - net.off_w1);
@@ -324,8 +325,9 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
             wave_sync_lds();
 #pragma unroll
             for (int cc = 0; cc < 2; ++cc) {
-                const float *hrow = stg + (64 * cc + lane) * STG;
-                asm volatile("" : "+v"(hrow));
+                int orow = (64 * cc + lane) * STG;
+                asm volatile("" : "+v"(orow));
+                const float *hrow = stg + orow;
 #pragma unroll
                 for (int q4 = 0; q4 < 4; ++q4) {
                     const floatx4 hv = *reinterpret_cast<const floatx4 *>(hrow + 4 * q4);
@@ -403,8 +405,9 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
             wave_sync_lds();
 #pragma unroll
             for (int cc = 0; cc < 2; ++cc) {
-                const float *grow = stg + (64 * cc + lane) * STG;
-                asm volatile("" : "+v"(grow));
+                int orow = (64 * cc + lane) * STG;
+                asm volatile("" : "+v"(orow));
+                const float *grow = stg + orow;
 #pragma unroll
                 for (int q4 = 0; q4 < 4; ++q4) {
                     const floatx4 gv = *reinterpret_cast<const floatx4 *>(grow + 4 * q4);
