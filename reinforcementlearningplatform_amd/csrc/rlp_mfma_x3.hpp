@@ -60,7 +60,9 @@ __device__ __forceinline__ void block_barrier_raw() {
 }
 
 // Every wave of the block must call this the same number of times (it contains block barriers).
-template <int H, int SUB, int KS1, int NOUT>
+// RG: chunks in the ring (3: two in flight while one is read; 2: one in flight, for kernels whose
+// other LDS leaves no room for a third 16-KiB slot).
+template <int H, int SUB, int KS1, int NOUT, int RG = kX3Ring>
 __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, const float *small,
                                                float *ring, const MfmaNet &net, const int nout,
                                                const float (&bobs)[SUB][KS1],
@@ -82,15 +84,16 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
     const float acc_scale = info[1];
     const float k_out = 2.8853900817779268f * info[2];  // exp(2x) constant with 2^-(sw+SH) folded
 
+    static_assert(RG == 2 || RG == 3, "ring of 2 or 3 chunks");
     auto issue = [&](int c) {
-        float *slot = my_part + (c % kX3Ring) * kX3ChunkFloats;
+        float *slot = my_part + (c % RG) * kX3ChunkFloats;
         const gptr<float> src = X + c * kX3ChunkFloats;
 #pragma unroll
         for (int q = 0; q < 4; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
     };
     block_barrier_raw();  // every wave is done reading the ring (previous call)
     issue(0);
-    issue(1);
+    if (RG == 3) issue(1);
 
     floatx4 acc[SUB][NT];
 #pragma unroll
@@ -148,16 +151,16 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
         for (int hf = 0; hf < 2; ++hf) {
             const int c = 2 * P + hf;
 #if RLP_EXPERIMENT < 7  // 7, 8: timing experiments only, no DMA waits (8: no DMA at all)
-            if (c + 1 < NC) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // own part of c landed
+            if (RG == 3 && c + 1 < NC) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // own part of c landed
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
 #if RLP_EXPERIMENT != 5 && RLP_EXPERIMENT < 7  // 5: no block barriers (chunks may be stale)
             block_barrier_raw();  // all parts of c landed; everyone is done with chunk c - 1
 #endif
 #if RLP_EXPERIMENT != 8
-            if (c + 2 < NC) issue(c + 2);  // into chunk c - 1's slot
+            if (c + RG - 1 < NC) issue(c + RG - 1);  // into chunk c - 1's slot
 #endif
-            const float *slot = ring + (c % kX3Ring) * kX3ChunkFloats + lane * 4;
+            const float *slot = ring + (c % RG) * kX3ChunkFloats + lane * 4;
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
 #if RLP_EXPERIMENT == 6  // timing experiment only: no fragment reads (B operands as A)

@@ -218,16 +218,21 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
 // env is reset right after its terminal step with the next step's counter (rollout_kernel does it
 // at the start of that step), except after the segment's last step, where need_reset carries it.
 // ------------------------------------------------------------------------------------------
-template <int KIND, int SUB>
+template <int KIND, int SUB, int RG>
 constexpr int rollout_sp_lds_bytes() {
     using E = Env<KIND>;
     constexpr int KS1 = (E::S + 3) / 4, EB = 4 * 16 * SUB;
-    return 4 * (2 * mlp_small_floats<256, KS1, E::A>() + EB * 8 + EB * (E::A + 1) + kX3RingFloats) +
+    return 4 * (2 * mlp_small_floats<256, KS1, E::A>() + EB * 8 + EB * (E::A + 1) + RG * kX3ChunkFloats) +
            8 * E::D * EB + 2 * EB;
 }
-// two blocks per CU must fit the CU's 160 KiB
+// two blocks per CU must fit the CU's 160 KiB: a 3-chunk W2 ring where it fits, else 2 (UAV)
 template <int KIND, int SUB>
-constexpr bool rollout_sp_fits() { return SUB <= 2 && rollout_sp_lds_bytes<KIND, SUB>() <= 80 * 1024; }
+constexpr int rollout_sp_ring() {
+    return rollout_sp_lds_bytes<KIND, SUB, 3>() <= 80 * 1024 ? 3
+         : rollout_sp_lds_bytes<KIND, SUB, 2>() <= 80 * 1024 ? 2 : 0;
+}
+template <int KIND, int SUB>
+constexpr bool rollout_sp_fits() { return SUB <= 2 && rollout_sp_ring<KIND, SUB>() != 0; }
 
 template <int KIND, int H, int SUB>
 __global__ void __launch_bounds__(256, 2)
@@ -238,8 +243,8 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
     constexpr int S = E::S, A = E::A, D = E::D, KS1 = (S + 3) / 4, WENV = 16 * SUB;
     constexpr int WAVES = 4, EB = WAVES * WENV, PW = EB / 64, ROT = WAVES / PW;
     static_assert(EB % 64 == 0, "physics waves are full: EB must be a multiple of 64");
-    constexpr int SMALL = mlp_small_floats<H, KS1, A>();
-    __shared__ __attribute__((aligned(16))) float lds[2 * SMALL + EB * 8 + EB * (A + 1) + kX3RingFloats];
+    constexpr int SMALL = mlp_small_floats<H, KS1, A>(), RG = rollout_sp_ring<KIND, SUB>();
+    __shared__ __attribute__((aligned(16))) float lds[2 * SMALL + EB * 8 + EB * (A + 1) + RG * kX3ChunkFloats];
     __shared__ double st[D][EB];
     __shared__ uint8_t s_need[EB], s_pdone[EB];
     float *small_a = lds, *small_c = lds + SMALL;
@@ -291,8 +296,8 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
 #if RLP_EXPERIMENT == 1  // timing experiment only: MLP skipped
             for (int sb = 0; sb < SUB; ++sb) for (int a = 0; a < A; ++a) out[sb][a] = bobs[sb][0] * 0.5f;
 #else
-            mlp_x3_forward<H, SUB, KS1, A>(which ? critic : actor, which ? small_c : small_a, ring,
-                                           which ? cn : an, which ? 1 : A, bobs, out);
+            mlp_x3_forward<H, SUB, KS1, A, RG>(which ? critic : actor, which ? small_c : small_a, ring,
+                                               which ? cn : an, which ? 1 : A, bobs, out);
 #endif
             // lane (sub-block g, env e) owns out[g]
             float sel[A];

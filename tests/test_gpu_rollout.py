@@ -134,7 +134,7 @@ def test_rollout_invariants_at_bench_size():
 
 
 @pytest.mark.parametrize("kind", [A.RLP_ENV_CARTPOLE, A.RLP_ENV_CARTPOLE_ANGLEONLY, A.RLP_ENV_SOI,
-                                  A.RLP_ENV_UGV_FORWARD])
+                                  A.RLP_ENV_UGV_FORWARD, A.RLP_ENV_UAV_HOVER_OUTER_LOOP])
 def test_shared_physics_kernel_equals_register_kernel(kind):
     """rlp_rollout's shared-physics kernel (state in LDS, full-lane physics waves, resets right
     after the terminal step) and the register-resident kernel give identical buffers, state and
