@@ -367,8 +367,9 @@ def main():
     ap.add_argument("--ddpg", type=int, default=1, help="also time SOI DDPG with the HBM replay (config 3)")
     ap.add_argument("--oa", type=int, default=1, help="also time UGVForwardObstacleAvoidance env steps (lidar)")
     ap.add_argument("--sac", type=int, default=1, help="also time UGVForwardObstacleAvoidance SAC (config 5 shard)")
-    ap.add_argument("--physics", default="shared", choices=["shared", "lanes"],
-                    help="rollout kernel: env state in LDS + full-lane physics waves, or per-wave registers")
+    ap.add_argument("--physics", default="shared", choices=["shared", "shared8", "lanes"],
+                    help="rollout kernel: env state in LDS + full-lane physics waves (4-wave blocks, or "
+                         "8-wave blocks of 16-env waves), or per-wave registers")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
@@ -393,7 +394,7 @@ def main():
             dist.init_process_group(backend)
     if args.sub:
         _native.set_rollout_sub(args.sub)
-    _native.set_rollout_physics(1 if args.physics == "shared" else 0)
+    _native.set_rollout_physics({"lanes": 0, "shared": 1, "shared8": 2}[args.physics])
     prec = _native.MLP_F16X3 if args.precision == "f16x3" else _native.MLP_FP32
     _native.set_mlp_precision(prec)
 

@@ -435,8 +435,9 @@ int64_t rlp_struct_size(int which);
  * 2 or 4. */
 int rlp_set_rollout_sub(int sub);
 /* Tuning knob of rlp_rollout (f16x3 path): 1 = shared-physics kernel (default where its LDS fits:
- * the block's env state in LDS, each step's f64 physics on full 64-lane waves), 0 = the
- * register-resident kernel (physics on the 16*sub lanes of each env's own wave). Same results. */
+ * the block's env state in LDS, each step's f64 physics on full 64-lane waves), 2 = the same with
+ * 8-wave blocks of 16-env waves (4 waves per SIMD), 0 = the register-resident kernel (physics on
+ * the 16*sub lanes of each env's own wave). Same results. */
 int rlp_set_rollout_physics(int shared);
 /* Arithmetic of rlp_rollout's hidden layer (the [256 x 256] GEMM, 99 % of its FLOPs):
  *   RLP_MLP_F16X3 (default): error-compensated split, w*x = wh*xh + wh*xl + wl*xh on f16 MFMA with

@@ -62,19 +62,22 @@ __device__ __forceinline__ void block_barrier_raw() {
 // Every wave of the block must call this the same number of times (it contains block barriers).
 // RG: chunks in the ring (3: two in flight while one is read; 2: one in flight, for kernels whose
 // other LDS leaves no room for a third 16-KiB slot).
-template <int H, int SUB, int KS1, int NOUT, int RG = kX3Ring>
+// W: waves of the block sharing the ring (4 or 8); each DMAs 16 / W of the 16 KiB of every chunk.
+template <int H, int SUB, int KS1, int NOUT, int RG = kX3Ring, int W = kX3Waves>
 __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, const float *small,
                                                float *ring, const MfmaNet &net, const int nout,
                                                const float (&bobs)[SUB][KS1],
                                                float (&out)[SUB][NOUT]) {
     static_assert(H == 256, "chunking assumes H = 256 (2 chunks of 8 output tiles per phase)");
     constexpr int NT = H / 16, NPH = H / 32, NC = 2 * NPH;
-    const int lane = threadIdx.x & 63, wv = (threadIdx.x >> 6) & (kX3Waves - 1);
+    static_assert(W == 4 || W == 8, "4 or 8 waves share the ring");
+    constexpr int NPW = 16 / W;  // 1-KiB DMA pieces per wave and chunk
+    const int lane = threadIdx.x & 63, wv = (threadIdx.x >> 6) & (W - 1);
     const int g = lane >> 4, e = lane & 15;
     const float *Pg = P0;
     asm volatile("" : "+s"(Pg));
-    const gptr<float> X = as_global(Pg) + net.off_x3 + wv * 4 * 256 + lane * 4;
-    float *const my_part = ring + wv * 4 * 256;
+    const gptr<float> X = as_global(Pg) + net.off_x3 + wv * NPW * 256 + lane * 4;
+    float *const my_part = ring + wv * NPW * 256;
     const float *W1c = small;
     const float *B1c = small + (net.off_b1 - net.off_w1);
     const float *B2c = small + (net.off_b2 - net.off_w1);
@@ -89,7 +92,7 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
         float *slot = my_part + (c % RG) * kX3ChunkFloats;
         const gptr<float> src = X + c * kX3ChunkFloats;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
+        for (int q = 0; q < NPW; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
     };
     block_barrier_raw();  // every wave is done reading the ring (previous call)
     issue(0);
@@ -151,8 +154,12 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
         for (int hf = 0; hf < 2; ++hf) {
             const int c = 2 * P + hf;
 #if RLP_EXPERIMENT < 7  // 7, 8: timing experiments only, no DMA waits (8: no DMA at all)
-            if (RG == 3 && c + 1 < NC) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // own part of c landed
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (RG == 3 && c + 1 < NC) {  // own part of c landed (c + 1's NPW pieces may not)
+                if constexpr (NPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
 #endif
 #if RLP_EXPERIMENT != 5 && RLP_EXPERIMENT < 7  // 5: no block barriers (chunks may be stale)
             block_barrier_raw();  // all parts of c landed; everyone is done with chunk c - 1

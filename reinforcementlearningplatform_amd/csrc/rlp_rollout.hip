@@ -218,32 +218,35 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
 // env is reset right after its terminal step with the next step's counter (rollout_kernel does it
 // at the start of that step), except after the segment's last step, where need_reset carries it.
 // ------------------------------------------------------------------------------------------
-template <int KIND, int SUB, int RG>
+template <int KIND, int SUB, int RG, int W = 4>
 constexpr int rollout_sp_lds_bytes() {
     using E = Env<KIND>;
-    constexpr int KS1 = (E::S + 3) / 4, EB = 4 * 16 * SUB;
+    constexpr int KS1 = (E::S + 3) / 4, EB = W * 16 * SUB;
     return 4 * (2 * mlp_small_floats<256, KS1, E::A>() + EB * 8 + EB * (E::A + 1) + RG * kX3ChunkFloats) +
            8 * E::D * EB + 2 * EB;
 }
 // two blocks per CU must fit the CU's 160 KiB: a 3-chunk W2 ring where it fits, else 2 (UAV)
-template <int KIND, int SUB>
+template <int KIND, int SUB, int W = 4>
 constexpr int rollout_sp_ring() {
-    return rollout_sp_lds_bytes<KIND, SUB, 3>() <= 80 * 1024 ? 3
-         : rollout_sp_lds_bytes<KIND, SUB, 2>() <= 80 * 1024 ? 2 : 0;
+    return rollout_sp_lds_bytes<KIND, SUB, 3, W>() <= 80 * 1024 ? 3
+         : rollout_sp_lds_bytes<KIND, SUB, 2, W>() <= 80 * 1024 ? 2 : 0;
 }
 template <int KIND, int SUB>
 constexpr bool rollout_sp_fits() { return SUB <= 2 && rollout_sp_ring<KIND, SUB>() != 0; }
 
-template <int KIND, int H, int SUB>
-__global__ void __launch_bounds__(256, 2)
+// W = 4: 4-wave blocks, two per CU (2 waves per SIMD, <= 256 registers); W = 8 (SUB = 1): 8-wave
+// blocks, two per CU (4 waves per SIMD, <= 128 registers): twice the waves to hide latency with,
+// each wave 16 envs, the ring shared by 8 waves.
+template <int KIND, int H, int SUB, int W = 4>
+__global__ void __launch_bounds__(64 * W, W / 2)  // (HIP's second argument: waves per SIMD)
 rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__restrict__ need_reset,
                   const float *__restrict__ actor, MfmaNet an, const float *__restrict__ critic,
                   MfmaNet cn, RolloutArgs ra, rlp_rollout_bufs b) {
     using E = Env<KIND>;
     constexpr int S = E::S, A = E::A, D = E::D, KS1 = (S + 3) / 4, WENV = 16 * SUB;
-    constexpr int WAVES = 4, EB = WAVES * WENV, PW = EB / 64, ROT = WAVES / PW;
+    constexpr int WAVES = W, EB = WAVES * WENV, PW = EB / 64, ROT = WAVES / PW;
     static_assert(EB % 64 == 0, "physics waves are full: EB must be a multiple of 64");
-    constexpr int SMALL = mlp_small_floats<H, KS1, A>(), RG = rollout_sp_ring<KIND, SUB>();
+    constexpr int SMALL = mlp_small_floats<H, KS1, A>(), RG = rollout_sp_ring<KIND, SUB, W>();
     __shared__ __attribute__((aligned(16))) float lds[2 * SMALL + EB * 8 + EB * (A + 1) + RG * kX3ChunkFloats];
     __shared__ double st[D][EB];
     __shared__ uint8_t s_need[EB], s_pdone[EB];
@@ -296,8 +299,8 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
 #if RLP_EXPERIMENT == 1  // timing experiment only: MLP skipped
             for (int sb = 0; sb < SUB; ++sb) for (int a = 0; a < A; ++a) out[sb][a] = bobs[sb][0] * 0.5f;
 #else
-            mlp_x3_forward<H, SUB, KS1, A, RG>(which ? critic : actor, which ? small_c : small_a, ring,
-                                               which ? cn : an, which ? 1 : A, bobs, out);
+            mlp_x3_forward<H, SUB, KS1, A, RG, W>(which ? critic : actor, which ? small_c : small_a,
+                                                  ring, which ? cn : an, which ? 1 : A, bobs, out);
 #endif
             // lane (sub-block g, env e) owns out[g]
             float sel[A];
@@ -490,6 +493,15 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     constexpr int threads = rollout_block<SUB, X3>();
     constexpr int envs_per_block = threads / 64 * 16 * SUB;
     const int blocks = (ra.n + envs_per_block - 1) / envs_per_block;
+    if constexpr (X3 && SUB == 1 && rollout_sp_ring<KIND, 1, 8>() != 0) {
+        if (g_rollout_shared_physics == 2) {  // 8-wave blocks, 16 envs per wave
+            const int blocks8 = (ra.n + 127) / 128;
+            rollout_sp_kernel<KIND, H, 1, 8><<<blocks8, 512, 0, stream>>>(p, state, need_reset, actor,
+                                                                         an, critic, cn, ra, b);
+            RLP_CHECK_LAUNCH("rlp_rollout");
+            return RLP_OK;
+        }
+    }
     if constexpr (X3 && rollout_sp_fits<KIND, SUB>()) {
         if (g_rollout_shared_physics)
             rollout_sp_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor,
@@ -517,6 +529,7 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
     if (an.H != 256 || cn.H != 256)
         return fail(RLP_EUNSUPPORTED, "rlp_rollout: hidden width %d/%d (built for 256)", an.H, cn.H);
     if (prec == RLP_MLP_F16X3) {
+        if (g_rollout_shared_physics == 2) sub = 1;  // the 8-wave variant runs 16-env waves
         if (sub == 0) {  // auto: 32-env waves unless that leaves fewer than 2 blocks per CU
             static int cus = 0;
             if (cus == 0) {
@@ -568,7 +581,7 @@ int rlp_get_mlp_precision(void) { return g_mlp_precision; }
 // tuning knob: 1 (default) = the shared-physics f16x3 kernel where its LDS fits (full-lane
 // physics), 0 = the register-resident kernel
 int rlp_set_rollout_physics(int shared) {
-    if (shared != 0 && shared != 1) return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
+    if (shared < 0 || shared > 2) return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
     g_rollout_shared_physics = shared;
     return RLP_OK;
 }

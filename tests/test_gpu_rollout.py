@@ -150,7 +150,7 @@ def test_shared_physics_kernel_equals_register_kernel(kind):
     apk, cpk = K.mfma_pack(ad, dev(ap)), K.mfma_pack(cd, dev(cp))
     runs = []
     try:
-        for phys in (1, 0):
+        for phys in (1, 0, 2):
             _native.set_rollout_physics(phys)
             st = K.new_state(kind, n)
             need = torch.ones(n, dtype=torch.uint8, device="cuda")
@@ -160,12 +160,13 @@ def test_shared_physics_kernel_equals_register_kernel(kind):
             runs.append(({k: v.clone() for k, v in bufs.items()}, st.clone(), need.clone()))
     finally:
         _native.set_rollout_physics(1)
-    (b1, s1, n1), (b0, s0, n0) = runs
+    (b1, s1, n1), (b0, s0, n0), (b2, s2, n2) = runs
     assert b1["done"][:-1].any(), "no env terminated inside the segment"
-    for key in b1:
-        assert torch.equal(b1[key], b0[key]), key
-    assert torch.equal(s1, s0)
-    assert torch.equal(n1, n0)
+    for bx, sx, nx in ((b0, s0, n0), (b2, s2, n2)):  # register kernel; 8-wave shared kernel
+        for key in b1:
+            assert torch.equal(b1[key], bx[key]), key
+        assert torch.equal(s1, sx)
+        assert torch.equal(n1, nx)
 
 
 def test_rollout_segments_chain():
