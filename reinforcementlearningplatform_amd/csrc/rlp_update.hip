@@ -472,10 +472,14 @@ template <int KS1>
 __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
     constexpr int H = kUpdH, SP = 4 * KS1, NT = 64 * kWgWaves;
     constexpr int SV = (kUpdRows * SP + NT - 1) / NT;
-    __shared__ float srow[kUpdRows][SP];
+    constexpr int FRAG = 2 * 16 * 2 * 64 * 8;  // halfs of one tile's h1 fragments (64 KiB)
+    constexpr int IPT = 2048 / NT;             // fragment items built per thread and tile
+    // double-buffered: tile i's MFMAs read hfrag[i & 1] while its waves build tile i + step's
+    // fragments into hfrag[(i + 1) & 1] from srow[(i + 1) & 1]
+    __shared__ float srow[2][kUpdRows][SP];
     __shared__ float w1s[H][SP + 1];
     __shared__ float b1s[H];
-    __shared__ __attribute__((aligned(16))) _Float16 hfrag[2 * 16 * 2 * 64 * 8];
+    __shared__ __attribute__((aligned(16))) _Float16 hfrag[2][FRAG];
     const MfmaNet &net = w.net;
     const int S = net.S;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, gq = lane >> 4, e = lane & 15;
@@ -501,57 +505,80 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
         for (int nt = 0; nt < 16; ++nt) acc2[jt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
     const int64_t ntiles = (w.rows + kUpdRows - 1) / kUpdRows;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        // this thread's s values for the tile, then the wave's G2 operands of both k-steps: the
-        // G2 loads stay in flight under the h1 fragment build (LDS-only barriers below do not
-        // drain vmcnt), instead of one exposed HBM round trip per k-step
-        float sv[SV];
+    auto load_s = [&](int64_t tile, float (&sv)[SV]) {  // this thread's s values of a tile
 #pragma unroll
         for (int u = 0; u < SV; ++u) {
             const int i = threadIdx.x + NT * u, rr = i / SP, k = i % SP;
             const int64_t r = tile * kUpdRows + rr;
-            sv[u] = (i < kUpdRows * SP && r < w.rows && k < S) ? w.s[(w.index ? w.index[r] : r) * S + k] : 0.f;
+            sv[u] = (tile < ntiles && i < kUpdRows * SP && r < w.rows && k < S)
+                        ? w.s[(w.index ? w.index[r] : r) * S + k] : 0.f;
         }
-        const float *g2base = w.g2t;
-        asm volatile("" : "+s"(g2base));
-        floatx4 gv[2][2][2];
+    };
+    auto store_s = [&](int buf, const float (&sv)[SV]) {
+#pragma unroll
+        for (int u = 0; u < SV; ++u) {
+            const int i = threadIdx.x + NT * u;
+            if (i < kUpdRows * SP) srow[buf][i / SP][i % SP] = sv[u];
+        }
+    };
+    // one fragment item (ks, nt, lane) of 8 rows: the k-ordered f32 fma chain of the forward's
+    // layer-1 MFMA, so h1 is bit-identical
+    auto build_item = [&](int buf, int it) {
+        const int ln = it & 63, nt = (it >> 6) & 15, ks = it >> 10;
+        const int n = 16 * nt + (ln & 15), r0 = 32 * ks + 8 * (ln >> 4);
+        float x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float pre = b1s[n];
+#pragma unroll
+            for (int k = 0; k < SP; ++k) pre = __builtin_fmaf(w1s[n][k], srow[buf][r0 + i][k], pre);
+            x[i] = kX3HScale * tanh_fast(pre);
+        }
+        half8 hh, hl;
+        split8(x, hh, hl);
+        *reinterpret_cast<half8 *>(&hfrag[buf][(((ks * 16 + nt) * 2 + 0) * 64 + ln) * 8]) = hh;
+        *reinterpret_cast<half8 *>(&hfrag[buf][(((ks * 16 + nt) * 2 + 1) * 64 + ln) * 8]) = hl;
+    };
+    const float *g2base = w.g2t;
+    asm volatile("" : "+s"(g2base));
+    auto load_g2 = [&](int64_t tile, floatx4 (&gv)[2][2][2]) {
+        const int64_t t = tile < ntiles ? tile : ntiles - 1;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
             for (int jt = 0; jt < 2; ++jt) {
                 // A operands: g2(rows 32 ks + 8 gq + i, j = 32 wv + 16 jt + e)
-                const gptr<float> src = as_global(g2base + tile * kUpdTileFloats +
+                const gptr<float> src = as_global(g2base + t * kUpdTileFloats +
                                                   (32 * wv + 16 * jt + e) * kUpdRows + 32 * ks + 8 * gq);
                 gv[ks][jt][0] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src);
                 gv[ks][jt][1] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 4);
             }
-        lds_barrier();  // previous tile's fragments are consumed
-#pragma unroll
-        for (int u = 0; u < SV; ++u) {
-            const int i = threadIdx.x + NT * u;
-            if (i < kUpdRows * SP) srow[i / SP][i % SP] = sv[u];
-        }
-        lds_barrier();
-        // h1 fragments: 2048 items (ks, nt, lane) of 8 rows, 4 per thread; the k-ordered f32 fma
-        // chain of the forward's layer-1 MFMA, so h1 is bit-identical
+    };
+
+    // prologue: the first tile's s rows and fragments
+    int64_t tile = blockIdx.x;
+    {
+        float sv[SV];
+        load_s(tile, sv);
+        store_s(0, sv);
+    }
+    lds_barrier();
 #pragma unroll 1
-        for (int it = threadIdx.x; it < 2048; it += NT) {
-            const int ln = it & 63, nt = (it >> 6) & 15, ks = it >> 10;
-            const int n = 16 * nt + (ln & 15), r0 = 32 * ks + 8 * (ln >> 4);
-            float x[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                float pre = b1s[n];
-#pragma unroll
-                for (int k = 0; k < SP; ++k) pre = __builtin_fmaf(w1s[n][k], srow[r0 + i][k], pre);
-                x[i] = kX3HScale * tanh_fast(pre);
-            }
-            half8 hh, hl;
-            split8(x, hh, hl);
-            *reinterpret_cast<half8 *>(hfrag + (((ks * 16 + nt) * 2 + 0) * 64 + ln) * 8) = hh;
-            *reinterpret_cast<half8 *>(hfrag + (((ks * 16 + nt) * 2 + 1) * 64 + ln) * 8) = hl;
-        }
+    for (int u = 0; u < IPT; ++u) build_item(0, threadIdx.x + NT * u);
+    float svn[SV];
+    load_s(tile + gridDim.x, svn);
+    floatx4 gv[2][2][2];
+    load_g2(tile, gv);
+    lds_barrier();
+    for (int i = 0; tile < ntiles; tile += gridDim.x, ++i) {
+        const int cur = i & 1, nxt = cur ^ 1;
+        // next tile's s rows (its fragments go into the other buffer during this tile's MFMAs;
+        // the barrier at the end of the previous tile freed that buffer)
+        store_s(nxt, svn);
         lds_barrier();
+        load_s(tile + 2 * (int64_t)gridDim.x, svn);
+        floatx4 gvn[2][2][2];
+        load_g2(tile + gridDim.x, gvn);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             // A operands scaled by 2^sg and split
@@ -568,8 +595,8 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
             }
 #pragma unroll
             for (int nt = 0; nt < 16; ++nt) {
-                const half8 bh = *reinterpret_cast<const half8 *>(hfrag + (((ks * 16 + nt) * 2 + 0) * 64 + lane) * 8);
-                const half8 bl = *reinterpret_cast<const half8 *>(hfrag + (((ks * 16 + nt) * 2 + 1) * 64 + lane) * 8);
+                const half8 bh = *reinterpret_cast<const half8 *>(&hfrag[cur][(((ks * 16 + nt) * 2 + 0) * 64 + lane) * 8]);
+                const half8 bl = *reinterpret_cast<const half8 *>(&hfrag[cur][(((ks * 16 + nt) * 2 + 1) * 64 + lane) * 8]);
 #pragma unroll
                 for (int jt = 0; jt < 2; ++jt) {
                     floatx4 v = acc2[jt][nt];
@@ -578,6 +605,9 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
                     v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jt], bh, v, 0, 0, 0);
                     acc2[jt][nt] = v;
                 }
+                // the next tile's fragments, spread over this tile's MFMAs (IPT items per thread)
+                if ((ks * 16 + nt) % (32 / IPT) == (32 / IPT) - 1)
+                    build_item(nxt, threadIdx.x + NT * ((ks * 16 + nt) / (32 / IPT)));
             }
 #pragma unroll
             for (int jt = 0; jt < 2; ++jt) {  // db2: g2 against a ones column
@@ -585,6 +615,13 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
                 accb[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jt], ones, accb[jt], 0, 0, 0);
             }
         }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) gv[a][b][c] = gvn[a][b][c];
+        lds_barrier();  // the next tile's fragments are complete; this tile's buffer is free
     }
     // C layout: lane holds rows m = 4 gq + q (j = 32 wv + 16 jt + m), column e (n = 16 nt + e)
     float *out = w.part + (size_t)blockIdx.x * (H * H + H);
