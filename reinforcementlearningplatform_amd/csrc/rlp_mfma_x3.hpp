@@ -168,13 +168,25 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
             if (c + RG - 1 < NC) issue(c + RG - 1);  // into chunk c - 1's slot
 #endif
             const float *slot = ring + (c % RG) * kX3ChunkFloats + lane * 4;
+            // fragments one output tile ahead: tile jj + 1's two reads are issued before tile
+            // jj's MFMAs, so an LDS round trip is not exposed per tile (the default schedule
+            // reads each pair right before its MFMAs and waits for it)
+#if RLP_EXPERIMENT == 6  // timing experiment only: no fragment reads (B operands as A)
+            half8 ahn = bh[0], aln = bl[0];
+#else
+            half8 ahn = *reinterpret_cast<const half8 *>(slot);
+            half8 aln = *reinterpret_cast<const half8 *>(slot + 256);
+#endif
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
-#if RLP_EXPERIMENT == 6  // timing experiment only: no fragment reads (B operands as A)
-                const half8 ah = bh[0], al = bl[0];
-#else
-                const half8 ah = *reinterpret_cast<const half8 *>(slot + (2 * jj) * 256);
-                const half8 al = *reinterpret_cast<const half8 *>(slot + (2 * jj + 1) * 256);
+                const half8 ah = ahn, al = aln;
+#if RLP_EXPERIMENT != 6
+                if (jj + 1 < 8) {
+                    ahn = *reinterpret_cast<const half8 *>(slot + (2 * jj + 2) * 256);
+                    aln = *reinterpret_cast<const half8 *>(slot + (2 * jj + 3) * 256);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                }
 #endif
 #pragma unroll
                 for (int sb = 0; sb < SUB; ++sb) {
@@ -184,6 +196,7 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
                     a = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[sb], a, 0, 0, 0);
                     acc[sb][8 * hf + jj] = a;
                 }
+                __builtin_amdgcn_sched_group_barrier(0x008, 3 * SUB, 0);
             }
         }
     }
