@@ -5,8 +5,8 @@ the GPU: T env-steps x n envs of {auto-reset, actor forward + Gaussian sample, c
 step, buffer append} in the fused HIP kernel (rlp_rollout), then the critic on terminal s', reward
 normalisation, GAE(lambda) and advantage normalisation — everything learn() consumes
 (SURVEY.md §8a rows a1-a6, a14, a15, a17-a19). `value` = env-steps/s of the whole job.
-With --e2e the K-epoch PPO update (torch autograd on the same GPU) is also timed and reported
-separately under "e2e".
+With --e2e the K-epoch PPO2 update (librlp's native HIP update kernels on the same GPU) is also
+timed and reported separately under "e2e".
 
 Launch: python bench.py [--gpus 1]   |   torchrun --nproc-per-node N bench.py --gpus N
 """
