@@ -32,6 +32,10 @@ PEAK_F16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS   # f16/bf16 dense MFMA = 16x 
 # f16x3 split: 3 f16 MFMAs per fp32-equivalent product -> the path's fp32-equivalent ceiling
 PEAK_F16X3_TFLOPS = PEAK_F16_MFMA_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0
+# the rollout kernel each --physics mode launches (rlp_rollout.hip; the name rocprof reports)
+ROLLOUT_KERNEL = {"shared": "rlp::rollout_sp_kernel<KIND,256,SUB,4>",
+                  "shared8": "rlp::rollout_sp_kernel<KIND,256,1,8>",
+                  "lanes": "rlp::rollout_kernel<KIND,256,SUB,true>"}
 
 ENVS = {
     "cartpole": (A.RLP_ENV_CARTPOLE, lambda: A.cartpole_params("ppo2"), 3),
@@ -451,7 +455,8 @@ def main():
                    "nets": "actor [S,256,256,A] tanh, critic [S,256,256,1]",
                    "parallelism": f"dp{world} (env shards, no data-path collective)",
                    "physics": "f64", "mlp": mlp},
-        "roofline": {"bound": "mfma", "kernel": "rlp::rollout_kernel", "achieved": achieved,
+        "roofline": {"bound": "mfma", "kernel": (ROLLOUT_KERNEL[args.physics] if args.precision == "f16x3"
+                                                else "rlp::rollout_kernel<KIND,256,SUB,false>"), "achieved": achieved,
                      "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                      "peak_basis": basis, "avg_launch_ms": rollout_ms, "flop_per_launch": flop_launch},
     }
