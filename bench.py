@@ -321,9 +321,22 @@ def ugvoa_sac_leg(rank, n=16384, steps=20, warmup=3, batch=4096, capacity=1 << 2
                       "per update (sample, gather, update, soft update, actor refresh)"}
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(env, seconds=10.0):
-    """Oracle (plain-C port of the reference loop, 1 thread) on a bounded sample of the same
-    workload: actor + critic forward, sampling and env step per env-step."""
+    """Oracle (plain-C port of the reference driver loop: actor + critic forward, sampling and env
+    step per env-step) on a bounded sample of the same workload, timed on 1 host thread and on
+    P threads (OpenMP over independent envs; P = OMP_NUM_THREADS or the process's CPU set — the
+    DPPO-style fan-out of BASELINE.md §3). `value`/`cores` are the P-thread run."""
     from oracle import oracle
     kind, pf, tflag = ENVS[env]
     p = pf()
@@ -343,14 +356,25 @@ def cpu_baseline(env, seconds=10.0):
         oracle.rollout(kind, p, st, need, ad, ap, cd, cp, cfg, want_buffers=True)
         return time.perf_counter() - t0
 
-    dt = run(16, 8)
-    T = 64
-    n = max(16, int(16 * 8 * seconds / max(dt, 1e-6) / T))
-    dt = run(n, T)
-    return {"value": n * T / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/rlp_oracle.c rollout (actor+critic 256x256 fp32 MLP, Philox sample, "
-                      f"f64 RK4 {env} step) for {n} envs x {T} steps = {n * T} env-steps in "
-                      f"{dt:.1f} s on 1 host thread"}
+    def sample(threads, secs):
+        oracle.set_threads(threads)
+        dt = run(16 * threads, 8)
+        T = 64
+        n = max(16 * threads, int(16 * threads * 8 * secs / max(dt, 1e-6) / T))
+        dt = run(n, T)
+        return n * T / dt, n, T, dt
+
+    P = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    v1, n1, T1, dt1 = sample(1, seconds / 2)
+    vp, n_p, Tp, dtp = sample(P, seconds / 2)
+    oracle.set_threads(P)
+    return {"value": vp, "unit": "env-steps/s", "cores": P, "kind": "port",
+            "cpu_model": _cpu_model(), "cpus_visible": os.cpu_count(),
+            "single_thread": {"value": v1, "cores": 1, "env_steps": n1 * T1, "seconds": dt1},
+            "sample": f"oracle/rlp_oracle.c rollout (actor+critic 256x256 fp32 MLP with double "
+                      f"accumulation, Philox sample, f64 RK4 {env} step): {n_p} envs x {Tp} steps = "
+                      f"{n_p * Tp} env-steps in {dtp:.1f} s on {P} host threads (OpenMP over envs); "
+                      f"1 thread: {n1} x {T1} in {dt1:.1f} s"}
 
 
 def main():

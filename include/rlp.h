@@ -381,8 +381,14 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
                   const float *s, const float *a, const float *a_logprob, const float *adv,
                   const float *v_target, const int64_t *index, int64_t rows, float *grad,
                   double *loss_sum, float *workspace, rlp_stream_t stream);
-/* out[0] += sum(grad^2) (torch.nn.utils.clip_grad_norm_'s total norm, squared). */
+/* out[0] += sum(grad^2) (torch.nn.utils.clip_grad_norm_'s total norm, squared), accumulated in
+ * double in a fixed order: bit-identical on every run and every data-parallel rank. */
 int rlp_grad_sqnorm(const float *grad, int64_t n, double *out, rlp_stream_t stream);
+/* grad *= min(1, max_norm / (sqrt(*sqnorm) + 1e-6)) in place — clip_grad_norm_ on a gradient
+ * buffer that persists (the DPPO2 Worker's local grads,
+ * demonstration/DPPO2/DPPO2-4-CartPole/Distributed_PPO2.py:88-91, 99-102). */
+int rlp_grad_clip(float *grad, int64_t n, const double *sqnorm, float max_norm,
+                  rlp_stream_t stream);
 /* torch.optim.Adam step (exp_avg.lerp_, exp_avg_sq.mul_.addcmul_, bias corrections, addcdiv).
  * With clip_sqnorm != NULL the gradient is first scaled by min(1, max_norm / (sqrt(*clip_sqnorm)
  * + 1e-6)) (clip_grad_norm_, :150-151), evaluated on the device. */

@@ -123,9 +123,17 @@ def reward_norm(r, rms=None):
     return out, rms
 
 
+def set_threads(n):
+    """Host threads of the oracle's env / row loops (OpenMP); returns the count in effect."""
+    return lib().oracle_set_threads(int(n))
+
+
 def rollout(kind, params, state, need_reset, actor_desc, actor_params, critic_desc,
-            critic_params, cfg, want_buffers=True):
-    """Whole rollout segment on the CPU (the reference driver loop batched over n envs)."""
+            critic_params, cfg, want_buffers=True, forced_action=None):
+    """Whole rollout segment on the CPU (the reference driver loop batched over n envs).
+
+    forced_action [T][n][A] f32: teacher forcing — the envs step with these actions while the
+    buffers record the oracle's own policy output / values (actor_params None: physics only)."""
     D, S, A = dims(kind)
     T, n = cfg.T, cfg.n
     bufs = None
@@ -137,10 +145,15 @@ def rollout(kind, params, state, need_reset, actor_desc, actor_params, critic_de
                       value_next=np.zeros((T, n), np.float32), done=np.zeros((T, n), np.uint8),
                       success=np.zeros((T, n), np.uint8), flag=np.zeros((T, n), np.int8))
         bufs = _abi.RolloutBufs(**{k: v.ctypes.data for k, v in arrays.items()})
-    ap = np.ascontiguousarray(actor_params, dtype=np.float32)
-    cp = np.ascontiguousarray(critic_params, dtype=np.float32)
-    rc = lib().oracle_rollout(kind, C.byref(params), _p(state), _p(need_reset), C.byref(actor_desc),
-                              _p(ap), C.byref(critic_desc), _p(cp), C.byref(cfg),
-                              C.byref(bufs) if bufs is not None else None)
+    nets = actor_params is not None
+    ap = np.ascontiguousarray(actor_params, dtype=np.float32) if nets else None
+    cp = np.ascontiguousarray(critic_params, dtype=np.float32) if nets else None
+    fa = None
+    if forced_action is not None:
+        fa = np.ascontiguousarray(forced_action, dtype=np.float32).reshape(T, n, A)
+    rc = lib().oracle_rollout_forced(kind, C.byref(params), _p(state), _p(need_reset),
+                                     C.byref(actor_desc) if nets else None, _p(ap),
+                                     C.byref(critic_desc) if nets else None, _p(cp), C.byref(cfg),
+                                     C.byref(bufs) if bufs is not None else None, _p(fa))
     assert rc == 0
     return arrays

@@ -17,6 +17,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include "../include/rlp.h"
 
@@ -969,7 +972,10 @@ int oracle_mlp_forward(const rlp_mlp_desc *desc, const float *params, const floa
                        int n) {
     int maxw = 0;
     for (int l = 0; l <= desc->n_layers; ++l) maxw = desc->dims[l] > maxw ? desc->dims[l] : maxw;
+#pragma omp parallel if (n > 64)
+    {
     double *a = (double *)malloc(sizeof(double) * maxw), *b = (double *)malloc(sizeof(double) * maxw);
+#pragma omp for schedule(static)
     for (int i = 0; i < n; ++i) {
         for (int k = 0; k < desc->dims[0]; ++k) a[k] = x[(size_t)i * desc->dims[0] + k];
         const float *pw = params;
@@ -993,6 +999,7 @@ int oracle_mlp_forward(const rlp_mlp_desc *desc, const float *params, const floa
     }
     free(a);
     free(b);
+    }
     return 0;
 }
 
@@ -1093,20 +1100,36 @@ int oracle_reward_norm(const float *rin, int T, int n, double *rms, float *rout)
 /* Whole rollout segment (the reference driver loop, batched): used as the CPU baseline and as */
 /* the closed-loop parity reference of rlp_rollout.                                            */
 /* ------------------------------------------------------------------------------------------ */
-int oracle_rollout(int kind, const void *env_params, double *state, uint8_t *need_reset,
-                   const rlp_mlp_desc *ad, const float *actor, const rlp_mlp_desc *cd,
-                   const float *critic, const rlp_rollout_cfg *cfg, const rlp_rollout_bufs *b) {
+/* The batched driver loop (demonstration/PPO2/PPO2-4-CartPole/train.py:184-217 with the reset of
+ * :186-190 and the success rules of rlp.h) for n independent envs, one env after another.
+ *
+ * forced_action [T][n][A] (nullable): teacher forcing. The env is stepped with the given actions
+ * (e.g. the ones a GPU rollout stored) while the buffers still record the oracle's own policy
+ * output (mean + std * Philox noise, clamped) and critic value for the oracle's own observations,
+ * so a GPU run can be checked step by step without the closed loop amplifying the ~1e-7
+ * difference between its f32 MLP and this double-accumulated one. actor == NULL (only with
+ * forced_action) skips the nets altogether: physics, rewards, flags and resets only (action,
+ * logp, value and value_next are then left untouched).
+ *
+ * Envs are independent: with OpenMP the env loop runs on all host threads (same results). */
+int oracle_rollout_forced(int kind, const void *env_params, double *state, uint8_t *need_reset,
+                          const rlp_mlp_desc *ad, const float *actor, const rlp_mlp_desc *cd,
+                          const float *critic, const rlp_rollout_cfg *cfg,
+                          const rlp_rollout_bufs *b, const float *forced_action) {
     int D, S, A;
     if (oracle_env_dims(kind, &D, &S, &A)) return -1;
+    if (!actor && !forced_action) return -1;
     int n = cfg->n;
-    double s[64];
-    float o[64], on[64], mean[8], eps[8], act[8], lp[8], v;
     float gain[4], off[4];
     for (int j = 0; j < A; ++j) {
         off[j] = (cfg->a_min[j] + cfg->a_max[j]) / 2.0f;
         gain[j] = cfg->a_max[j] - off[j];
     }
+    const int nets = actor != NULL;
+#pragma omp parallel for schedule(dynamic, 16)
     for (int i = 0; i < n; ++i) {
+        double s[64];
+        float o[64], on[64], mean[8], eps[8], act[8], lp[8], v = 0.f;
         gather(state, D, n, i, s);
         uint64_t eid = cfg->env_id0 + (uint64_t)i;
         for (int t = 0; t < cfg->T; ++t) {
@@ -1117,20 +1140,23 @@ int oracle_rollout(int kind, const void *env_params, double *state, uint8_t *nee
                 need_reset[i] = 0;
             }
             env_obs1(kind, env_params, s, o);
-            oracle_mlp_forward(ad, actor, o, mean, 1);
-            for (int j = 0; j < A; ++j) mean[j] = mean[j] * gain[j] + off[j];
-            oracle_mlp_forward(cd, critic, o, &v, 1);
-            oracle_philox_normal_f32(cfg->seed, g, eid, A, eps);
-            for (int j = 0; j < A; ++j) {
-                float a = mean[j] + cfg->std[j] * eps[j];
-                a = fmaxf(fminf(a, cfg->a_max[j]), cfg->a_min[j]);
-                act[j] = a;
-                lp[j] = normal_logp(a, mean[j], cfg->std[j]);
+            if (nets) {
+                oracle_mlp_forward(ad, actor, o, mean, 1);
+                for (int j = 0; j < A; ++j) mean[j] = mean[j] * gain[j] + off[j];
+                oracle_mlp_forward(cd, critic, o, &v, 1);
+                oracle_philox_normal_f32(cfg->seed, g, eid, A, eps);
+                for (int j = 0; j < A; ++j) {
+                    float a = mean[j] + cfg->std[j] * eps[j];
+                    a = fmaxf(fminf(a, cfg->a_max[j]), cfg->a_min[j]);
+                    act[j] = a;
+                    lp[j] = normal_logp(a, mean[j], cfg->std[j]);
+                }
             }
             double r;
             int32_t f;
             uint8_t dn;
-            env_step1(kind, env_params, s, act, NULL, on, &r, &f, &dn);
+            env_step1(kind, env_params, s, forced_action ? forced_action + k * A : act, NULL, on,
+                      &r, &f, &dn);
             int su;
             switch (cfg->success_rule) {
             case RLP_SUCCESS_FLAG_NE: su = f != cfg->success_flag; break;
@@ -1142,20 +1168,22 @@ int oracle_rollout(int kind, const void *env_params, double *state, uint8_t *nee
                     b->obs[k * S + q] = o[q];
                     b->obs_next[k * S + q] = on[q];
                 }
-                for (int j = 0; j < A; ++j) {
-                    b->action[k * A + j] = act[j];
-                    b->logp[k * A + j] = lp[j];
+                if (nets) {
+                    for (int j = 0; j < A; ++j) {
+                        b->action[k * A + j] = act[j];
+                        b->logp[k * A + j] = lp[j];
+                    }
+                    b->value[k] = v;
+                    if (t > 0 && !b->done[k - n]) b->value_next[k - n] = v;
                 }
                 b->reward[k] = (float)r;
-                b->value[k] = v;
                 b->done[k] = dn;
                 b->success[k] = (uint8_t)su;
                 b->flag[k] = (int8_t)f;
-                if (t > 0 && !b->done[k - n]) b->value_next[k - n] = v;
             }
             if (dn) need_reset[i] = 1;
         }
-        if (b && !need_reset[i]) {
+        if (b && nets && !need_reset[i]) {
             env_obs1(kind, env_params, s, o);
             oracle_mlp_forward(cd, critic, o, &v, 1);
             b->value_next[(size_t)(cfg->T - 1) * n + i] = v;
@@ -1163,4 +1191,22 @@ int oracle_rollout(int kind, const void *env_params, double *state, uint8_t *nee
         scatter(state, D, n, i, s);
     }
     return 0;
+}
+
+int oracle_rollout(int kind, const void *env_params, double *state, uint8_t *need_reset,
+                   const rlp_mlp_desc *ad, const float *actor, const rlp_mlp_desc *cd,
+                   const float *critic, const rlp_rollout_cfg *cfg, const rlp_rollout_bufs *b) {
+    return oracle_rollout_forced(kind, env_params, state, need_reset, ad, actor, cd, critic, cfg,
+                                 b, NULL);
+}
+
+/* Host threads for the env / row loops (bench.py's cpu_baseline times 1 and all cores). */
+int oracle_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
 }

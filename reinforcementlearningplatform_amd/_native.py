@@ -53,6 +53,7 @@ def _declare(lib):
         "rlp_ppo2_workspace_floats": (i64, [vp, i64]),
         "rlp_ppo2_grad": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp]),
         "rlp_grad_sqnorm": (i32, [vp, i64, vp, vp]),
+        "rlp_grad_clip": (i32, [vp, i64, vp, C.c_float, vp]),
         "rlp_adam_step": (i32, [vp, vp, vp, vp, i64, vp, vp, vp]),
         "rlp_replay_store": (i32, [vp, i64, vp, vp, vp, vp, vp, i64, vp]),
         "rlp_replay_sample_uniform": (i32, [i64, i64, u64, u64, vp, vp]),

@@ -10,16 +10,62 @@ Launch one process per GPU (torchrun --nproc-per-node N ...); with WORLD_SIZE un
 single GPU. The class keeps the reference's surface: constructor (env, actor_lr, critic_lr,
 num_of_pro, path), global_actor / global_critic / eval_actor, save_ac, global_evaluate, evaluate,
 start_multi_process, DPPO2_info; `Worker` is the per-rank VecPPO2 learner.
+
+Worker semantics follow the DPPO2 demo copy of the env's kind (DPPO2_COPY below, overridable
+through ppo_msg): the Worker.learn() update (update_rule 'dppo2': frozen local nets, gradients
+accumulated in never-zeroed local buffers and clipped in place, SharedAdam betas (0.9, 0.99)), the
+copy's clip norm and success rule, no lr decay (the Worker stores use_lr_decay and never applies
+it, Distributed_PPO2.py:50), and the copy's exploration-std schedule after every learn().
 """
 import os
 
 import numpy as np
 import torch
 
+from ... import _abi
 from ...utils.classes import PPOActor_Gaussian, PPOCritic
 from .vec_ppo2 import VecPPO2
 
 Worker = VecPPO2
+
+# Per-kind DPPO2 demo-copy semantics: clip_grad_norm_ max_norm, the buffer's success rule
+# (rlp_success_rule, flag) and the std schedule (kind, period, step, floor):
+#   "reset": std = std0 * max(1 - t / period * step, floor), std0 = (a_max - a_min) / 6
+#   "scale": std *= max(1 - t / period * step, floor)
+# applied when t % period == 0 and t > 0, t = this worker's learn() count.
+_CP_SOI = dict(clip=0.2, rule=(_abi.RLP_SUCCESS_FLAG_NE, 1), std=("reset", 250, 0.05, 0.05))
+_OTHERS = dict(clip=0.5, rule=(_abi.RLP_SUCCESS_DONE_AND_FLAG_NE, 2), std=("scale", 1000, 0.05, 0.2))
+DPPO2_COPY = {
+    # demonstration/DPPO2/DPPO2-4-CartPole/Distributed_PPO2.py:88-102 (0.2), :138, :160-165
+    _abi.RLP_ENV_CARTPOLE: _CP_SOI,
+    # demonstration/DPPO2/DPPO2-4-SecondOrderIntegration/Distributed_PPO2.py: same as CartPole
+    _abi.RLP_ENV_SOI: _CP_SOI,
+    # demonstration/DPPO2/DPPO2-4-{CartPoleAngleOnly,UGVForward,UGVBidirectional,
+    # UGVForwardObstacleAvoidance}/Distributed_PPO2.py:89,100 (0.5), :135-141, :163-168
+    _abi.RLP_ENV_CARTPOLE_ANGLEONLY: _OTHERS,
+    _abi.RLP_ENV_UGV_FORWARD: _OTHERS,
+    _abi.RLP_ENV_UGV_BIDIRECTIONAL: _OTHERS,
+    _abi.RLP_ENV_UGV_OBSTACLE_AVOIDANCE: _OTHERS,
+    # no DPPO2 copy for the UAV: the PPO2 convention (terminal && flag != 1, the UAV time-out)
+    _abi.RLP_ENV_UAV_HOVER_OUTER_LOOP: dict(clip=0.5, rule=(_abi.RLP_SUCCESS_DONE_AND_FLAG_NE, 1),
+                                            std=("scale", 1000, 0.05, 0.2)),
+}
+
+
+def dppo2_std_schedule(copy, action_range):
+    """The Worker.run() std schedule of a DPPO2 copy as a callable (t_epoch, actor) -> None."""
+    kind, period, step, floor = copy["std"]
+    ar = np.asarray(action_range, dtype=np.float64)
+    std0 = torch.tensor((ar[:, 1] - ar[:, 0]) / 2 / 3, dtype=torch.float)
+
+    def schedule(t, actor):
+        if t % period == 0 and t > 0:
+            ratio = max(1 - t / period * step, floor)
+            if kind == "reset":
+                actor.std = (std0 * ratio).to(torch.as_tensor(actor.std).device)
+            else:
+                actor.std = actor.std * ratio
+    return schedule
 
 
 def init_distributed(backend=None):
@@ -61,10 +107,17 @@ class Distributed_PPO2:
         self.global_critic = critic if critic is not None else PPOCritic(
             state_dim=env.state_dim, use_orthogonal_init=True)
         self.eval_actor = self.global_actor
+        self.copy = DPPO2_COPY[env.KIND]
         msg = dict(ppo_msg or {})
         msg.setdefault('a_lr', actor_lr)
         msg.setdefault('c_lr', critic_lr)
+        msg.setdefault('update_rule', 'dppo2')
+        msg.setdefault('grad_clip_norm', self.copy["clip"])
+        msg.setdefault('adam_betas', (0.9, 0.99))        # SharedAdam (utils/classes.py:677)
+        msg.setdefault('use_grad_clip', True)
+        self.msg = msg
         self.worker = Worker(env, self.global_actor, self.global_critic, msg, T=T, seed=seed,
+                             success_rule=msg.get('success_rule', self.copy["rule"]),
                              process_group=self.group, device=device)
         self.global_actor, self.global_critic = self.worker.actor, self.worker.critic
         self.eval_actor = self.global_actor
@@ -104,14 +157,23 @@ class Distributed_PPO2:
 
     def start_multi_process(self, iterations: int = 1, eval_every: int = 500, std_schedule=None):
         """Run `iterations` synchronous PPO2 iterations on every rank (the reference loops
-        forever). std_schedule(t_epoch, actor) may decay the exploration std like the drivers."""
-        for t in range(iterations):
+        forever). After each learn() the exploration std follows the copy's schedule
+        (Worker.run :160-165), or std_schedule(t_epoch, actor) if given (False: none). Checkpoint
+        + evaluation whenever global_training_num crosses a multiple of eval_every (the reference
+        evaluator tests `% 500 == 0` on a counter every worker bumps by one)."""
+        if std_schedule is None:
+            std_schedule = dppo2_std_schedule(self.copy, self.env.action_range)
+        if not hasattr(self, "t_epoch"):
+            self.t_epoch = 0
+        for _ in range(iterations):
             self.worker.iteration(learn=True)
+            before = self.global_training_num
             self.global_training_num += self.world
             self.training_record.append(self.worker.episode_stats())
-            if std_schedule is not None:
-                std_schedule(t, self.global_actor)
-            if eval_every and self.global_training_num % eval_every == 0:
+            if std_schedule:
+                std_schedule(self.t_epoch, self.global_actor)
+            self.t_epoch += 1
+            if eval_every and before // eval_every != self.global_training_num // eval_every:
                 self.global_evaluate()
         return self.training_record
 

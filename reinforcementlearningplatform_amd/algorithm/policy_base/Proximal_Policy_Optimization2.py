@@ -6,7 +6,10 @@ PPO2_info). What runs where:
   choose_action / evaluate   actor forward on fp32 MFMA + Philox Gaussian sample (librlp)
   learn(): V(s), V(s')       critic forward on fp32 MFMA (librlp)
            GAE(lambda)       rlp_gae (bit-identical to the reference's NumPy-2 loop)
-           K epochs          torch autograd + Adam on the same GPU (reference semantics)
+           K epochs          learner="native" (default for the drivers' [S,256,256,A] tanh nets):
+                             librlp's update kernels (NativePPO2Learner); learner="torch": torch
+                             autograd + Adam on the same GPU. Both pinned to the reference's
+                             learn() (tests/test_learn_golden.py, tests/test_gpu_transcript.py).
 The reference pins PPO2 to the CPU (:11-13); here everything lives on `device` (default cuda).
 """
 import numpy as np
@@ -14,6 +17,7 @@ import torch
 import torch.nn.functional as F
 from torch.utils.data.sampler import BatchSampler, SubsetRandomSampler
 
+from ... import _abi
 from ... import kernels as K
 from ...utils.classes import GPUNet, PPOActor_Gaussian, PPOCritic, RolloutBuffer, RolloutBuffer2
 
@@ -22,7 +26,7 @@ _ACTOR_TENSOR_ATTRS = ("a_min", "a_max", "off", "gain", "std")
 
 class Proximal_Policy_Optimization2:
     def __init__(self, env_msg: dict = None, ppo_msg: dict = None, actor=None, critic=None,
-                 device=None, seed=None):
+                 device=None, seed=None, learner=None):
         self.env_msg = env_msg
         self.ppo_msg = ppo_msg
         self.device = torch.device(device) if device is not None else torch.device("cuda")
@@ -56,6 +60,18 @@ class Proximal_Policy_Optimization2:
         self.seed = int(seed) if seed is not None else int(np.random.randint(0, 2 ** 31 - 1))
         self.sample_counter = 0
         self.cnt = 0
+        fits = all(n.mfma_ok and n.desc.n_layers == 3 and n.desc.dims[1] == 256 and
+                   n.desc.dims[2] == 256 and n.desc.act[0] == _abi.RLP_ACT_TANH
+                   for n in (self.gpu_actor, self.gpu_critic))
+        self.learner = learner or ("native" if fits else "torch")
+        self.native = None
+        if self.learner == "native":
+            if not fits:
+                raise ValueError("learner='native' needs [S<=8 -> 256 -> 256 -> A<=4] tanh nets")
+            from .native_ppo2 import NativePPO2Learner
+            self.native = NativePPO2Learner(self.actor, self.critic, ppo_msg, device=self.device)
+        elif self.learner != "torch":
+            raise ValueError(f"learner {learner!r} (native | torch)")
 
     # driver-defined actors keep a_min / a_max / gain / off / std as plain tensor attributes;
     # keep them on the learner's device
@@ -74,14 +90,19 @@ class Proximal_Policy_Optimization2:
         s = torch.as_tensor(np.asarray(state, dtype=np.float32), device=self.device).view(1, -1)
         return self.gpu_actor(s).cpu().numpy().flatten()
 
-    def choose_action(self, state: np.ndarray):
-        """mean = actor(s); a = clamp(mean + std * eps, a_min, a_max); log_prob(a) per dim."""
+    def choose_action(self, state: np.ndarray, noise=None):
+        """mean = actor(s); a = clamp(mean + std * eps, a_min, a_max); log_prob(a) per dim.
+        eps is a Philox N(0,1) draw, or `noise` ([action_dim] float32) when given — the injected
+        exploration noise a transcript replay uses (tests/test_gpu_transcript.py)."""
         self._sync_actor_attrs()
         s = torch.as_tensor(np.asarray(state, dtype=np.float32), device=self.device).view(1, -1)
         mean = self.gpu_actor(s).contiguous()
         a_min = torch.as_tensor(self.actor.a_min).reshape(-1).cpu().tolist()
         a_max = torch.as_tensor(self.actor.a_max).reshape(-1).cpu().tolist()
-        a, lp = K.policy_sample(mean, self._std_list(), a_min, a_max, seed=self.seed,
+        nz = None
+        if noise is not None:
+            nz = torch.as_tensor(np.asarray(noise, np.float32).reshape(mean.shape), device=self.device)
+        a, lp = K.policy_sample(mean, self._std_list(), a_min, a_max, noise=nz, seed=self.seed,
                                 counter=self.sample_counter)
         self.sample_counter += 1
         return a.cpu().numpy().flatten(), lp.cpu().numpy().flatten()
@@ -130,6 +151,14 @@ class Proximal_Policy_Optimization2:
 
     def update(self, s, a, a_lp, adv, v_target):
         """K epochs of clipped-surrogate + entropy (actor) and MSE (critic), :102-160."""
+        if self.native is not None:
+            perms = None
+            if self.using_mini_batch:   # SubsetRandomSampler's draws (torch's global CPU RNG)
+                perms = [torch.randperm(s.shape[0]) for _ in range(self.K_epochs)]
+            self.native.update(s, a, a_lp, adv, v_target, perms=perms)
+            self.gpu_actor.refresh()
+            self.gpu_critic.refresh()
+            return
         for _ in range(self.K_epochs):
             if self.using_mini_batch:
                 for idx in BatchSampler(SubsetRandomSampler(range(s.shape[0])), self.mini_batch_size, False):
@@ -148,6 +177,8 @@ class Proximal_Policy_Optimization2:
                 p['lr'] = lr_a
             for p in self.optimizer_critic.param_groups:
                 p['lr'] = lr_c
+            if self.native is not None:
+                self.native.lr = {"a": lr_a, "c": lr_c}
 
     def action_linear_trans(self, action):
         out = []

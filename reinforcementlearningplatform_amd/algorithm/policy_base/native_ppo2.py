@@ -10,6 +10,18 @@ against.
 
 The modules' parameters become views of the learner's flat fp32 buffers, so `actor.state_dict()`
 (save_ac), GPUNet.refresh and evaluation see every update without a copy.
+
+msg keys beyond the reference's ppo_msg (all optional):
+  update_rule     'ppo2' (Proximal_Policy_Optimization2.learn) or 'dppo2' (the DPPO2 Worker.learn,
+                  demonstration/DPPO2/DPPO2-4-CartPole/Distributed_PPO2.py:54-103: the local nets
+                  stay frozen for the k_epo epochs, so every epoch's gradient is the same one; it
+                  is ADDED to the local .grad buffers, which are never zeroed — SharedAdam's
+                  zero_grad() only drops the global nets' aliases — clipped in place, and the
+                  global nets take one Adam step on the accumulated buffer per epoch; the buffer
+                  carries over to the next learn())
+  grad_clip_norm  clip_grad_norm_'s max_norm (PPO2 0.5, :150; DPPO2 CartPole/SOI copies 0.2)
+  adam_betas      (0.9, 0.999) for torch.optim.Adam; SharedAdam's default is (0.9, 0.99)
+                  (utils/classes.py:676-679), which every DPPO2 driver uses
 """
 import numpy as np
 import torch
@@ -37,6 +49,7 @@ class _Net:
             p.data = self.flat[off:off + p.numel()].view_as(p)
             off += p.numel()
         self.grad = torch.zeros_like(self.flat)
+        self.acc = None        # the DPPO2 Worker's persistent local gradient buffer
         self.exp_avg = torch.zeros_like(self.flat)
         self.exp_avg_sq = torch.zeros_like(self.flat)
         self.packed = K.mfma_pack(self.desc, self.flat)
@@ -66,6 +79,11 @@ class NativePPO2Learner:
             self.broadcast_params()
         self.lr = {"a": msg['a_lr'], "c": msg['c_lr']}
         self.eps = 1e-5 if msg['set_adam_eps'] else 1e-8
+        self.betas = tuple(msg.get('adam_betas', (0.9, 0.999)))
+        self.max_norm = float(msg.get('grad_clip_norm', 0.5))
+        self.rule = msg.get('update_rule', 'ppo2')
+        if self.rule not in ('ppo2', 'dppo2'):
+            raise ValueError(f"NativePPO2Learner: update_rule {self.rule!r} (ppo2 | dppo2)")
         self.loss = torch.zeros(2, dtype=torch.float64, device=self.device)
         self.ws = None
         self.total_steps = 0
@@ -122,6 +140,12 @@ class NativePPO2Learner:
         self.net_a.grad.copy_(flat[:na])
         self.net_c.grad.copy_(flat[na:])
 
+    def _adam(self, net, lr, grad, clip_sqnorm=None):
+        net.step += 1
+        K.adam_step(net.flat, grad, net.exp_avg, net.exp_avg_sq, lr, net.step, beta1=self.betas[0],
+                    beta2=self.betas[1], eps=self.eps, clip_sqnorm=clip_sqnorm,
+                    max_norm=self.max_norm)
+
     def step(self, s, a, a_lp, adv, vt, index=None):
         rows = self.grads(s, a, a_lp, adv, vt, index)
         if self.distributed:
@@ -129,24 +153,46 @@ class NativePPO2Learner:
         clip = self.msg['use_grad_clip']
         for net, lr in ((self.net_a, self.lr["a"]), (self.net_c, self.lr["c"])):
             sq = None
-            if clip:  # clip_grad_norm_(params, 0.5), :150-151 / :158-159
+            if clip:  # clip_grad_norm_(params, max_norm), :150-151 / :158-159
                 net.sqnorm.zero_()
                 K.grad_sqnorm(net.grad, net.sqnorm)
                 sq = net.sqnorm
-            net.step += 1
-            K.adam_step(net.flat, net.grad, net.exp_avg, net.exp_avg_sq, lr, net.step, eps=self.eps,
-                        clip_sqnorm=sq, max_norm=0.5)
+            self._adam(net, lr, net.grad, sq)
         return self.loss[0] / rows, self.loss[1] / rows
 
-    def update(self, s, a, a_lp, adv, vt, generator=None):
+    def _update_dppo2(self, s, a, a_lp, adv, vt):
+        """Worker.learn (DPPO2-4-CartPole/Distributed_PPO2.py:76-103): one gradient at the frozen
+        local nets, then per epoch: local.grad += g, clip_grad_norm_ in place, global Adam step."""
+        rows = self.grads(s, a, a_lp, adv, vt)
+        if self.distributed:
+            self._allreduce_grads()
+        for _ in range(self.msg['K_epochs']):
+            for net, lr in ((self.net_a, self.lr["a"]), (self.net_c, self.lr["c"])):
+                if net.acc is None:
+                    net.acc = torch.zeros_like(net.grad)
+                net.acc += net.grad
+                if self.msg['use_grad_clip']:
+                    net.sqnorm.zero_()
+                    K.grad_sqnorm(net.acc, net.sqnorm)
+                    K.grad_clip(net.acc, net.sqnorm, self.max_norm)
+                self._adam(net, lr, net.acc)
+        return self.loss[0] / rows, self.loss[1] / rows
+
+    def update(self, s, a, a_lp, adv, vt, generator=None, perms=None):
+        """K epochs over the batch. perms (optional, one index tensor per epoch) replays recorded
+        SubsetRandomSampler permutations (mini-batch mode); otherwise they are drawn from
+        `generator`."""
         m = self.msg
         N = s.shape[0]
         losses = None
         s, a, a_lp = s.contiguous(), a.contiguous(), a_lp.contiguous()
         adv, vt = adv.reshape(-1).contiguous(), vt.reshape(-1).contiguous()
-        for _ in range(m['K_epochs']):
+        if self.rule == 'dppo2':
+            return self._update_dppo2(s, a, a_lp, adv, vt)
+        for k in range(m['K_epochs']):
             if m['using_mini_batch']:
-                perm = torch.randperm(N, device=s.device, generator=generator)
+                perm = (perms[k].to(s.device) if perms is not None else
+                        torch.randperm(N, device=s.device, generator=generator))
                 mb = m['mini_batch_size']
                 for i in range(0, N, mb):  # BatchSampler(..., drop_last=False)
                     losses = self.step(s, a, a_lp, adv, vt, index=perm[i:i + mb].contiguous())
@@ -155,7 +201,9 @@ class NativePPO2Learner:
         return losses
 
     def lr_decay(self, total_steps):
-        if not self.msg['use_lr_decay']:
+        """Proximal_Policy_Optimization2.lr_decay (:165-174): lr unchanged once total_steps
+        reaches max_train_steps."""
+        if not self.msg['use_lr_decay'] or total_steps >= self.msg['max_train_steps']:
             return
-        frac = max(1 - total_steps / self.msg['max_train_steps'], 0)
+        frac = 1 - total_steps / self.msg['max_train_steps']
         self.lr = {"a": max(self.msg['a_lr'] * frac, 1e-6), "c": max(self.msg['c_lr'] * frac, 1e-6)}

@@ -52,8 +52,14 @@ class PPO2Learner:
         if self.distributed:
             self.broadcast_params()
         eps = dict(eps=1e-5) if msg['set_adam_eps'] else {}
-        self.opt_a = torch.optim.Adam(self.actor.parameters(), lr=msg['a_lr'], **eps)
-        self.opt_c = torch.optim.Adam(self.critic.parameters(), lr=msg['c_lr'], **eps)
+        betas = tuple(msg.get('adam_betas', (0.9, 0.999)))   # SharedAdam: (0.9, 0.99)
+        self.opt_a = torch.optim.Adam(self.actor.parameters(), lr=msg['a_lr'], betas=betas, **eps)
+        self.opt_c = torch.optim.Adam(self.critic.parameters(), lr=msg['c_lr'], betas=betas, **eps)
+        self.max_norm = float(msg.get('grad_clip_norm', 0.5))
+        self.rule = msg.get('update_rule', 'ppo2')   # see native_ppo2.py's docstring
+        if self.rule not in ('ppo2', 'dppo2'):
+            raise ValueError(f"PPO2Learner: update_rule {self.rule!r} (ppo2 | dppo2)")
+        self.acc = None
         self.total_steps = 0
 
     def params(self):
@@ -96,19 +102,56 @@ class PPO2Learner:
         if self.distributed:
             self._allreduce_grads()
         if m['use_grad_clip']:
-            torch.nn.utils.clip_grad_norm_(self.actor.parameters(), 0.5)
-            torch.nn.utils.clip_grad_norm_(self.critic.parameters(), 0.5)
+            torch.nn.utils.clip_grad_norm_(self.actor.parameters(), self.max_norm)
+            torch.nn.utils.clip_grad_norm_(self.critic.parameters(), self.max_norm)
         self.opt_a.step()
         self.opt_c.step()
         return actor_loss.detach(), critic_loss.detach()
 
-    def update(self, s, a, a_lp, adv, vt, generator=None):
+    def _update_dppo2(self, s, a, a_lp, adv, vt):
+        """Worker.learn (demonstration/DPPO2/DPPO2-4-CartPole/Distributed_PPO2.py:76-103): the
+        local nets are frozen during learn(), so each epoch's gradient is the same; it is added to
+        the never-zeroed local .grad buffers, clipped in place, and the global Adam steps on them."""
+        m = self.msg
+        dist = self.actor.get_dist(s)
+        ent = dist.entropy().sum(1, keepdim=True)
+        ratios = torch.exp(dist.log_prob(a).sum(1, keepdim=True) - a_lp.sum(1, keepdim=True))
+        surr1 = ratios * adv
+        surr2 = torch.clamp(ratios, 1 - m['eps_clip'], 1 + m['eps_clip']) * adv
+        actor_loss = (-torch.min(surr1, surr2) - m['entropy_coef'] * ent).mean()
+        critic_loss = F.mse_loss(vt, self.critic(s))
+        pa, pc = list(self.actor.parameters()), list(self.critic.parameters())
+        g = list(torch.autograd.grad(actor_loss, pa)) + list(torch.autograd.grad(critic_loss, pc))
+        if self.distributed:
+            flat = torch.cat([t.reshape(-1) for t in g])
+            torch.distributed.all_reduce(flat, group=self.pg)
+            flat /= self.world
+            off = 0
+            for t in g:
+                t.copy_(flat[off:off + t.numel()].view_as(t))
+                off += t.numel()
+        if self.acc is None:
+            self.acc = [torch.zeros_like(t) for t in g]
+        for _ in range(m['K_epochs']):
+            for params, opt, lo in ((pa, self.opt_a, 0), (pc, self.opt_c, len(pa))):
+                for j, p in enumerate(params):
+                    self.acc[lo + j] += g[lo + j]
+                    p.grad = self.acc[lo + j]          # the global nets alias the local grads
+                if m['use_grad_clip']:
+                    torch.nn.utils.clip_grad_norm_(params, self.max_norm)
+                opt.step()
+        return actor_loss.detach(), critic_loss.detach()
+
+    def update(self, s, a, a_lp, adv, vt, generator=None, perms=None):
         m = self.msg
         N = s.shape[0]
         losses = None
-        for _ in range(m['K_epochs']):
+        if self.rule == 'dppo2':
+            return self._update_dppo2(s, a, a_lp, adv, vt)
+        for k in range(m['K_epochs']):
             if m['using_mini_batch']:
-                perm = torch.randperm(N, device=s.device, generator=generator)
+                perm = (perms[k].to(s.device) if perms is not None else
+                        torch.randperm(N, device=s.device, generator=generator))
                 mb = m['mini_batch_size']
                 for i in range(0, N, mb):  # BatchSampler(..., drop_last=False)
                     idx = perm[i:i + mb]
@@ -118,9 +161,11 @@ class PPO2Learner:
         return losses
 
     def lr_decay(self, total_steps):
-        if not self.msg['use_lr_decay']:
+        """Proximal_Policy_Optimization2.lr_decay (:165-174): no change once total_steps reaches
+        max_train_steps."""
+        if not self.msg['use_lr_decay'] or total_steps >= self.msg['max_train_steps']:
             return
-        frac = max(1 - total_steps / self.msg['max_train_steps'], 0)
+        frac = 1 - total_steps / self.msg['max_train_steps']
         for g, lr in ((self.opt_a, self.msg['a_lr']), (self.opt_c, self.msg['c_lr'])):
             for p in g.param_groups:
                 p['lr'] = max(lr * frac, 1e-6)
@@ -200,7 +245,8 @@ class VecPPO2:
                                      self.v_target.view(-1, 1), self.gen)
         self.gpu_actor.refresh()
         self.gpu_critic.refresh()
-        self.learner.lr_decay(self.total_steps)
+        if self.learner.rule == 'ppo2':   # the DPPO2 Worker stores use_lr_decay but never decays
+            self.learner.lr_decay(self.total_steps)
         return losses
 
     def iteration(self, learn=True):

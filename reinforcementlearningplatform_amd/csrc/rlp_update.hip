@@ -670,11 +670,14 @@ ppo2_reduce_kernel(MfmaNet net, const float *__restrict__ part, int nw,
     }
 }
 
-__global__ void sqnorm_kernel(const float *__restrict__ g, int64_t n, double *out) {
+// One block, fixed summation order (per-thread strided partials, then a fixed shuffle / LDS
+// tree): the same bits on every run and every rank, so data-parallel replicas that each clip
+// the all-reduced gradient compute the same clip coefficient. The learner's nets are <= a few
+// 100K parameters: one 1024-thread block reads them in a few microseconds.
+__global__ void __launch_bounds__(1024) sqnorm_kernel(const float *__restrict__ g, int64_t n,
+                                                      double *out) {
     double acc = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x)
-        acc += (double)g[i] * (double)g[i];
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) acc += (double)g[i] * (double)g[i];
     for (int o = 1; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
     __shared__ double red[16];
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
@@ -682,8 +685,20 @@ __global__ void sqnorm_kernel(const float *__restrict__ g, int64_t n, double *ou
     if (threadIdx.x == 0) {
         double t = 0.0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
-        atomicAdd(out, t);
+        out[0] += t;
     }
+}
+
+// clip_grad_norm_ applied in place (torch.nn.utils.clip_grad_norm_: coef = max_norm /
+// (norm + 1e-6) in f32, clamped to <= 1, grads.mul_(coef)) — the DPPO2 Worker clips its
+// persistent gradient buffer this way (DPPO2-4-CartPole/Distributed_PPO2.py:88-89, 99-100).
+__global__ void grad_clip_kernel(float *__restrict__ g, int64_t n, const double *sqnorm,
+                                 float max_norm) {
+    const float norm = (float)sqrt(*sqnorm);
+    const float scale = fminf(max_norm / (norm + 1e-6f), 1.f);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        g[i] = g[i] * scale;
 }
 
 __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
@@ -810,10 +825,19 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
 int rlp_grad_sqnorm(const float *grad, int64_t n, double *out, rlp_stream_t stream) {
     RLP_REQUIRE(grad && out && n >= 0, "rlp_grad_sqnorm: bad argument");
     if (n == 0) return RLP_OK;
-    int64_t blocks = (n + 1023) / 1024;
-    if (blocks > 1024) blocks = 1024;
-    sqnorm_kernel<<<(int)blocks, 1024, 0, as_stream(stream)>>>(grad, n, out);
+    sqnorm_kernel<<<1, 1024, 0, as_stream(stream)>>>(grad, n, out);
     RLP_CHECK_LAUNCH("rlp_grad_sqnorm");
+    return RLP_OK;
+}
+
+int rlp_grad_clip(float *grad, int64_t n, const double *sqnorm, float max_norm,
+                  rlp_stream_t stream) {
+    RLP_REQUIRE(grad && sqnorm && n >= 0 && max_norm > 0.f, "rlp_grad_clip: bad argument");
+    if (n == 0) return RLP_OK;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    grad_clip_kernel<<<(int)blocks, 256, 0, as_stream(stream)>>>(grad, n, sqnorm, max_norm);
+    RLP_CHECK_LAUNCH("rlp_grad_clip");
     return RLP_OK;
 }
 

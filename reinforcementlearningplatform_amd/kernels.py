@@ -57,7 +57,8 @@ def mlp_forward(desc, params, x, mask=None, out=None):
     n = x.shape[0]
     outn = desc.dims[desc.n_layers]
     out = out if out is not None else torch.empty((n, outn), dtype=torch.float32, device=x.device)
-    check(lib().rlp_mlp_forward(C.byref(desc), ptr(params), ptr(x.contiguous()), ptr(out), n,
+    x_ = x.contiguous()
+    check(lib().rlp_mlp_forward(C.byref(desc), ptr(params), ptr(x_), ptr(out), n,
                                 ptr(mask), stream_ptr()), "rlp_mlp_forward")
     return out
 
@@ -76,7 +77,8 @@ def mfma_forward(desc, packed, x, out=None):
     rows = x.shape[0]
     outn = desc.dims[desc.n_layers]
     out = out if out is not None else torch.empty((rows, outn), dtype=torch.float32, device=x.device)
-    check(lib().rlp_mfma_forward(C.byref(desc), ptr(packed), ptr(x.contiguous()), ptr(out), rows,
+    x_ = x.contiguous()
+    check(lib().rlp_mfma_forward(C.byref(desc), ptr(packed), ptr(x_), ptr(out), rows,
                                  stream_ptr()), "rlp_mfma_forward")
     return out
 
@@ -102,7 +104,8 @@ def policy_sample(mean, std, a_min, a_max, noise=None, seed=0, counter=0, env_id
     n, A = mean.shape
     a = torch.empty_like(mean)
     lp = torch.empty_like(mean)
-    check(lib().rlp_policy_sample(ptr(mean.contiguous()), n, A, _host_f32(std, A),
+    mean_ = mean.contiguous()
+    check(lib().rlp_policy_sample(ptr(mean_), n, A, _host_f32(std, A),
                                   _host_f32(a_min, A), _host_f32(a_max, A), ptr(noise), seed,
                                   counter, env_id0, ptr(a), ptr(lp), stream_ptr()),
           "rlp_policy_sample")
@@ -117,7 +120,8 @@ def sac_sample(head, ls_lo, ls_hi, gain, off, a_min=None, a_max=None, determinis
     a = torch.empty((n, A), dtype=torch.float32, device=head.device)
     lp = torch.empty(n, dtype=torch.float32, device=head.device) if with_logprob else None
     clamp = a_min is not None
-    check(lib().rlp_sac_sample(ptr(head.contiguous()), n, A, _host_f32(ls_lo, A),
+    head_ = head.contiguous()
+    check(lib().rlp_sac_sample(ptr(head_), n, A, _host_f32(ls_lo, A),
                                _host_f32(ls_hi, A), _host_f32(gain, A), _host_f32(off, A),
                                _host_f32(a_min, A) if clamp else None,
                                _host_f32(a_max, A) if clamp else None, int(bool(deterministic)),
@@ -213,17 +217,25 @@ def ppo2_grad(desc, packed, cfg, s, a=None, a_logprob=None, adv=None, v_target=N
                                                      device=dev)
     if workspace is None:
         workspace = ppo2_workspace(desc, rows, dev)
-    f = lambda t: None if t is None else t.contiguous()
-    check(lib().rlp_ppo2_grad(C.byref(desc), ptr(packed), C.byref(cfg), ptr(f(s)), ptr(f(a)),
-                              ptr(f(a_logprob)), ptr(f(adv)), ptr(f(v_target)), ptr(f(index)),
-                              rows, ptr(grad), ptr(loss_sum), ptr(workspace), stream_ptr()),
-          "rlp_ppo2_grad")
+    # converted tensors are bound to locals so they outlive the (asynchronous) launch
+    s_, a_, lp_, adv_, vt_, idx_ = (None if t is None else t.contiguous()
+                                    for t in (s, a, a_logprob, adv, v_target, index))
+    check(lib().rlp_ppo2_grad(C.byref(desc), ptr(packed), C.byref(cfg), ptr(s_), ptr(a_),
+                              ptr(lp_), ptr(adv_), ptr(vt_), ptr(idx_), rows, ptr(grad),
+                              ptr(loss_sum), ptr(workspace), stream_ptr()), "rlp_ppo2_grad")
     return grad
 
 
 def grad_sqnorm(grad, out):
     check(lib().rlp_grad_sqnorm(ptr(grad), grad.numel(), ptr(out), stream_ptr()), "rlp_grad_sqnorm")
     return out
+
+
+def grad_clip(grad, sqnorm, max_norm):
+    """clip_grad_norm_ in place on a flat gradient whose squared norm is in sqnorm (f64 [1])."""
+    check(lib().rlp_grad_clip(ptr(grad), grad.numel(), ptr(sqnorm), float(max_norm), stream_ptr()),
+          "rlp_grad_clip")
+    return grad
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, lr, step, beta1=0.9, beta2=0.999, eps=1e-8,
@@ -253,11 +265,12 @@ def replay_alloc(capacity, S, A, device=None):
 
 def replay_store(rb, counter, s, a, reward, s_next, done):
     n = int(s.shape[0])
-    f = lambda t, dt: t.to(dtype=dt).contiguous()
-    check(lib().rlp_replay_store(C.byref(rb), int(counter), ptr(f(s, torch.float32)),
-                                 ptr(f(a, torch.float32)), ptr(f(reward, torch.float64)),
-                                 ptr(f(s_next, torch.float32)), ptr(f(done, torch.uint8)), n,
-                                 stream_ptr()), "rlp_replay_store")
+    # converted tensors are bound to locals so they outlive the (asynchronous) launch
+    s_, a_ = s.to(dtype=torch.float32).contiguous(), a.to(dtype=torch.float32).contiguous()
+    r_, s2_ = reward.to(dtype=torch.float64).contiguous(), s_next.to(dtype=torch.float32).contiguous()
+    d_ = done.to(dtype=torch.uint8).contiguous()
+    check(lib().rlp_replay_store(C.byref(rb), int(counter), ptr(s_), ptr(a_), ptr(r_), ptr(s2_),
+                                 ptr(d_), n, stream_ptr()), "rlp_replay_store")
     return n
 
 
@@ -294,6 +307,7 @@ def replay_gather(rb, index, out=None):
         torch.empty((B, rb.S), **f32), torch.empty((B, rb.A), **f32), torch.empty(B, **f32),
         torch.empty((B, rb.S), **f32), torch.empty(B, **f32))
     s, a, r, s2, e = out
-    check(lib().rlp_replay_gather(C.byref(rb), ptr(index.contiguous()), B, ptr(s), ptr(a), ptr(r),
+    index_ = index.contiguous()
+    check(lib().rlp_replay_gather(C.byref(rb), ptr(index_), B, ptr(s), ptr(a), ptr(r),
                                   ptr(s2), ptr(e), stream_ptr()), "rlp_replay_gather")
     return out

@@ -740,10 +740,256 @@ def gen_sac():
            for k in ("actor", "critic", "target_critic")})
 
 
+# ---------------------------------------------------------------------------------------------
+# PPO2 learn() (Proximal_Policy_Optimization2.py:78-174) on a fixed buffer, the DPPO2 Worker's
+# learn() (demonstration/DPPO2/DPPO2-4-CartPole/Distributed_PPO2.py:54-103), and N=1 driver
+# transcripts (demonstration/PPO2/PPO2-4-{CartPole,CartPoleAngleOnly}/train.py:184-217). Each
+# generator seeds its own RNGs, so it reproduces when run alone.
+# ---------------------------------------------------------------------------------------------
+def _flat(m):
+    return torch.cat([p.detach().reshape(-1) for p in m.parameters()]).numpy().copy()
+
+
+class _RandpermTape:
+    """Records the permutations SubsetRandomSampler draws (torch.randperm) inside learn()."""
+
+    def __init__(self):
+        self.perms, self.orig = [], torch.randperm
+
+    def __enter__(self):
+        tape = self
+
+        def randperm(n, *a, **k):
+            out = tape.orig(n, *a, **k)
+            tape.perms.append(out.clone())
+            return out
+        torch.randperm = randperm
+        return self
+
+    def __exit__(self, *a):
+        torch.randperm = self.orig
+
+
+def _learn_buffer(g, B, S, actor, lp_noise):
+    s = g.uniform(-2, 2, (B, S))
+    with torch.no_grad():
+        mean = actor(torch.tensor(s, dtype=torch.float))
+        a = torch.clamp(mean + actor.std * torch.tensor(g.normal(size=mean.shape), dtype=torch.float),
+                        actor.a_min, actor.a_max)
+        lp = torch.distributions.Normal(mean, actor.std).log_prob(a).numpy().astype(np.float64)
+    lp = lp + lp_noise * g.normal(size=lp.shape)      # old-policy log-probs: ratios off 1
+    r = g.normal(-1, 2, B)
+    s2 = s + 0.05 * g.normal(size=(B, S))
+    done = (g.uniform(size=B) < 0.03).astype(np.float64)
+    success = done * (g.uniform(size=B) < 0.5)
+    return s, a.numpy().astype(np.float64), lp, r, s2, done, success
+
+
+def gen_ppo2_learn():
+    """Three learn() calls (K=3) on one 1000-row buffer with the PPO2-CartPole driver's nets
+    (train.py:39-125): full batch; use_grad_clip=True; mini-batch (64) with the sampler's
+    permutations recorded. The GAE / v_target / normalised advantages learn() feeds the epochs
+    are recorded too (probes on the reference module's torch name)."""
+    g = np.random.default_rng(20261)
+    out = {}
+    B = 1000
+    for mode, over in (("full", {}), ("clip", {'use_grad_clip': True}),
+                       ("mini", {'using_mini_batch': True})):
+        torch.manual_seed(17)
+        actor = drv.PPOActor_Gaussian(state_dim=4, action_dim=1, a_min=np.array([-8.]),
+                                      a_max=np.array([8.]), init_std=8 / 3, use_orthogonal_init=True)
+        critic = drv.PPOCritic(state_dim=4, use_orthogonal_init=True)
+        with torch.no_grad():   # a last layer large enough for a non-trivial tanh'(z3)
+            torch.nn.init.orthogonal_(actor.mean_layer.weight, gain=1.0)
+        ppo_msg = {'gamma': 0.999, 'K_epochs': 3, 'eps_clip': 0.2, 'buffer_size': B,
+                   'state_dim': 4, 'action_dim': 1, 'a_lr': 3e-4, 'c_lr': 1e-3,
+                   'set_adam_eps': True, 'lmd': 0.95, 'use_adv_norm': True,
+                   'mini_batch_size': 64, 'entropy_coef': 0.01, 'use_grad_clip': False,
+                   'use_lr_decay': False, 'max_train_steps': int(5e6), 'using_mini_batch': False}
+        ppo_msg.update(over)
+        env_msg = {'state_dim': 4, 'action_dim': 1, 'name': 'CartPole', 'action_range': [[-8., 8.]]}
+        agent = ppo2_mod.Proximal_Policy_Optimization2(env_msg, ppo_msg, actor=actor, critic=critic)
+        s, a, lp, r, s2, done, success = _learn_buffer(g, B, 4, actor, 0.3)
+        for i in range(B):
+            agent.buffer.append(s=s[i], a=a[i], log_prob=lp[i], r=r[i], s_=s2[i], done=done[i],
+                                success=success[i], index=i)
+        before_a, before_c = _flat(actor), _flat(critic)
+        with torch.no_grad():
+            st = torch.tensor(s, dtype=torch.float)
+            vs = critic(st)
+        rec = {}
+        real = ppo2_mod.torch
+        ppo2_mod.torch = _TorchProbe(rec)
+        try:
+            with _RandpermTape() as tape:
+                agent.learn(0, buf_num=1)
+        finally:
+            ppo2_mod.torch = real
+        adv = torch.tensor(rec["gae_list"]).view(-1, 1)
+        v_target = adv + vs
+        adv_n = (adv - adv.mean()) / (adv.std() + 1e-5)
+        out.update({f"{mode}_s": s, f"{mode}_a": a, f"{mode}_a_lp": lp, f"{mode}_r": r,
+                    f"{mode}_s_": s2, f"{mode}_done": done, f"{mode}_success": success,
+                    f"{mode}_before_actor": before_a, f"{mode}_before_critic": before_c,
+                    f"{mode}_after_actor": _flat(actor), f"{mode}_after_critic": _flat(critic),
+                    f"{mode}_adv_norm": adv_n.numpy()[:, 0], f"{mode}_v_target": v_target.numpy()[:, 0]})
+        if mode == "mini":
+            out["mini_perms"] = np.stack([p.numpy() for p in tape.perms])
+        print("ppo2_learn", mode, "max |dW| actor %.3e critic %.3e" % (
+            np.abs(out[f"{mode}_after_actor"] - before_a).max(),
+            np.abs(out[f"{mode}_after_critic"] - before_c).max()), len(tape.perms), "perms")
+    np.savez_compressed(os.path.join(OUT, "ppo2_learn.npz"), std=np.float32(8 / 3), **out)
+
+
+def gen_dppo2_learn():
+    """Two consecutive Worker.learn() iterations of the DPPO2-CartPole copy (SharedAdam with the
+    driver's lr / eps, k_epo = 6, use_grad_clip=True, clip 0.2), the local nets reloaded from the
+    global ones before each, as Worker.run() does (:124-125). Captures the global nets after each
+    learn() — they carry the never-zeroed local gradient buffers' accumulation."""
+    with quiet():
+        dmod = load("demonstration/DPPO2/DPPO2-4-CartPole/Distributed_PPO2.py", "ref_dppo2_cp")
+        ddrv = load("demonstration/DPPO2/DPPO2-4-CartPole/train.py", "ref_dppo2_cp_train")
+    g = np.random.default_rng(20262)
+    torch.manual_seed(23)
+    mk_a = lambda: ddrv.PPOActor_Gaussian(state_dim=4, action_dim=1, a_min=np.array([-8.]),
+                                          a_max=np.array([8.]), init_std=1.2,
+                                          use_orthogonal_init=True)
+    g_actor, l_actor = mk_a(), mk_a()
+    g_critic = ddrv.PPOCritic(state_dim=4, use_orthogonal_init=True)
+    l_critic = ddrv.PPOCritic(state_dim=4, use_orthogonal_init=True)
+    with torch.no_grad():
+        torch.nn.init.orthogonal_(g_actor.fc3.weight, gain=1.0)
+    P = 20
+    a_lr, c_lr, k_epo = 1e-4 / min(P, 5), 1e-3 / min(P, 5), int(30 / min(P, 5))
+    opt_a = cls_mod.SharedAdam([{'params': g_actor.parameters(), 'lr': a_lr}], eps=1e-5)
+    opt_c = cls_mod.SharedAdam([{'params': g_critic.parameters(), 'lr': c_lr}], eps=1e-5)
+    B = 1000
+    ppo_msg = {'gamma': 0.99, 'k_epo': k_epo, 'eps_clip': 0.2, 'buffer_size': B, 'state_dim': 4,
+               'action_dim': 1, 'device': 'cpu', 'set_adam_eps': True, 'lmd': 0.95,
+               'use_adv_norm': True, 'mini_batch_size': 64, 'entropy_coef': 0.01,
+               'use_grad_clip': True, 'use_lr_decay': True, 'max_train_steps': int(5e6),
+               'using_mini_batch': False, 'action_range': [[-8., 8.]]}
+
+    class _Env:
+        state_dim, action_dim = 4, 1
+    w = dmod.Worker(g_actor, l_actor, g_critic, l_critic, opt_c, opt_a, None, 0, "w0", _Env(),
+                    None, None, ppo_msg)
+    out = {"before_actor": _flat(g_actor), "before_critic": _flat(g_critic), "a_lr": a_lr,
+           "c_lr": c_lr, "k_epo": k_epo, "gamma": 0.99, "std": np.float32(1.2)}
+    for it in range(2):
+        l_actor.load_state_dict(g_actor.state_dict())
+        l_critic.load_state_dict(g_critic.state_dict())
+        s, a, lp, r, s2, done, _ = _learn_buffer(g, B, 4, l_actor, 0.3)
+        success = (g.uniform(size=B) < 0.9).astype(np.float64)     # `0 if flag == 1 else 1` (:138)
+        for i in range(B):
+            w.buffer.append(s=s[i], a=a[i], log_prob=lp[i], r=r[i], s_=s2[i], done=done[i],
+                            success=success[i], index=i)
+        w.learn()
+        out.update({f"it{it}_s": s, f"it{it}_a": a, f"it{it}_a_lp": lp, f"it{it}_r": r,
+                    f"it{it}_s_": s2, f"it{it}_done": done, f"it{it}_success": success,
+                    f"it{it}_after_actor": _flat(g_actor), f"it{it}_after_critic": _flat(g_critic)})
+    print("dppo2_learn", {k: float(np.abs(out[f"it1_after_{k}"] - out[f"before_{k}"]).max())
+                          for k in ("actor", "critic")})
+    np.savez_compressed(os.path.join(OUT, "dppo2_learn.npz"), **out)
+
+
+class _NoiseTape:
+    """Normal.sample() as loc + eps * scale with eps ~ N(0,1) drawn here and recorded: the
+    driver's exploration noise becomes data a replay can inject."""
+
+    def __init__(self):
+        self.tape, self.orig = [], torch.distributions.Normal.sample
+
+    def __enter__(self):
+        tape = self
+
+        def sample(dist, sample_shape=torch.Size()):
+            shape = dist._extended_shape(sample_shape)
+            eps = torch.randn(shape)
+            tape.tape.append(eps.clone())
+            return dist.loc + eps * dist.scale
+        torch.distributions.Normal.sample = sample
+        return self
+
+    def __exit__(self, *a):
+        torch.distributions.Normal.sample = self.orig
+
+
+def gen_ppo2_transcript(key):
+    """The N=1 PPO2 driver loop (train.py:184-224) for one buffer (1000 steps, int(timeMax/dt)*4)
+    then learn() with the demo's ppo_msg (K_epochs 30, full batch; AngleOnly: grad clip + lr
+    decay). Episode starts come from the env's own reset law (numpy seeded here) and are recorded,
+    the exploration noise is recorded (_NoiseTape): a replay injects both."""
+    if key == "cartpole":
+        with quiet():
+            tdrv = drv
+        env = mods["cp_ppo2"].CartPole(0., 0.)
+        over = {}
+    else:
+        with quiet():
+            tdrv = load("demonstration/PPO2/PPO2-4-CartPoleAngleOnly/train.py", "ref_ppo2_ao_train")
+        env = mods["ao_ppo2"].CartPoleAngleOnly(0.)
+        over = {'use_grad_clip': True, 'use_lr_decay': True}
+    np.random.seed(31 if key == "cartpole" else 32)
+    torch.manual_seed(41 if key == "cartpole" else 42)
+    ar = np.array(env.action_range)
+    actor = tdrv.PPOActor_Gaussian(state_dim=env.state_dim, action_dim=env.action_dim,
+                                   a_min=ar[:, 0], a_max=ar[:, 1], init_std=env.fm / 3,
+                                   use_orthogonal_init=True)
+    critic = tdrv.PPOCritic(state_dim=env.state_dim, use_orthogonal_init=True)
+    B = int(env.timeMax / env.dt) * 4
+    ppo_msg = {'gamma': 0.999, 'K_epochs': 30, 'eps_clip': 0.2, 'buffer_size': B,
+               'state_dim': env.state_dim, 'action_dim': env.action_dim, 'a_lr': 3e-4, 'c_lr': 1e-3,
+               'set_adam_eps': True, 'lmd': 0.95, 'use_adv_norm': True, 'mini_batch_size': 64,
+               'entropy_coef': 0.01, 'use_grad_clip': False, 'use_lr_decay': False,
+               'max_train_steps': int(5e6), 'using_mini_batch': False}
+    ppo_msg.update(over)
+    env_msg = {'state_dim': env.state_dim, 'action_dim': env.action_dim, 'name': env.name,
+               'action_range': env.action_range}
+    agent = ppo2_mod.Proximal_Policy_Optimization2(env_msg, ppo_msg, actor=actor, critic=critic)
+    reward_norm = cls_mod.Normalization(shape=1)
+    before_a, before_c = _flat(actor), _flat(critic)
+    resets, raw_r, flags = [], [], []
+    env.is_terminal = True
+    idx = 0
+    with _NoiseTape() as tape, quiet():
+        while idx < B:
+            if env.is_terminal:
+                env.reset(True)
+                resets.append([env.initTheta, getattr(env, "initX", 0.)])
+            else:
+                env.current_state = env.next_state.copy()
+                a, a_lp = agent.choose_action(env.current_state)
+                env.step_update(a)
+                success = 0 if (env.is_terminal and env.terminal_flag == 3) else \
+                    (1 if env.is_terminal else 0)
+                raw_r.append(env.reward)
+                flags.append(env.terminal_flag)
+                agent.buffer.append(s=env.current_state, a=a, log_prob=a_lp,
+                                    r=reward_norm(env.reward), s_=env.next_state,
+                                    done=1.0 if env.is_terminal else 0.0, success=success,
+                                    index=idx)
+                idx += 1
+        timestep = B
+        agent.learn(timestep, buf_num=1)
+    b = agent.buffer
+    np.savez_compressed(
+        os.path.join(OUT, f"ppo2_transcript_{key}.npz"), resets=np.array(resets),
+        noise=np.concatenate([e.numpy().reshape(-1) for e in tape.tape]).astype(np.float32),
+        s=b.s, a=b.a, a_lp=b.a_lp, r=b.r[:, 0], s_=b.s_, done=b.done[:, 0],
+        success=b.success[:, 0], raw_reward=np.array(raw_r), flag=np.array(flags),
+        before_actor=before_a, before_critic=before_c, after_actor=_flat(actor),
+        after_critic=_flat(critic), std=np.float32(env.fm / 3), B=B)
+    print("ppo2_transcript", key, len(resets), "episodes", "max |dW| actor %.3e critic %.3e" % (
+        np.abs(_flat(actor) - before_a).max(), np.abs(_flat(critic) - before_c).max()))
+
+
 if __name__ == "__main__" and len(sys.argv) > 2:   # selected generators only
     for name in sys.argv[2:]:
         if name.startswith("ugvoa_"):
             gen_ugvoa(name, n=400 if name == "ugvoa_env" else 300)
+        elif name.startswith("ppo2_transcript_"):
+            gen_ppo2_transcript(name[len("ppo2_transcript_"):])
         else:
             globals()["gen_" + name]()
     sys.exit(0)
@@ -769,6 +1015,10 @@ if __name__ == "__main__":
     gen_replay()
     gen_ddpg()
     gen_sac()
+    gen_ppo2_learn()
+    gen_dppo2_learn()
+    gen_ppo2_transcript("cartpole")
+    gen_ppo2_transcript("angleonly")
     with open(os.path.join(OUT, "VERSIONS.txt"), "w") as f:
         f.write(f"numpy {np.__version__}\ntorch {torch.__version__}\npython {sys.version.split()[0]}\n"
                 f"reference {REF} (HKPolyU-UAV/ReinforcementLearningPlatform @ 2025-02-28)\n")

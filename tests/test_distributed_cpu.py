@@ -43,10 +43,14 @@ def _nets(seed=1):
     return actor, critic
 
 
-MSG = dict(DEFAULT_PPO_MSG, K_epochs=3, use_grad_clip=True)
+MSGS = {"ppo2": dict(DEFAULT_PPO_MSG, K_epochs=3, use_grad_clip=True),
+        # the DPPO2 Worker.learn rule (Distributed_PPO2's default): clip 0.2, SharedAdam betas
+        "dppo2": dict(DEFAULT_PPO_MSG, K_epochs=6, use_grad_clip=True, update_rule='dppo2',
+                      grad_clip_norm=0.2, adam_betas=(0.9, 0.99))}
 
 
-def _worker(rank, world, port, N, out):
+def _worker(rank, world, port, N, out, rule="ppo2"):
+    MSG = MSGS[rule]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
@@ -60,14 +64,16 @@ def _worker(rank, world, port, N, out):
     torch.distributed.destroy_process_group()
 
 
-def test_data_parallel_update_equals_single_rank():
+@pytest.mark.parametrize("rule", ["ppo2", "dppo2"])
+def test_data_parallel_update_equals_single_rank(rule):
+    MSG = MSGS[rule]
     N, world = 512, 2
     mgr = mp.Manager()
     out = mgr.dict()
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, N, out), nprocs=world, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, N, out, rule), nprocs=world, start_method="spawn")
     r0, r1 = np.asarray(out[0]), np.asarray(out[1])
-    np.testing.assert_allclose(r0, r1, rtol=0, atol=1e-6)          # replicas stay identical
+    np.testing.assert_array_equal(r0, r1)                         # replicas stay identical
     actor, critic = _nets(seed=100)
     single = PPO2Learner(actor, critic, MSG, device="cpu")
     single.update(*_batch(N))

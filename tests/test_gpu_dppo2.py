@@ -1,0 +1,133 @@
+"""Distributed_PPO2 (the DPPO2 drop-in) at world size 2: two ranks on one GPU over gloo (the
+N-GPU runs use RCCL with one GPU per rank; the arithmetic is the same).
+
+Reference: demonstration/DPPO2/DPPO2-4-CartPole/train.py:136-210 (20 Worker processes) and
+Distributed_PPO2.py:13-172. Here each rank is one Worker with n envs; rank r's envs have global
+ids r*n .. r*n+n-1 and draw from the Philox stream keyed by those ids, so
+  (1) the union of the ranks' rollout buffers equals a single rank's buffers on 2n envs, bit for
+      bit, and
+  (2) after the synchronous update (one gradient all-reduce, the Worker.learn() rule) the replicas
+      are bit-identical, and stay so for the next iteration's rollout.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from reinforcementlearningplatform_amd.algorithm.policy_base.Distributed_PPO2 import (
+    DPPO2_COPY, Distributed_PPO2, dppo2_std_schedule)
+from reinforcementlearningplatform_amd.environment.CartPole.CartPole import CartPole
+from reinforcementlearningplatform_amd.utils.classes import PPOActor_Gaussian, PPOCritic
+from reinforcementlearningplatform_amd import _abi
+
+pytestmark = pytest.mark.gpu
+
+N, T = 2048, 64
+KEYS = ("obs", "obs_next", "action", "logp", "reward", "value", "value_next", "done", "success",
+        "flag")
+
+
+def _agent(n, env_id0):
+    torch.manual_seed(0)   # the same initial nets on every rank (rank 0's are broadcast anyway)
+    env = CartPole(n_envs=n, seed=5, env_id0=env_id0, variant="dppo2")
+    actor = PPOActor_Gaussian(4, 1, np.array([-8.]), np.array([8.]), init_std=1.2)
+    critic = PPOCritic(4)
+    P = 20   # train.py:136-140
+    return Distributed_PPO2(env, actor_lr=1e-4 / min(P, 5), critic_lr=1e-3 / min(P, 5),
+                            num_of_pro=P, ppo_msg={'k_epo': int(30 / min(P, 5)), 'gamma': 0.99},
+                            T=T, actor=actor, critic=critic, seed=3407)
+
+
+def _flat(ag):
+    return torch.cat([p.detach().reshape(-1) for p in
+                      list(ag.global_actor.parameters()) + list(ag.global_critic.parameters())]
+                     ).cpu().numpy()
+
+
+def _run(ag):
+    """Two iterations; per iteration the rollout buffers, then the params after learn()."""
+    rec = []
+    for _ in range(2):
+        w = ag.worker
+        w.rollout()
+        bufs = {k: w.bufs[k].cpu().numpy().copy() for k in KEYS}
+        w.advantages()
+        w.update()
+        rec.append((bufs, _flat(ag)))
+    return rec
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    ag = _agent(N, rank * N)
+    assert ag.world == world and ag.worker.learner.distributed
+    out[rank] = _run(ag)
+    torch.distributed.destroy_process_group()
+
+
+def test_dppo2_two_ranks_union_and_replicas():
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_rank, args=(2, _free_port(), out), nprocs=2, start_method="spawn")
+    r0, r1 = out[0], out[1]
+    for key in ("WORLD_SIZE", "RANK"):
+        os.environ.pop(key, None)
+    single = _run(_agent(2 * N, 0))
+    # (1) the first iteration's rollouts: the union is the 2n-env run, bit for bit
+    b0, b1, bs = r0[0][0], r1[0][0], single[0][0]
+    for k in KEYS:
+        np.testing.assert_array_equal(np.concatenate([b0[k], b1[k]], axis=1), bs[k], err_msg=k)
+    assert bs["done"].any()
+    # (2) replicas identical after each synchronous update, and the second rollout too
+    for it in range(2):
+        np.testing.assert_array_equal(r0[it][1], r1[it][1])
+    assert np.abs(r0[0][1] - single[0][1]).max() < 1e-2      # same objective, per-rank adv-norm
+    for k in ("action", "value"):
+        assert not np.array_equal(r0[1][0][k], r0[0][0][k])   # the second rollout used new nets
+
+
+def test_dppo2_copy_semantics_selected():
+    """Distributed_PPO2 picks the DPPO2-CartPole copy's Worker: success = (flag != 1) on every
+    step, clip 0.2, SharedAdam betas, Worker.learn update rule, no lr decay."""
+    ag = _agent(256, 0)
+    w = ag.worker
+    assert (w.rule, w.flag) == (_abi.RLP_SUCCESS_FLAG_NE, 1)
+    lr = w.learner
+    assert lr.rule == 'dppo2' and lr.max_norm == 0.2 and lr.betas == (0.9, 0.99)
+    a_lr = lr.lr["a"]
+    ag.msg['use_lr_decay'] = True
+    ag.start_multi_process(iterations=1, eval_every=0, std_schedule=False)
+    assert lr.lr["a"] == a_lr
+    su = w.bufs["success"].cpu().numpy()
+    fl = w.bufs["flag"].cpu().numpy()
+    np.testing.assert_array_equal(su, (fl != 1).astype(np.uint8))
+
+
+def test_dppo2_std_schedules():
+    """Worker.run's exploration schedules (DPPO2-4-CartPole :160-165; the other copies :163-168)."""
+    class A:
+        std = torch.tensor(1.2)
+    a = A()
+    sch = dppo2_std_schedule(DPPO2_COPY[_abi.RLP_ENV_CARTPOLE], [[-8., 8.]])
+    for t in range(501):
+        sch(t, a)
+    # t=250: 8/3 * 0.95; t=500: 8/3 * 0.9
+    assert float(a.std.reshape(-1)[0]) == pytest.approx(8 / 3 * 0.9, rel=1e-6)
+    b = A()
+    sch = dppo2_std_schedule(DPPO2_COPY[_abi.RLP_ENV_UGV_FORWARD], [[-3., 3.], [-6.28, 6.28]])
+    for t in range(2001):
+        sch(t, b)
+    assert float(b.std) == pytest.approx(1.2 * 0.95 * 0.9, rel=1e-6)

@@ -1,8 +1,7 @@
 """GPU parity of the fused rollout kernel (rlp_rollout) — the bench's hot path.
 
-(1) Closed loop vs the CPU oracle's batched driver loop on the same seeds, short segments (the
-    float32 MLP differs from the oracle's double-accumulated one by ~1e-7, so long closed loops
-    drift apart; 8-16 steps stay within 1e-4).
+(1) Teacher-forced parity against the oracle and the reference's shipped nets lives in
+    test_gpu_rollout_parity.py.
 (2) Size-independent invariants at the bench size (65 536 envs): s'_t == s_{t+1} and
     V(s'_t) == V(s_{t+1}) where not done; teacher-forced critic / actor log-prob recomputation.
 """
@@ -67,28 +66,6 @@ def run_both(kind, n, T, seed=3407, sub=None, params=None, success=None):
     oneed = np.ones(n, np.uint8)
     ob = oracle.rollout(kind, p, ost, oneed, ad, ap, cd, cp, cfg)
     return {k: host(v) for k, v in bufs.items()}, ob, host(st), ost, host(need), oneed, (ad, ap, cd, cp)
-
-
-@pytest.mark.parametrize("kind", sorted(A.ROLLOUT_KINDS))
-@pytest.mark.parametrize("sub", [1, 2, 4])
-def test_rollout_closed_loop_vs_oracle(kind, sub):
-    T = 12
-    g, o, st, ost, need, oneed, _ = run_both(kind, 2048 + 37, T, sub=sub)
-    # the trajectories branch only if a terminal threshold is straddled; compare on envs whose
-    # done/flag sequences agree (>= 99%)
-    same = (g["flag"] == o["flag"]).all(axis=0)
-    assert same.mean() > 0.99
-    for key, rtol, atol in [("obs", 1e-4, 1e-5), ("obs_next", 1e-4, 1e-5), ("action", 1e-4, 1e-4),
-                            ("logp", 1e-4, 1e-4), ("value", 1e-4, 1e-4), ("reward", 1e-4, 1e-4)]:
-        a, b = g[key][:, same], o[key][:, same]
-        bad = np.abs(a - b) > atol + rtol * np.abs(b)
-        assert bad.mean() < 1e-3, f"{key}: {bad.sum()} mismatches, max err {np.abs(a - b).max()}"
-    np.testing.assert_array_equal(g["done"][:, same], o["done"][:, same])
-    np.testing.assert_array_equal(g["success"][:, same], o["success"][:, same])
-    np.testing.assert_array_equal(need[same], oneed[same])
-    vn_ok = g["done"][:, same] == 0
-    a, b = g["value_next"][:, same][vn_ok], o["value_next"][:, same][vn_ok]
-    assert (np.abs(a - b) <= 1e-4 + 1e-4 * np.abs(b)).mean() > 0.999
 
 
 def test_rollout_rejects_lidar_env():

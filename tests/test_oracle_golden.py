@@ -6,6 +6,7 @@ import pytest
 
 from oracle import oracle
 from reinforcementlearningplatform_amd import _abi as A
+from reinforcementlearningplatform_amd import kernels as K
 
 ENV_CASES = [
     ("cartpole_ppo2", A.RLP_ENV_CARTPOLE, lambda: A.cartpole_params("ppo2")),
@@ -213,3 +214,31 @@ def test_ugvoa_reset_maps_legal(golden, variant):
     ref_r = golden("ugvoa_" + variant)["maps"][..., 2].ravel()
     ours = st[10::3][:p.n_obs][placed[:p.n_obs]].ravel()
     assert abs(ours.mean() - ref_r.mean()) < 0.02
+
+
+@pytest.mark.parametrize("kind", sorted(A.ROLLOUT_KINDS))
+def test_oracle_forced_replay_reproduces_closed_loop(kind):
+    """Teacher forcing with the oracle's own actions reproduces its closed loop bit for bit, with
+    and without the nets (the GPU rollout parity tests replay the kernel's actions this way)."""
+    D, S, Ad = A.ENV_DIMS[kind]
+    p = A.default_params(kind)
+    rng = np.random.default_rng(kind)
+    ad = A.MLPDesc.make([S, 32, 32, Ad], [1, 1, 1])
+    cd = A.MLPDesc.make([S, 32, 32, 1], [1, 1, 0])
+    ap = (rng.normal(0, 1, ad.param_count()) / 4).astype(np.float32)
+    cp = (rng.normal(0, 1, cd.param_count()) / 4).astype(np.float32)
+    lo, hi = A.action_bounds(kind, p)
+    n, T = 67, 40
+    cfg = K.make_rollout_cfg(T, n, 9, 0, 0, [(h - l) / 3 for l, h in zip(lo, hi)], lo, hi,
+                             A.RLP_SUCCESS_DONE_AND_FLAG_NE, A.timeout_flag(kind))
+    st0, need0 = np.zeros((D, n)), np.ones(n, np.uint8)
+    ref = oracle.rollout(kind, p, st0, need0, ad, ap, cd, cp, cfg)
+    for nets in (True, False):
+        st, need = np.zeros((D, n)), np.ones(n, np.uint8)
+        args = (ad, ap, cd, cp) if nets else (None, None, None, None)
+        out = oracle.rollout(kind, p, st, need, *args, cfg, forced_action=ref["action"])
+        keys = ref.keys() if nets else ("obs", "obs_next", "reward", "done", "success", "flag")
+        for key in keys:
+            np.testing.assert_array_equal(out[key], ref[key], err_msg=key)
+        np.testing.assert_array_equal(st, st0)
+        np.testing.assert_array_equal(need, need0)
