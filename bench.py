@@ -101,7 +101,7 @@ class Segment:
         self.need = torch.ones(n, dtype=torch.uint8, device="cuda")
         self.bufs = K.rollout_buffers(kind, T, n)
         self.rms = torch.zeros(4, dtype=torch.float64, device="cuda")
-        self.work = torch.empty(3 * T, dtype=torch.float64, device="cuda")
+        self.work = K.reward_norm_workspace(T, n, "cuda")
         self.rnorm = torch.empty((T, n), dtype=torch.float32, device="cuda")
         self.adv = torch.empty((T, n), dtype=torch.float32, device="cuda")
         self.vt = torch.empty((T, n), dtype=torch.float32, device="cuda")
@@ -390,6 +390,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e", type=int, default=2, help="PPO2 iterations incl. the K-epoch update to time (0: skip)")
+    ap.add_argument("--e2e-k30", type=int, default=1, help="also time e2e at the PPO2 demo's K=30")
     ap.add_argument("--uav", type=int, default=1, help="also time the UavRobust rollout (32768 envs/GPU)")
     ap.add_argument("--fp32-leg", type=int, default=1, help="also time the exact-f32 MLP path")
     ap.add_argument("--ddpg", type=int, default=1, help="also time SOI DDPG with the HBM replay (config 3)")
@@ -498,22 +499,40 @@ def main():
     if traffic is not None:
         out["roofline"]["traffic"] = traffic
     if args.uav and args.env == "cartpole":
-        useg = Segment("uav", 32768, 64, args.seed + 1, env_id0=rank * 32768)
+        un, uT, usteps = 32768, 64, 5
+        useg = Segment("uav", un, uT, args.seed + 1, env_id0=rank * un)
         for _ in range(2):
             useg.iteration()
-        torch.cuda.synchronize()
+        barrier()
         t1 = time.perf_counter()
-        for _ in range(3):
-            useg.iteration()
-        torch.cuda.synchronize()
+        uev = []
+        for _ in range(usteps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            useg.rollout()
+            e1.record()
+            useg.learn_side()
+            uev.append((e0, e1))
+        barrier()
         uel = time.perf_counter() - t1
         if dist is not None:
             t = torch.tensor([uel], device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             uel = float(t.item())
-        out["uav_ppo2_rollout"] = {"value": 32768 * 64 * 3 * world / uel, "unit": "env-steps/s",
-                                   "envs_per_gpu": 32768, "global_envs": 32768 * world, "T": 64,
-                                   "config": "UavRobust hover outer loop (6-DoF + FNTSMC), PPO2 [6,256,256,3]"}
+        ums = float(np.mean([a.elapsed_time(b) for a, b in uev]))
+        uflop = un * uT * (mlp_flops(useg.ad) + mlp_flops(useg.cd)) + un * mlp_flops(useg.cd)
+        uach = uflop / (ums * 1e-3) / 1e12
+        upeak = PEAK_F16X3_TFLOPS if prec == _native.MLP_F16X3 else PEAK_FP32_MFMA_TFLOPS
+        out["uav_ppo2_rollout"] = {
+            "value": un * uT * usteps * world / uel, "unit": "env-steps/s", "envs_per_gpu": un,
+            "global_envs": un * world, "T": uT,
+            "config": "UavRobust hover outer loop (6-DoF + FNTSMC), PPO2 [6,256,256,3]",
+            "roofline": {"bound": "mfma", "kernel": (ROLLOUT_KERNEL[args.physics]
+                                                     if args.precision == "f16x3"
+                                                     else "rlp::rollout_kernel<KIND,256,SUB,false>"),
+                         "achieved": uach, "peak": upeak, "unit": "TFLOP/s", "frac": uach / upeak,
+                         "traffic": pmc_traffic("uav_ppo2_rollout", un, uT),
+                         "avg_launch_ms": ums, "flop_per_launch": uflop}}
         del useg
     if args.ddpg and args.env == "cartpole":
         d = soi_ddpg_leg(rank)
@@ -537,13 +556,17 @@ def main():
             d["value"], d["env_only"] = float(t[0]), float(t[1])
         out["ugvoa_sac"] = d
     if args.e2e:
+        upd = ("librlp rlp_ppo2_grad + rlp_adam_step" if args.learner == "native"
+               else "torch autograd + Adam (fp32)")
         v, it_s = e2e_iterations(seg, args.e2e, learner=args.learner)
-        v_all = v * world
-        out["e2e"] = {"value": v_all, "unit": "env-steps/s", "s_per_iteration": it_s,
-                      "update": ("K=6 full-batch epochs per iteration, " +
-                                 ("librlp rlp_ppo2_grad + rlp_adam_step" if args.learner == "native"
-                                  else "torch autograd + Adam (fp32)")),
+        out["e2e"] = {"value": v * world, "unit": "env-steps/s", "s_per_iteration": it_s,
+                      "update": f"K=6 full-batch epochs per iteration (DPPO2 drivers' k_epo), {upd}",
                       "note": "rollout + GAE + PPO update; `value` above is the rollout hot path"}
+        if args.e2e_k30:
+            v30, it30 = e2e_iterations(seg, max(1, args.e2e // 2), k_epochs=30, learner=args.learner)
+            out["e2e"]["k30"] = {
+                "value": v30 * world, "unit": "env-steps/s", "s_per_iteration": it30,
+                "update": f"K=30 full-batch epochs per iteration (PPO2-4-CartPole/train.py:146), {upd}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.env, args.cpu_seconds)
     if rank == 0:

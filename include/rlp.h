@@ -90,17 +90,29 @@ typedef struct rlp_cartpole_params {
     int32_t reserved;
 } rlp_cartpole_params;
 
-/* cartpole_angleonly.py:27-41, get_reward :170-195 (Q_theta, Q_omega, R), reset :245-279. */
+/* Two copies (variant):
+ * RLP_ANGLEONLY_PPO2_COPY  demonstration/PPO2/PPO2-4-CartPoleAngleOnly/cartpole_angleonly.py:27-41
+ *   (== the DPPO2 copy): one RK4 step of h = dt = 0.02 (:218-229), fm 5, timeMax 5, flags
+ *   1 angle / 3 time / 4 success (later overrides), reward -Q_theta th^2 ... (:170-195);
+ * RLP_ANGLEONLY_ENV_FILE  environment/CartPole/CartPoleAngleOnly.py:36-39: dt 0.01 in 10 RK4
+ *   sub-steps of h = dt/10 under the fp64 `while time < tt` loop (:231-244, 10 or 11 by step
+ *   index), fm 8, timeMax 6, flags 1 angle (wins) else 3 time, no success flag (:144-166), and the
+ *   angle-increment reward (:168-208: -2 / 0 / +2 as |theta| grows / holds / shrinks in degrees,
+ *   +5 inside 0.5 deg, -100 on flag 1, +500 on flag 3). Reset :245-279 / :266-300 alike. */
+#define RLP_ANGLEONLY_PPO2_COPY 0
+#define RLP_ANGLEONLY_ENV_FILE 1
 typedef struct rlp_angleonly_params {
     double theta_max;   /* deg2rad(45) */
     double static_gain; /* 2.0 */
     double norm_dtheta; /* norm_4_boundless_state = 4 */
     double M, m, g, ell, kf;
-    double fm;       /* 5 */
-    double dt;       /* 0.02: one RK4 step of h = dt (:218-229) */
-    double time_max; /* 5 */
+    double fm;       /* 5 (env file: 8) */
+    double dt;       /* 0.02 (env file: 0.01) */
+    double time_max; /* 5 (env file: 6) */
     double reset_theta_lo, reset_theta_hi;
-    double Q_theta, Q_omega, R; /* 10, 0, 0 */
+    double Q_theta, Q_omega, R; /* 10, 0, 0 (PPO2 copy's reward) */
+    int32_t variant;            /* RLP_ANGLEONLY_PPO2_COPY | RLP_ANGLEONLY_ENV_FILE */
+    int32_t n_sub_div;          /* env file: 10 (rk44 :232) */
 } rlp_angleonly_params;
 
 /* SecondOrderIntegration.py:13-60, reward :251-284, reset :328-352. */
@@ -302,6 +314,11 @@ typedef struct rlp_rollout_cfg {
     int32_t success_flag; /* F */
     float std[4];         /* actor.std per action dim (host values) */
     float a_min[4], a_max[4];
+    /* per-call kernel selection; 0 = the library-wide default set by rlp_set_mlp_precision /
+     * rlp_set_rollout_physics / rlp_set_rollout_sub, else value + 1 (mlp_precision: 1 RLP_MLP_FP32,
+     * 2 RLP_MLP_F16X3; physics: 1 register-resident, 2 shared, 3 shared 8-wave); sub: 0 default,
+     * 1, 2, 4 */
+    int32_t mlp_precision, physics, sub, reserved;
 } rlp_rollout_cfg;
 
 /* state: [D][n] f64 in/out, carried across segments. need_reset: [n] u8 in/out (1 = env is
@@ -336,7 +353,8 @@ int rlp_value_fixup(const rlp_mlp_desc *critic_desc, const float *critic_packed,
  * n == 1, reproducing the reference exactly including the first-call std = x quirk; Chan's
  * parallel merge otherwise), then every reward of step t is normalised with the statistics
  * after that merge. rms: device f64[4] = {count, mean, S, std}, in/out across segments.
- * work: device f64[3*T] scratch. reward_out may alias reward_in. */
+ * work: device f64[rlp_reward_norm_workspace(T, n)] scratch. reward_out may alias reward_in. */
+int64_t rlp_reward_norm_workspace(int T, int n);
 int rlp_reward_norm(const float *reward_in, int T, int n, double *rms, double *work,
                     float *reward_out, rlp_stream_t stream);
 

@@ -186,46 +186,84 @@ static void ao_obs(const rlp_angleonly_params *p, const double *s, float *o) { /
     o[1] = (float)((s[1] / p->norm_dtheta) * p->static_gain);
 }
 
+static void ao_rk4(const rlp_angleonly_params *p, double force, double h, double xx[4]) {
+    double K1[4], K2[4], K3[4], K4[4], tmp[4], d[4];
+    ao_ode(p, force, xx, d);
+    for (int i = 0; i < 4; ++i) K1[i] = h * d[i];
+    for (int i = 0; i < 4; ++i) tmp[i] = xx[i] + K1[i] / 2;
+    ao_ode(p, force, tmp, d);
+    for (int i = 0; i < 4; ++i) K2[i] = h * d[i];
+    for (int i = 0; i < 4; ++i) tmp[i] = xx[i] + K2[i] / 2;
+    ao_ode(p, force, tmp, d);
+    for (int i = 0; i < 4; ++i) K3[i] = h * d[i];
+    for (int i = 0; i < 4; ++i) tmp[i] = xx[i] + K3[i];
+    ao_ode(p, force, tmp, d);
+    for (int i = 0; i < 4; ++i) K4[i] = h * d[i];
+    for (int i = 0; i < 4; ++i) xx[i] = xx[i] + (K1[i] + 2 * K2[i] + 2 * K3[i] + K4[i]) / 6;
+}
+
+/* |rad2deg(current_state[0] / staticGain * thetaMax)| (environment/CartPole/
+ * CartPoleAngleOnly.py:187-188; rad2deg = deg * 180. / pi, utils/functions.py:8-9) */
+static double ao_abs_deg(const rlp_angleonly_params *p, double th) {
+    double o = th / p->theta_max * p->static_gain;
+    return fabs(o / p->static_gain * p->theta_max * 180. / PI);
+}
+
 static void ao_step(const rlp_angleonly_params *p, double *s, float a, float *obs_cur,
                     float *obs_next, double *reward, int32_t *flag, uint8_t *done) {
     if (obs_cur) ao_obs(p, s, obs_cur);
     double force = (double)a;
     double xx[4] = {s[0], s[1], s[2], s[3]};
-    double K1[4], K2[4], K3[4], K4[4], tmp[4], d[4];
-    double dt = p->dt;
-    ao_ode(p, force, xx, d); /* rk44 :218-229, one step of dt */
-    for (int i = 0; i < 4; ++i) K1[i] = dt * d[i];
-    for (int i = 0; i < 4; ++i) tmp[i] = xx[i] + K1[i] / 2;
-    ao_ode(p, force, tmp, d);
-    for (int i = 0; i < 4; ++i) K2[i] = dt * d[i];
-    for (int i = 0; i < 4; ++i) tmp[i] = xx[i] + K2[i] / 2;
-    ao_ode(p, force, tmp, d);
-    for (int i = 0; i < 4; ++i) K3[i] = dt * d[i];
-    for (int i = 0; i < 4; ++i) tmp[i] = xx[i] + K3[i];
-    ao_ode(p, force, tmp, d);
-    for (int i = 0; i < 4; ++i) K4[i] = dt * d[i];
-    for (int i = 0; i < 4; ++i) xx[i] = xx[i] + (K1[i] + 2 * K2[i] + 2 * K3[i] + K4[i]) / 6;
-    double time = s[4] + dt;
+    double th0 = s[0];
+    double time = s[4];
+    if (p->variant == RLP_ANGLEONLY_ENV_FILE) { /* env file rk44 :231-244 */
+        double h = p->dt / (double)p->n_sub_div, tt = time + p->dt;
+        while (time < tt) {
+            ao_rk4(p, force, h, xx);
+            time += h;
+        }
+    } else { /* PPO2 copy rk44 :218-229, one step of dt */
+        ao_rk4(p, force, p->dt, xx);
+        time = s[4] + p->dt;
+    }
     s[0] = xx[0]; s[1] = xx[1]; s[2] = xx[2]; s[3] = xx[3]; s[4] = time;
     double th = s[0], dth = s[1];
     double eth = 0. - th;
     int f = 0;
     uint8_t term = 0;
-    if ((th > p->theta_max + deg2rad(1)) || th < -p->theta_max - deg2rad(1)) { f = 1; term = 1; }
-    if (time > p->time_max) { f = 3; term = 1; }
-    if (sqrt(eth * eth + dth * dth) < 1e-2) { f = 4; term = 1; }
+    int out = (th > p->theta_max + deg2rad(1)) || th < -p->theta_max - deg2rad(1);
     ao_obs(p, s, obs_next);
-    /* get_reward :170-195 (r3 in float32: np.float32 force) */
-    double r1 = -(th * th) * p->Q_theta;
-    double r2 = -(dth * dth) * p->Q_omega;
-    float r3f = -(a * a) * (float)p->R;
-    double r3 = (double)r3f;
-    double r4 = 0.;
-    if (f == 1) {
-        double n_ = (p->time_max - time) / p->dt;
-        r4 = n_ * (r1 + r2 + r3);
+    if (p->variant == RLP_ANGLEONLY_ENV_FILE) {
+        /* is_Terminal :144-166 (angle first, returns early; no success flag) */
+        if (out) f = 1;
+        else if (time > p->time_max) f = 3;
+        term = f != 0;
+        /* get_reward :168-208 */
+        double cur = ao_abs_deg(p, th0), nex = ao_abs_deg(p, th);
+        double r;
+        if (nex > cur) r = -2;
+        else if (nex == cur) r = 0;
+        else r = 2;
+        if (cur <= 0.5 && nex <= 0.5) r += 5;
+        if (f == 1) r -= 100;
+        else if (f == 3) r += 500;
+        *reward = r;
+    } else {
+        if (out) { f = 1; term = 1; }
+        if (time > p->time_max) { f = 3; term = 1; }
+        if (sqrt(eth * eth + dth * dth) < 1e-2) { f = 4; term = 1; }
+        /* get_reward :170-195 (r3 in float32: np.float32 force) */
+        double r1 = -(th * th) * p->Q_theta;
+        double r2 = -(dth * dth) * p->Q_omega;
+        float r3f = -(a * a) * (float)p->R;
+        double r3 = (double)r3f;
+        double r4 = 0.;
+        if (f == 1) {
+            double n_ = (p->time_max - time) / p->dt;
+            r4 = n_ * (r1 + r2 + r3);
+        }
+        *reward = r1 + r2 + r3 + r4;
     }
-    *reward = r1 + r2 + r3 + r4;
     *flag = f;
     *done = term;
 }

@@ -62,7 +62,11 @@ class CartPoleParams(C.Structure):
 class AngleOnlyParams(C.Structure):
     _fields_ = [(n, C.c_double) for n in (
         "theta_max", "static_gain", "norm_dtheta", "M", "m", "g", "ell", "kf", "fm", "dt",
-        "time_max", "reset_theta_lo", "reset_theta_hi", "Q_theta", "Q_omega", "R")]
+        "time_max", "reset_theta_lo", "reset_theta_hi", "Q_theta", "Q_omega", "R")] + [
+        ("variant", C.c_int32), ("n_sub_div", C.c_int32)]
+
+
+RLP_ANGLEONLY_PPO2_COPY, RLP_ANGLEONLY_ENV_FILE = 0, 1
 
 
 class SOIParams(C.Structure):
@@ -123,7 +127,10 @@ class MLPDesc(C.Structure):
 class RolloutCfg(C.Structure):
     _fields_ = [("T", C.c_int32), ("n", C.c_int32), ("seed", C.c_uint64), ("step0", C.c_uint64),
                 ("env_id0", C.c_uint64), ("success_rule", C.c_int32), ("success_flag", C.c_int32),
-                ("std", C.c_float * 4), ("a_min", C.c_float * 4), ("a_max", C.c_float * 4)]
+                ("std", C.c_float * 4), ("a_min", C.c_float * 4), ("a_max", C.c_float * 4),
+                # per-call kernel selection (include/rlp.h): 0 = library default, else value + 1
+                ("mlp_precision", C.c_int32), ("physics", C.c_int32), ("sub", C.c_int32),
+                ("reserved", C.c_int32)]
 
 
 class RolloutBufs(C.Structure):
@@ -196,18 +203,25 @@ def cartpole_params(variant="ppo2"):
     return p
 
 
-def angleonly_params():
-    """demonstration/PPO2/PPO2-4-CartPoleAngleOnly/cartpole_angleonly.py:27-41, :174-176."""
+def angleonly_params(variant="ppo2"):
+    """variant 'ppo2' (== 'dppo2'): demonstration/PPO2/PPO2-4-CartPoleAngleOnly/
+    cartpole_angleonly.py:27-41, :174-176; 'env': environment/CartPole/CartPoleAngleOnly.py:16-70
+    (dt 0.01 in 10 sub-steps, fm 8, timeMax 6, the angle-increment reward; include/rlp.h)."""
     p = AngleOnlyParams()
     p.theta_max = deg2rad(45)
     p.static_gain = 2.0
     p.norm_dtheta = 4
     p.M, p.m, p.g, p.ell, p.kf = 1.0, 0.1, 9.8, 0.2, 0.2
-    p.fm = 5
-    p.dt = 0.02
-    p.time_max = 5
     p.reset_theta_lo, p.reset_theta_hi = -p.theta_max * 0.5, p.theta_max * 0.5
     p.Q_theta, p.Q_omega, p.R = 10, 0.0, 0.00
+    if variant == "env":
+        p.fm, p.dt, p.time_max = 8, 0.01, 6
+        p.variant, p.n_sub_div = RLP_ANGLEONLY_ENV_FILE, 10
+    elif variant in ("ppo2", "dppo2"):
+        p.fm, p.dt, p.time_max = 5, 0.02, 5
+        p.variant, p.n_sub_div = RLP_ANGLEONLY_PPO2_COPY, 1
+    else:
+        raise ValueError(f"angleonly_params: variant {variant!r} (ppo2 | dppo2 | env)")
     return p
 
 
@@ -325,7 +339,7 @@ def default_params(kind, variant=None):
     if kind == RLP_ENV_CARTPOLE:
         return cartpole_params(variant or "ppo2")
     if kind == RLP_ENV_CARTPOLE_ANGLEONLY:
-        return angleonly_params()
+        return angleonly_params(variant or "ppo2")
     if kind == RLP_ENV_SOI:
         return soi_params(variant or "env")
     if kind in (RLP_ENV_UGV_FORWARD, RLP_ENV_UGV_BIDIRECTIONAL):

@@ -48,6 +48,7 @@ def _declare(lib):
         "rlp_set_mlp_precision": (i32, [i32]),
         "rlp_get_mlp_precision": (i32, []),
         "rlp_reward_norm": (i32, [vp, i32, i32, vp, vp, vp, vp]),
+        "rlp_reward_norm_workspace": (i64, [i32, i32]),
         "rlp_gae": (i32, [vp, vp, vp, vp, vp, dbl, dbl, i32, i32, vp, vp, vp, vp]),
         "rlp_adv_normalize": (i32, [vp, i64, vp, vp]),
         "rlp_ppo2_workspace_floats": (i64, [vp, i64]),

@@ -207,7 +207,7 @@ class VecPPO2:
         self.adv = torch.empty((self.T, self.n), **f32)
         self.v_target = torch.empty((self.T, self.n), **f32)
         self.rms = torch.zeros(4, dtype=torch.float64, device=self.device)
-        self.work = torch.empty(3 * self.T, dtype=torch.float64, device=self.device)
+        self.work = K.reward_norm_workspace(self.T, self.n, self.device)
         self.stats = torch.zeros(2, dtype=torch.float64, device=self.device)
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(self.seed + 7919 * (self.env_id0 + 1))

@@ -166,7 +166,8 @@ template <> struct Env<RLP_ENV_CARTPOLE> {
 };
 
 // ==========================================================================================
-// CartPoleAngleOnly — demonstration/PPO2/PPO2-4-CartPoleAngleOnly/cartpole_angleonly.py
+// CartPoleAngleOnly — demonstration/PPO2/PPO2-4-CartPoleAngleOnly/cartpole_angleonly.py (variant
+// 0, == the DPPO2 copy) and environment/CartPole/CartPoleAngleOnly.py (variant 1), include/rlp.h
 // ==========================================================================================
 template <> struct Env<RLP_ENV_CARTPOLE_ANGLEONLY> {
     using P = rlp_angleonly_params;
@@ -189,43 +190,71 @@ template <> struct Env<RLP_ENV_CARTPOLE_ANGLEONLY> {
         o[0] = (float)((s[0] / p.theta_max) * p.static_gain);  // :137-143
         o[1] = (float)((s[1] / p.norm_dtheta) * p.static_gain);
     }
+    // one classic RK4 step of h (running-sum average, bit-identical, see CartPole)
+    __device__ static __forceinline__ void rk4(const P &p, double force, double h, double xx[4]) {
+        double sum[4], tmp[4], d[4];
+        ode(p, force, xx, d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = k; tmp[i] = xx[i] + k / 2; }
+        ode(p, force, tmp, d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k / 2; }
+        ode(p, force, tmp, d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k; }
+        ode(p, force, tmp, d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xx[i] = xx[i] + div6(sum[i] + h * d[i]);
+    }
+    __device__ static __forceinline__ double abs_deg(const P &p, double th) {
+        // |rad2deg(state[0] / staticGain * thetaMax)| of the obs array (env file :187-188)
+        const double o = th / p.theta_max * p.static_gain;
+        return fabs(o / p.static_gain * p.theta_max * 180. / kPi);
+    }
     __device__ static __forceinline__ void step(const P &p, double *s, const float *a, float *on,
                                                 double &reward, int &flag, bool &done) {
         const float af = a[0];
         const double force = (double)af, dt = p.dt;
+        const double th0 = s[0];
         double xx[4] = {s[0], s[1], s[2], s[3]};
-        double sum[4], tmp[4], d[4];  // running RK4 sum (bit-identical, see CartPole)
-        ode(p, force, xx, d);  // rk44 :218-229 (one RK4 step of dt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { const double k = dt * d[i]; sum[i] = k; tmp[i] = xx[i] + k / 2; }
-        ode(p, force, tmp, d);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k / 2; }
-        ode(p, force, tmp, d);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k; }
-        ode(p, force, tmp, d);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            xx[i] = xx[i] + div6(sum[i] + dt * d[i]);
+        double time = s[4];
+        if (p.variant == RLP_ANGLEONLY_ENV_FILE) {   // rk44 :231-244: fp64 `while time < tt`
+            const double h = dt / (double)p.n_sub_div, tt = time + dt;
+            while (time < tt) {
+                rk4(p, force, h, xx);
+                time += h;
+            }
+        } else {                                      // rk44 :218-229: one step of dt
+            rk4(p, force, dt, xx);
+            time = time + dt;
         }
-        const double time = s[4] + dt;
         s[0] = xx[0]; s[1] = xx[1]; s[2] = xx[2]; s[3] = xx[3]; s[4] = time;
         const double th = xx[0], dth = xx[1], eth = 0. - th;
-        int f = 0;  // is_Terminal :150-168
-        if ((th > p.theta_max + deg2rad(1)) || th < -p.theta_max - deg2rad(1)) f = 1;
-        if (time > p.time_max) f = 3;
-        if (sqrt(eth * eth + dth * dth) < 1e-2) f = 4;
+        const bool out = (th > p.theta_max + deg2rad(1)) || th < -p.theta_max - deg2rad(1);
         observe(p, s, on);
-        const double r1 = -(th * th) * p.Q_theta;  // get_reward :170-195
-        const double r2 = -(dth * dth) * p.Q_omega;
-        const double r3 = (double)(-(af * af) * (float)p.R);
-        double r4 = 0.;
-        if (f == 1) {
-            const double n_ = (p.time_max - time) / p.dt;
-            r4 = n_ * (r1 + r2 + r3);
+        int f = 0;
+        if (p.variant == RLP_ANGLEONLY_ENV_FILE) {
+            f = out ? 1 : (time > p.time_max ? 3 : 0);     // is_Terminal :144-166 (returns early)
+            const double cur = abs_deg(p, th0), nex = abs_deg(p, th);   // get_reward :168-208
+            double r = nex > cur ? -2. : (nex == cur ? 0. : 2.);
+            if (cur <= 0.5 && nex <= 0.5) r += 5.;
+            if (f == 1) r -= 100.;
+            else if (f == 3) r += 500.;
+            reward = r;
+        } else {
+            if (out) f = 1;  // is_Terminal :150-168 (later checks override)
+            if (time > p.time_max) f = 3;
+            if (sqrt(eth * eth + dth * dth) < 1e-2) f = 4;
+            const double r1 = -(th * th) * p.Q_theta;  // get_reward :170-195
+            const double r2 = -(dth * dth) * p.Q_omega;
+            const double r3 = (double)(-(af * af) * (float)p.R);
+            double r4 = 0.;
+            if (f == 1) {
+                const double n_ = (p.time_max - time) / p.dt;
+                r4 = n_ * (r1 + r2 + r3);
+            }
+            reward = r1 + r2 + r3 + r4;
         }
-        reward = r1 + r2 + r3 + r4;
         flag = f;
         done = f != 0;
     }

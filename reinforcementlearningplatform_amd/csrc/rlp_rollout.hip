@@ -488,13 +488,13 @@ template <int KIND, int H, int SUB, bool X3>
 static int launch_rollout(const void *params, double *state, uint8_t *need_reset,
                           const float *actor, const MfmaNet &an, const float *critic,
                           const MfmaNet &cn, const RolloutArgs &ra, const rlp_rollout_bufs &b,
-                          hipStream_t stream) {
+                          int physics, hipStream_t stream) {
     const auto &p = *static_cast<const typename Env<KIND>::P *>(params);
     constexpr int threads = rollout_block<SUB, X3>();
     constexpr int envs_per_block = threads / 64 * 16 * SUB;
     const int blocks = (ra.n + envs_per_block - 1) / envs_per_block;
     if constexpr (X3 && SUB == 1 && rollout_sp_ring<KIND, 1, 8>() != 0) {
-        if (g_rollout_shared_physics == 2) {  // 8-wave blocks, 16 envs per wave
+        if (physics == 2) {  // 8-wave blocks, 16 envs per wave
             const int blocks8 = (ra.n + 127) / 128;
             rollout_sp_kernel<KIND, H, 1, 8><<<blocks8, 512, 0, stream>>>(p, state, need_reset, actor,
                                                                          an, critic, cn, ra, b);
@@ -503,7 +503,7 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
         }
     }
     if constexpr (X3 && rollout_sp_fits<KIND, SUB>()) {
-        if (g_rollout_shared_physics)
+        if (physics)
             rollout_sp_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor,
                                                                           an, critic, cn, ra, b);
         else
@@ -521,7 +521,7 @@ template <int KIND>
 static int rollout_kind(const void *params, double *state, uint8_t *need_reset, const float *actor,
                         const MfmaNet &an, const float *critic, const MfmaNet &cn,
                         const RolloutArgs &ra, const rlp_rollout_bufs &b, int sub, int prec,
-                        hipStream_t stream) {
+                        int physics, hipStream_t stream) {
     using E = Env<KIND>;
     if (an.S != E::S || cn.S != E::S || an.A != E::A || cn.A != 1)
         return fail(RLP_EINVAL, "rlp_rollout: net dims (S=%d,A=%d / S=%d,A=%d) != env (S=%d,A=%d)",
@@ -529,7 +529,7 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
     if (an.H != 256 || cn.H != 256)
         return fail(RLP_EUNSUPPORTED, "rlp_rollout: hidden width %d/%d (built for 256)", an.H, cn.H);
     if (prec == RLP_MLP_F16X3) {
-        if (g_rollout_shared_physics == 2) sub = 1;  // the 8-wave variant runs 16-env waves
+        if (physics == 2) sub = 1;  // the 8-wave variant runs 16-env waves
         if (sub == 0) {  // auto: 32-env waves unless that leaves fewer than 2 blocks per CU
             static int cus = 0;
             if (cus == 0) {
@@ -543,18 +543,18 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
         }
         if (sub == 1)
             return launch_rollout<KIND, 256, 1, true>(params, state, need_reset, actor, an, critic,
-                                                      cn, ra, b, stream);
+                                                      cn, ra, b, physics, stream);
         if (sub == 4)
             return launch_rollout<KIND, 256, 4, true>(params, state, need_reset, actor, an, critic,
-                                                      cn, ra, b, stream);
+                                                      cn, ra, b, physics, stream);
         return launch_rollout<KIND, 256, 2, true>(params, state, need_reset, actor, an, critic, cn,
-                                                  ra, b, stream);
+                                                  ra, b, physics, stream);
     }
     if (sub <= 2)
         return launch_rollout<KIND, 256, 2, false>(params, state, need_reset, actor, an, critic, cn,
-                                                   ra, b, stream);
+                                                   ra, b, physics, stream);
     return launch_rollout<KIND, 256, 4, false>(params, state, need_reset, actor, an, critic, cn, ra,
-                                               b, stream);
+                                               b, physics, stream);
 }
 
 static int g_rollout_sub = 0;  // 0: auto
@@ -643,27 +643,35 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
         ra.gain[a] = cfg->a_max[a] - ra.off[a];              //                   a_max - off
     }
     hipStream_t s = as_stream(stream);
-    const int sub = g_rollout_sub, prec = g_mlp_precision;
+    // per-call selections (cfg, 0 = the library-wide default of the rlp_set_* knobs)
+    RLP_REQUIRE(cfg->mlp_precision >= 0 && cfg->mlp_precision <= 2 && cfg->physics >= 0 &&
+                    cfg->physics <= 3 && (cfg->sub == 0 || cfg->sub == 1 || cfg->sub == 2 ||
+                                          cfg->sub == 4),
+                "rlp_rollout: cfg mlp_precision=%d physics=%d sub=%d", cfg->mlp_precision,
+                cfg->physics, cfg->sub);
+    const int sub = cfg->sub ? cfg->sub : g_rollout_sub;
+    const int prec = cfg->mlp_precision ? cfg->mlp_precision - 1 : g_mlp_precision;
+    const int physics = cfg->physics ? cfg->physics - 1 : g_rollout_shared_physics;
     switch (kind) {
     case RLP_ENV_CARTPOLE:
         return rollout_kind<RLP_ENV_CARTPOLE>(env_params, state, need_reset, actor_packed, an,
-                                              critic_packed, cn, ra, b, sub, prec, s);
+                                              critic_packed, cn, ra, b, sub, prec, physics, s);
     case RLP_ENV_CARTPOLE_ANGLEONLY:
         return rollout_kind<RLP_ENV_CARTPOLE_ANGLEONLY>(env_params, state, need_reset, actor_packed,
-                                                        an, critic_packed, cn, ra, b, sub, prec, s);
+                                                        an, critic_packed, cn, ra, b, sub, prec, physics, s);
     case RLP_ENV_SOI:
         return rollout_kind<RLP_ENV_SOI>(env_params, state, need_reset, actor_packed, an,
-                                         critic_packed, cn, ra, b, sub, prec, s);
+                                         critic_packed, cn, ra, b, sub, prec, physics, s);
     case RLP_ENV_UGV_FORWARD:
         return rollout_kind<RLP_ENV_UGV_FORWARD>(env_params, state, need_reset, actor_packed, an,
-                                                 critic_packed, cn, ra, b, sub, prec, s);
+                                                 critic_packed, cn, ra, b, sub, prec, physics, s);
     case RLP_ENV_UGV_BIDIRECTIONAL:
         return rollout_kind<RLP_ENV_UGV_BIDIRECTIONAL>(env_params, state, need_reset, actor_packed,
-                                                       an, critic_packed, cn, ra, b, sub, prec, s);
+                                                       an, critic_packed, cn, ra, b, sub, prec, physics, s);
     case RLP_ENV_UAV_HOVER_OUTER_LOOP:
         return rollout_kind<RLP_ENV_UAV_HOVER_OUTER_LOOP>(env_params, state, need_reset,
                                                           actor_packed, an, critic_packed, cn, ra,
-                                                          b, sub, prec, s);
+                                                          b, sub, prec, physics, s);
     }
     return fail(RLP_EINVAL, "rlp_rollout: unknown env kind %d", kind);
 }

@@ -151,8 +151,15 @@ def rollout(kind, params, state, need_reset, actor_desc, actor_packed, critic_de
                             C.byref(cfg), C.byref(cb), stream_ptr()), "rlp_rollout")
 
 
-def make_rollout_cfg(T, n, seed, step0, env_id0, std, a_min, a_max, success_rule, success_flag):
+def make_rollout_cfg(T, n, seed, step0, env_id0, std, a_min, a_max, success_rule, success_flag,
+                     mlp_precision=None, physics=None, sub=None):
+    """rlp_rollout_cfg. mlp_precision (RLP_MLP_FP32 | RLP_MLP_F16X3), physics (0 register-resident,
+    1 shared, 2 shared 8-wave) and sub (1 | 2 | 4) select the kernel for this call only; None
+    keeps the library-wide defaults (rlp_set_*)."""
     cfg = _abi.RolloutCfg()
+    cfg.mlp_precision = 0 if mlp_precision is None else int(mlp_precision) + 1
+    cfg.physics = 0 if physics is None else int(physics) + 1
+    cfg.sub = 0 if sub is None else int(sub)
     cfg.T, cfg.n, cfg.seed, cfg.step0, cfg.env_id0 = T, n, seed, step0, env_id0
     cfg.success_rule, cfg.success_flag = success_rule, success_flag
     A = len(a_min)
@@ -164,10 +171,16 @@ def make_rollout_cfg(T, n, seed, step0, env_id0, std, a_min, a_max, success_rule
     return cfg
 
 
+def reward_norm_workspace(T, n, device=None):
+    cnt = lib().rlp_reward_norm_workspace(int(T), int(n))
+    check(cnt if cnt < 0 else 0, "rlp_reward_norm_workspace")
+    return torch.empty(int(cnt), dtype=torch.float64, device=_dev(device))
+
+
 def reward_norm(reward, rms, work=None, out=None):
     """reward [T][n] f32 -> normalised (in `out`, may alias); rms: f64[4] device running stats."""
     T, n = reward.shape
-    work = work if work is not None else torch.empty(3 * T, dtype=torch.float64, device=reward.device)
+    work = work if work is not None else reward_norm_workspace(T, n, reward.device)
     out = out if out is not None else torch.empty_like(reward)
     check(lib().rlp_reward_norm(ptr(reward), T, n, ptr(rms), ptr(work), ptr(out), stream_ptr()),
           "rlp_reward_norm")

@@ -77,6 +77,7 @@ with quiet():
     mods["cp_dppo2"] = load("demonstration/DPPO2/DPPO2-4-CartPole/CartPole.py", "ref_cp_dppo2")
     mods["ao_ppo2"] = load("demonstration/PPO2/PPO2-4-CartPoleAngleOnly/cartpole_angleonly.py",
                            "ref_ao_ppo2")
+    mods["ao_env"] = load("environment/CartPole/CartPoleAngleOnly.py", "ref_ao_env")
     mods["soi_env"] = load("environment/SecondOrderIntegration/SecondOrderIntegration.py", "ref_soi")
     mods["soi_dppo2"] = load("demonstration/DPPO2/DPPO2-4-SecondOrderIntegration/"
                              "SecondOrderIntegration.py", "ref_soi_dppo2")
@@ -204,6 +205,56 @@ def gen_angleonly(key, mod, n=400):
     out["action"] = out["action"].astype(np.float32)
     np.savez(os.path.join(OUT, f"{key}.npz"), **out)
     print(key, "flags", np.bincount(out["flag"]))
+
+
+def gen_angleonly_env(key="angleonly_env", n=500):
+    """environment/CartPole/CartPoleAngleOnly.py: dt 0.01 in `while time < tt` sub-steps of
+    dt/10 (10 or 11 by step index: the time table comes from the env's own rk44), flag 1 before
+    flag 3, the angle-increment reward (incl. the `==` branch: an env at rest stays put)."""
+    g = np.random.default_rng(20263)
+    mod = mods["ao_env"]
+    env = mod.CartPoleAngleOnly(0.)
+    env.reset(False)
+    tt = []
+    for _ in range(606):
+        tt.append(env.time)
+        env.rk44(np.array([np.float32(0.)]))
+    rows = {k: [] for k in ("state", "action", "state_next", "obs_cur", "obs_next", "reward",
+                            "flag", "done")}
+    th_hi = env.thetaMax + np.pi / 180
+    for i in range(n):
+        k = int(g.integers(0, 606))
+        th, dth = g.uniform(-0.85, 0.85), g.uniform(-4, 4)
+        x, dx = g.uniform(-2, 2), g.uniform(-2, 2)
+        a = np.float32(g.uniform(-8, 8))
+        j = i % 8
+        if j == 1:    # angle bound straddled
+            th = np.sign(g.uniform(-1, 1)) * (th_hi + g.uniform(-2e-3, 2e-3)); dth = g.uniform(-0.05, 0.05)
+        elif j == 2:  # time-out regime
+            k = int(g.integers(596, 606))
+        elif j == 3:  # angle out AND time out: flag 1 wins here
+            k = int(g.integers(598, 606)); th = np.sign(g.uniform(-1, 1)) * (th_hi + 0.05)
+        elif j == 4:  # inside 0.5 deg
+            th, dth = g.uniform(-0.008, 0.008), g.uniform(-0.02, 0.02)
+        elif j == 5:  # at rest: theta unchanged, the `==` branch
+            th, dth, x, dx, a = 0., 0., g.uniform(-1, 1), 0., np.float32(0.)
+        with quiet():
+            env.reset(False)
+            env.theta, env.dtheta, env.x, env.dx, env.time = th, dth, x, dx, tt[k]
+            rows["state"].append([th, dth, x, dx, tt[k]])
+            env.step_update(np.array([a], dtype=np.float32))
+        rows["action"].append([a])
+        rows["state_next"].append([env.theta, env.dtheta, env.x, env.dx, env.time])
+        rows["obs_cur"].append(env.current_state)
+        rows["obs_next"].append(env.next_state)
+        rows["reward"].append(float(env.reward))
+        rows["flag"].append(env.terminal_flag)
+        rows["done"].append(int(env.is_terminal))
+    out = {k: np.array(v) for k, v in rows.items()}
+    out["action"] = out["action"].astype(np.float32)
+    out["time_table"] = np.array(tt)
+    np.savez(os.path.join(OUT, f"{key}.npz"), **out)
+    print(key, "flags", np.bincount(out["flag"]), "rewards", np.unique(out["reward"]))
 
 
 def gen_soi(key, mod, n=400):
@@ -998,6 +1049,7 @@ if __name__ == "__main__":
     gen_cartpole("cartpole_ppo2", mods["cp_ppo2"])
     gen_cartpole("cartpole_dppo2", mods["cp_dppo2"], n=100)
     gen_angleonly("angleonly_ppo2", mods["ao_ppo2"])
+    gen_angleonly_env()
     gen_soi("soi_env", mods["soi_env"])
     gen_soi("soi_dppo2", mods["soi_dppo2"], n=200)
     gen_ugv("ugvf_env", mods["ugvf_env"].UGVForward)

@@ -44,7 +44,8 @@ def shipped_actor_critic(golden, std=8 / 3):
 
 @pytest.mark.parametrize("cls,kind,golden_name", [
     (CartPole, A.RLP_ENV_CARTPOLE, "cartpole_ppo2"),
-    (CartPoleAngleOnly, A.RLP_ENV_CARTPOLE_ANGLEONLY, "angleonly_ppo2"),
+    (lambda: CartPoleAngleOnly(variant="ppo2"), A.RLP_ENV_CARTPOLE_ANGLEONLY, "angleonly_ppo2"),
+    (CartPoleAngleOnly, A.RLP_ENV_CARTPOLE_ANGLEONLY, "angleonly_env"),
     (SecondOrderIntegration, A.RLP_ENV_SOI, "soi_env"),
     (UGVForward, A.RLP_ENV_UGV_FORWARD, "ugvf_env"),
     (uav_hover_outer_loop, A.RLP_ENV_UAV_HOVER_OUTER_LOOP, "uav_hover")])

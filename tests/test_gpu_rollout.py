@@ -42,32 +42,6 @@ def nets(S, Ad, seed, H=256):
     return ad, init(ad, 1.0), cd, init(cd, 1.0)
 
 
-def run_both(kind, n, T, seed=3407, sub=None, params=None, success=None):
-    D, S, Ad = A.ENV_DIMS[kind]
-    p = params or A.default_params(kind)
-    ad, ap, cd, cp = nets(S, Ad, seed=kind)
-    lo, hi = A.action_bounds(kind, p)
-    std = [(h - l) / 6 for l, h in zip(lo, hi)]
-    rule, F = success or (A.RLP_SUCCESS_DONE_AND_FLAG_NE, A.timeout_flag(kind))
-    cfg = K.make_rollout_cfg(T, n, seed, 1000, 0, std, lo, hi, rule, F)
-    # GPU
-    if sub:
-        _native.set_rollout_sub(sub)
-    st = K.new_state(kind, n)
-    need = torch.ones(n, dtype=torch.uint8, device="cuda")
-    bufs = K.rollout_buffers(kind, T, n)
-    apk, cpk = K.mfma_pack(ad, dev(ap)), K.mfma_pack(cd, dev(cp))
-    K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs)
-    torch.cuda.synchronize()
-    if sub:
-        _native.set_rollout_sub(0)
-    # oracle
-    ost = np.zeros((D, n))
-    oneed = np.ones(n, np.uint8)
-    ob = oracle.rollout(kind, p, ost, oneed, ad, ap, cd, cp, cfg)
-    return {k: host(v) for k, v in bufs.items()}, ob, host(st), ost, host(need), oneed, (ad, ap, cd, cp)
-
-
 def test_rollout_rejects_lidar_env():
     """The 41-input lidar env is outside the fused kernel's net shapes: a clean error, no launch."""
     kind = A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE
@@ -122,21 +96,17 @@ def test_shared_physics_kernel_equals_register_kernel(kind):
     lo, hi = A.action_bounds(kind, p)
     std = [(h - l) / 3 for l, h in zip(lo, hi)]
     n, T = 16384 + 37, 96
-    cfg = K.make_rollout_cfg(T, n, 99, 5, 0, std, lo, hi, A.RLP_SUCCESS_DONE_AND_FLAG_NE,
-                             A.timeout_flag(kind))
     apk, cpk = K.mfma_pack(ad, dev(ap)), K.mfma_pack(cd, dev(cp))
     runs = []
-    try:
-        for phys in (1, 0, 2):
-            _native.set_rollout_physics(phys)
-            st = K.new_state(kind, n)
-            need = torch.ones(n, dtype=torch.uint8, device="cuda")
-            bufs = K.rollout_buffers(kind, T, n)
-            for seg in range(2):  # a second segment starts from the first's state / need_reset
-                K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs)
-            runs.append(({k: v.clone() for k, v in bufs.items()}, st.clone(), need.clone()))
-    finally:
-        _native.set_rollout_physics(1)
+    for phys in (1, 0, 2):   # per-call selection (rlp_rollout_cfg.physics)
+        cfg = K.make_rollout_cfg(T, n, 99, 5, 0, std, lo, hi, A.RLP_SUCCESS_DONE_AND_FLAG_NE,
+                                 A.timeout_flag(kind), physics=phys)
+        st = K.new_state(kind, n)
+        need = torch.ones(n, dtype=torch.uint8, device="cuda")
+        bufs = K.rollout_buffers(kind, T, n)
+        for seg in range(2):  # a second segment starts from the first's state / need_reset
+            K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs)
+        runs.append(({k: v.clone() for k, v in bufs.items()}, st.clone(), need.clone()))
     (b1, s1, n1), (b0, s0, n0), (b2, s2, n2) = runs
     assert b1["done"][:-1].any(), "no env terminated inside the segment"
     for bx, sx, nx in ((b0, s0, n0), (b2, s2, n2)):  # register kernel; 8-wave shared kernel
@@ -205,25 +175,50 @@ def test_mlp_precision_modes_vs_float64(kind):
     lo, hi = A.action_bounds(kind, p)
     std = [(h - l) / 6 for l, h in zip(lo, hi)]
     n, T = 8192, 8
-    cfg = K.make_rollout_cfg(T, n, 11, 0, 0, std, lo, hi, A.RLP_SUCCESS_DONE_AND_FLAG_NE,
-                             A.timeout_flag(kind))
     apk, cpk = K.mfma_pack(ad, dev(ap)), K.mfma_pack(cd, dev(cp))
     errs = {}
-    old = _native.get_mlp_precision()
-    try:
-        for mode in (_native.MLP_FP32, _native.MLP_F16X3):
-            _native.set_mlp_precision(mode)
-            st = K.new_state(kind, n)
-            need = torch.ones(n, dtype=torch.uint8, device="cuda")
-            bufs = K.rollout_buffers(kind, T, n)
-            K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs)
-            obs = host(bufs["obs"]).reshape(-1, S)
-            v64 = oracle.mlp_forward(cd, cp, obs)[:, 0]
-            v = host(bufs["value"]).reshape(-1).astype(np.float64)
-            errs[mode] = np.abs(v - v64) / (np.abs(v64) + 1.0)
-    finally:
-        _native.set_mlp_precision(old)
+    for mode in (_native.MLP_FP32, _native.MLP_F16X3):   # per call (rlp_rollout_cfg)
+        cfg = K.make_rollout_cfg(T, n, 11, 0, 0, std, lo, hi, A.RLP_SUCCESS_DONE_AND_FLAG_NE,
+                                 A.timeout_flag(kind), mlp_precision=mode)
+        st = K.new_state(kind, n)
+        need = torch.ones(n, dtype=torch.uint8, device="cuda")
+        bufs = K.rollout_buffers(kind, T, n)
+        K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs)
+        obs = host(bufs["obs"]).reshape(-1, S)
+        v64 = oracle.mlp_forward(cd, cp, obs)[:, 0]
+        v = host(bufs["value"]).reshape(-1).astype(np.float64)
+        errs[mode] = np.abs(v - v64) / (np.abs(v64) + 1.0)
     e32, ex3 = errs[_native.MLP_FP32], errs[_native.MLP_F16X3]
     assert e32.max() < 1e-5 and ex3.max() < 1e-5
     assert ex3.max() <= 4 * e32.max() + 1e-7, (ex3.max(), e32.max())
     assert ex3.mean() <= 4 * e32.mean() + 1e-8, (ex3.mean(), e32.mean())
+
+
+def test_per_call_selection_overrides_library_default():
+    """rlp_rollout_cfg's mlp_precision / physics / sub apply to that call only, whatever the
+    library-wide rlp_set_* defaults are (a multi-threaded host needs no global knob)."""
+    kind = A.RLP_ENV_CARTPOLE
+    p = A.cartpole_params()
+    ad, ap, cd, cp = nets(4, 1, seed=2)
+    apk, cpk = K.mfma_pack(ad, dev(ap)), K.mfma_pack(cd, dev(cp))
+    n, T = 4096, 16
+
+    def run(**sel):
+        cfg = K.make_rollout_cfg(T, n, 3, 0, 0, [8 / 3], [-8], [8], A.RLP_SUCCESS_DONE_AND_FLAG_NE, 3,
+                                 **sel)
+        st = K.new_state(kind, n)
+        need = torch.ones(n, dtype=torch.uint8, device="cuda")
+        bufs = K.rollout_buffers(kind, T, n)
+        K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs)
+        return bufs["value"].clone()
+    v32 = run(mlp_precision=_native.MLP_FP32)
+    vx3 = run(mlp_precision=_native.MLP_F16X3)
+    assert not torch.equal(v32, vx3)
+    old = _native.get_mlp_precision()
+    try:
+        _native.set_mlp_precision(_native.MLP_FP32)
+        assert torch.equal(run(mlp_precision=_native.MLP_F16X3), vx3)
+        assert torch.equal(run(), v32)
+    finally:
+        _native.set_mlp_precision(old)
+    assert torch.equal(run(mlp_precision=_native.MLP_F16X3, physics=0, sub=4), vx3)

@@ -36,7 +36,7 @@ def _replay(g, key, learner):
         env = CartPole(0., 0.)
         over = {}
     else:
-        env = CartPoleAngleOnly(0.)
+        env = CartPoleAngleOnly(0., variant="ppo2")
         over = {'use_grad_clip': True, 'use_lr_decay': True}
     ar = np.array(env.action_range)
     actor = PPOActor_Gaussian(env.state_dim, env.action_dim, ar[:, 0], ar[:, 1],
