@@ -133,12 +133,8 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
             for (int i = 0; i < 8; i += 2) {
                 const float2v pre = i < 4 ? (float2v){hp0[sb][i], hp0[sb][i + 1]}
                                           : (float2v){hp1[sb][i - 4], hp1[sb][i - 3]};
-#if RLP_EXPERIMENT == 4  // timing experiment only: no hidden tanh
-                const float2v x = pre * kX3HScale;
-#else
                 // 2^SH tanh(pre), bit-identical to kX3HScale * tanh_fast(pre)
                 const float2v x = tanh2_scaled(pre, 2.8853900817779268f, kX3HScale);
-#endif
                 half2v hi, lo;
                 split2(x, hi, lo);
                 bh[sb][i] = hi.x;
@@ -153,41 +149,29 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             const int c = 2 * P + hf;
-#if RLP_EXPERIMENT < 7  // 7, 8: timing experiments only, no DMA waits (8: no DMA at all)
             if (RG == 3 && c + 1 < NC) {  // own part of c landed (c + 1's NPW pieces may not)
                 if constexpr (NPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                 else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
             } else {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-#endif
-#if RLP_EXPERIMENT != 5 && RLP_EXPERIMENT < 7  // 5: no block barriers (chunks may be stale)
             block_barrier_raw();  // all parts of c landed; everyone is done with chunk c - 1
-#endif
-#if RLP_EXPERIMENT != 8
             if (c + RG - 1 < NC) issue(c + RG - 1);  // into chunk c - 1's slot
-#endif
             const float *slot = ring + (c % RG) * kX3ChunkFloats + lane * 4;
             // fragments one output tile ahead: tile jj + 1's two reads are issued before tile
             // jj's MFMAs, so an LDS round trip is not exposed per tile (the default schedule
             // reads each pair right before its MFMAs and waits for it)
-#if RLP_EXPERIMENT == 6  // timing experiment only: no fragment reads (B operands as A)
-            half8 ahn = bh[0], aln = bl[0];
-#else
             half8 ahn = *reinterpret_cast<const half8 *>(slot);
             half8 aln = *reinterpret_cast<const half8 *>(slot + 256);
-#endif
             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
                 const half8 ah = ahn, al = aln;
-#if RLP_EXPERIMENT != 6
                 if (jj + 1 < 8) {
                     ahn = *reinterpret_cast<const half8 *>(slot + (2 * jj + 2) * 256);
                     aln = *reinterpret_cast<const half8 *>(slot + (2 * jj + 3) * 256);
                     __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
                 }
-#endif
 #pragma unroll
                 for (int sb = 0; sb < SUB; ++sb) {
                     floatx4 a = acc[sb][8 * hf + jj];
@@ -219,11 +203,7 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
         for (int sb = 0; sb < SUB; ++sb)
 #pragma unroll
             for (int r = 0; r < 4; r += 2) {
-#if RLP_EXPERIMENT == 3  // timing experiment only: no output-layer tanh
-                const float2v h = (float2v){acc[sb][j][r], acc[sb][j][r + 1]} * k_out;
-#else
                 const float2v h = tanh2_scaled((float2v){acc[sb][j][r], acc[sb][j][r + 1]}, k_out, 1.0f);
-#endif
 #pragma unroll
                 for (int a = 0; a < NOUT; ++a)
                     part[sb][a] = __builtin_elementwise_fma((float2v){w3[a][r], w3[a][r + 1]}, h,

@@ -13,10 +13,6 @@
 #include "rlp_mfma_layout.hpp"
 #include "rlp_mfma_x3.hpp"
 
-#ifndef RLP_EXPERIMENT
-#define RLP_EXPERIMENT 0
-#endif
-
 namespace rlp {
 
 // Each wave stages only its own envs' observations in LDS, so a wave-level fence suffices; no
@@ -106,9 +102,6 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
 #pragma unroll 1
         for (int which = 0; which < 2; ++which) {
             float out[SUB][A];
-#if RLP_EXPERIMENT == 1  // timing experiment only: MLP skipped
-            for (int sb = 0; sb < SUB; ++sb) for (int a = 0; a < A; ++a) out[sb][a] = bobs[sb][0] * 0.5f;
-#else
             if constexpr (X3)
                 mlp_x3_forward<H, SUB, KS1, A>(which ? critic : actor, which ? small_c : small_a,
                                                ring, which ? cn : an, which ? 1 : A, bobs, out);
@@ -116,7 +109,6 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
                 mlp_fused_forward<H, SUB, KS1, A, RING>(which ? critic : actor,
                                                         which ? small_c : small_a, ring,
                                                         which ? cn : an, which ? 1 : A, bobs, out);
-#endif
             // the physics lane (sub-block g, env e) owns out[g]
             float sel[A];
 #pragma unroll
@@ -149,11 +141,7 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
             double r;
             int f;
             bool dn;
-#if RLP_EXPERIMENT == 2  // timing experiment only: env dynamics skipped
-            s[0] += 1e-3 * act[0]; E::observe(p, s, on); r = s[0]; f = 0; dn = false;
-#else
             E::step(p, s, act, on, r, f, dn);
-#endif
 #pragma unroll
             for (int j = 0; j < S; ++j) {
                 b.obs[k * S + j] = o[j];
@@ -296,12 +284,8 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
 #pragma unroll 1
         for (int which = both ? 0 : 1; which < 2; ++which) {
             float out[SUB][A];
-#if RLP_EXPERIMENT == 1  // timing experiment only: MLP skipped
-            for (int sb = 0; sb < SUB; ++sb) for (int a = 0; a < A; ++a) out[sb][a] = bobs[sb][0] * 0.5f;
-#else
             mlp_x3_forward<H, SUB, KS1, A, RG, W>(which ? critic : actor, which ? small_c : small_a,
                                                   ring, which ? cn : an, which ? 1 : A, bobs, out);
-#endif
             // lane (sub-block g, env e) owns out[g]
             float sel[A];
 #pragma unroll
@@ -353,11 +337,7 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
                 double r;
                 int f;
                 bool dn;
-#if RLP_EXPERIMENT == 2  // timing experiment only: env dynamics skipped
-                s[0] += 1e-3 * act[0]; E::observe(p, s, on); r = s[0]; f = 0; dn = false;
-#else
                 E::step(p, s, act, on, r, f, dn);
-#endif
 #pragma unroll
                 for (int j = 0; j < S; ++j) {
                     b.obs[k * S + j] = o[j];
