@@ -1,5 +1,5 @@
 #!/bin/bash
-# Timing A/B builds (load one with RLP_LIB=<path> python bench.py ...): librlp.so from the csrc sources in SRC_DIR (default:
+# Timing A/B builds (load one with RLP_LIBRARY=<path> python bench.py ...): librlp.so from the csrc sources in SRC_DIR (default:
 # this tree's) with extra hipcc flags, into csrc/build/exp<X>/librlp.so.
 #   scripts/build_variant.sh X [SRC_DIR] [hipcc flags...]
 set -euo pipefail
