@@ -253,7 +253,7 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
     // state -> LDS; the first step's resets and observations (threads 0..EB-1, one env each)
     for (int i = threadIdx.x; i < D * EB; i += blockDim.x) {
         const int d = i / EB, le = i % EB;
-        st[d][le] = base + le < n ? state[(size_t)d * n + base + le] : 0.0;
+        st[d][le] = base + le < n ? state[d * n + base + le] : 0.0;
     }
     __syncthreads();
     if (threadIdx.x < EB) {
@@ -315,7 +315,7 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
             const int le = 64 * (wave % PW) + lane, env = base + le;
             if (env < n) {
                 const uint64_t eid = ra.env_id0 + (uint64_t)env;
-                const size_t k = (size_t)t * n + env;
+                const int k = t * n + env;  // 32-bit: T * n * 8 < 2^31 (rlp_rollout)
                 double s[D];
 #pragma unroll
                 for (int d = 0; d < D; ++d) s[d] = st[d][le];
@@ -376,9 +376,9 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
     if (threadIdx.x < EB) {
         const int le = threadIdx.x, env = base + le;
         if (env < n) {
-            if (!s_pdone[le]) b.value_next[(size_t)(ra.T - 1) * n + env] = mv[le][A];
+            if (!s_pdone[le]) b.value_next[(ra.T - 1) * n + env] = mv[le][A];
 #pragma unroll
-            for (int d = 0; d < D; ++d) state[(size_t)d * n + env] = st[d][le];
+            for (int d = 0; d < D; ++d) state[d * n + env] = st[d][le];
             need_reset[env] = s_need[le];
         }
     }
@@ -607,6 +607,9 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
                     b.done && b.success && b.flag,
                 "rlp_rollout: null buffer");
     RLP_REQUIRE(cfg->T >= 1 && cfg->n >= 0, "rlp_rollout: T=%d n=%d", cfg->T, cfg->n);
+    RLP_REQUIRE((int64_t)cfg->T * cfg->n * 8 <= 2147483647 && (int64_t)cfg->n * 32 <= 2147483647,
+                "rlp_rollout: T*n = %lld too large for one segment (32-bit buffer indices)",
+                (long long)cfg->T * cfg->n);
     if (cfg->n == 0) return RLP_OK;
     MfmaNet an, cn;
     if (!mfma_net_from_desc(*actor_desc, &an) || !mfma_net_from_desc(*critic_desc, &cn))
