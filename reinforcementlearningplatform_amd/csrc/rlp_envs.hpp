@@ -47,6 +47,27 @@ __device__ __forceinline__ void sincos_fast(double x, double *sp, double *cp) {
     *cp = ((q + 1) & 2) ? -c0 : c0;
 }
 
+// sin / cos of theta + d for an RK4 stage offset d (h * dtheta / 2 or h * dtheta) from sb, cb =
+// sin / cos theta: the angle-addition identities with d's sine and cos - 1 from their Taylor
+// series to d^11 / d^12 (truncation < 2e-19 for |d| <= 0.25, i.e. |dtheta| < 125 rad/s at CartPole's
+// h = 2 ms, and < 2e-14 at |d| = 0.5), the small corrections added last: within ~1 ulp of
+// sincos_fast(theta + d) at ~19 VALU ops instead of ~35.
+__device__ __forceinline__ void sincos_step(double sb, double cb, double d, double *sp, double *cp) {
+    const double z = d * d;
+    // sin d = d + d z (-1/3! + z (1/5! + z (-1/7! + z (1/9! - z / 11!))))
+    const double ps = fma(z, fma(z, fma(z, fma(z, -2.505210838544172e-08, 2.755731922398589e-06),
+                                        -1.984126984126984e-04), 8.333333333333333e-03),
+                          -1.666666666666667e-01);
+    const double sd = fma(d * z, ps, d);
+    // cos d - 1 = z (-1/2! + z (1/4! + z (-1/6! + z (1/8! + z (-1/10! + z / 12!)))))
+    const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, 2.087675698786810e-09, -2.755731922398589e-07),
+                                                  2.48015873015873e-05), -1.388888888888889e-03),
+                                 4.166666666666667e-02), -0.5);
+    const double cm1 = z * pc;
+    *sp = sb + fma(sb, cm1, cb * sd);
+    *cp = cb + fma(cb, cm1, -(sb * sd));
+}
+
 // x / 6 (the RK4 average): x * (1/6) plus one FMA residual correction (Markstein) — the correctly
 // rounded quotient but for rare ties, <= 1 ulp always; 3 VALU ops instead of the ~12 of the
 // general f64 division (scale / rcp / Newton / fmas / fixup)
@@ -82,12 +103,10 @@ template <> struct Env<RLP_ENV_CARTPOLE> {
     using P = rlp_cartpole_params;
     static constexpr int D = RLP_CARTPOLE_D, S = 4, A = 1;
 
-    // CartPole.ode :219-238
-    __device__ static __forceinline__ void ode(const P &p, double force, const double xx[4],
-                                               double d[4]) {
-        double th = xx[0], dth = xx[1], dx = xx[3];
-        double Sv, Cv;
-        sincos_fast(th, &Sv, &Cv);
+    // CartPole.ode :219-238 (sin / cos of xx[0] given)
+    __device__ static __forceinline__ void ode_sc(const P &p, double force, const double xx[4],
+                                                  double Sv, double Cv, double d[4]) {
+        double dth = xx[1], dx = xx[3];
         double num = force + p.m * p.ell * (dth * dth) * Sv;
         num = num - p.kf * dx;
         num = num - 3.0 / 4.0 * p.m * p.g * Sv * Cv;
@@ -95,6 +114,12 @@ template <> struct Env<RLP_ENV_CARTPOLE> {
         double ddx = div_nr(num, den);
         double ddth = 3.0 / 4.0 / p.m / p.ell * (p.m * p.g * Sv - p.m * ddx * Cv);
         d[0] = dth; d[1] = ddth; d[2] = dx; d[3] = ddx;
+    }
+    __device__ static __forceinline__ void ode(const P &p, double force, const double xx[4],
+                                               double d[4]) {
+        double Sv, Cv;
+        sincos_fast(xx[0], &Sv, &Cv);
+        ode_sc(p, force, xx, Sv, Cv, d);
     }
     // get_state :145-153
     __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
@@ -113,18 +138,25 @@ template <> struct Env<RLP_ENV_CARTPOLE> {
         const double tt = time + p.dt;
         double xx[4] = {s[0], s[1], s[2], s[3]};
         while (time < tt) {  // fp64 time accumulation => 10 or 11 sub-steps
-            // (K1 + 2*K2 + 2*K3 + K4) / 6 evaluates left to right: a running sum is bit-identical
-            double sum[4], tmp[4], d[4];
-            ode(p, force, xx, d);
+            // (K1 + 2*K2 + 2*K3 + K4) / 6 evaluates left to right: a running sum is bit-identical.
+            // xx + K/2 and sum + 2K as one FMA each: the power-of-two products are exact, so the
+            // single rounding equals numpy's. Stage angles theta + K/2 etc. take sin / cos from the
+            // sub-step's sincos by angle addition (sincos_step of the stage offset tmp - theta).
+            double sum[4], tmp[4], d[4], S0, C0, Ss, Cs;
+            sincos_fast(xx[0], &S0, &C0);
+            ode_sc(p, force, xx, S0, C0, d);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = k; tmp[i] = xx[i] + k / 2; }
-            ode(p, force, tmp, d);
+            for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = k; tmp[i] = fma(k, 0.5, xx[i]); }
+            sincos_step(S0, C0, tmp[0] - xx[0], &Ss, &Cs);
+            ode_sc(p, force, tmp, Ss, Cs, d);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k / 2; }
-            ode(p, force, tmp, d);
+            for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = fma(k, 2.0, sum[i]); tmp[i] = fma(k, 0.5, xx[i]); }
+            sincos_step(S0, C0, tmp[0] - xx[0], &Ss, &Cs);
+            ode_sc(p, force, tmp, Ss, Cs, d);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k; }
-            ode(p, force, tmp, d);
+            for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = fma(k, 2.0, sum[i]); tmp[i] = xx[i] + k; }
+            sincos_step(S0, C0, tmp[0] - xx[0], &Ss, &Cs);
+            ode_sc(p, force, tmp, Ss, Cs, d);
 #pragma unroll
             for (int i = 0; i < 4; ++i) xx[i] = xx[i] + div6(sum[i] + h * d[i]);
             time += h;
@@ -195,13 +227,13 @@ template <> struct Env<RLP_ENV_CARTPOLE_ANGLEONLY> {
         double sum[4], tmp[4], d[4];
         ode(p, force, xx, d);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = k; tmp[i] = xx[i] + k / 2; }
+        for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = k; tmp[i] = fma(k, 0.5, xx[i]); }
         ode(p, force, tmp, d);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k / 2; }
+        for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = fma(k, 2.0, sum[i]); tmp[i] = fma(k, 0.5, xx[i]); }
         ode(p, force, tmp, d);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; tmp[i] = xx[i] + k; }
+        for (int i = 0; i < 4; ++i) { const double k = h * d[i]; sum[i] = fma(k, 2.0, sum[i]); tmp[i] = xx[i] + k; }
         ode(p, force, tmp, d);
 #pragma unroll
         for (int i = 0; i < 4; ++i) xx[i] = xx[i] + div6(sum[i] + h * d[i]);
@@ -409,13 +441,13 @@ template <bool BIDIR> struct UGV {
         double sum[5], t[5], d[5];  // running RK4 sum (bit-identical, see CartPole)
         ode(p, al, aa, xx, d);  // rk44 :294-313
 #pragma unroll
-        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = k; t[i] = xx[i] + k / 2; }
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = k; t[i] = fma(k, 0.5, xx[i]); }
         ode(p, al, aa, t, d);
 #pragma unroll
-        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; t[i] = xx[i] + k / 2; }
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = fma(k, 2.0, sum[i]); t[i] = fma(k, 0.5, xx[i]); }
         ode(p, al, aa, t, d);
 #pragma unroll
-        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; t[i] = xx[i] + k; }
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = fma(k, 2.0, sum[i]); t[i] = xx[i] + k; }
         ode(p, al, aa, t, d);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
@@ -585,13 +617,13 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
         double sum[12], t[12], d[12];
         ode(p, uf, tq, s, d);
 #pragma unroll
-        for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = k; t[i] = s[i] + k / 2; }
+        for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = k; t[i] = fma(k, 0.5, s[i]); }
         ode(p, uf, tq, t, d);
 #pragma unroll
-        for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; t[i] = s[i] + k / 2; }
+        for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = fma(k, 2.0, sum[i]); t[i] = fma(k, 0.5, s[i]); }
         ode(p, uf, tq, t, d);
 #pragma unroll
-        for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = sum[i] + 2 * k; t[i] = s[i] + k; }
+        for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = fma(k, 2.0, sum[i]); t[i] = s[i] + k; }
         ode(p, uf, tq, t, d);
 #pragma unroll
         for (int i = 0; i < 12; ++i) s[i] = s[i] + div6(sum[i] + h * d[i]);
@@ -853,13 +885,13 @@ template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
         double sum[5], t[5], d[5];  // rk44 :484-502, running RK4 sum (bit-identical, see CartPole)
         ode(p, al, aa, s, d);
 #pragma unroll
-        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = k; t[i] = s[i] + k / 2; }
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = k; t[i] = fma(k, 0.5, s[i]); }
         ode(p, al, aa, t, d);
 #pragma unroll
-        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; t[i] = s[i] + k / 2; }
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = fma(k, 2.0, sum[i]); t[i] = fma(k, 0.5, s[i]); }
         ode(p, al, aa, t, d);
 #pragma unroll
-        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = sum[i] + 2 * k; t[i] = s[i] + k; }
+        for (int i = 0; i < 5; ++i) { const double k = dt * d[i]; sum[i] = fma(k, 2.0, sum[i]); t[i] = s[i] + k; }
         ode(p, al, aa, t, d);
         if (p.shaped && s[V] < 0.) {  // demo copy rk44 :496-500: gate on the pre-step velocity
             s[PHI] = s[PHI] + div6(sum[PHI] + dt * d[PHI]);

@@ -17,6 +17,10 @@
 //   W2p [t][r][jq][lane][4]   W2[16(4jq+q) + (l&15)][16t + 4(l>>4) + r]      (offset 0)
 //   W1c [H][4*KS1]            W1[j][k] (0 for k >= S)                         (LDS-resident part:)
 //   B1c [H], B2c [H], W3c [A][H], b3 [4], info [4] = {2^sw, 2^(sw+SH), 2^-(sw+SH), 0}
+//   small_r                   the resident part in the f16x3 forward's form (same internal
+//                             offsets; rlp_mfma_x3.hpp): W1, b1 times 2 / ln 2 (layer 1 yields
+//                             tanh's exp2 argument), B2c times 2^(sw+SH), info {2^sw, 1,
+//                             2^-(sw+SH), 0}
 //   X3  (256-B aligned)       W2 * 2^sw split into f16 hi + lo, the f16x3 path's chunks
 //                             (rlp_mfma_x3.hpp)
 //   X3T                       the same for W2^T (the PPO2 update's backward GEMM, rlp_update.hip)
@@ -33,6 +37,7 @@ struct MfmaNet {
     int out_tanh;  // last layer activation is tanh (actor) vs identity (critic)
     int off_w1, off_b1, off_b2, off_w3, off_b3, off_info;  // offsets of the LDS-resident part
     int small_count;                                         // floats from off_w1 to info's end
+    int off_small_r;                                         // the f16x3 form of the same part
     int off_x3;                                              // f16 hi/lo W2 chunks (H*H floats)
     int off_x3t;                                             // the same for W2^T
     int64_t count;
@@ -55,7 +60,8 @@ inline bool mfma_net_from_desc(const rlp_mlp_desc &d, MfmaNet *net) {
     net->off_b3 = net->off_w3 + A * H;
     net->off_info = net->off_b3 + 4;
     net->small_count = net->off_info + 4 - net->off_w1;
-    net->off_x3 = (net->off_info + 4 + 63) / 64 * 64;
+    net->off_small_r = net->off_info + 4;
+    net->off_x3 = (net->off_small_r + net->small_count + 63) / 64 * 64;
     net->off_x3t = net->off_x3 + H * H;
     net->count = net->off_x3t + (int64_t)H * H;
     return true;
@@ -67,9 +73,11 @@ constexpr int mlp_small_floats() { return H * 4 * KS1 + 2 * H + NOUT * H + 8; }
 template <int H>
 constexpr int mlp_phase_floats() { return H / 64 * 256; }  // one k-phase of W2 fragments
 
-// Cooperative copy of a net's resident part to LDS (all threads of the block; caller syncs).
-__device__ __forceinline__ void mlp_small_to_lds(const float *P, const MfmaNet &net, float *dst) {
-    const gptr<float> src = as_global(P) + net.off_w1;
+// Cooperative copy of a net's resident part to LDS (all threads of the block; caller syncs);
+// x3: its f16x3 form (small_r) for mlp_x3_forward.
+__device__ __forceinline__ void mlp_small_to_lds(const float *P, const MfmaNet &net, float *dst,
+                                                 bool x3 = false) {
+    const gptr<float> src = as_global(P) + (x3 ? net.off_small_r : net.off_w1);
     for (int i = threadIdx.x; i < net.small_count; i += blockDim.x) dst[i] = src[i];
 }
 

@@ -8,8 +8,12 @@
 // (f16 x f16 products are exact in the f32 accumulator), so the dropped wl xl and the rounding of
 // lo leave ~3 * 2^-22 |w x| per product — the same order as the f32 MFMA's own accumulation
 // rounding (MI355X_MICROARCH.md "FP32-input MFMA": 0.75-1.5e-7 sum|ab|). The accumulator carries
-// 2^(sw + SH) (bias pre-scaled, removed inside the output tanh's exponent constant, exact powers
-// of two). tests/test_gpu_rollout.py measures the error of both paths against float64.
+// 2^(sw + SH) (bias pre-scaled in small_r, removed inside the output tanh's exponent constant,
+// exact powers of two); small_r's W1, b1 carry tanh's 2 / ln 2, so layer 1 yields the exp2
+// argument directly. tests/test_gpu_rollout.py measures the error of both paths against float64.
+// (Feeding layer 2 with 2^SH (1 - tanh) and a rowsum correction would save one more op per pair,
+// but the accumulator then carries the rowsum's large offset: ~10x the error on the shipped
+// PPO2-CartPole actor, outside the parity bound.)
 //
 // Operands ("env on lane", as rlp_mfma_layout.hpp): for phase P (K = 32 neurons), lane (g, e) of
 // sub-block sb holds B[k = 8g + i][env e] = x(neuron 32P + 4g + i) for i < 4 (layer-1 tile 2P, its
@@ -31,15 +35,14 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 typedef float float2v __attribute__((ext_vector_type(2)));
 
-// scale * tanh(x) for two values on the packed FP32 pipe (v_pk_mul/add/fma_f32 around the two
-// transcendentals): bit-identical per element to scale * tanh_fast(x) (exact power-of-two scale)
-__device__ __forceinline__ float2v tanh2_scaled(float2v x, float k, float scale) {
+// tanh(x) for two values on the packed FP32 pipe (v_pk_mul/add/fma_f32 around the two
+// transcendentals), k = 2 / ln 2 times any exact scale of x
+__device__ __forceinline__ float2v tanh2(float2v x, float k) {
     const float2v t = x * k;
     const float2v e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
     const float2v d = e + 1.0f;
     const float2v r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-    return __builtin_elementwise_fma(r, (float2v){-2.0f * scale, -2.0f * scale},
-                                     (float2v){scale, scale});
+    return __builtin_elementwise_fma(r, (float2v){-2.0f, -2.0f}, (float2v){1.0f, 1.0f});
 }
 
 // f16 hi + lo of two values (packed RNE converts)
@@ -84,7 +87,6 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
     const float *W3c = small + (net.off_w3 - net.off_w1);
     const float *b3c = small + (net.off_b3 - net.off_w1);
     const float *info = small + (net.off_info - net.off_w1);
-    const float acc_scale = info[1];
     const float k_out = 2.8853900817779268f * info[2];  // exp(2x) constant with 2^-(sw+SH) folded
 
     static_assert(RG == 2 || RG == 3, "ring of 2 or 3 chunks");
@@ -101,9 +103,7 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
     floatx4 acc[SUB][NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-        floatx4 b2 = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * g);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) b2[r] *= acc_scale;
+        const floatx4 b2 = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * g);
 #pragma unroll
         for (int sb = 0; sb < SUB; ++sb) acc[sb][j] = b2;
     }
@@ -133,8 +133,12 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
             for (int i = 0; i < 8; i += 2) {
                 const float2v pre = i < 4 ? (float2v){hp0[sb][i], hp0[sb][i + 1]}
                                           : (float2v){hp1[sb][i - 4], hp1[sb][i - 3]};
-                // 2^SH tanh(pre), bit-identical to kX3HScale * tanh_fast(pre)
-                const float2v x = tanh2_scaled(pre, 2.8853900817779268f, kX3HScale);
+                // 2^SH tanh(h1) = 2^SH - 2^(SH+1) / (1 + exp2(pre)), pre = 2 h1 / ln 2 (small_r)
+                const float2v ex = {__builtin_amdgcn_exp2f(pre.x), __builtin_amdgcn_exp2f(pre.y)};
+                const float2v dn = ex + 1.0f;
+                const float2v rc = {__builtin_amdgcn_rcpf(dn.x), __builtin_amdgcn_rcpf(dn.y)};
+                const float2v x = __builtin_elementwise_fma(
+                    rc, (float2v){-2.0f * kX3HScale, -2.0f * kX3HScale}, (float2v){kX3HScale, kX3HScale});
                 half2v hi, lo;
                 split2(x, hi, lo);
                 bh[sb][i] = hi.x;
@@ -203,7 +207,7 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
         for (int sb = 0; sb < SUB; ++sb)
 #pragma unroll
             for (int r = 0; r < 4; r += 2) {
-                const float2v h = tanh2_scaled((float2v){acc[sb][j][r], acc[sb][j][r + 1]}, k_out, 1.0f);
+                const float2v h = tanh2((float2v){acc[sb][j][r], acc[sb][j][r + 1]}, k_out);
 #pragma unroll
                 for (int a = 0; a < NOUT; ++a)
                     part[sb][a] = __builtin_elementwise_fma((float2v){w3[a][r], w3[a][r + 1]}, h,

@@ -138,8 +138,27 @@ __global__ void mfma_pack_kernel(MfmaNet net, const float *__restrict__ P, float
         } else if (idx < net.off_info) {  // b3 [4]
             const int a = idx - net.off_b3;
             v = a < A ? b3[a] : 0.f;
-        } else if (idx < net.off_x3) {  // info (mfma_scale_kernel) + alignment pad
+        } else if (idx < net.off_small_r) {  // info (mfma_scale_kernel)
             continue;
+        } else if (idx < net.off_x3) {  // small_r + alignment pad
+            const int q = idx - net.off_small_r + net.off_w1;
+            constexpr float k2 = 2.8853900817779268f;  // 2 / ln 2: tanh's exp(2x) as exp2
+            if (q < net.off_b1) {
+                const int j = (q - net.off_w1) / (4 * KS1), k = (q - net.off_w1) % (4 * KS1);
+                v = k < S ? W1[j * S + k] * k2 : 0.f;
+            } else if (q < net.off_b2) {
+                v = b1[q - net.off_b1] * k2;
+            } else if (q < net.off_w3) {
+                v = b2[q - net.off_b2] * (sw * kX3HScale);
+            } else if (q < net.off_b3) {
+                v = W3[q - net.off_w3];
+            } else if (q < net.off_info) {
+                const int a = q - net.off_b3;
+                v = a < A ? b3[a] : 0.f;
+            } else if (q < net.off_info + 4) {
+                const int i = q - net.off_info;
+                v = i == 0 ? sw : (i == 1 ? 1.f : (i == 2 ? 1.f / (sw * kX3HScale) : 0.f));
+            }
         } else {  // X3 / X3T [P][j][part][lane][8 halfs]: two halfs per float slot
             const bool tr = idx >= net.off_x3t;
             const int q = idx - (tr ? net.off_x3t : net.off_x3);

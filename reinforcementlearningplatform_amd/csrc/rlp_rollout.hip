@@ -58,8 +58,8 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
     float *small_a = lds, *small_c = lds + SMALL;
     float(*sobs)[WENV][8] = reinterpret_cast<float(*)[WENV][8]>(lds + 2 * SMALL);
     float *ring = lds + 2 * SMALL + WAVES * WENV * 8 + (X3 ? 0 : (threadIdx.x >> 6) * RING * PF);
-    mlp_small_to_lds(actor, an, small_a);
-    mlp_small_to_lds(critic, cn, small_c);
+    mlp_small_to_lds(actor, an, small_a, X3);
+    mlp_small_to_lds(critic, cn, small_c, X3);
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -242,8 +242,8 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
     float(*sob)[8] = reinterpret_cast<float(*)[8]>(lds + 2 * SMALL);
     float(*mv)[A + 1] = reinterpret_cast<float(*)[A + 1]>(lds + 2 * SMALL + EB * 8);
     float *ring = lds + 2 * SMALL + EB * 8 + EB * (A + 1);
-    mlp_small_to_lds(actor, an, small_a);
-    mlp_small_to_lds(critic, cn, small_c);
+    mlp_small_to_lds(actor, an, small_a, true);
+    mlp_small_to_lds(critic, cn, small_c, true);
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, e = lane & 15;

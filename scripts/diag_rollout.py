@@ -84,17 +84,29 @@ VARIANTS = {
 }
 
 
-def lib_path(variant):
-    return os.path.join(DIAG, f"librlp_diag_{variant}.so")
+def lib_path(variant, rev=None):
+    return os.path.join(DIAG, f"librlp_diag_{variant}{'_' + rev if rev else ''}.so")
 
 
-def build(variant="base"):
+def build(variant="base", rev=None):
     src_root = os.path.join(DIAG, "a", "b", "csrc")
     if os.path.exists(os.path.join(DIAG, "a")):
         shutil.rmtree(os.path.join(DIAG, "a"))
     shutil.copytree(CSRC, src_root, ignore=shutil.ignore_patterns("build"))
     os.makedirs(os.path.join(DIAG, "a", "include"), exist_ok=True)
     shutil.copy(os.path.join(ROOT, "include", "rlp.h"), os.path.join(DIAG, "a", "include", "rlp.h"))
+    if rev:   # A/B against a committed revision of the whole native tree
+        shutil.rmtree(src_root)
+        tmp = os.path.join(DIAG, "rev")
+        if os.path.exists(tmp):
+            shutil.rmtree(tmp)
+        os.makedirs(tmp)
+        arc = subprocess.run(["git", "-C", ROOT, "archive", rev, "reinforcementlearningplatform_amd/csrc",
+                              "include"], check=True, capture_output=True).stdout
+        subprocess.run(["tar", "-x", "-C", tmp], input=arc, check=True)
+        shutil.copytree(os.path.join(tmp, "reinforcementlearningplatform_amd", "csrc"), src_root)
+        shutil.copy(os.path.join(tmp, "include", "rlp.h"), os.path.join(DIAG, "a", "include", "rlp.h"))
+        shutil.rmtree(tmp)
     p = os.path.join(src_root, "rlp_rollout.hip")
     with open(p) as f:
         s = f.read()
@@ -107,12 +119,12 @@ def build(variant="base"):
         assert a in t, (variant, a)
         with open(q, "w") as f:
             f.write(t.replace(a, b))
-    subprocess.run(["make", "-s", "-j8", "-C", src_root, f"OUT={lib_path(variant)}"], check=True)
-    print("built", lib_path(variant))
+    subprocess.run(["make", "-s", "-j8", "-C", src_root, f"OUT={lib_path(variant, rev)}"], check=True)
+    print("built", lib_path(variant, rev))
 
 
-def run(n, T, iters, variant="base", sub=0, physics=1):
-    LIB = lib_path(variant)
+def run(n, T, iters, variant="base", sub=0, physics=1, rev=None):
+    LIB = lib_path(variant, rev)
     os.environ["RLP_LIBRARY"] = LIB
     sys.path.insert(0, ROOT)
     import ctypes
@@ -141,7 +153,7 @@ def run(n, T, iters, variant="base", sub=0, physics=1):
     steps = d[:, 5]
     mlp, bar1, phys, bar2, nphys = (d[:, i] / steps for i in range(5))
     phys_per = d[:, 2] / np.maximum(d[:, 4], 1)
-    print(f"[{variant}] n={n} T={T} sub={sub or 'auto'} physics={physics}: cycles per step per wave (mean over {nw} waves):")
+    print(f"[{variant}{' @' + rev if rev else ''}] n={n} T={T} sub={sub or 'auto'} physics={physics}: cycles per step per wave (mean over {nw} waves):")
     print(f"  MLP pass (actor+critic) {mlp.mean():9.0f}  (min {mlp.min():.0f} max {mlp.max():.0f})")
     print(f"  barrier after MLP       {bar1.mean():9.0f}")
     print(f"  physics (its waves)     {phys_per.mean():9.0f}  per physics turn; share {nphys.mean():.2f}")
@@ -158,10 +170,11 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--variant", default="base", choices=sorted(VARIANTS) + ["all"])
     ap.add_argument("--sub", type=int, default=0)
+    ap.add_argument("--rev", default=None, help="build / run the native tree of this git revision")
     ap.add_argument("--physics", type=int, default=1, help="rlp_set_rollout_physics (3: 32x32x16 MLP)")
     a = ap.parse_args()
     if a.build:
         for v in (VARIANTS if a.variant == "all" else [a.variant]):
-            build(v)
+            build(v, a.rev)
     if a.run:
-        run(a.n, a.T, a.iters, a.variant, a.sub, a.physics)
+        run(a.n, a.T, a.iters, a.variant, a.sub, a.physics, a.rev)
