@@ -139,13 +139,13 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
     float *const g3s = lds + kFdRegion + SMALL + (threadIdx.x >> 6) * 64;            // [16][4]
     float *const srw = lds + kFdRegion + SMALL + 4 * 64 + (threadIdx.x >> 6) * 128;  // [16][8]
     const MfmaNet &net = g.net;
-    mlp_small_to_lds(g.packed, net, small);
+    mlp_small_to_lds(g.packed, net, small, true);  // small_r: W1, b1 x 2/ln 2, b2 x 2^(sw+SH)
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, gq = lane >> 4, e = lane & 15;
     const int S = net.S;
     const float *info = small + (net.off_info - net.off_w1);
-    const float sw = info[0], acc_scale = info[1];
+    const float sw = info[0];
     const float k_out = 2.8853900817779268f * info[2];
     float *const my_part = ring + wv * 4 * 256;
     // stage neurons [128 h, 128 h + 128) of the wave's [256 neurons][16 rows] register tile
@@ -159,19 +159,6 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) stg[ob + (16 * j + q) * STG] = t[8 * h + j][q];
     };
-    // the staged half -> G[tile][n][64 rows] columns 16 wv .. 16 wv + 15 (8 coalesced float4 stores)
-    auto store_half = [&](__attribute__((address_space(1))) float *Gt, int h) {
-        int ob = (lane >> 2) * STG + 4 * (lane & 3);
-        asm volatile("" : "+v"(ob));
-        int oo = (128 * h + (lane >> 2)) * kUpdRows + 16 * wv + 4 * (lane & 3);
-        asm volatile("" : "+v"(oo));
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {  // n = 16 i + lane / 4, columns 4 (lane % 4) ..
-            const floatx4 v = *reinterpret_cast<const floatx4 *>(stg + ob + 16 * i * STG);
-            *reinterpret_cast<__attribute__((address_space(1))) floatx4 *>(Gt + oo + 16 * i * kUpdRows) = v;
-        }
-    };
-
     float dW3p[A][4];  // neurons 64 c + lane
     float db3p[A];
 #pragma unroll
@@ -232,19 +219,14 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
         // ---- forward: z2 (scaled by 2^(sw+SH)) = W2 h1 + b2
         floatx4 acc[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            floatx4 b2 = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * gq);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) b2[q] *= acc_scale;
-            acc[j] = b2;
-        }
+        for (int j = 0; j < 16; ++j) acc[j] = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * gq);
         x3_gemm16(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
             const floatx4 p0 = layer1(2 * P), p1 = layer1(2 * P + 1);
             float x[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const float pre = i < 4 ? p0[i] : p1[i - 4];
-                const float ex = __builtin_amdgcn_exp2f(pre * 2.8853900817779268f);
+                const float ex = __builtin_amdgcn_exp2f(pre);  // pre = 2 h1 / ln 2 (small_r)
                 x[i] = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + ex), kX3HScale);
             }
             split8(x, bh, bl);
@@ -254,16 +236,19 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
         for (int a = 0; a < A; ++a) z3[a] = 0.f;
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
+        for (int j = 0; j < 16; ++j) {
+            floatx4 w3[A];
+#pragma unroll
+            for (int a = 0; a < A; ++a) w3[a] = *reinterpret_cast<const floatx4 *>(W3c + a * H + 16 * j + 4 * gq);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float ex = __builtin_amdgcn_exp2f(acc[j][q] * k_out);
                 const float h = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + ex), 1.0f);
                 acc[j][q] = h;
 #pragma unroll
-                for (int a = 0; a < A; ++a)
-                    z3[a] = __builtin_fmaf(W3c[a * H + 16 * j + 4 * gq + q], h, z3[a]);
+                for (int a = 0; a < A; ++a) z3[a] = __builtin_fmaf(w3[a][q], h, z3[a]);
             }
+        }
 #pragma unroll
         for (int a = 0; a < A; ++a) {
             z3[a] += __shfl_xor(z3[a], 16);
@@ -342,24 +327,24 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
             }
             wave_sync_lds();
         }
-        // ---- g2 = (W3^T g3) * (1 - h2^2) in place, to HBM through the staging tile
+        // ---- g2 = (W3^T g3) * (1 - h2^2) in place, to HBM in G2's [tile][neuron][64 rows] layout
+        // straight from the registers (lane (gq, e): rows 16 wv + e of neurons 16 j + 4 gq + q;
+        // each store instruction writes four 64-B row runs)
+        auto *g2row = g2base + tile * kUpdTileFloats + (4 * gq) * kUpdRows + 16 * wv + e;
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
+        for (int j = 0; j < 16; ++j) {
+            floatx4 w3[A];
+#pragma unroll
+            for (int a = 0; a < A; ++a) w3[a] = *reinterpret_cast<const floatx4 *>(W3c + a * H + 16 * j + 4 * gq);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float h = acc[j][q];
                 float dh = 0.f;
 #pragma unroll
-                for (int a = 0; a < A; ++a)
-                    dh = __builtin_fmaf(W3c[a * H + 16 * j + 4 * gq + q], g3[a], dh);
+                for (int a = 0; a < A; ++a) dh = __builtin_fmaf(w3[a][q], g3[a], dh);
                 acc[j][q] = dh * (1.f - h * h);
+                g2row[(16 * j + q) * kUpdRows] = acc[j][q];
             }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            stage_half(acc, h);
-            wave_sync_lds();
-            store_half(g2base + tile * kUpdTileFloats, h);
-            wave_sync_lds();
         }
 
         // ---- backward: dh1 = W2^T g2, with g2 scaled per row into f16 range; B operands of phase
@@ -374,7 +359,8 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
         g2max = fmaxf(g2max, m);
         const int ex = m > 0.f ? __builtin_amdgcn_frexp_expf(m) : 0;  // m in [2^(ex-1), 2^ex)
         const float sc = __builtin_amdgcn_ldexpf(1.f, 14 - ex);
-        const float unscale = __builtin_amdgcn_ldexpf(1.f, ex - 14) / sw;  // exact powers of two
+        // exact powers of two; x 4: 1 - h1^2 = 4 r (1 - r) for h1 = 1 - 2 r
+        const float unscale4 = 4.f * __builtin_amdgcn_ldexpf(1.f, ex - 14) / sw;
         floatx4 dh1[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) dh1[j] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -388,14 +374,14 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
             split8(x, bh, bl);
         });
         lds_barrier();  // the ring is free again: g1 goes through the staging tiles
-        // ---- g1 = dh1 * (1 - h1^2), h1 recomputed (bit-identical to the forward's)
+        // ---- g1 = dh1 * (1 - h1^2), h1 = 1 - 2 r recomputed (r as in the forward's)
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const floatx4 pre = layer1(t);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const float h1 = tanh_fast(pre[q]);
-                dh1[t][q] = dh1[t][q] * unscale * (1.f - h1 * h1);
+                const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(pre[q]));
+                dh1[t][q] = dh1[t][q] * unscale4 * __builtin_fmaf(-r, r, r);
             }
         }
         // ---- dW1 | db1 = sum_rows g1 [s | 1]^T through the staging tile, by halves
@@ -484,7 +470,9 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
     const int S = net.S;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, gq = lane >> 4, e = lane & 15;
     {
-        const float *W1c = w.packed + net.off_w1, *B1c = w.packed + net.off_b1;
+        // small_r: W1, b1 x 2/ln 2 (h1 as in the FD forward)
+        const float *W1c = w.packed + net.off_small_r;
+        const float *B1c = w.packed + net.off_small_r + (net.off_b1 - net.off_w1);
         for (int i = threadIdx.x; i < H * SP; i += blockDim.x) w1s[i / SP][i % SP] = W1c[i];
         for (int i = threadIdx.x; i < H; i += blockDim.x) b1s[i] = B1c[i];
     }
@@ -532,7 +520,8 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
             float pre = b1s[n];
 #pragma unroll
             for (int k = 0; k < SP; ++k) pre = __builtin_fmaf(w1s[n][k], srow[buf][r0 + i][k], pre);
-            x[i] = kX3HScale * tanh_fast(pre);
+            x[i] = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(pre)),
+                                  kX3HScale);
         }
         half8 hh, hl;
         split8(x, hh, hl);

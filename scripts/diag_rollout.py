@@ -88,7 +88,7 @@ def lib_path(variant, rev=None):
     return os.path.join(DIAG, f"librlp_diag_{variant}{'_' + rev if rev else ''}.so")
 
 
-def build(variant="base", rev=None):
+def build(variant="base", rev=None, target="rlp_rollout.hip", patcher=None):
     src_root = os.path.join(DIAG, "a", "b", "csrc")
     if os.path.exists(os.path.join(DIAG, "a")):
         shutil.rmtree(os.path.join(DIAG, "a"))
@@ -107,12 +107,12 @@ def build(variant="base", rev=None):
         shutil.copytree(os.path.join(tmp, "reinforcementlearningplatform_amd", "csrc"), src_root)
         shutil.copy(os.path.join(tmp, "include", "rlp.h"), os.path.join(DIAG, "a", "include", "rlp.h"))
         shutil.rmtree(tmp)
-    p = os.path.join(src_root, "rlp_rollout.hip")
+    p = os.path.join(src_root, target)
     with open(p) as f:
         s = f.read()
     with open(p, "w") as f:
-        f.write(patch(s))
-    for fname, a, b in VARIANTS[variant]:
+        f.write((patcher or patch)(s))
+    for fname, a, b in VARIANTS.get(variant, []):
         q = os.path.join(src_root, fname)
         with open(q) as f:
             t = f.read()
