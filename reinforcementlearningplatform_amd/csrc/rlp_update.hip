@@ -49,7 +49,9 @@ __device__ __forceinline__ void lds_barrier() {
 // acc[j] += A-chunks(Xw) x B(P), B(P) = bop(P) as f16 hi/lo (rlp_mfma_x3.hpp layout). The phase
 // loop is fully unrolled, so bop may read register arrays at compile-time indices; the next
 // phase's B operands are prepared inside the second chunk's MFMA region.
-template <class BOp>
+// SWAP: the chunk fragments are the B operand and bop's the A operand (C = [rows][chunk outputs]:
+// "neuron on lane" instead of "row on lane"; the register contents of both operands are the same).
+template <bool SWAP = false, class BOp>
 __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, float *my_part,
                                           floatx4 (&acc)[16], BOp &&bop) {
     constexpr int NC = 16;
@@ -92,9 +94,15 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     floatx4 v = acc[8 * hf + 4 * g4 + u];
-                    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[u], bh, v, 0, 0, 0);
-                    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[u], bl, v, 0, 0, 0);
-                    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[u], bh, v, 0, 0, 0);
+                    if constexpr (SWAP) {
+                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, ah[u], v, 0, 0, 0);
+                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, ah[u], v, 0, 0, 0);
+                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, al[u], v, 0, 0, 0);
+                    } else {
+                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[u], bh, v, 0, 0, 0);
+                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[u], bl, v, 0, 0, 0);
+                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[u], bh, v, 0, 0, 0);
+                    }
                     acc[8 * hf + 4 * g4 + u] = v;
                 }
             }
@@ -122,22 +130,39 @@ __device__ __forceinline__ void split8(const float (&x)[8], half8 &bh, half8 &bl
     }
 }
 
-// LDS of one FD block (floats): [ ring (3 x 16 KiB) aliased by the 4 waves' half-tile staging
-// buffers | small weights | g3s | srw ]. The staging buffers are only used between the two GEMMs
-// and after the second, each window opened and closed by a block barrier, so two blocks fit a CU.
-constexpr int kFdStg = 20;  // staging row pitch: conflict-free b32 writes, 16-B aligned b128 reads
-constexpr int kFdStgFloats = 128 * kFdStg;  // [128 neurons][16 rows] (half of the 256 neurons)
-constexpr int kFdRegion = kX3RingFloats > 4 * kFdStgFloats ? kX3RingFloats : 4 * kFdStgFloats;
+// Cross-lane sums without LDS (the weight gradients' row reductions):
+// pair_sum_rows16: x + (x of the lane in the partner set), DPP within a 16-lane row; the lanes
+// whose `bit` is set keep value b, the others a (a butterfly stage: the pair's two sums).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ float pair_sum_rows16(float a, float b, bool bit) {
+    const float keep = bit ? b : a, send = bit ? a : b;
+    return dpp_f<CTRL>(send) + keep;
+}
+// the same across 16-lane rows: lanes 0-31 (even rows) keep a, 32-63 (odd rows) keep b
+__device__ __forceinline__ float pair_sum_x32(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float pair_sum_x16(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+constexpr int kDppRowMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1;
+
+// LDS of one FD block (floats): [ ring (3 x 16 KiB) | small weights | srw ]; two blocks per CU.
+constexpr int kFdRegion = kX3RingFloats;
 
 template <int KS1, int A, int LOSS>
 __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
     constexpr int H = kUpdH, SMALL = mlp_small_floats<H, KS1, A>();
-    constexpr int STG = kFdStg;
-    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + 4 * 16 * 4 + 4 * 16 * 8];
+    constexpr int NC = 4 * KS1 + 1;  // dW1 columns per neuron: s features | bias
+    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + 4 * 16 * 8];
     float *ring = lds, *small = lds + kFdRegion;
-    float *const stg = lds + (threadIdx.x >> 6) * kFdStgFloats;  // aliases the ring
-    float *const g3s = lds + kFdRegion + SMALL + (threadIdx.x >> 6) * 64;            // [16][4]
-    float *const srw = lds + kFdRegion + SMALL + 4 * 64 + (threadIdx.x >> 6) * 128;  // [16][8]
+    float *const srw = lds + kFdRegion + SMALL + (threadIdx.x >> 6) * 128;  // [16 rows][8]
     const MfmaNet &net = g.net;
     mlp_small_to_lds(g.packed, net, small, true);  // small_r: W1, b1 x 2/ln 2, b2 x 2^(sw+SH)
     __syncthreads();
@@ -148,18 +173,7 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
     const float sw = info[0];
     const float k_out = 2.8853900817779268f * info[2];
     float *const my_part = ring + wv * 4 * 256;
-    // stage neurons [128 h, 128 h + 128) of the wave's [256 neurons][16 rows] register tile
-    // (the staging addresses are made opaque per use: otherwise the compiler hoists dozens of
-    // lane-dependent LDS addresses out of the tile loop and spills them)
-    auto stage_half = [&](const floatx4 (&t)[16], int h) {
-        int ob = (4 * gq) * STG + e;
-        asm volatile("" : "+v"(ob));
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) stg[ob + (16 * j + q) * STG] = t[8 * h + j][q];
-    };
-    float dW3p[A][4];  // neurons 64 c + lane
+    float dW3p[A][4];  // neurons 16 e + 4 gq + m (the row butterfly's result)
     float db3p[A];
 #pragma unroll
     for (int a = 0; a < A; ++a) {
@@ -168,13 +182,11 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
         for (int c = 0; c < 4; ++c) dW3p[a][c] = 0.f;
     }
     double lsum = 0.0;
-    float dW1p[4][4 * KS1], db1p[4];  // neurons 64 c + lane
+    float dW1p[2][2 * NC];  // [h][i]: neuron 16 (8 h + 2 gq + i / NC) + e, column i % NC
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        db1p[c] = 0.f;
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int k = 0; k < 4 * KS1; ++k) dW1p[c][k] = 0.f;
-    }
+        for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] = 0.f;
     float g2max = 0.f;
 
     const int64_t ntiles = (g.rows + kUpdRows - 1) / kUpdRows;
@@ -213,6 +225,18 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
             for (int kk = 0; kk < KS1; ++kk)
                 c = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[kk], bobs[kk], c, 0, 0, 0);
+            return c;
+        };
+        // the same tile "neuron on lane": C[row 4 gq + q][neuron 16 t + e] (operands swapped)
+        auto layer1_t = [&](int t) {
+            float w1[KS1];
+#pragma unroll
+            for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[(16 * t + e) * (4 * KS1) + 4 * kk + gq];
+            const float b1 = B1c[16 * t + e];
+            floatx4 c = {b1, b1, b1, b1};
+#pragma unroll
+            for (int kk = 0; kk < KS1; ++kk)
+                c = __builtin_amdgcn_mfma_f32_16x16x4f32(bobs[kk], w1[kk], c, 0, 0, 0);
             return c;
         };
 
@@ -296,36 +320,26 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
         if (gq == 0) {
             lsum += (double)lrow;
 #pragma unroll
-            for (int a = 0; a < A; ++a) {
-                db3p[a] += g3[a];
-                g3s[e * 4 + a] = g3[a];
-            }
+            for (int a = 0; a < A; ++a) db3p[a] += g3[a];
         }
-        lds_barrier();  // every wave is done reading the ring: the staging tiles may overwrite it
-        // ---- dW3 = sum_rows g3 h2^T through the staging tile, one half of the neurons at a time
-        // (transpose: lane owns neurons 64 c + lane and sums over the wave's 16 rows)
+        // ---- dW3 = sum_rows g3 h2^T: the 64 products g3 h2 of the lane's row, summed over the 16
+        // rows of its lane group by a 4-stage DPP butterfly (64 -> 4 values: neurons 16 e + 4 gq + m)
+        {
+            const bool b3 = e & 8, b2 = e & 4, b1 = e & 2, b0 = e & 1;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            stage_half(acc, h);
-            wave_sync_lds();
+            for (int a = 0; a < A; ++a) {
+                float pv[64];
 #pragma unroll
-            for (int cc = 0; cc < 2; ++cc) {
-                int orow = (64 * cc + lane) * STG;
-                asm volatile("" : "+v"(orow));
-                const float *hrow = stg + orow;
+                for (int i = 0; i < 64; ++i) pv[i] = g3[a] * acc[i >> 2][i & 3];
 #pragma unroll
-                for (int q4 = 0; q4 < 4; ++q4) {
-                    const floatx4 hv = *reinterpret_cast<const floatx4 *>(hrow + 4 * q4);
+                for (int i = 0; i < 32; ++i) pv[i] = pair_sum_rows16<kDppRowMirror>(pv[i], pv[i + 32], b3);
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const floatx4 gr = *reinterpret_cast<const floatx4 *>(g3s + (4 * q4 + u) * 4);
+                for (int i = 0; i < 16; ++i) pv[i] = pair_sum_rows16<kDppHalfMirror>(pv[i], pv[i + 16], b2);
 #pragma unroll
-                        for (int a = 0; a < A; ++a)
-                            dW3p[a][2 * h + cc] = __builtin_fmaf(gr[a], hv[u], dW3p[a][2 * h + cc]);
-                    }
-                }
+                for (int i = 0; i < 8; ++i) pv[i] = pair_sum_rows16<kDppXor2>(pv[i], pv[i + 8], b1);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dW3p[a][i] += pair_sum_rows16<kDppXor1>(pv[i], pv[i + 4], b0);
             }
-            wave_sync_lds();
         }
         // ---- g2 = (W3^T g3) * (1 - h2^2) in place, to HBM in G2's [tile][neuron][64 rows] layout
         // straight from the registers (lane (gq, e): rows 16 wv + e of neurons 16 j + 4 gq + q;
@@ -347,15 +361,17 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
             }
         }
 
-        // ---- backward: dh1 = W2^T g2, with g2 scaled per row into f16 range; B operands of phase
+        // ---- backward: dh1 = W2^T g2, with g2 scaled per wave tile into f16 range; operands of phase
         // P straight from the g2 registers (neurons 32 P + 4 gq + i and 32 P + 16 + 4 gq + i)
         float m = 0.f;
 #pragma unroll
         for (int j = 0; j < 16; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) m = fmaxf(m, fabsf(acc[j][q]));
-        m = fmaxf(m, __shfl_xor(m, 16));
-        m = fmaxf(m, __shfl_xor(m, 32));
+        // one power-of-two scale per wave tile (the swapped GEMM's output rows are spread over the
+        // lane groups, so a per-row scale would not be the lane's own)
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
         g2max = fmaxf(g2max, m);
         const int ex = m > 0.f ? __builtin_amdgcn_frexp_expf(m) : 0;  // m in [2^(ex-1), 2^ex)
         const float sc = __builtin_amdgcn_ldexpf(1.f, 14 - ex);
@@ -364,7 +380,8 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
         floatx4 dh1[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) dh1[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-        x3_gemm16(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
+        // (operands swapped: dh1 comes out "neuron on lane", dh1[t][q] = row 4 gq + q, neuron 16 t + e)
+        x3_gemm16<true>(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -373,59 +390,69 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
             }
             split8(x, bh, bl);
         });
-        lds_barrier();  // the ring is free again: g1 goes through the staging tiles
-        // ---- g1 = dh1 * (1 - h1^2), h1 = 1 - 2 r recomputed (r as in the forward's)
+        // ---- g1 = dh1 * (1 - h1^2), h1 = 1 - 2 r recomputed (r as in the forward's), neuron on lane
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
-            const floatx4 pre = layer1(t);
+            const floatx4 pre = layer1_t(t);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(pre[q]));
                 dh1[t][q] = dh1[t][q] * unscale4 * __builtin_fmaf(-r, r, r);
             }
         }
-        // ---- dW1 | db1 = sum_rows g1 [s | 1]^T through the staging tile, by halves
+        // ---- dW1 | db1 = sum_rows g1 [s | 1]^T: the lane's 4 rows in registers (s rows from srw),
+        // then the 4 lane groups by a 2-stage permlane butterfly, per half of the neuron tiles
+        // (8 NC -> 2 NC values)
+        {
+            float sv[4][4 * KS1];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            stage_half(dh1, h);
-            wave_sync_lds();
+            for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int cc = 0; cc < 2; ++cc) {
-                int orow = (64 * cc + lane) * STG;
-                asm volatile("" : "+v"(orow));
-                const float *grow = stg + orow;
+                for (int kk = 0; kk < KS1; ++kk) {
+                    const floatx4 v = *reinterpret_cast<const floatx4 *>(srw + (4 * gq + q) * 8 + 4 * kk);
 #pragma unroll
-                for (int q4 = 0; q4 < 4; ++q4) {
-                    const floatx4 gv = *reinterpret_cast<const floatx4 *>(grow + 4 * q4);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        db1p[2 * h + cc] += gv[u];
-#pragma unroll
-                        for (int k = 0; k < 4 * KS1; ++k)
-                            dW1p[2 * h + cc][k] = __builtin_fmaf(gv[u], srw[(4 * q4 + u) * 8 + k],
-                                                                 dW1p[2 * h + cc][k]);
-                    }
+                    for (int u = 0; u < 4; ++u) sv[q][4 * kk + u] = v[u];
                 }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                float v[8 * NC];
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt) {
+                    const floatx4 gt = dh1[8 * h + tt];
+#pragma unroll
+                    for (int f = 0; f < 4 * KS1; ++f) {
+                        float x = gt[0] * sv[0][f];
+#pragma unroll
+                        for (int q = 1; q < 4; ++q) x = __builtin_fmaf(gt[q], sv[q][f], x);
+                        v[tt * NC + f] = x;
+                    }
+                    v[tt * NC + 4 * KS1] = (gt[0] + gt[1]) + (gt[2] + gt[3]);
+                }
+#pragma unroll
+                for (int i = 0; i < 4 * NC; ++i) v[i] = pair_sum_x32(v[i], v[i + 4 * NC]);
+#pragma unroll
+                for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] += pair_sum_x16(v[i], v[i + 2 * NC]);
             }
-            wave_sync_lds();
         }
     }
 
     // ---- per-wave partials: dW3 (lane's neurons) | db3 summed over the 16 row lanes | dW1 | db1
     float *out = g.part3 + (size_t)(blockIdx.x * 4 + wv) * (A * H + A + H * S + H);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int n = 64 * c + lane;
-        for (int k = 0; k < S; ++k) out[A * H + A + n * S + k] = dW1p[c][k];
-        out[A * H + A + H * S + n] = db1p[c];
-    }
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2 * NC; ++i) {
+            const int n = 16 * (8 * h + 2 * gq + i / NC) + e, f = i % NC;
+            if (f < S) out[A * H + A + n * S + f] = dW1p[h][i];
+            else if (f == 4 * KS1) out[A * H + A + H * S + n] = dW1p[h][i];
+        }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) g2max = fmaxf(g2max, __shfl_xor(g2max, o));
     if (lane == 0) atomicMax(g.g2max, __float_as_uint(g2max));  // non-negative: uint order
 #pragma unroll
     for (int a = 0; a < A; ++a) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) out[a * H + 64 * c + lane] = dW3p[a][c];
+        for (int m = 0; m < 4; ++m) out[a * H + 16 * e + 4 * gq + m] = dW3p[a][m];
         float b = db3p[a];
         b += __shfl_xor(b, 1);
         b += __shfl_xor(b, 2);

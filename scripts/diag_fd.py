@@ -18,14 +18,14 @@ ST = "__builtin_amdgcn_s_memtime()"
 MARKS = [  # (anchor text in the tile loop, phase index the time since the previous mark goes to)
     ("        // ---- h2 = tanh(z2), z3 = W3 h2 + b3", 0),
     ("        // ---- head gradient g3 = dL/dz3", 1),
-    ("        lds_barrier();  // every wave is done reading the ring: the staging tiles may overwrite it", 2),
+    ("        // ---- dW3 = sum_rows g3 h2^T", 2),
     ("        // ---- g2 = (W3^T g3) * (1 - h2^2) in place", 3),
     ("        // ---- backward: dh1 = W2^T g2", 4),
-    ("        lds_barrier();  // the ring is free again", 5),
+    ("        // ---- g1 = dh1 * (1 - h1^2)", 5),
     ("        // ---- dW1 | db1 = sum_rows g1", 6),
 ]
-NAMES = ["fwd GEMM (+layer1/tanh/split)", "h2 tanh + z3", "loss head g3", "dW3 transpose",
-         "g2 + G2 store + max", "bwd GEMM", "g1 (h1 recompute)", "dW1 transpose"]
+NAMES = ["fwd GEMM (+layer1/tanh/split)", "h2 tanh + z3", "loss head g3", "dW3 (row butterfly)",
+         "g2 + G2 store + max", "bwd GEMM", "g1 (h1 recompute)", "dW1 (lane-group butterfly)"]
 
 
 def patch(s):
@@ -38,13 +38,15 @@ def patch(s):
         assert anchor in s, anchor
         s = s.replace(anchor, f"        {{ const unsigned long long tn = {ST}; dg[{ph}] += tn - tp; tp = tn; }}\n" +
                       anchor, 1)
-    old = """            wave_sync_lds();
+    old = """                for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] += pair_sum_x16(v[i], v[i + 2 * NC]);
+            }
         }
     }
 
     // ---- per-wave partials"""
     assert old in s
-    s = s.replace(old, f"""            wave_sync_lds();
+    s = s.replace(old, f"""                for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] += pair_sum_x16(v[i], v[i + 2 * NC]);
+            }}
         }}
         {{ const unsigned long long tn = {ST}; dg[7] += tn - tp; tp = tn; }}
     }}
