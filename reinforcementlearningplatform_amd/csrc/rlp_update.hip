@@ -51,9 +51,12 @@ __device__ __forceinline__ void lds_barrier() {
 // phase's B operands are prepared inside the second chunk's MFMA region.
 // SWAP: the chunk fragments are the B operand and bop's the A operand (C = [rows][chunk outputs]:
 // "neuron on lane" instead of "row on lane"; the register contents of both operands are the same).
-template <bool SWAP = false, class BOp>
+// pre(P) runs at the head of phase P - 1, so its results (the forward's layer-1 MFMAs) are ready
+// when bop(P) needs them half a phase later (diag_fd.py: -1.2k cycles per tile; pinning bop's VALU
+// between the second chunk's MFMAs with sched_group_barrier measured within noise).
+template <bool SWAP = false, class BOp, class Pre>
 __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, float *my_part,
-                                          floatx4 (&acc)[16], BOp &&bop) {
+                                          floatx4 (&acc)[16], BOp &&bop, Pre &&pre) {
     constexpr int NC = 16;
     const int lane = threadIdx.x & 63;
     auto issue = [&](int c) {
@@ -64,10 +67,11 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
 #pragma unroll
         for (int q = 0; q < 4; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
     };
-    lds_barrier();  // every wave is done with the ring (and the staging tiles aliasing it)
+    lds_barrier();  // every wave is done with the ring
     issue(0);
     issue(1);
     half8 bh, bl;
+    pre(0);
     bop(0, bh, bl);
 #pragma unroll
     for (int P = 0; P < 8; ++P) {
@@ -80,6 +84,7 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
             block_barrier_raw();
             if (c + 2 < NC) issue(c + 2);
             const float *slot = ring + (c % kX3Ring) * kX3ChunkFloats + lane * 4;
+            if (hf == 0 && P + 1 < 8) pre(P + 1);
             if (hf == 1 && P + 1 < 8) bop(P + 1, nbh, nbl);
             // the chunk's 8 output tiles in two groups of 4 (8 fragment reads, then 12 MFMAs):
             // 32 fragment registers instead of 64 keep two waves per SIMD within 256 registers
@@ -244,8 +249,8 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
         floatx4 acc[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[j] = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * gq);
+        floatx4 p0, p1;  // layer-1 tiles of the next phase (pre), consumed by its B operands (bop)
         x3_gemm16(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
-            const floatx4 p0 = layer1(2 * P), p1 = layer1(2 * P + 1);
             float x[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -254,7 +259,7 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
                 x[i] = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + ex), kX3HScale);
             }
             split8(x, bh, bl);
-        });
+        }, [&](int P) { p0 = layer1(2 * P); p1 = layer1(2 * P + 1); });
         // ---- h2 = tanh(z2), z3 = W3 h2 + b3 (every lane group ends with its row's z3)
         float z3[A];
 #pragma unroll
@@ -389,7 +394,7 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
                 x[i + 4] = acc[2 * P + 1][i] * sc;
             }
             split8(x, bh, bl);
-        });
+        }, [](int) {});
         // ---- g1 = dh1 * (1 - h1^2), h1 = 1 - 2 r recomputed (r as in the forward's), neuron on lane
 #pragma unroll
         for (int t = 0; t < 16; ++t) {

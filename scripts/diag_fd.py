@@ -63,12 +63,12 @@ extern "C" int rlp_diag_fd_read(void *host, long long bytes) {
     return s
 
 
-def build(rev=None):
-    dr.build("fd", rev, target="rlp_update.hip", patcher=patch)
+def build(rev=None, variant="fd"):
+    dr.build(variant, rev, target="rlp_update.hip", patcher=patch)
 
 
-def run(rev=None, n=65536, T=128, epochs=2):
-    LIB = dr.lib_path("fd", rev)
+def run(rev=None, n=65536, T=128, epochs=2, variant="fd"):
+    LIB = dr.lib_path(variant, rev)
     os.environ["RLP_LIBRARY"] = LIB
     sys.path.insert(0, dr.ROOT)
     import ctypes
@@ -85,7 +85,7 @@ def run(rev=None, n=65536, T=128, epochs=2):
     d = d[d[:, 9] > 0]
     tiles = d[:, 9]
     per = d[:, :8] / tiles[:, None]
-    print(f"[fd{' @' + rev if rev else ''}] n={n} T={T}: cycles per 16-row wave tile (mean over "
+    print(f"[{variant}{' @' + rev if rev else ''}] n={n} T={T}: cycles per 16-row wave tile (mean over "
           f"{d.shape[0]} waves, {tiles.mean():.0f} tiles each over all launches):")
     for i, nm in enumerate(NAMES):
         print(f"  {nm:32s} {per[:, i].mean():9.0f}")
@@ -99,7 +99,8 @@ if __name__ == "__main__":
     ap.add_argument("--rev", default=None)
     ap.add_argument("--epochs", type=int, default=2)
     a = ap.parse_args()
+    variant = "fd"
     if a.build:
-        build(a.rev)
+        build(a.rev, variant)
     if a.run:
-        run(a.rev, epochs=a.epochs)
+        run(a.rev, epochs=a.epochs, variant=variant)
