@@ -33,6 +33,7 @@ struct Ppo2Args {
     int64_t rows;
     float inv_rows, eps_clip, ent_row;  // ent_row = entropy_coef * sum_a entropy_a (constant)
     float std_[4], gain[4], off[4];
+    float log_std[4], inv_var[4];  // per-launch constants of the Normal log-prob and its gradient
     float *g2t;         // [tiles][256][64]
     unsigned *g2max;    // bits of max|g2| (atomicMax)
     float *part3;       // [grid * 4][A*256 + A + 256*S + 256]: per-wave dW3 | db3 | dW1 | db1
@@ -296,7 +297,9 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
                 const float mean = t[a] * g.gain[a] + g.off[a];
                 const float act = valid ? g.a[src * A + a] : mean;
                 d[a] = act - mean;
-                lp_now += normal_logp(act, mean, g.std_[a]);
+                // Normal(mean, std).log_prob(act) (torch's expression, the division by 2 var and
+                // log(std) as launch constants)
+                lp_now += -(d[a] * d[a]) * (0.5f * g.inv_var[a]) - g.log_std[a] - 0.91893853320467274178f;
                 lp_old += valid ? g.lp[src * A + a] : 0.f;
             }
             const float ratio = expf(lp_now - lp_old);
@@ -312,8 +315,7 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
             const float dl_dlp = dl_dratio * ratio * g.inv_rows;
 #pragma unroll
             for (int a = 0; a < A; ++a) {
-                const float var = g.std_[a] * g.std_[a];
-                g3[a] = valid ? dl_dlp * (d[a] / var) * g.gain[a] * (1.f - t[a] * t[a]) : 0.f;
+                g3[a] = valid ? dl_dlp * (d[a] * g.inv_var[a]) * g.gain[a] * (1.f - t[a] * t[a]) : 0.f;
             }
             lrow = valid ? -fminf(s1, s2) - g.ent_row : 0.f;
         } else {
@@ -806,6 +808,8 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
         g.std_[k] = cfg->std[k];
         g.off[k] = (cfg->a_min[k] + cfg->a_max[k]) / 2.0f;
         g.gain[k] = cfg->a_max[k] - g.off[k];
+        g.log_std[k] = logf(cfg->std[k]);
+        g.inv_var[k] = 1.0f / (cfg->std[k] * cfg->std[k]);
         ent += 0.5f + 0.91893853320467274178f + logf(cfg->std[k]);  // Normal.entropy()
     }
     g.ent_row = cfg->entropy_coef * ent;
