@@ -55,10 +55,11 @@ __device__ __forceinline__ void lds_barrier() {
 // pre(P) runs at the head of phase P - 1, so its results (the forward's layer-1 MFMAs) are ready
 // when bop(P) needs them half a phase later (diag_fd.py: -1.2k cycles per tile; pinning bop's VALU
 // between the second chunk's MFMAs with sched_group_barrier measured within noise).
-template <bool SWAP = false, class BOp, class Pre>
+// W: waves of the block sharing the ring (each DMAs 16 / W KiB of every chunk).
+template <bool SWAP = false, int W = 4, class BOp, class Pre>
 __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, float *my_part,
                                           floatx4 (&acc)[16], BOp &&bop, Pre &&pre) {
-    constexpr int NC = 16;
+    constexpr int NC = 16, NPW = 16 / W;
     const int lane = threadIdx.x & 63;
     auto issue = [&](int c) {
         float *slot = my_part + (c % kX3Ring) * kX3ChunkFloats;
@@ -66,7 +67,7 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
         // opaque: the unrolled loop would otherwise materialise all 64 piece addresses up front
         asm volatile("" : "+v"(src));
 #pragma unroll
-        for (int q = 0; q < 4; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
+        for (int q = 0; q < NPW; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
     };
     lds_barrier();  // every wave is done with the ring
     issue(0);
@@ -80,8 +81,12 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             const int c = 2 * P + hf;
-            if (c + 1 < NC) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (c + 1 < NC) {  // own part of c landed (c + 1's NPW pieces may not)
+                if constexpr (NPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             block_barrier_raw();
             if (c + 2 < NC) issue(c + 2);
             const float *slot = ring + (c % kX3Ring) * kX3ChunkFloats + lane * 4;
@@ -159,14 +164,21 @@ __device__ __forceinline__ float pair_sum_x16(float a, float b) {
 }
 constexpr int kDppRowMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1;
 
-// LDS of one FD block (floats): [ ring (3 x 16 KiB) | small weights | srw ]; two blocks per CU.
+// LDS of one FD block (floats): [ ring (3 x 16 KiB) | small weights | srw ].
 constexpr int kFdRegion = kX3RingFloats;
+// waves per FD block: 4 (two blocks per CU) or 8 (one block per CU, half the W2 DMA per CU);
+// 2 waves per SIMD either way. A block iteration covers kFdWaves / 4 G2 tiles of 64 rows.
+#ifndef RLP_FD_WAVES
+#define RLP_FD_WAVES 4
+#endif
+constexpr int kFdWaves = RLP_FD_WAVES;
+constexpr int kFdRows = 16 * kFdWaves;
 
 template <int KS1, int A, int LOSS>
-__global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
+__global__ void __launch_bounds__(64 * kFdWaves, 8 / kFdWaves) ppo2_fd_kernel(Ppo2Args g) {
     constexpr int H = kUpdH, SMALL = mlp_small_floats<H, KS1, A>();
     constexpr int NC = 4 * KS1 + 1;  // dW1 columns per neuron: s features | bias
-    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + 4 * 16 * 8];
+    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + kFdWaves * 16 * 8];
     float *ring = lds, *small = lds + kFdRegion;
     float *const srw = lds + kFdRegion + SMALL + (threadIdx.x >> 6) * 128;  // [16 rows][8]
     const MfmaNet &net = g.net;
@@ -178,7 +190,7 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
     const float *info = small + (net.off_info - net.off_w1);
     const float sw = info[0];
     const float k_out = 2.8853900817779268f * info[2];
-    float *const my_part = ring + wv * 4 * 256;
+    float *const my_part = ring + wv * (16 / kFdWaves) * 256;
     float dW3p[A][4];  // neurons 16 e + 4 gq + m (the row butterfly's result)
     float db3p[A];
 #pragma unroll
@@ -195,13 +207,14 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
         for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] = 0.f;
     float g2max = 0.f;
 
-    const int64_t ntiles = (g.rows + kUpdRows - 1) / kUpdRows;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t nbt = (g.rows + kFdRows - 1) / kFdRows;  // block tiles of kFdRows rows
+    for (int64_t bt = blockIdx.x; bt < nbt; bt += gridDim.x) {
+        const int64_t tile = bt * (kFdWaves / 4) + (wv >> 2);  // this wave's 64-row G2 tile
         // opaque per iteration: keeps the 2 x 64 chunk addresses from being hoisted (and spilled)
         const float *Pg = g.packed;
         asm volatile("" : "+s"(Pg));
-        const gptr<float> Xf = as_global(Pg) + net.off_x3 + wv * 4 * 256 + lane * 4;
-        const gptr<float> Xb = as_global(Pg) + net.off_x3t + wv * 4 * 256 + lane * 4;
+        const gptr<float> Xf = as_global(Pg) + net.off_x3 + wv * (16 / kFdWaves) * 256 + lane * 4;
+        const gptr<float> Xb = as_global(Pg) + net.off_x3t + wv * (16 / kFdWaves) * 256 + lane * 4;
         auto *g2base = (__attribute__((address_space(1))) float *)g.g2t;
         asm volatile("" : "+s"(g2base));
         // the small weights are re-read from LDS per use, not hoisted into registers
@@ -213,7 +226,7 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
         const float *B2c = sm + (net.off_b2 - net.off_w1);
         const float *W3c = sm + (net.off_w3 - net.off_w1);
         const float *b3c = sm + (net.off_b3 - net.off_w1);
-        const int64_t r = tile * kUpdRows + 16 * wv + e;
+        const int64_t r = bt * kFdRows + 16 * wv + e;
         const bool valid = r < g.rows;
         const int64_t src = valid ? (g.index ? g.index[r] : r) : 0;
         float bobs[KS1];
@@ -251,7 +264,7 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[j] = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * gq);
         floatx4 p0, p1;  // layer-1 tiles of the next phase (pre), consumed by its B operands (bop)
-        x3_gemm16(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
+        x3_gemm16<false, kFdWaves>(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -351,7 +364,8 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
         // ---- g2 = (W3^T g3) * (1 - h2^2) in place, to HBM in G2's [tile][neuron][64 rows] layout
         // straight from the registers (lane (gq, e): rows 16 wv + e of neurons 16 j + 4 gq + q;
         // each store instruction writes four 64-B row runs)
-        auto *g2row = g2base + tile * kUpdTileFloats + (4 * gq) * kUpdRows + 16 * wv + e;
+        auto *g2row = g2base + tile * kUpdTileFloats + (4 * gq) * kUpdRows + 16 * (wv & 3) + e;
+        const bool tile_ok = tile * kUpdRows < g.rows;  // (8-wave blocks: the last pair's 2nd tile)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             floatx4 w3[A];
@@ -364,7 +378,7 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
                 for (int a = 0; a < A; ++a) dh = __builtin_fmaf(w3[a][q], g3[a], dh);
                 acc[j][q] = dh * (1.f - h * h);
-                g2row[(16 * j + q) * kUpdRows] = acc[j][q];
+                if (tile_ok) g2row[(16 * j + q) * kUpdRows] = acc[j][q];
             }
         }
 
@@ -388,7 +402,7 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) dh1[j] = floatx4{0.f, 0.f, 0.f, 0.f};
         // (operands swapped: dh1 comes out "neuron on lane", dh1[t][q] = row 4 gq + q, neuron 16 t + e)
-        x3_gemm16<true>(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
+        x3_gemm16<true, kFdWaves>(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -444,7 +458,7 @@ __global__ void __launch_bounds__(256, 2) ppo2_fd_kernel(Ppo2Args g) {
     }
 
     // ---- per-wave partials: dW3 (lane's neurons) | db3 summed over the 16 row lanes | dW1 | db1
-    float *out = g.part3 + (size_t)(blockIdx.x * 4 + wv) * (A * H + A + H * S + H);
+    float *out = g.part3 + (size_t)(blockIdx.x * kFdWaves + wv) * (A * H + A + H * S + H);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -797,7 +811,9 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     hipStream_t st = as_stream(stream);
     const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
     const int grid = (int)(tiles < ppo2_grid() ? tiles : ppo2_grid());         // wgrad: 1 per CU
-    const int gfd = (int)(tiles < 2 * ppo2_grid() ? tiles : 2 * ppo2_grid());  // FD: 2 per CU
+    const int64_t fd_tiles = (rows + kFdRows - 1) / kFdRows;
+    const int fd_per_cu = 8 / kFdWaves;  // 2 waves per SIMD
+    const int gfd = (int)(fd_tiles < fd_per_cu * ppo2_grid() ? fd_tiles : fd_per_cu * ppo2_grid());
     const int gfull = ppo2_grid();
     Ppo2Args g{};
     g.packed = packed; g.net = net;
@@ -821,7 +837,7 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     if (hipMemsetAsync(g.g2max, 0, sizeof(unsigned), st) != hipSuccess)
         return fail(RLP_EINVAL, "rlp_ppo2_grad: memset");
     g.loss_sum = loss_sum;
-#define RLP_FD(KS1, A_, L) ppo2_fd_kernel<KS1, A_, L><<<gfd, 256, 0, st>>>(g)
+#define RLP_FD(KS1, A_, L) ppo2_fd_kernel<KS1, A_, L><<<gfd, 64 * kFdWaves, 0, st>>>(g)
     if (actor) {
         if (net.ks1 == 1) {
             if (net.A == 1) RLP_FD(1, 1, 0); else if (net.A == 2) RLP_FD(1, 2, 0); else if (net.A == 3) RLP_FD(1, 3, 0); else RLP_FD(1, 4, 0);
@@ -842,7 +858,7 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     const int64_t total = (int64_t)net.H * net.S + net.H + (int64_t)net.H * net.H + net.H +
                           (int64_t)net.A * net.H + net.A;
     ppo2_reduce_kernel<<<(int)((total + 63) / 64), 64 * kRedSplit, 0, st>>>(net, partw, grid,
-                                                                          g.part3, gfd * 4, grad);
+                                                                          g.part3, gfd * kFdWaves, grad);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (reduce)");
     return RLP_OK;
 }

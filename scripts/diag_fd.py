@@ -30,7 +30,7 @@ NAMES = ["fwd GEMM (+layer1/tanh/split)", "h2 tanh + z3", "loss head g3", "dW3 (
 
 def patch(s):
     s = s.replace("namespace rlp {\n", "namespace rlp {\n__device__ unsigned long long rlp_fd_acc[16384][10];\n", 1)
-    old = "    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {\n"
+    old = "    for (int64_t bt = blockIdx.x; bt < nbt; bt += gridDim.x) {\n"
     assert old in s
     s = s.replace(old, "    unsigned long long dg[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};\n" + old +
                   f"        unsigned long long tp = {ST};\n        dg[9] += 1;\n", 1)
@@ -50,8 +50,8 @@ def patch(s):
         }}
         {{ const unsigned long long tn = {ST}; dg[7] += tn - tp; tp = tn; }}
     }}
-    if (lane == 0 && blockIdx.x * 4 + wv < 16384)
-        for (int q = 0; q < 10; ++q) atomicAdd(&rlp_fd_acc[blockIdx.x * 4 + wv][q], dg[q]);
+    if (lane == 0 && blockIdx.x * kFdWaves + wv < 16384)
+        for (int q = 0; q < 10; ++q) atomicAdd(&rlp_fd_acc[blockIdx.x * kFdWaves + wv][q], dg[q]);
 
     // ---- per-wave partials""", 1)
     s += """
@@ -63,8 +63,11 @@ extern "C" int rlp_diag_fd_read(void *host, long long bytes) {
     return s
 
 
-def build(rev=None, variant="fd"):
-    dr.build(variant, rev, target="rlp_update.hip", patcher=patch)
+def build(rev=None, variant="fd", waves=None):
+    pt = patch
+    if waves:
+        pt = lambda s: patch(s.replace("#define RLP_FD_WAVES 4", f"#define RLP_FD_WAVES {waves}"))
+    dr.build(variant, rev, target="rlp_update.hip", patcher=pt)
 
 
 def run(rev=None, n=65536, T=128, epochs=2, variant="fd"):
@@ -98,9 +101,10 @@ if __name__ == "__main__":
     ap.add_argument("--run", action="store_true")
     ap.add_argument("--rev", default=None)
     ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--waves", type=int, default=None, help="RLP_FD_WAVES of the build (4 | 8)")
     a = ap.parse_args()
-    variant = "fd"
+    variant = "fd" if a.waves is None else f"fd_w{a.waves}"
     if a.build:
-        build(a.rev, variant)
+        build(a.rev, variant, a.waves)
     if a.run:
         run(a.rev, epochs=a.epochs, variant=variant)
