@@ -51,6 +51,20 @@ __device__ __forceinline__ void split2(float2v x, half2v &hi, half2v &lo) {
     lo = __builtin_convertvector(x - __builtin_convertvector(hi, float2v), half2v);
 }
 
+// the same with lo = f16(x - hi) by v_fma_mix (the f16 hi read as a source operand, x - hi exact in
+// f32, one rounding to f16 into the low / high half): bit-identical, 3 VALU ops instead of 5
+// (tools/mix_split_probe.hip checks the identity on the GPU). The PPO2 update's B operands use it
+// (-1.6 % FD cycles); in the rollout the opaque asm costs more in scheduling than it saves (+3 %).
+__device__ __forceinline__ void split2_mix(float2v x, half2v &hi, half2v &lo) {
+    hi = __builtin_convertvector(x, half2v);
+    const unsigned h = __builtin_bit_cast(unsigned, hi);
+    unsigned l = 0;
+    asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+        : "+v"(l) : "v"(h), "v"(x.x), "v"(x.y));
+    lo = __builtin_bit_cast(half2v, l);
+}
+
 constexpr int kX3Waves = 4;             // waves per block sharing the W2 ring
 constexpr int kX3Ring = 3;              // chunks resident in the ring
 constexpr int kX3ChunkFloats = 4096;    // 16 KiB

@@ -134,10 +134,13 @@ __device__ __forceinline__ void wave_sync_lds() {
 
 __device__ __forceinline__ void split8(const float (&x)[8], half8 &bh, half8 &bl) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const _Float16 hi = (_Float16)x[i];
-        bh[i] = hi;
-        bl[i] = (_Float16)(x[i] - (float)hi);
+    for (int i = 0; i < 8; i += 2) {
+        half2v hi, lo;
+        split2_mix((float2v){x[i], x[i + 1]}, hi, lo);
+        bh[i] = hi.x;
+        bh[i + 1] = hi.y;
+        bl[i] = lo.x;
+        bl[i + 1] = lo.y;
     }
 }
 
