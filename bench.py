@@ -35,7 +35,17 @@ PEAK_HBM_GBS = 8000.0
 # the rollout kernel each --physics mode launches (rlp_rollout.hip; the name rocprof reports)
 ROLLOUT_KERNEL = {"shared": "rlp::rollout_sp_kernel<KIND,256,SUB,4>",
                   "shared8": "rlp::rollout_sp_kernel<KIND,256,1,8>",
+                  "cu": "rlp::rollout_sp_kernel<KIND,256,2,8>",
                   "lanes": "rlp::rollout_kernel<KIND,256,SUB,true>"}
+
+
+def rollout_kernel_name(physics, n):
+    """The kernel rlp_rollout runs for `physics` (auto: one 8-wave block per CU when n fills every
+    CU with a 256-env block, include/rlp.h rlp_set_rollout_physics)."""
+    if physics == "auto":
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        physics = "cu" if (n + 255) // 256 >= cus else "shared"
+    return ROLLOUT_KERNEL[physics]
 
 ENVS = {
     "cartpole": (A.RLP_ENV_CARTPOLE, lambda: A.cartpole_params("ppo2"), 3),
@@ -396,9 +406,10 @@ def main():
     ap.add_argument("--ddpg", type=int, default=1, help="also time SOI DDPG with the HBM replay (config 3)")
     ap.add_argument("--oa", type=int, default=1, help="also time UGVForwardObstacleAvoidance env steps (lidar)")
     ap.add_argument("--sac", type=int, default=1, help="also time UGVForwardObstacleAvoidance SAC (config 5 shard)")
-    ap.add_argument("--physics", default="shared", choices=["shared", "shared8", "lanes"],
-                    help="rollout kernel: env state in LDS + full-lane physics waves (4-wave blocks, or "
-                         "8-wave blocks of 16-env waves), or per-wave registers")
+    ap.add_argument("--physics", default="auto", choices=["auto", "shared", "shared8", "cu", "lanes"],
+                    help="rollout kernel: env state in LDS + full-lane physics waves (4-wave blocks, "
+                         "8-wave blocks of 16-env waves, or one 8-wave block per CU; auto: the "
+                         "last when the envs fill every CU), or per-wave registers")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
@@ -423,7 +434,7 @@ def main():
             dist.init_process_group(backend)
     if args.sub:
         _native.set_rollout_sub(args.sub)
-    _native.set_rollout_physics({"lanes": 0, "shared": 1, "shared8": 2}[args.physics])
+    _native.set_rollout_physics({"auto": -1, "lanes": 0, "shared": 1, "shared8": 2, "cu": 3}[args.physics])
     prec = _native.MLP_F16X3 if args.precision == "f16x3" else _native.MLP_FP32
     _native.set_mlp_precision(prec)
 
@@ -480,7 +491,7 @@ def main():
                    "nets": "actor [S,256,256,A] tanh, critic [S,256,256,1]",
                    "parallelism": f"dp{world} (env shards, no data-path collective)",
                    "physics": "f64", "mlp": mlp},
-        "roofline": {"bound": "mfma", "kernel": (ROLLOUT_KERNEL[args.physics] if args.precision == "f16x3"
+        "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(args.physics, n) if args.precision == "f16x3"
                                                 else "rlp::rollout_kernel<KIND,256,SUB,false>"), "achieved": achieved,
                      "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                      "peak_basis": basis, "avg_launch_ms": rollout_ms, "flop_per_launch": flop_launch},
@@ -527,7 +538,7 @@ def main():
             "value": un * uT * usteps * world / uel, "unit": "env-steps/s", "envs_per_gpu": un,
             "global_envs": un * world, "T": uT,
             "config": "UavRobust hover outer loop (6-DoF + FNTSMC), PPO2 [6,256,256,3]",
-            "roofline": {"bound": "mfma", "kernel": (ROLLOUT_KERNEL[args.physics]
+            "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(args.physics, un)
                                                      if args.precision == "f16x3"
                                                      else "rlp::rollout_kernel<KIND,256,SUB,false>"),
                          "achieved": uach, "peak": upeak, "unit": "TFLOP/s", "frac": uach / upeak,

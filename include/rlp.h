@@ -316,7 +316,8 @@ typedef struct rlp_rollout_cfg {
     float a_min[4], a_max[4];
     /* per-call kernel selection; 0 = the library-wide default set by rlp_set_mlp_precision /
      * rlp_set_rollout_physics / rlp_set_rollout_sub, else value + 1 (mlp_precision: 1 RLP_MLP_FP32,
-     * 2 RLP_MLP_F16X3; physics: 1 register-resident, 2 shared, 3 shared 8-wave); sub: 0 default,
+     * 2 RLP_MLP_F16X3; physics: 1 register-resident, 2 shared, 3 shared 8-wave, 4 shared
+     * one-block-per-CU); sub: 0 default,
      * 1, 2, 4 */
     int32_t mlp_precision, physics, sub, reserved;
 } rlp_rollout_cfg;
@@ -458,10 +459,12 @@ int64_t rlp_struct_size(int which);
  * takes 1 when 2 would leave fewer than two blocks per CU, e.g. 32 768 UAV envs), 1 (f16x3 only),
  * 2 or 4. */
 int rlp_set_rollout_sub(int sub);
-/* Tuning knob of rlp_rollout (f16x3 path): 1 = shared-physics kernel (default where its LDS fits:
- * the block's env state in LDS, each step's f64 physics on full 64-lane waves), 2 = the same with
- * 8-wave blocks of 16-env waves (4 waves per SIMD), 0 = the register-resident kernel (physics on
- * the 16*sub lanes of each env's own wave). Same results. */
+/* Tuning knob of rlp_rollout (f16x3 path): -1 = auto (default: 3 when the envs fill every CU with
+ * a 256-env block, else 1), 1 = shared-physics kernel (the block's env state in LDS, each step's
+ * f64 physics on full 64-lane waves; two 4-wave blocks per CU), 2 = the same with
+ * 8-wave blocks of 16-env waves (4 waves per SIMD), 3 = one 8-wave block of 32-env waves per CU
+ * (2 waves per SIMD), 0 = the register-resident kernel (physics on the 16*sub lanes of each env's
+ * own wave). Same results. */
 int rlp_set_rollout_physics(int shared);
 /* Arithmetic of rlp_rollout's hidden layer (the [256 x 256] GEMM, 99 % of its FLOPs):
  *   RLP_MLP_F16X3 (default): error-compensated split, w*x = wh*xh + wh*xl + wl*xh on f16 MFMA with

@@ -213,20 +213,28 @@ constexpr int rollout_sp_lds_bytes() {
     return 4 * (2 * mlp_small_floats<256, KS1, E::A>() + EB * 8 + EB * (E::A + 1) + RG * kX3ChunkFloats) +
            8 * E::D * EB + 2 * EB;
 }
-// two blocks per CU must fit the CU's 160 KiB: a 3-chunk W2 ring where it fits, else 2 (UAV)
+// blocks per CU at two waves per SIMD (W = 8 with 32-env waves: one block per CU)
+template <int SUB, int W>
+constexpr int rollout_sp_blocks_per_cu() { return (W == 8 && SUB == 2) ? 1 : 2; }
+// the CU's 160 KiB split over its blocks: a 3-chunk W2 ring where it fits, else 2 (UAV)
 template <int KIND, int SUB, int W = 4>
 constexpr int rollout_sp_ring() {
-    return rollout_sp_lds_bytes<KIND, SUB, 3, W>() <= 80 * 1024 ? 3
-         : rollout_sp_lds_bytes<KIND, SUB, 2, W>() <= 80 * 1024 ? 2 : 0;
+    constexpr int budget = 160 * 1024 / rollout_sp_blocks_per_cu<SUB, W>();
+    return rollout_sp_lds_bytes<KIND, SUB, 3, W>() <= budget ? 3
+         : rollout_sp_lds_bytes<KIND, SUB, 2, W>() <= budget ? 2 : 0;
 }
 template <int KIND, int SUB>
 constexpr bool rollout_sp_fits() { return SUB <= 2 && rollout_sp_ring<KIND, SUB>() != 0; }
 
 // W = 4: 4-wave blocks, two per CU (2 waves per SIMD, <= 256 registers); W = 8 (SUB = 1): 8-wave
 // blocks, two per CU (4 waves per SIMD, <= 128 registers): twice the waves to hide latency with,
-// each wave 16 envs, the ring shared by 8 waves.
+// each wave 16 envs, the ring shared by 8 waves; W = 8, SUB = 2: ONE 8-wave block per CU (2 waves
+// per SIMD, 256 registers). Two co-resident 4-wave blocks do not share a CU fairly: the SQ's
+// oldest-first issue arbitration lets one run ahead (measured: half the blocks finish their
+// segment in 12.0M cycles, the other half in 16.9M, and the launch waits for the slow half); in
+// one block the barriers keep all eight waves in step.
 template <int KIND, int H, int SUB, int W = 4>
-__global__ void __launch_bounds__(64 * W, W / 2)  // (HIP's second argument: waves per SIMD)
+__global__ void __launch_bounds__(64 * W, SUB == 1 ? W / 2 : 2)  // (HIP's 2nd argument: waves per SIMD)
 rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__restrict__ need_reset,
                   const float *__restrict__ actor, MfmaNet an, const float *__restrict__ critic,
                   MfmaNet cn, RolloutArgs ra, rlp_rollout_bufs b) {
@@ -462,7 +470,7 @@ static int launch_packed_forward(const MfmaNet &net, const float *P, const float
     return RLP_OK;
 }
 
-static int g_rollout_shared_physics = 1;  // rlp_set_rollout_physics
+static int g_rollout_shared_physics = -1;  // rlp_set_rollout_physics (-1: auto)
 
 template <int KIND, int H, int SUB, bool X3>
 static int launch_rollout(const void *params, double *state, uint8_t *need_reset,
@@ -477,6 +485,15 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
         if (physics == 2) {  // 8-wave blocks, 16 envs per wave
             const int blocks8 = (ra.n + 127) / 128;
             rollout_sp_kernel<KIND, H, 1, 8><<<blocks8, 512, 0, stream>>>(p, state, need_reset, actor,
+                                                                         an, critic, cn, ra, b);
+            RLP_CHECK_LAUNCH("rlp_rollout");
+            return RLP_OK;
+        }
+    }
+    if constexpr (X3 && SUB == 2 && rollout_sp_ring<KIND, 2, 8>() != 0) {
+        if (physics == 3) {  // one 8-wave block per CU, 32 envs per wave
+            const int blocks8 = (ra.n + 255) / 256;
+            rollout_sp_kernel<KIND, H, 2, 8><<<blocks8, 512, 0, stream>>>(p, state, need_reset, actor,
                                                                          an, critic, cn, ra, b);
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
@@ -509,18 +526,21 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
     if (an.H != 256 || cn.H != 256)
         return fail(RLP_EUNSUPPORTED, "rlp_rollout: hidden width %d/%d (built for 256)", an.H, cn.H);
     if (prec == RLP_MLP_F16X3) {
-        if (physics == 2) sub = 1;  // the 8-wave variant runs 16-env waves
-        if (sub == 0) {  // auto: 32-env waves unless that leaves fewer than 2 blocks per CU
-            static int cus = 0;
-            if (cus == 0) {
-                int dev = 0;
-                if (hipGetDevice(&dev) != hipSuccess ||
-                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                        hipSuccess || cus <= 0)
-                    cus = 256;
-            }
-            sub = (ra.n + 127) / 128 < 2 * cus ? 1 : 2;
+        static int cus = 0;
+        if (cus == 0) {
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                    hipSuccess || cus <= 0)
+                cus = 256;
         }
+        if (physics < 0)  // auto: one 8-wave block per CU when the envs fill every CU, else 4-wave
+            physics = (sub == 0 || sub == 2) && (ra.n + 255) / 256 >= cus &&
+                              rollout_sp_ring<KIND, 2, 8>() != 0 ? 3 : 1;
+        if (physics == 2) sub = 1;  // the 8-wave variant runs 16-env waves
+        if (physics == 3) sub = 2;  // the one-block-per-CU variant runs 32-env waves
+        if (sub == 0)  // auto: 32-env waves unless that leaves fewer than 2 blocks per CU
+            sub = (ra.n + 127) / 128 < 2 * cus ? 1 : 2;
         if (sub == 1)
             return launch_rollout<KIND, 256, 1, true>(params, state, need_reset, actor, an, critic,
                                                       cn, ra, b, physics, stream);
@@ -561,7 +581,7 @@ int rlp_get_mlp_precision(void) { return g_mlp_precision; }
 // tuning knob: 1 (default) = the shared-physics f16x3 kernel where its LDS fits (full-lane
 // physics), 0 = the register-resident kernel
 int rlp_set_rollout_physics(int shared) {
-    if (shared < 0 || shared > 2) return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
+    if (shared < -1 || shared > 3) return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
     g_rollout_shared_physics = shared;
     return RLP_OK;
 }
@@ -628,7 +648,7 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
     hipStream_t s = as_stream(stream);
     // per-call selections (cfg, 0 = the library-wide default of the rlp_set_* knobs)
     RLP_REQUIRE(cfg->mlp_precision >= 0 && cfg->mlp_precision <= 2 && cfg->physics >= 0 &&
-                    cfg->physics <= 3 && (cfg->sub == 0 || cfg->sub == 1 || cfg->sub == 2 ||
+                    cfg->physics <= 4 && (cfg->sub == 0 || cfg->sub == 1 || cfg->sub == 2 ||
                                           cfg->sub == 4),
                 "rlp_rollout: cfg mlp_precision=%d physics=%d sub=%d", cfg->mlp_precision,
                 cfg->physics, cfg->sub);

@@ -21,13 +21,15 @@ STAMP = "__builtin_amdgcn_s_memtime()"
 
 def patch(src):
     s = src
-    s = s.replace("namespace rlp {\n", "namespace rlp {\n__device__ unsigned long long rlp_diag_acc[65536][6];\n", 1)
+    s = s.replace("namespace rlp {\n", "namespace rlp {\n__device__ unsigned long long rlp_diag_acc[65536][9];\n", 1)
     old = """    for (int t = 0; t < ra.T; ++t) {
         const uint64_t gstep = ra.step0 + (uint64_t)t;
         mlp_pass(true);
         asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");  // (mean, V) of every env
         if (wave / PW == t % ROT) {  // this step's physics waves"""
-    new = """    unsigned long long dg[6] = {0, 0, 0, 0, 0, 0};
+    new = """    unsigned long long dg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    dg[6] = __builtin_amdgcn_s_memrealtime();
+    dg[8] = __smid();
     for (int t = 0; t < ra.T; ++t) {
         const uint64_t gstep = ra.step0 + (uint64_t)t;
         const unsigned long long t0 = %s;
@@ -55,8 +57,9 @@ def patch(src):
         dg[3] += t4 - t3;
     }
     dg[5] = ra.T;
+    dg[7] = __builtin_amdgcn_s_memrealtime();
     if (lane == 0)
-        for (int q = 0; q < 6; ++q) rlp_diag_acc[blockIdx.x * W + wave][q] = dg[q];""" % (STAMP, STAMP)
+        for (int q = 0; q < 9; ++q) rlp_diag_acc[blockIdx.x * W + wave][q] = dg[q];""" % (STAMP, STAMP)
     assert old in s, "stamp site 2"
     s = s.replace(old, new)
     s += """
@@ -143,7 +146,7 @@ def run(n, T, iters, variant="base", sub=0, physics=1, rev=None):
     for _ in range(iters):
         seg.rollout()
         torch.cuda.synchronize()
-        buf = np.zeros((65536, 6), np.uint64)
+        buf = np.zeros((65536, 9), np.uint64)
         lib = ctypes.CDLL(LIB)
         assert lib.rlp_diag_read(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_longlong(buf.nbytes)) == 0
         es = sub or (2 if (n + 127) // 128 >= 512 else 1)     # rlp_rollout's auto choice
@@ -159,6 +162,27 @@ def run(n, T, iters, variant="base", sub=0, physics=1, rev=None):
     print(f"  physics (its waves)     {phys_per.mean():9.0f}  per physics turn; share {nphys.mean():.2f}")
     print(f"  barrier after physics   {bar2.mean():9.0f}")
     print(f"  step total              {(mlp + bar1 + phys + bar2).mean():9.0f}")
+    # block start / end on the 100 MHz real-time clock (last iteration), per wave 0 of each block
+    b = res[-1][:nw].astype(np.float64)
+    w0 = b[::4] if nw % 4 == 0 else b
+    st, en = (w0[:, 6] - w0[:, 6].min()) / 100.0, (w0[:, 7] - w0[:, 6].min()) / 100.0   # us
+    dur = en - st
+    print(f"  blocks: start spread {st.max():.1f} us (p50 {np.median(st):.1f}), end min {en.min():.1f} "
+          f"p50 {np.median(en):.1f} max {en.max():.1f} us; duration min {dur.min():.1f} p50 "
+          f"{np.median(dur):.1f} max {dur.max():.1f} us")
+    tot = (b[:, 0] + b[:, 1] + b[:, 2] + b[:, 3])
+    hw = b[:, 8].astype(np.int64)
+    print(f"  per-wave loop cycles: min {tot.min():.0f} p10 {np.percentile(tot, 10):.0f} p50 {np.median(tot):.0f} "
+          f"p90 {np.percentile(tot, 90):.0f} max {tot.max():.0f}")
+    np.save(os.path.join(ROOT, "gpurun_out", f"diag_waves_{variant}.npy"), b)
+    try:   # by XCD (HW_ID's SE bits vary by ISA; report the raw low bits' grouping as a hint)
+        import collections
+        grp = collections.defaultdict(list)
+        for h, t in zip(hw, tot):
+            grp[int(h) % 8].append(t)
+        print("  loop cycles by __smid() % 8:", {k: round(float(np.mean(v))) for k, v in sorted(grp.items())})
+    except Exception as ex:
+        print("  smid grouping failed:", ex)
 
 
 if __name__ == "__main__":
