@@ -169,13 +169,19 @@ constexpr int kDppRowMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kD
 
 // LDS of one FD block (floats): [ ring (3 x 16 KiB) | small weights | srw ].
 constexpr int kFdRegion = kX3RingFloats;
-// waves per FD block: 4 (two blocks per CU) or 8 (one block per CU, half the W2 DMA per CU);
-// 2 waves per SIMD either way. A block iteration covers kFdWaves / 4 G2 tiles of 64 rows.
+// waves per FD block: 8 (default: one block per CU, half the W2 DMA per CU) or 4 (two blocks per
+// CU); 2 waves per SIMD either way. A block iteration covers kFdWaves / 4 G2 tiles of 64 rows.
+// The 8-wave block is ~2 % slower per wave tile (diag_fd.py: its barriers span 8 waves) but 4-5 %
+// faster per launch: two co-resident 4-wave blocks do not get equal shares of the CU (oldest-first
+// issue arbitration) and the launch waits for the slower half; a tile queue (atomic counter)
+// instead of the static grid stride recovered only half of that (rocprof A/B,
+// scripts/ab_fdwaves.sh).
 #ifndef RLP_FD_WAVES
-#define RLP_FD_WAVES 4
+#define RLP_FD_WAVES 8
 #endif
 constexpr int kFdWaves = RLP_FD_WAVES;
 constexpr int kFdRows = 16 * kFdWaves;
+
 
 template <int KS1, int A, int LOSS>
 __global__ void __launch_bounds__(64 * kFdWaves, 8 / kFdWaves) ppo2_fd_kernel(Ppo2Args g) {

@@ -66,7 +66,7 @@ extern "C" int rlp_diag_fd_read(void *host, long long bytes) {
 def build(rev=None, variant="fd", waves=None):
     pt = patch
     if waves:
-        pt = lambda s: patch(s.replace("#define RLP_FD_WAVES 4", f"#define RLP_FD_WAVES {waves}"))
+        pt = lambda s: patch(s.replace("#define RLP_FD_WAVES 8", f"#define RLP_FD_WAVES {waves}"))
     dr.build(variant, rev, target="rlp_update.hip", patcher=pt)
 
 
