@@ -36,6 +36,7 @@ PEAK_HBM_GBS = 8000.0
 ROLLOUT_KERNEL = {"shared": "rlp::rollout_sp_kernel<KIND,256,SUB,4>",
                   "shared8": "rlp::rollout_sp_kernel<KIND,256,1,8>",
                   "cu": "rlp::rollout_sp_kernel<KIND,256,2,8>",
+                  "cu16": "rlp::rollout_sp_kernel<KIND,256,1,8,2>",
                   "lanes": "rlp::rollout_kernel<KIND,256,SUB,true>"}
 
 
@@ -406,10 +407,10 @@ def main():
     ap.add_argument("--ddpg", type=int, default=1, help="also time SOI DDPG with the HBM replay (config 3)")
     ap.add_argument("--oa", type=int, default=1, help="also time UGVForwardObstacleAvoidance env steps (lidar)")
     ap.add_argument("--sac", type=int, default=1, help="also time UGVForwardObstacleAvoidance SAC (config 5 shard)")
-    ap.add_argument("--physics", default="auto", choices=["auto", "shared", "shared8", "cu", "lanes"],
+    ap.add_argument("--physics", default="auto", choices=["auto", "shared", "shared8", "cu", "cu16", "lanes"],
                     help="rollout kernel: env state in LDS + full-lane physics waves (4-wave blocks, "
-                         "8-wave blocks of 16-env waves, or one 8-wave block per CU; auto: the "
-                         "last when the envs fill every CU), or per-wave registers")
+                         "8-wave blocks of 16-env waves, or one 8-wave block of 32- / 16-env waves "
+                         "per CU; auto: those when the envs fill every CU), or per-wave registers")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
@@ -434,7 +435,7 @@ def main():
             dist.init_process_group(backend)
     if args.sub:
         _native.set_rollout_sub(args.sub)
-    _native.set_rollout_physics({"auto": -1, "lanes": 0, "shared": 1, "shared8": 2, "cu": 3}[args.physics])
+    _native.set_rollout_physics({"auto": -1, "lanes": 0, "shared": 1, "shared8": 2, "cu": 3, "cu16": 4}[args.physics])
     prec = _native.MLP_F16X3 if args.precision == "f16x3" else _native.MLP_FP32
     _native.set_mlp_precision(prec)
 

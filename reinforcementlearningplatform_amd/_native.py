@@ -125,7 +125,8 @@ def set_rollout_sub(sub):
 
 
 def set_rollout_physics(shared):
-    """-1: auto (default: 3 when the envs fill every CU, else 1), 1: shared-physics rollout kernel
-    (two 4-wave blocks per CU), 2: 8-wave blocks of 16-env waves, 3: one 8-wave block of 32-env
-    waves per CU, 0: register-resident kernel."""
+    """-1: auto (default: 3 when the envs fill every CU, else 1), 1: shared-physics rollout
+    kernel (two 4-wave blocks per CU), 2: 8-wave blocks of 16-env waves (4 waves per SIMD), 3: one
+    8-wave block of 32-env waves per CU, 4: one 8-wave block of 16-env waves per CU, 0:
+    register-resident kernel."""
     check(lib().rlp_set_rollout_physics(int(shared)), "rlp_set_rollout_physics")

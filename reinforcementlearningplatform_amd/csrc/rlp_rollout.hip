@@ -213,13 +213,17 @@ constexpr int rollout_sp_lds_bytes() {
     return 4 * (2 * mlp_small_floats<256, KS1, E::A>() + EB * 8 + EB * (E::A + 1) + RG * kX3ChunkFloats) +
            8 * E::D * EB + 2 * EB;
 }
-// blocks per CU at two waves per SIMD (W = 8 with 32-env waves: one block per CU)
+// waves per SIMD of a variant: 4-wave blocks 2; 8-wave blocks of 32-env waves 2 (one block per
+// CU); 8-wave blocks of 16-env waves 4 (two blocks per CU, <= 128 registers) or, with WPS = 2, 2
+// (one block per CU, 256 registers)
 template <int SUB, int W>
-constexpr int rollout_sp_blocks_per_cu() { return (W == 8 && SUB == 2) ? 1 : 2; }
+constexpr int rollout_sp_default_wps() { return SUB == 1 ? W / 2 : 2; }
+template <int SUB, int W, int WPS>
+constexpr int rollout_sp_blocks_per_cu() { return 4 * WPS / W; }
 // the CU's 160 KiB split over its blocks: a 3-chunk W2 ring where it fits, else 2 (UAV)
-template <int KIND, int SUB, int W = 4>
+template <int KIND, int SUB, int W = 4, int WPS = rollout_sp_default_wps<SUB, W>()>
 constexpr int rollout_sp_ring() {
-    constexpr int budget = 160 * 1024 / rollout_sp_blocks_per_cu<SUB, W>();
+    constexpr int budget = 160 * 1024 / rollout_sp_blocks_per_cu<SUB, W, WPS>();
     return rollout_sp_lds_bytes<KIND, SUB, 3, W>() <= budget ? 3
          : rollout_sp_lds_bytes<KIND, SUB, 2, W>() <= budget ? 2 : 0;
 }
@@ -233,8 +237,8 @@ constexpr bool rollout_sp_fits() { return SUB <= 2 && rollout_sp_ring<KIND, SUB>
 // oldest-first issue arbitration lets one run ahead (measured: half the blocks finish their
 // segment in 12.0M cycles, the other half in 16.9M, and the launch waits for the slow half); in
 // one block the barriers keep all eight waves in step.
-template <int KIND, int H, int SUB, int W = 4>
-__global__ void __launch_bounds__(64 * W, SUB == 1 ? W / 2 : 2)  // (HIP's 2nd argument: waves per SIMD)
+template <int KIND, int H, int SUB, int W = 4, int WPS = rollout_sp_default_wps<SUB, W>()>
+__global__ void __launch_bounds__(64 * W, WPS)  // (HIP's second argument: waves per SIMD)
 rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__restrict__ need_reset,
                   const float *__restrict__ actor, MfmaNet an, const float *__restrict__ critic,
                   MfmaNet cn, RolloutArgs ra, rlp_rollout_bufs b) {
@@ -242,7 +246,7 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
     constexpr int S = E::S, A = E::A, D = E::D, KS1 = (S + 3) / 4, WENV = 16 * SUB;
     constexpr int WAVES = W, EB = WAVES * WENV, PW = EB / 64, ROT = WAVES / PW;
     static_assert(EB % 64 == 0, "physics waves are full: EB must be a multiple of 64");
-    constexpr int SMALL = mlp_small_floats<H, KS1, A>(), RG = rollout_sp_ring<KIND, SUB, W>();
+    constexpr int SMALL = mlp_small_floats<H, KS1, A>(), RG = rollout_sp_ring<KIND, SUB, W, WPS>();
     __shared__ __attribute__((aligned(16))) float lds[2 * SMALL + EB * 8 + EB * (A + 1) + RG * kX3ChunkFloats];
     __shared__ double st[D][EB];
     __shared__ uint8_t s_need[EB], s_pdone[EB];
@@ -490,6 +494,15 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
             return RLP_OK;
         }
     }
+    if constexpr (X3 && SUB == 1 && rollout_sp_ring<KIND, 1, 8, 2>() != 0) {
+        if (physics == 4) {  // one 8-wave block of 16-env waves per CU (2 waves per SIMD)
+            const int blocks8 = (ra.n + 127) / 128;
+            rollout_sp_kernel<KIND, H, 1, 8, 2><<<blocks8, 512, 0, stream>>>(p, state, need_reset,
+                                                                            actor, an, critic, cn, ra, b);
+            RLP_CHECK_LAUNCH("rlp_rollout");
+            return RLP_OK;
+        }
+    }
     if constexpr (X3 && SUB == 2 && rollout_sp_ring<KIND, 2, 8>() != 0) {
         if (physics == 3) {  // one 8-wave block per CU, 32 envs per wave
             const int blocks8 = (ra.n + 255) / 256;
@@ -534,10 +547,13 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
                     hipSuccess || cus <= 0)
                 cus = 256;
         }
-        if (physics < 0)  // auto: one 8-wave block per CU when the envs fill every CU, else 4-wave
+        // auto: one 8-wave block of 32-env waves per CU where the envs fill every CU; else two
+        // 4-wave blocks (one 8-wave block of 16-env waves, mode 4, measured the same on the UAV
+        // shard: that kernel is bound by its physics' register spills, not by co-residency)
+        if (physics < 0)
             physics = (sub == 0 || sub == 2) && (ra.n + 255) / 256 >= cus &&
                               rollout_sp_ring<KIND, 2, 8>() != 0 ? 3 : 1;
-        if (physics == 2) sub = 1;  // the 8-wave variant runs 16-env waves
+        if (physics == 2 || physics == 4) sub = 1;  // the 8-wave variants of 16-env waves
         if (physics == 3) sub = 2;  // the one-block-per-CU variant runs 32-env waves
         if (sub == 0)  // auto: 32-env waves unless that leaves fewer than 2 blocks per CU
             sub = (ra.n + 127) / 128 < 2 * cus ? 1 : 2;
@@ -581,7 +597,7 @@ int rlp_get_mlp_precision(void) { return g_mlp_precision; }
 // tuning knob: 1 (default) = the shared-physics f16x3 kernel where its LDS fits (full-lane
 // physics), 0 = the register-resident kernel
 int rlp_set_rollout_physics(int shared) {
-    if (shared < -1 || shared > 3) return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
+    if (shared < -1 || shared > 4) return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
     g_rollout_shared_physics = shared;
     return RLP_OK;
 }
@@ -648,7 +664,7 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
     hipStream_t s = as_stream(stream);
     // per-call selections (cfg, 0 = the library-wide default of the rlp_set_* knobs)
     RLP_REQUIRE(cfg->mlp_precision >= 0 && cfg->mlp_precision <= 2 && cfg->physics >= 0 &&
-                    cfg->physics <= 4 && (cfg->sub == 0 || cfg->sub == 1 || cfg->sub == 2 ||
+                    cfg->physics <= 5 && (cfg->sub == 0 || cfg->sub == 1 || cfg->sub == 2 ||
                                           cfg->sub == 4),
                 "rlp_rollout: cfg mlp_precision=%d physics=%d sub=%d", cfg->mlp_precision,
                 cfg->physics, cfg->sub);

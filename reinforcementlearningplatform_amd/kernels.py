@@ -154,7 +154,8 @@ def rollout(kind, params, state, need_reset, actor_desc, actor_packed, critic_de
 def make_rollout_cfg(T, n, seed, step0, env_id0, std, a_min, a_max, success_rule, success_flag,
                      mlp_precision=None, physics=None, sub=None):
     """rlp_rollout_cfg. mlp_precision (RLP_MLP_FP32 | RLP_MLP_F16X3), physics (0 register-resident,
-    1 shared, 2 shared 8-wave, 3 shared one-block-per-CU) and sub (1 | 2 | 4) select the kernel for
+    1 shared, 2 shared 8-wave, 3 / 4 shared one-block-per-CU of 32- / 16-env waves) and sub
+    (1 | 2 | 4) select the kernel for
     this call only; None
     keeps the library-wide defaults (rlp_set_*)."""
     cfg = _abi.RolloutCfg()

@@ -126,7 +126,7 @@ def build(variant="base", rev=None, target="rlp_rollout.hip", patcher=None):
     print("built", lib_path(variant, rev))
 
 
-def run(n, T, iters, variant="base", sub=0, physics=1, rev=None):
+def run(n, T, iters, variant="base", sub=0, physics=1, rev=None, env="cartpole"):
     LIB = lib_path(variant, rev)
     os.environ["RLP_LIBRARY"] = LIB
     sys.path.insert(0, ROOT)
@@ -138,7 +138,7 @@ def run(n, T, iters, variant="base", sub=0, physics=1, rev=None):
     if sub:
         _native.set_rollout_sub(sub)
     _native.set_rollout_physics(physics)
-    seg = bench.Segment("cartpole", n, T, 3407, 0)
+    seg = bench.Segment(env, n, T, 3407, 0)
     for _ in range(2):
         seg.rollout()
     torch.cuda.synchronize()
@@ -195,10 +195,11 @@ if __name__ == "__main__":
     ap.add_argument("--variant", default="base", choices=sorted(VARIANTS) + ["all"])
     ap.add_argument("--sub", type=int, default=0)
     ap.add_argument("--rev", default=None, help="build / run the native tree of this git revision")
+    ap.add_argument("--env", default="cartpole")
     ap.add_argument("--physics", type=int, default=1, help="rlp_set_rollout_physics (3: 32x32x16 MLP)")
     a = ap.parse_args()
     if a.build:
         for v in (VARIANTS if a.variant == "all" else [a.variant]):
             build(v, a.rev)
     if a.run:
-        run(a.n, a.T, a.iters, a.variant, a.sub, a.physics, a.rev)
+        run(a.n, a.T, a.iters, a.variant, a.sub, a.physics, a.rev, a.env)
