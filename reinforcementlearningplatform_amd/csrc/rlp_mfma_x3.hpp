@@ -77,8 +77,8 @@ __device__ __forceinline__ void block_barrier_raw() {
 }
 
 // Every wave of the block must call this the same number of times (it contains block barriers).
-// RG: chunks in the ring (3: two in flight while one is read; 2: one in flight, for kernels whose
-// other LDS leaves no room for a third 16-KiB slot).
+// RG: chunks in the ring (RG - 1 in flight while one is read: 3 for two blocks per CU, 2 where the
+// other LDS leaves no room for a third 16-KiB slot, 4 for one block per CU).
 // W: waves of the block sharing the ring (4 or 8); each DMAs 16 / W of the 16 KiB of every chunk.
 template <int H, int SUB, int KS1, int NOUT, int RG = kX3Ring, int W = kX3Waves>
 __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, const float *small,
@@ -103,7 +103,7 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
     const float *info = small + (net.off_info - net.off_w1);
     const float k_out = 2.8853900817779268f * info[2];  // exp(2x) constant with 2^-(sw+SH) folded
 
-    static_assert(RG == 2 || RG == 3, "ring of 2 or 3 chunks");
+    static_assert(RG >= 2 && RG <= 4, "ring of 2 to 4 chunks");
     auto issue = [&](int c) {
         float *slot = my_part + (c % RG) * kX3ChunkFloats;
         const gptr<float> src = X + c * kX3ChunkFloats;
@@ -111,8 +111,8 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
         for (int q = 0; q < NPW; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
     };
     block_barrier_raw();  // every wave is done reading the ring (previous call)
-    issue(0);
-    if (RG == 3) issue(1);
+#pragma unroll
+    for (int c = 0; c < RG - 1; ++c) issue(c);
 
     floatx4 acc[SUB][NT];
 #pragma unroll
@@ -167,12 +167,12 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             const int c = 2 * P + hf;
-            if (RG == 3 && c + 1 < NC) {  // own part of c landed (c + 1's NPW pieces may not)
-                if constexpr (NPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+            // own part of c landed; the younger chunks' pieces (up to RG - 2 chunks) may not
+            const int ahead = (RG - 2 < NC - 1 - c ? RG - 2 : NC - 1 - c) * NPW;
+            if (ahead >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (ahead >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else if (ahead >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             block_barrier_raw();  // all parts of c landed; everyone is done with chunk c - 1
             if (c + RG - 1 < NC) issue(c + RG - 1);  // into chunk c - 1's slot
             const float *slot = ring + (c % RG) * kX3ChunkFloats + lane * 4;

@@ -213,6 +213,9 @@ constexpr int rollout_sp_lds_bytes() {
     return 4 * (2 * mlp_small_floats<256, KS1, E::A>() + EB * 8 + EB * (E::A + 1) + RG * kX3ChunkFloats) +
            8 * E::D * EB + 2 * EB;
 }
+#ifndef RLP_SP_RING1
+#define RLP_SP_RING1 3  // W2 ring chunks of the one-block-per-CU variants (4 measured 1 % slower)
+#endif
 // waves per SIMD of a variant: 4-wave blocks 2; 8-wave blocks of 32-env waves 2 (one block per
 // CU); 8-wave blocks of 16-env waves 4 (two blocks per CU, <= 128 registers) or, with WPS = 2, 2
 // (one block per CU, 256 registers)
@@ -223,8 +226,9 @@ constexpr int rollout_sp_blocks_per_cu() { return 4 * WPS / W; }
 // the CU's 160 KiB split over its blocks: a 3-chunk W2 ring where it fits, else 2 (UAV)
 template <int KIND, int SUB, int W = 4, int WPS = rollout_sp_default_wps<SUB, W>()>
 constexpr int rollout_sp_ring() {
-    constexpr int budget = 160 * 1024 / rollout_sp_blocks_per_cu<SUB, W, WPS>();
-    return rollout_sp_lds_bytes<KIND, SUB, 3, W>() <= budget ? 3
+    constexpr int bpc = rollout_sp_blocks_per_cu<SUB, W, WPS>(), budget = 160 * 1024 / bpc;
+    return bpc == 1 && rollout_sp_lds_bytes<KIND, SUB, 4, W>() <= budget ? RLP_SP_RING1
+         : rollout_sp_lds_bytes<KIND, SUB, 3, W>() <= budget ? 3
          : rollout_sp_lds_bytes<KIND, SUB, 2, W>() <= budget ? 2 : 0;
 }
 template <int KIND, int SUB>
