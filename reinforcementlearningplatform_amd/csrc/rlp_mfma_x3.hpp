@@ -80,7 +80,9 @@ __device__ __forceinline__ void block_barrier_raw() {
 // RG: chunks in the ring (RG - 1 in flight while one is read: 3 for two blocks per CU, 2 where the
 // other LDS leaves no room for a third 16-KiB slot, 4 for one block per CU).
 // W: waves of the block sharing the ring (4 or 8); each DMAs 16 / W of the 16 KiB of every chunk.
-template <int H, int SUB, int KS1, int NOUT, int RG = kX3Ring, int W = kX3Waves>
+// CPB: 16-KiB chunks per ring slot and block barrier (2: one barrier per k-phase instead of per
+// half-phase; the ring then holds RG x CPB chunks).
+template <int H, int SUB, int KS1, int NOUT, int RG = kX3Ring, int W = kX3Waves, int CPB = 1>
 __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, const float *small,
                                                float *ring, const MfmaNet &net, const int nout,
                                                const float (&bobs)[SUB][KS1],
@@ -103,16 +105,21 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
     const float *info = small + (net.off_info - net.off_w1);
     const float k_out = 2.8853900817779268f * info[2];  // exp(2x) constant with 2^-(sw+SH) folded
 
-    static_assert(RG >= 2 && RG <= 4, "ring of 2 to 4 chunks");
-    auto issue = [&](int c) {
-        float *slot = my_part + (c % RG) * kX3ChunkFloats;
-        const gptr<float> src = X + c * kX3ChunkFloats;
+    static_assert(RG >= 2 && RG <= 4, "ring of 2 to 4 slots");
+    static_assert(CPB == 1 || CPB == 2, "1 or 2 chunks per slot");
+    constexpr int NS = NC / CPB;  // ring slots' worth of chunks per pass
+    auto issue = [&](int sc) {    // slot-sized group sc (chunks CPB sc .. CPB sc + CPB - 1)
 #pragma unroll
-        for (int q = 0; q < NPW; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
+        for (int cc = 0; cc < CPB; ++cc) {
+            float *slot = my_part + ((sc % RG) * CPB + cc) * kX3ChunkFloats;
+            const gptr<float> src = X + (sc * CPB + cc) * kX3ChunkFloats;
+#pragma unroll
+            for (int q = 0; q < NPW; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
+        }
     };
     block_barrier_raw();  // every wave is done reading the ring (previous call)
 #pragma unroll
-    for (int c = 0; c < RG - 1; ++c) issue(c);
+    for (int sc = 0; sc < RG - 1; ++sc) issue(sc);
 
     floatx4 acc[SUB][NT];
 #pragma unroll
@@ -167,15 +174,18 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             const int c = 2 * P + hf;
-            // own part of c landed; the younger chunks' pieces (up to RG - 2 chunks) may not
-            const int ahead = (RG - 2 < NC - 1 - c ? RG - 2 : NC - 1 - c) * NPW;
-            if (ahead >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else if (ahead >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else if (ahead >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            block_barrier_raw();  // all parts of c landed; everyone is done with chunk c - 1
-            if (c + RG - 1 < NC) issue(c + RG - 1);  // into chunk c - 1's slot
-            const float *slot = ring + (c % RG) * kX3ChunkFloats + lane * 4;
+            if (c % CPB == 0) {
+                const int sc = c / CPB;
+                // own part of slot group sc landed; the younger groups' pieces (up to RG - 2) may not
+                const int ahead = (RG - 2 < NS - 1 - sc ? RG - 2 : NS - 1 - sc) * NPW * CPB;
+                if (ahead >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else if (ahead >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else if (ahead >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                block_barrier_raw();  // all parts of sc landed; everyone is done with group sc - 1
+                if (sc + RG - 1 < NS) issue(sc + RG - 1);  // into group sc - 1's slot
+            }
+            const float *slot = ring + (((c / CPB) % RG) * CPB + c % CPB) * kX3ChunkFloats + lane * 4;
             // fragments one output tile ahead: tile jj + 1's two reads are issued before tile
             // jj's MFMAs, so an LDS round trip is not exposed per tile (the default schedule
             // reads each pair right before its MFMAs and waits for it)

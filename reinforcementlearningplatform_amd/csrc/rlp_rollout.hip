@@ -214,7 +214,10 @@ constexpr int rollout_sp_lds_bytes() {
            8 * E::D * EB + 2 * EB;
 }
 #ifndef RLP_SP_RING1
-#define RLP_SP_RING1 3  // W2 ring chunks of the one-block-per-CU variants (4 measured 1 % slower)
+#define RLP_SP_RING1 3  // W2 ring slots of the one-block-per-CU variants (4 measured 1 % slower)
+#endif
+#ifndef RLP_SP_CPB1
+#define RLP_SP_CPB1 2   // 16-KiB chunks per ring slot / block barrier there (one barrier per k-phase)
 #endif
 // waves per SIMD of a variant: 4-wave blocks 2; 8-wave blocks of 32-env waves 2 (one block per
 // CU); 8-wave blocks of 16-env waves 4 (two blocks per CU, <= 128 registers) or, with WPS = 2, 2
@@ -227,7 +230,8 @@ constexpr int rollout_sp_blocks_per_cu() { return 4 * WPS / W; }
 template <int KIND, int SUB, int W = 4, int WPS = rollout_sp_default_wps<SUB, W>()>
 constexpr int rollout_sp_ring() {
     constexpr int bpc = rollout_sp_blocks_per_cu<SUB, W, WPS>(), budget = 160 * 1024 / bpc;
-    return bpc == 1 && rollout_sp_lds_bytes<KIND, SUB, 4, W>() <= budget ? RLP_SP_RING1
+    return bpc == 1 && rollout_sp_lds_bytes<KIND, SUB, RLP_SP_RING1 * RLP_SP_CPB1, W>() <= budget
+               ? RLP_SP_RING1
          : rollout_sp_lds_bytes<KIND, SUB, 3, W>() <= budget ? 3
          : rollout_sp_lds_bytes<KIND, SUB, 2, W>() <= budget ? 2 : 0;
 }
@@ -251,7 +255,11 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
     constexpr int WAVES = W, EB = WAVES * WENV, PW = EB / 64, ROT = WAVES / PW;
     static_assert(EB % 64 == 0, "physics waves are full: EB must be a multiple of 64");
     constexpr int SMALL = mlp_small_floats<H, KS1, A>(), RG = rollout_sp_ring<KIND, SUB, W, WPS>();
-    __shared__ __attribute__((aligned(16))) float lds[2 * SMALL + EB * 8 + EB * (A + 1) + RG * kX3ChunkFloats];
+    // one block per CU: ring slots of RLP_SP_CPB1 chunks (fewer block barriers per k-phase)
+    constexpr int CPB = rollout_sp_blocks_per_cu<SUB, W, WPS>() == 1 &&
+                                rollout_sp_lds_bytes<KIND, SUB, RG * RLP_SP_CPB1, W>() <= 160 * 1024
+                            ? RLP_SP_CPB1 : 1;
+    __shared__ __attribute__((aligned(16))) float lds[2 * SMALL + EB * 8 + EB * (A + 1) + RG * CPB * kX3ChunkFloats];
     __shared__ double st[D][EB];
     __shared__ uint8_t s_need[EB], s_pdone[EB];
     float *small_a = lds, *small_c = lds + SMALL;
@@ -300,7 +308,7 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
 #pragma unroll 1
         for (int which = both ? 0 : 1; which < 2; ++which) {
             float out[SUB][A];
-            mlp_x3_forward<H, SUB, KS1, A, RG, W>(which ? critic : actor, which ? small_c : small_a,
+            mlp_x3_forward<H, SUB, KS1, A, RG, W, CPB>(which ? critic : actor, which ? small_c : small_a,
                                                   ring, which ? cn : an, which ? 1 : A, bobs, out);
             // lane (sub-block g, env e) owns out[g]
             float sel[A];
