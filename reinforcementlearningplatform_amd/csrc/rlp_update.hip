@@ -55,19 +55,23 @@ __device__ __forceinline__ void lds_barrier() {
 // pre(P) runs at the head of phase P - 1, so its results (the forward's layer-1 MFMAs) are ready
 // when bop(P) needs them half a phase later (diag_fd.py: -1.2k cycles per tile; pinning bop's VALU
 // between the second chunk's MFMAs with sched_group_barrier measured within noise).
-// W: waves of the block sharing the ring (each DMAs 16 / W KiB of every chunk).
-template <bool SWAP = false, int W = 4, class BOp, class Pre>
+// W: waves of the block sharing the ring (each DMAs 16 / W KiB of every chunk). CPB: 16-KiB
+// chunks per ring slot and block barrier (the ring holds kX3Ring x CPB chunks).
+template <bool SWAP = false, int W = 4, int CPB = 1, class BOp, class Pre>
 __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, float *my_part,
                                           floatx4 (&acc)[16], BOp &&bop, Pre &&pre) {
-    constexpr int NC = 16, NPW = 16 / W;
+    constexpr int NC = 16, NPW = 16 / W, NS = NC / CPB;
     const int lane = threadIdx.x & 63;
-    auto issue = [&](int c) {
-        float *slot = my_part + (c % kX3Ring) * kX3ChunkFloats;
-        gptr<float> src = Xw + c * kX3ChunkFloats;
-        // opaque: the unrolled loop would otherwise materialise all 64 piece addresses up front
-        asm volatile("" : "+v"(src));
+    auto issue = [&](int sc) {  // chunks CPB sc .. CPB sc + CPB - 1
 #pragma unroll
-        for (int q = 0; q < NPW; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
+        for (int cc = 0; cc < CPB; ++cc) {
+            float *slot = my_part + ((sc % kX3Ring) * CPB + cc) * kX3ChunkFloats;
+            gptr<float> src = Xw + (sc * CPB + cc) * kX3ChunkFloats;
+            // opaque: the unrolled loop would otherwise materialise all 64 piece addresses up front
+            asm volatile("" : "+v"(src));
+#pragma unroll
+            for (int q = 0; q < NPW; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
+        }
     };
     lds_barrier();  // every wave is done with the ring
     issue(0);
@@ -81,15 +85,19 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             const int c = 2 * P + hf;
-            if (c + 1 < NC) {  // own part of c landed (c + 1's NPW pieces may not)
-                if constexpr (NPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (c % CPB == 0) {
+                const int sc = c / CPB;
+                if (sc + 1 < NS) {  // own part of group sc landed (sc + 1's pieces may not)
+                    if constexpr (NPW * CPB == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                    else if constexpr (NPW * CPB == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                block_barrier_raw();
+                if (sc + 2 < NS) issue(sc + 2);
             }
-            block_barrier_raw();
-            if (c + 2 < NC) issue(c + 2);
-            const float *slot = ring + (c % kX3Ring) * kX3ChunkFloats + lane * 4;
+            const float *slot = ring + (((c / CPB) % kX3Ring) * CPB + c % CPB) * kX3ChunkFloats + lane * 4;
             if (hf == 0 && P + 1 < 8) pre(P + 1);
             if (hf == 1 && P + 1 < 8) bop(P + 1, nbh, nbl);
             // the chunk's 8 output tiles in two groups of 4 (8 fragment reads, then 12 MFMAs):
@@ -167,8 +175,7 @@ __device__ __forceinline__ float pair_sum_x16(float a, float b) {
 }
 constexpr int kDppRowMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1;
 
-// LDS of one FD block (floats): [ ring (3 x 16 KiB) | small weights | srw ].
-constexpr int kFdRegion = kX3RingFloats;
+// LDS of one FD block (floats): [ ring (3 x CPB x 16 KiB) | small weights | srw ].
 // waves per FD block: 8 (default: one block per CU, half the W2 DMA per CU) or 4 (two blocks per
 // CU); 2 waves per SIMD either way. A block iteration covers kFdWaves / 4 G2 tiles of 64 rows.
 // The 8-wave block is ~2 % slower per wave tile (diag_fd.py: its barriers span 8 waves) but 4-5 %
@@ -181,6 +188,13 @@ constexpr int kFdRegion = kX3RingFloats;
 #endif
 constexpr int kFdWaves = RLP_FD_WAVES;
 constexpr int kFdRows = 16 * kFdWaves;
+// chunks per ring slot / block barrier: 2 (one barrier per k-phase) measured no faster here (the
+// actor's FD spills 56 B with it) — unlike the rollout
+#ifndef RLP_FD_CPB
+#define RLP_FD_CPB 1
+#endif
+constexpr int kFdCpb = RLP_FD_CPB;
+constexpr int kFdRegion = kX3RingFloats * kFdCpb;
 
 
 template <int KS1, int A, int LOSS>
@@ -273,7 +287,7 @@ __global__ void __launch_bounds__(64 * kFdWaves, 8 / kFdWaves) ppo2_fd_kernel(Pp
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[j] = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * gq);
         floatx4 p0, p1;  // layer-1 tiles of the next phase (pre), consumed by its B operands (bop)
-        x3_gemm16<false, kFdWaves>(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
+        x3_gemm16<false, kFdWaves, kFdCpb>(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -411,7 +425,7 @@ __global__ void __launch_bounds__(64 * kFdWaves, 8 / kFdWaves) ppo2_fd_kernel(Pp
 #pragma unroll
         for (int j = 0; j < 16; ++j) dh1[j] = floatx4{0.f, 0.f, 0.f, 0.f};
         // (operands swapped: dh1 comes out "neuron on lane", dh1[t][q] = row 4 gq + q, neuron 16 t + e)
-        x3_gemm16<true, kFdWaves>(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
+        x3_gemm16<true, kFdWaves, kFdCpb>(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
