@@ -521,7 +521,9 @@ struct WArgs {
 };
 
 // B fragments of h1 for one 64-row tile: [ks 2][nt 16][hi, lo][64 lanes][8 halfs] (64 KiB):
-// lane (g, e) of MFMA step ks holds h1(rows 32 ks + 8 g + i, neuron 16 nt + e) * 2^SH.
+// lane (g, e) of MFMA step ks holds h1(row, neuron 16 nt + e) * 2^SH for rows 32 ks + 4 g + i and
+// 32 ks + 16 + 4 g + i (i < 4): the C layout of two layer-1 MFMA tiles (rows on the lane groups),
+// with the A operands (g2 rows) loaded in the same K order.
 // 8 waves (2 per SIMD): wave wv owns output rows j in [32 wv, 32 wv + 32) of dW2 (128 accumulator
 // registers), all waves share the tile's h1 fragments.
 constexpr int kWgWaves = 8;
@@ -530,7 +532,7 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
     constexpr int H = kUpdH, SP = 4 * KS1, NT = 64 * kWgWaves;
     constexpr int SV = (kUpdRows * SP + NT - 1) / NT;
     constexpr int FRAG = 2 * 16 * 2 * 64 * 8;  // halfs of one tile's h1 fragments (64 KiB)
-    constexpr int IPT = 2048 / NT;             // fragment items built per thread and tile
+    constexpr int FPW = 32 / kWgWaves;         // fragments (ks, nt) built per wave and tile
     // double-buffered: tile i's MFMAs read hfrag[i & 1] while its waves build tile i + step's
     // fragments into hfrag[(i + 1) & 1] from srow[(i + 1) & 1]
     __shared__ float srow[2][kUpdRows][SP];
@@ -580,24 +582,30 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
             if (i < kUpdRows * SP) srow[buf][i / SP][i % SP] = sv[u];
         }
     };
-    // one fragment item (ks, nt, lane) of 8 rows: the k-ordered f32 fma chain of the forward's
-    // layer-1 MFMA, so h1 is bit-identical
-    auto build_item = [&](int buf, int it) {
-        const int ln = it & 63, nt = (it >> 6) & 15, ks = it >> 10;
-        const int n = 16 * nt + (ln & 15), r0 = 32 * ks + 8 * (ln >> 4);
+    // fragment F = (ks, nt) of a tile by the wave: layer 1 of rows 32 ks .. 32 ks + 31 on two f32
+    // MFMA tiles with the operands swapped (C = [rows][neurons 16 nt ..], the FD's layer1_t), so
+    // h1 is the FD forward's (same products, same MFMA), then tanh, the f16 split, two b128 stores
+    auto build_frag = [&](int buf, int F) {
+        const int ks = F >> 4, nt = F & 15;
         float x[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            float pre = b1s[n];
+        for (int hh = 0; hh < 2; ++hh) {
+            const float b1 = b1s[16 * nt + e];
+            floatx4 c = {b1, b1, b1, b1};
 #pragma unroll
-            for (int k = 0; k < SP; ++k) pre = __builtin_fmaf(w1s[n][k], srow[buf][r0 + i][k], pre);
-            x[i] = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(pre)),
-                                  kX3HScale);
+            for (int kk = 0; kk < KS1; ++kk)
+                c = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[buf][32 * ks + 16 * hh + e][4 * kk + gq],
+                                                         w1s[16 * nt + e][4 * kk + gq], c, 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                x[4 * hh + q] = __builtin_fmaf(-2.0f * kX3HScale,
+                                               __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c[q])),
+                                               kX3HScale);
         }
-        half8 hh, hl;
-        split8(x, hh, hl);
-        *reinterpret_cast<half8 *>(&hfrag[buf][(((ks * 16 + nt) * 2 + 0) * 64 + ln) * 8]) = hh;
-        *reinterpret_cast<half8 *>(&hfrag[buf][(((ks * 16 + nt) * 2 + 1) * 64 + ln) * 8]) = hl;
+        half8 hh8, hl8;
+        split8(x, hh8, hl8);
+        *reinterpret_cast<half8 *>(&hfrag[buf][(((ks * 16 + nt) * 2 + 0) * 64 + lane) * 8]) = hh8;
+        *reinterpret_cast<half8 *>(&hfrag[buf][(((ks * 16 + nt) * 2 + 1) * 64 + lane) * 8]) = hl8;
     };
     const float *g2base = w.g2t;
     asm volatile("" : "+s"(g2base));
@@ -607,11 +615,12 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
             for (int jt = 0; jt < 2; ++jt) {
-                // A operands: g2(rows 32 ks + 8 gq + i, j = 32 wv + 16 jt + e)
+                // A operands: g2(rows 32 ks + 4 gq + i and 32 ks + 16 + 4 gq + i, j = 32 wv + 16 jt + e)
+                // (the fragments' K order)
                 const gptr<float> src = as_global(g2base + t * kUpdTileFloats +
-                                                  (32 * wv + 16 * jt + e) * kUpdRows + 32 * ks + 8 * gq);
+                                                  (32 * wv + 16 * jt + e) * kUpdRows + 32 * ks + 4 * gq);
                 gv[ks][jt][0] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src);
-                gv[ks][jt][1] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 4);
+                gv[ks][jt][1] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 16);
             }
     };
 
@@ -624,7 +633,7 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
     }
     lds_barrier();
 #pragma unroll 1
-    for (int u = 0; u < IPT; ++u) build_item(0, threadIdx.x + NT * u);
+    for (int u = 0; u < FPW; ++u) build_frag(0, FPW * wv + u);
     float svn[SV];
     load_s(tile + gridDim.x, svn);
     floatx4 gv[2][2][2];
@@ -665,9 +674,9 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
                     v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jt], bh, v, 0, 0, 0);
                     acc2[jt][nt] = v;
                 }
-                // the next tile's fragments, spread over this tile's MFMAs (IPT items per thread)
-                if ((ks * 16 + nt) % (32 / IPT) == (32 / IPT) - 1)
-                    build_item(nxt, threadIdx.x + NT * ((ks * 16 + nt) / (32 / IPT)));
+                // the next tile's fragments, spread over this tile's MFMAs (FPW per wave)
+                if ((ks * 16 + nt) % (32 / FPW) == (32 / FPW) - 1)
+                    build_frag(nxt, FPW * wv + (ks * 16 + nt) / (32 / FPW));
             }
 #pragma unroll
             for (int jt = 0; jt < 2; ++jt) {  // db2: g2 against a ones column
