@@ -219,6 +219,15 @@ constexpr int rollout_sp_lds_bytes() {
 #ifndef RLP_SP_CPB1
 #define RLP_SP_CPB1 2   // 16-KiB chunks per ring slot / block barrier there (one barrier per k-phase)
 #endif
+// UAV physics lanes per physics wave: 64 (half waves, 32, measured 6 % slower: the UAV step is
+// issue-bound, not latency-bound, so spreading it over more waves only adds issue)
+#ifndef RLP_SP_UAV_PHL
+#define RLP_SP_UAV_PHL 64
+#endif
+template <int KIND, int SUB, int W>
+constexpr int rollout_sp_physics_lanes() {
+    return (KIND == RLP_ENV_UAV_HOVER_OUTER_LOOP && W * 16 * SUB / RLP_SP_UAV_PHL <= W) ? RLP_SP_UAV_PHL : 64;
+}
 // waves per SIMD of a variant: 4-wave blocks 2; 8-wave blocks of 32-env waves 2 (one block per
 // CU); 8-wave blocks of 16-env waves 4 (two blocks per CU, <= 128 registers) or, with WPS = 2, 2
 // (one block per CU, 256 registers)
@@ -252,8 +261,10 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
                   MfmaNet cn, RolloutArgs ra, rlp_rollout_bufs b) {
     using E = Env<KIND>;
     constexpr int S = E::S, A = E::A, D = E::D, KS1 = (S + 3) / 4, WENV = 16 * SUB;
-    constexpr int WAVES = W, EB = WAVES * WENV, PW = EB / 64, ROT = WAVES / PW;
-    static_assert(EB % 64 == 0, "physics waves are full: EB must be a multiple of 64");
+    // physics lanes per physics wave: 64 (full waves; RLP_SP_UAV_PHL can give the UAV half waves)
+    constexpr int PHL = rollout_sp_physics_lanes<KIND, SUB, W>();
+    constexpr int WAVES = W, EB = WAVES * WENV, PW = EB / PHL, ROT = WAVES / PW;
+    static_assert(EB % PHL == 0 && WAVES % PW == 0, "physics waves cover the block's envs");
     constexpr int SMALL = mlp_small_floats<H, KS1, A>(), RG = rollout_sp_ring<KIND, SUB, W, WPS>();
     // one block per CU: ring slots of RLP_SP_CPB1 chunks (fewer block barriers per k-phase)
     constexpr int CPB = rollout_sp_blocks_per_cu<SUB, W, WPS>() == 1 &&
@@ -335,8 +346,8 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
         const uint64_t gstep = ra.step0 + (uint64_t)t;
         mlp_pass(true);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // (mean, V) of every env
-        if (wave / PW == t % ROT) {  // this step's physics waves
-            const int le = 64 * (wave % PW) + lane, env = base + le;
+        if (wave / PW == t % ROT && lane < PHL) {  // this step's physics waves
+            const int le = PHL * (wave % PW) + lane, env = base + le;
             if (env < n) {
                 const uint64_t eid = ra.env_id0 + (uint64_t)env;
                 const int k = t * n + env;  // 32-bit: T * n * 8 < 2^31 (rlp_rollout)

@@ -6,7 +6,7 @@ ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; export TMPDIR=/tmp
 for V in ${VARIANTS:-R3 R4 R3 R4}; do
   (cd /tmp && RLP_LIBRARY=$ROOT/reinforcementlearningplatform_amd/csrc/build/exp$V/librlp.so timeout -k 10 300 \
      rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_ab_$V" -o run -- python3 "$ROOT/bench.py" \
-     --steps 5 --warmup 2 --no-cpu-baseline --e2e 0 --uav 0 --ddpg 0 --oa 0 --sac 0 --fp32-leg 0) \
+     --steps 5 --warmup 2 --no-cpu-baseline --e2e 0 --uav ${UAV:-0} --ddpg 0 --oa 0 --sac 0 --fp32-leg 0) \
      > "$OUT/b_ab_$V.log" 2>&1 || exit 1
   python3 - "$OUT/prof_ab_$V" "$V" <<'PY'
 import csv, glob, sys
