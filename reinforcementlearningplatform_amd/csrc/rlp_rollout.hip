@@ -29,7 +29,14 @@ struct RolloutArgs {
     uint64_t seed, step0, env_id0;
     int success_rule, success_flag;
     float std_[4], a_min[4], a_max[4], gain[4], off[4];
+    float log_std[4], half_inv_var[4];  // launch constants of the Normal log-prob
 };
+
+// Normal(mean, std).log_prob(x) in torch's expression, with log(std) and 1 / (2 var) per launch
+__device__ __forceinline__ float normal_logp_c(float x, float mean, float half_inv_var, float log_std) {
+    const float d = x - mean;
+    return -(d * d) * half_inv_var - log_std - 0.91893853320467274178f;
+}
 
 // fp32 path: SUB == 4 -> 256 threads (1 wave per SIMD); SUB == 2 -> 512 threads, waves w and w+4
 // share a SIMD (MI355X_MICROARCH.md "Two waves per SIMD"); one block per CU, per-wave W2 rings.
@@ -135,7 +142,7 @@ rollout_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__r
                 float x = m + ra.std_[a] * eps[a];
                 x = fmaxf(fminf(x, ra.a_max[a]), ra.a_min[a]);
                 act[a] = x;
-                lp[a] = normal_logp(x, m, ra.std_[a]);
+                lp[a] = normal_logp_c(x, m, ra.half_inv_var[a], ra.log_std[a]);
             }
             float on[S];
             double r;
@@ -366,7 +373,7 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
                     float x = m + ra.std_[a] * eps[a];
                     x = fmaxf(fminf(x, ra.a_max[a]), ra.a_min[a]);
                     act[a] = x;
-                    lp[a] = normal_logp(x, m, ra.std_[a]);
+                    lp[a] = normal_logp_c(x, m, ra.half_inv_var[a], ra.log_std[a]);
                 }
                 float on[S];
                 double r;
@@ -683,6 +690,8 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
         ra.a_max[a] = cfg->a_max[a];
         ra.off[a] = (cfg->a_min[a] + cfg->a_max[a]) / 2.0f;  // PPOActor_Gaussian: (a_min+a_max)/2
         ra.gain[a] = cfg->a_max[a] - ra.off[a];              //                   a_max - off
+        ra.log_std[a] = logf(cfg->std[a]);
+        ra.half_inv_var[a] = 0.5f / (cfg->std[a] * cfg->std[a]);
     }
     hipStream_t s = as_stream(stream);
     // per-call selections (cfg, 0 = the library-wide default of the rlp_set_* knobs)

@@ -26,7 +26,7 @@ def patch(src):
         const uint64_t gstep = ra.step0 + (uint64_t)t;
         mlp_pass(true);
         asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");  // (mean, V) of every env
-        if (wave / PW == t % ROT) {  // this step's physics waves"""
+        if (wave / PW == t % ROT && lane < PHL) {  // this step's physics waves"""
     new = """    unsigned long long dg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     dg[6] = __builtin_amdgcn_s_memrealtime();
     dg[8] = __smid();
@@ -39,7 +39,7 @@ def patch(src):
         const unsigned long long t2 = %s;
         dg[0] += t1 - t0; dg[1] += t2 - t1;
         const bool physw = wave / PW == t %% ROT;
-        if (wave / PW == t %% ROT) {  // this step's physics waves""" % (STAMP, STAMP, STAMP)
+        if (wave / PW == t %% ROT && lane < PHL) {  // this step's physics waves""" % (STAMP, STAMP, STAMP)
     assert old in s, "stamp site 1"
     s = s.replace(old, new)
     old = """                for (int j = 0; j < S; ++j) sob[le][j] = on[j];
