@@ -37,7 +37,11 @@ ROLLOUT_KERNEL = {"shared": "rlp::rollout_sp_kernel<KIND,256,SUB,4>",
                   "shared8": "rlp::rollout_sp_kernel<KIND,256,1,8>",
                   "cu": "rlp::rollout_sp_kernel<KIND,256,2,8>",
                   "cu16": "rlp::rollout_sp_kernel<KIND,256,1,8,2>",
+                  "cu4": "rlp::rollout_sp_kernel<KIND,256,2,4,1>",
+                  "cu64": "rlp::rollout_sp_kernel<KIND,256,4,4,1>",
                   "lanes": "rlp::rollout_kernel<KIND,256,SUB,true>"}
+
+PHYSICS_MODES = {"auto": -1, "lanes": 0, "shared": 1, "shared8": 2, "cu": 3, "cu16": 4, "cu4": 5, "cu64": 6}
 
 
 def rollout_kernel_name(physics, n):
@@ -407,10 +411,13 @@ def main():
     ap.add_argument("--ddpg", type=int, default=1, help="also time SOI DDPG with the HBM replay (config 3)")
     ap.add_argument("--oa", type=int, default=1, help="also time UGVForwardObstacleAvoidance env steps (lidar)")
     ap.add_argument("--sac", type=int, default=1, help="also time UGVForwardObstacleAvoidance SAC (config 5 shard)")
-    ap.add_argument("--physics", default="auto", choices=["auto", "shared", "shared8", "cu", "cu16", "lanes"],
+    ap.add_argument("--physics", default="auto", choices=list(PHYSICS_MODES),
                     help="rollout kernel: env state in LDS + full-lane physics waves (4-wave blocks, "
                          "8-wave blocks of 16-env waves, or one 8-wave block of 32- / 16-env waves "
                          "per CU; auto: those when the envs fill every CU), or per-wave registers")
+    ap.add_argument("--uav-envs", type=int, default=32768, help="UavRobust leg's envs per GPU (config 4: 262144 / 8)")
+    ap.add_argument("--uav-physics", default=None, choices=list(PHYSICS_MODES),
+                    help="rollout kernel of the UavRobust leg (default: --physics)")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
@@ -435,7 +442,7 @@ def main():
             dist.init_process_group(backend)
     if args.sub:
         _native.set_rollout_sub(args.sub)
-    _native.set_rollout_physics({"auto": -1, "lanes": 0, "shared": 1, "shared8": 2, "cu": 3, "cu16": 4}[args.physics])
+    _native.set_rollout_physics(PHYSICS_MODES[args.physics])
     prec = _native.MLP_F16X3 if args.precision == "f16x3" else _native.MLP_FP32
     _native.set_mlp_precision(prec)
 
@@ -511,7 +518,9 @@ def main():
     if traffic is not None:
         out["roofline"]["traffic"] = traffic
     if args.uav and args.env == "cartpole":
-        un, uT, usteps = 32768, 64, 5
+        un, uT, usteps = args.uav_envs, 64, 5
+        uphys = args.uav_physics or args.physics
+        _native.set_rollout_physics(PHYSICS_MODES[uphys])
         useg = Segment("uav", un, uT, args.seed + 1, env_id0=rank * un)
         for _ in range(2):
             useg.iteration()
@@ -539,13 +548,14 @@ def main():
             "value": un * uT * usteps * world / uel, "unit": "env-steps/s", "envs_per_gpu": un,
             "global_envs": un * world, "T": uT,
             "config": "UavRobust hover outer loop (6-DoF + FNTSMC), PPO2 [6,256,256,3]",
-            "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(args.physics, un)
+            "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(uphys, un)
                                                      if args.precision == "f16x3"
                                                      else "rlp::rollout_kernel<KIND,256,SUB,false>"),
                          "achieved": uach, "peak": upeak, "unit": "TFLOP/s", "frac": uach / upeak,
                          "traffic": pmc_traffic("uav_ppo2_rollout", un, uT),
                          "avg_launch_ms": ums, "flop_per_launch": uflop}}
         del useg
+        _native.set_rollout_physics(PHYSICS_MODES[args.physics])
     if args.ddpg and args.env == "cartpole":
         d = soi_ddpg_leg(rank)
         if dist is not None:

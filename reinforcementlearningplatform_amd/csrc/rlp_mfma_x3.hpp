@@ -65,6 +65,10 @@ __device__ __forceinline__ void split2_mix(float2v x, half2v &hi, half2v &lo) {
     lo = __builtin_bit_cast(half2v, l);
 }
 
+#ifndef RLP_X3_SPLIT_MIX
+#define RLP_X3_SPLIT_MIX 0  // rollout B operands' lo halves by v_fma_mix (split2_mix)
+#endif
+
 constexpr int kX3Waves = 4;             // waves per block sharing the W2 ring
 constexpr int kX3Ring = 3;              // chunks resident in the ring
 constexpr int kX3ChunkFloats = 4096;    // 16 KiB
@@ -161,7 +165,11 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
                 const float2v x = __builtin_elementwise_fma(
                     rc, (float2v){-2.0f * kX3HScale, -2.0f * kX3HScale}, (float2v){kX3HScale, kX3HScale});
                 half2v hi, lo;
+#if RLP_X3_SPLIT_MIX
+                split2_mix(x, hi, lo);
+#else
                 split2(x, hi, lo);
+#endif
                 bh[sb][i] = hi.x;
                 bh[sb][i + 1] = hi.y;
                 bl[sb][i] = lo.x;

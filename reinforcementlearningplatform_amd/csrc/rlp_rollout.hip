@@ -542,6 +542,24 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
             return RLP_OK;
         }
     }
+    if constexpr (X3 && SUB == 2 && rollout_sp_ring<KIND, 2, 4, 1>() != 0) {
+        if (physics == 5) {  // one 4-wave block of 32-env waves per CU (1 wave per SIMD, 512 registers)
+            const int blocks4 = (ra.n + 127) / 128;
+            rollout_sp_kernel<KIND, H, 2, 4, 1><<<blocks4, 256, 0, stream>>>(p, state, need_reset,
+                                                                            actor, an, critic, cn, ra, b);
+            RLP_CHECK_LAUNCH("rlp_rollout");
+            return RLP_OK;
+        }
+    }
+    if constexpr (X3 && SUB == 4 && rollout_sp_ring<KIND, 4, 4, 1>() != 0) {
+        if (physics == 6) {  // one 4-wave block of 64-env waves per CU (1 wave per SIMD, 512 registers)
+            const int blocks4 = (ra.n + 255) / 256;
+            rollout_sp_kernel<KIND, H, 4, 4, 1><<<blocks4, 256, 0, stream>>>(p, state, need_reset,
+                                                                            actor, an, critic, cn, ra, b);
+            RLP_CHECK_LAUNCH("rlp_rollout");
+            return RLP_OK;
+        }
+    }
     if constexpr (X3 && rollout_sp_fits<KIND, SUB>()) {
         if (physics)
             rollout_sp_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor,
@@ -584,7 +602,8 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
             physics = (sub == 0 || sub == 2) && (ra.n + 255) / 256 >= cus &&
                               rollout_sp_ring<KIND, 2, 8>() != 0 ? 3 : 1;
         if (physics == 2 || physics == 4) sub = 1;  // the 8-wave variants of 16-env waves
-        if (physics == 3) sub = 2;  // the one-block-per-CU variant runs 32-env waves
+        if (physics == 3 || physics == 5) sub = 2;  // the one-block-per-CU variants of 32-env waves
+        if (physics == 6) sub = 4;                  // ... of 64-env waves
         if (sub == 0)  // auto: 32-env waves unless that leaves fewer than 2 blocks per CU
             sub = (ra.n + 127) / 128 < 2 * cus ? 1 : 2;
         if (sub == 1)
@@ -627,7 +646,7 @@ int rlp_get_mlp_precision(void) { return g_mlp_precision; }
 // tuning knob: 1 (default) = the shared-physics f16x3 kernel where its LDS fits (full-lane
 // physics), 0 = the register-resident kernel
 int rlp_set_rollout_physics(int shared) {
-    if (shared < -1 || shared > 4) return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
+    if (shared < -1 || shared > 6) return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
     g_rollout_shared_physics = shared;
     return RLP_OK;
 }
@@ -696,7 +715,7 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
     hipStream_t s = as_stream(stream);
     // per-call selections (cfg, 0 = the library-wide default of the rlp_set_* knobs)
     RLP_REQUIRE(cfg->mlp_precision >= 0 && cfg->mlp_precision <= 2 && cfg->physics >= 0 &&
-                    cfg->physics <= 5 && (cfg->sub == 0 || cfg->sub == 1 || cfg->sub == 2 ||
+                    cfg->physics <= 7 && (cfg->sub == 0 || cfg->sub == 1 || cfg->sub == 2 ||
                                           cfg->sub == 4),
                 "rlp_rollout: cfg mlp_precision=%d physics=%d sub=%d", cfg->mlp_precision,
                 cfg->physics, cfg->sub);

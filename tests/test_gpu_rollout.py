@@ -98,7 +98,7 @@ def test_shared_physics_kernel_equals_register_kernel(kind):
     n, T = 16384 + 37, 96
     apk, cpk = K.mfma_pack(ad, dev(ap)), K.mfma_pack(cd, dev(cp))
     runs = []
-    for phys in (1, 0, 2, 3, 4):   # per-call selection (rlp_rollout_cfg.physics)
+    for phys in (1, 0, 2, 3, 4, 5, 6):   # per-call selection (rlp_rollout_cfg.physics)
         cfg = K.make_rollout_cfg(T, n, 99, 5, 0, std, lo, hi, A.RLP_SUCCESS_DONE_AND_FLAG_NE,
                                  A.timeout_flag(kind), physics=phys)
         st = K.new_state(kind, n)
@@ -109,7 +109,8 @@ def test_shared_physics_kernel_equals_register_kernel(kind):
         runs.append(({k: v.clone() for k, v in bufs.items()}, st.clone(), need.clone()))
     (b1, s1, n1), *others = runs
     assert b1["done"][:-1].any(), "no env terminated inside the segment"
-    # register kernel; 8-wave shared kernels (16-env waves; one block of 32- / 16-env waves per CU)
+    # register kernel; 8-wave shared kernels (16-env waves; one block of 32- / 16-env waves per CU);
+    # one 4-wave block of 32- / 64-env waves per CU (1 wave per SIMD)
     for bx, sx, nx in others:
         for key in b1:
             assert torch.equal(b1[key], bx[key]), key
@@ -227,3 +228,5 @@ def test_per_call_selection_overrides_library_default():
     assert torch.equal(run(mlp_precision=_native.MLP_F16X3, physics=2), vx3)
     assert torch.equal(run(mlp_precision=_native.MLP_F16X3, physics=3), vx3)
     assert torch.equal(run(mlp_precision=_native.MLP_F16X3, physics=4), vx3)
+    assert torch.equal(run(mlp_precision=_native.MLP_F16X3, physics=5), vx3)
+    assert torch.equal(run(mlp_precision=_native.MLP_F16X3, physics=6), vx3)
