@@ -44,12 +44,13 @@ ROLLOUT_KERNEL = {"shared": "rlp::rollout_sp_kernel<KIND,256,SUB,4>",
 PHYSICS_MODES = {"auto": -1, "lanes": 0, "shared": 1, "shared8": 2, "cu": 3, "cu16": 4, "cu4": 5, "cu64": 6}
 
 
-def rollout_kernel_name(physics, n):
+def rollout_kernel_name(physics, n, env="cartpole"):
     """The kernel rlp_rollout runs for `physics` (auto: one 8-wave block per CU when n fills every
-    CU with a 256-env block, include/rlp.h rlp_set_rollout_physics)."""
+    CU with a 256-env block, else — and always for the UAV — one 4-wave block of 32-env waves per
+    CU; include/rlp.h rlp_set_rollout_physics)."""
     if physics == "auto":
         cus = torch.cuda.get_device_properties(0).multi_processor_count
-        physics = "cu" if (n + 255) // 256 >= cus else "shared"
+        physics = "cu" if env != "uav" and (n + 255) // 256 >= cus else "cu4"
     return ROLLOUT_KERNEL[physics]
 
 ENVS = {
@@ -79,9 +80,14 @@ def mlp_flops(desc):
     return sum(2 * ds[i] * ds[i + 1] for i in range(desc.n_layers))
 
 
-def pmc_traffic(workload, n, T):
+def _template_args(name):
+    return [a.strip() for a in name[name.find("<") + 1:name.rfind(">")].split(",")][1:]
+
+
+def pmc_traffic(workload, n, T, kernel=None):
     """HBM bytes per rollout launch from the committed rocprofv3 PMC pass of this workload
-    (profiles/pmc_traffic.json: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE)."""
+    (profiles/pmc_traffic.json: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE);
+    None when that pass profiled another kernel variant than `kernel` (the one this run launches)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
@@ -90,6 +96,10 @@ def pmc_traffic(workload, n, T):
     e = d.get(workload)
     if not e or e.get("envs_per_gpu") != n or e.get("T") != T:
         return None
+    if kernel is not None and e.get("kernel"):
+        want, have = _template_args(kernel), _template_args(e["kernel"])
+        if all(a.isdigit() for a in want) and want != have[:len(want)]:
+            return None
     return e["hbm_bytes_per_launch"]
 
 
@@ -499,7 +509,7 @@ def main():
                    "nets": "actor [S,256,256,A] tanh, critic [S,256,256,1]",
                    "parallelism": f"dp{world} (env shards, no data-path collective)",
                    "physics": "f64", "mlp": mlp},
-        "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(args.physics, n) if args.precision == "f16x3"
+        "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(args.physics, n, args.env) if args.precision == "f16x3"
                                                 else "rlp::rollout_kernel<KIND,256,SUB,false>"), "achieved": achieved,
                      "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                      "peak_basis": basis, "avg_launch_ms": rollout_ms, "flop_per_launch": flop_launch},
@@ -514,7 +524,7 @@ def main():
         out["fp32_mfma_path"] = {"value": n * T * world * max(2, args.steps // 2) / el32,
                                  "unit": "env-steps/s", "avg_launch_ms": ms32, "achieved": ach32,
                                  "peak": PEAK_FP32_MFMA_TFLOPS, "frac": ach32 / PEAK_FP32_MFMA_TFLOPS}
-    traffic = pmc_traffic(out["config"]["workload"], n, T)
+    traffic = pmc_traffic(out["config"]["workload"], n, T, out["roofline"]["kernel"])
     if traffic is not None:
         out["roofline"]["traffic"] = traffic
     if args.uav and args.env == "cartpole":
@@ -548,11 +558,12 @@ def main():
             "value": un * uT * usteps * world / uel, "unit": "env-steps/s", "envs_per_gpu": un,
             "global_envs": un * world, "T": uT,
             "config": "UavRobust hover outer loop (6-DoF + FNTSMC), PPO2 [6,256,256,3]",
-            "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(uphys, un)
+            "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(uphys, un, "uav")
                                                      if args.precision == "f16x3"
                                                      else "rlp::rollout_kernel<KIND,256,SUB,false>"),
                          "achieved": uach, "peak": upeak, "unit": "TFLOP/s", "frac": uach / upeak,
-                         "traffic": pmc_traffic("uav_ppo2_rollout", un, uT),
+                         "traffic": pmc_traffic("uav_ppo2_rollout", un, uT,
+                                                rollout_kernel_name(uphys, un, "uav")),
                          "avg_launch_ms": ums, "flop_per_launch": uflop}}
         del useg
         _native.set_rollout_physics(PHYSICS_MODES[args.physics])

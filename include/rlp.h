@@ -317,7 +317,8 @@ typedef struct rlp_rollout_cfg {
     /* per-call kernel selection; 0 = the library-wide default set by rlp_set_mlp_precision /
      * rlp_set_rollout_physics / rlp_set_rollout_sub, else value + 1 (mlp_precision: 1 RLP_MLP_FP32,
      * 2 RLP_MLP_F16X3; physics: 1 register-resident, 2 shared, 3 shared 8-wave, 4 shared
-     * one-block-per-CU, 5 shared one-block-per-CU of 16-env waves); sub: 0 default,
+     * one-block-per-CU, 5 shared one-block-per-CU of 16-env waves, 6 / 7 one 4-wave block of 32- /
+     * 64-env waves per CU); sub: 0 default,
      * 1, 2, 4 */
     int32_t mlp_precision, physics, sub, reserved;
 } rlp_rollout_cfg;
@@ -460,7 +461,9 @@ int64_t rlp_struct_size(int which);
  * 2 or 4. */
 int rlp_set_rollout_sub(int sub);
 /* Tuning knob of rlp_rollout (f16x3 path): -1 = auto (default: 3 when the envs fill every CU with
- * a 256-env block, else 1), 1 = shared-physics
+ * a 256-env block, else — and always for RLP_ENV_UAV_HOVER_OUTER_LOOP — 5), 5 = one 4-wave block
+ * of 32-env waves per CU (1 wave per SIMD, VGPR + AGPR budget), 6 = the same with 64-env waves,
+ * 1 = shared-physics
  * kernel (the block's env state in LDS, each step's f64 physics on full 64-lane waves; two 4-wave
  * blocks per CU), 4 = one 8-wave block of 16-env waves per CU (2 waves per SIMD), 2 = 8-wave
  * blocks of 16-env waves, two per CU (4 waves per SIMD), 3 = one 8-wave block of 32-env waves per CU

@@ -595,12 +595,22 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
                     hipSuccess || cus <= 0)
                 cus = 256;
         }
-        // auto: one 8-wave block of 32-env waves per CU where the envs fill every CU; else two
-        // 4-wave blocks (one 8-wave block of 16-env waves, mode 4, measured the same on the UAV
-        // shard: that kernel is bound by its physics' register spills, not by co-residency)
-        if (physics < 0)
-            physics = (sub == 0 || sub == 2) && (ra.n + 255) / 256 >= cus &&
-                              rollout_sp_ring<KIND, 2, 8>() != 0 ? 3 : 1;
+        // auto: one 8-wave block of 32-env waves per CU where the envs fill every CU; else one
+        // 4-wave block of 32-env waves per CU (mode 5: 1 wave per SIMD with the VGPR + AGPR
+        // budget). The UAV's physics spills at 256 registers (584 B per lane at 2 waves per SIMD,
+        // 112 B in mode 5), so the UAV runs mode 5 at every n (measured: 32768 envs 3.77 ->
+        // 2.93 ms, 65536 envs 7.23 -> 5.84 ms; CartPole at 32768 envs 5.16 -> 4.75 ms against
+        // two 4-wave blocks of 16-env waves)
+        if (physics < 0) {
+            const bool fill256 = (ra.n + 255) / 256 >= cus;
+            if (KIND != RLP_ENV_UAV_HOVER_OUTER_LOOP && (sub == 0 || sub == 2) && fill256 &&
+                rollout_sp_ring<KIND, 2, 8>() != 0)
+                physics = 3;
+            else if ((sub == 0 || sub == 2) && rollout_sp_ring<KIND, 2, 4, 1>() != 0)
+                physics = 5;
+            else
+                physics = 1;
+        }
         if (physics == 2 || physics == 4) sub = 1;  // the 8-wave variants of 16-env waves
         if (physics == 3 || physics == 5) sub = 2;  // the one-block-per-CU variants of 32-env waves
         if (physics == 6) sub = 4;                  // ... of 64-env waves

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKLOADS = {  # workload -> (kernel name prefix, envs per GPU, T, algorithmic bytes per launch)
     "cartpole_ppo2_rollout": ("rlp::rollout_sp_kernel<1, 256, 2, 8, 2>", 65536, 128,
                               65536 * 128 * 55 + 65536 * (2 * 5 * 8 + 2)),
-    "uav_ppo2_rollout": ("rlp::rollout_sp_kernel<6, 256, 1, 4, 2>", 32768, 64,
+    "uav_ppo2_rollout": ("rlp::rollout_sp_kernel<6, 256, 2, 4, 1>", 32768, 64,
                          # obs / obs_next 2 x 6 f32 + action / logp 2 x 3 f32 + reward, value,
                          # value_next + done / success / flag per transition; f64 state 22 x 8 r+w
                          32768 * 64 * (48 + 24 + 12 + 3) + 32768 * (2 * 22 * 8 + 2)),
