@@ -65,6 +65,9 @@ __device__ __forceinline__ void split2_mix(float2v x, half2v &hi, half2v &lo) {
     lo = __builtin_bit_cast(half2v, l);
 }
 
+#ifndef RLP_X3_ASM_DMA
+#define RLP_X3_ASM_DMA 0  // the W2 ring's LDS-DMA as inline asm (lds_dma_1k_untracked)
+#endif
 #ifndef RLP_X3_SPLIT_MIX
 #define RLP_X3_SPLIT_MIX 0  // rollout B operands' lo halves by v_fma_mix (split2_mix)
 #endif
@@ -118,7 +121,13 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
             float *slot = my_part + ((sc % RG) * CPB + cc) * kX3ChunkFloats;
             const gptr<float> src = X + (sc * CPB + cc) * kX3ChunkFloats;
 #pragma unroll
-            for (int q = 0; q < NPW; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
+            for (int q = 0; q < NPW; ++q) {
+#if RLP_X3_ASM_DMA
+                lds_dma_1k_untracked(src + q * 256, slot + q * 256);
+#else
+                lds_dma_1k(src + q * 256, slot + q * 256);
+#endif
+            }
         }
     };
     block_barrier_raw();  // every wave is done reading the ring (previous call)
