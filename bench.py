@@ -130,7 +130,7 @@ class Segment:
         self.rnorm = torch.empty((T, n), dtype=torch.float32, device="cuda")
         self.adv = torch.empty((T, n), dtype=torch.float32, device="cuda")
         self.vt = torch.empty((T, n), dtype=torch.float32, device="cuda")
-        self.stats = torch.zeros(2, dtype=torch.float64, device="cuda")
+        self.stats = K.adv_stats_buffer(n, device="cuda")
         self.step0 = 0
 
     def rollout(self):
@@ -145,7 +145,6 @@ class Segment:
         # V(s'_t) of terminal transitions (non-terminal ones were written by the rollout)
         K.value_fixup(self.cd, self.cpk, b["obs_next"], b["done"], b["success"], b["value_next"])
         K.reward_norm(b["reward"], self.rms, self.work, out=self.rnorm)
-        self.stats.zero_()
         K.gae(self.rnorm, b["value"], b["value_next"], b["done"], b["success"], 0.999, 0.95,
               adv=self.adv, v_target=self.vt, stats=self.stats)
         K.adv_normalize(self.adv, self.stats)

@@ -360,18 +360,40 @@ int64_t rlp_reward_norm_workspace(int T, int n);
 int rlp_reward_norm(const float *reward_in, int T, int n, double *rms, double *work,
                     float *reward_out, rlp_stream_t stream);
 
+/* rlp_reward_norm in two stages, for one running normaliser shared by `world` ranks of n envs
+ * each (the Welford/Chan merge across ranks):
+ *   rlp_reward_norm_stats  writes this rank's chunk statistics, the first
+ *                          rlp_reward_norm_parts(T, n) doubles of `work`;
+ *   (the caller all-gathers those doubles of every rank into `parts`, rank-major)
+ *   rlp_reward_norm_finish merges, per time step, all world * chunks in global env order, runs
+ *                          the running-statistics recurrence with world * n rewards per step and
+ *                          normalises this rank's rewards.
+ * Every rank then holds the same rms, and the result equals one rank of world * n envs bit for
+ * bit when n is a multiple of 4096. world = 1 with parts = work is rlp_reward_norm. */
+int64_t rlp_reward_norm_parts(int T, int n);
+int rlp_reward_norm_stats(const float *reward_in, int T, int n, double *work, rlp_stream_t stream);
+int rlp_reward_norm_finish(const float *reward_in, int T, int n, int world, const double *parts,
+                           double *rms, double *work, float *reward_out, rlp_stream_t stream);
+
 /* GAE(lambda) backward scan per env (Proximal_Policy_Optimization2.py:93-98), fp32 in the
  * reference's exact operation order (bit-identical to the NumPy-2 loop):
  *   delta = (r + ((float)gamma * (1 - success)) * v_next) - v
  *   gae   = delta + ((float)(gamma*lambda) * gae) * (1 - done)
  *   adv = gae; v_target = adv + v
- * All arrays [T][n]. adv_stats (device f64[2], nullable): += {sum(adv), sum(adv^2)}. */
+ * All arrays [T][n]. adv_stats (device f64, nullable; at least 3 * rlp_adv_stats_parts(n) + 2):
+ * overwritten with one (count, mean, M2) partial per 256-env block, f64, computed without atomics
+ * (per-lane shifted sums, a fixed-order Chan combine): run-to-run deterministic. */
+int rlp_adv_stats_parts(int n);
 int rlp_gae(const float *reward, const float *value, const float *value_next, const uint8_t *done,
             const uint8_t *success, double gamma, double lambda, int T, int n, float *adv,
             float *v_target, double *adv_stats, rlp_stream_t stream);
 
-/* adv = (adv - mean) / (std_unbiased + 1e-5) from adv_stats = {sum, sumsq} (Trick 1, :99-100). */
-int rlp_adv_normalize(float *adv, int64_t count, const double *adv_stats, rlp_stream_t stream);
+/* adv = (adv - mean) / (std_unbiased + 1e-5) (Trick 1, :99-100; torch's two-pass std over the
+ * whole buffer), mean / std from the first `parts` partials of adv_stats combined in a fixed
+ * order (Chan); they are written to adv_stats[3 * parts], [3 * parts + 1]. Under data-parallel
+ * ranks, all-gather every rank's partials (rank-major) and pass parts = world * parts: the
+ * normalisation is then global and identical on every rank. */
+int rlp_adv_normalize(float *adv, int64_t count, double *adv_stats, int parts, rlp_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* PPO2 update (Proximal_Policy_Optimization2.learn, algorithm/policy_base/

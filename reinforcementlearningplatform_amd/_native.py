@@ -50,7 +50,11 @@ def _declare(lib):
         "rlp_reward_norm": (i32, [vp, i32, i32, vp, vp, vp, vp]),
         "rlp_reward_norm_workspace": (i64, [i32, i32]),
         "rlp_gae": (i32, [vp, vp, vp, vp, vp, dbl, dbl, i32, i32, vp, vp, vp, vp]),
-        "rlp_adv_normalize": (i32, [vp, i64, vp, vp]),
+        "rlp_adv_normalize": (i32, [vp, i64, vp, i32, vp]),
+        "rlp_adv_stats_parts": (i32, [i32]),
+        "rlp_reward_norm_parts": (i64, [i32, i32]),
+        "rlp_reward_norm_stats": (i32, [vp, i32, i32, vp, vp]),
+        "rlp_reward_norm_finish": (i32, [vp, i32, i32, i32, vp, vp, vp, vp, vp]),
         "rlp_ppo2_workspace_floats": (i64, [vp, i64]),
         "rlp_ppo2_grad": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp]),
         "rlp_grad_sqnorm": (i32, [vp, i64, vp, vp]),

@@ -4,8 +4,12 @@ replaced by one fused HIP rollout launch per segment.
 
 One iteration:
   rollout     rlp_rollout: T steps x n envs (reset, actor + sample, critic, env step, append)
-  advantages  rlp_value_fixup (V(s') of time-outs), rlp_reward_norm (Normalization, per rank as
-              each DPPO2 worker keeps its own), rlp_gae + rlp_adv_normalize
+  advantages  rlp_value_fixup (V(s') of time-outs), rlp_reward_norm (Normalization), rlp_gae +
+              rlp_adv_normalize. Under torch.distributed both statistics are global by default
+              (ppo_msg 'norm_scope': 'global'): the ranks' reward chunk statistics and
+              advantage (count, mean, M2) partials are gathered (one small all-reduce each) and
+              merged in global env order, so W ranks of n envs normalise exactly as one rank of
+              W * n envs; 'rank' keeps one normaliser per rank, as each DPPO2 worker keeps its own
   update      K epochs of the PPO2 clipped objective (Proximal_Policy_Optimization2.py:102-160)
               on librlp's kernels (NativePPO2Learner: rlp_ppo2_grad + rlp_adam_step; learner=
               "torch" selects the torch-autograd PPO2Learner below, the parity reference); under
@@ -208,7 +212,12 @@ class VecPPO2:
         self.v_target = torch.empty((self.T, self.n), **f32)
         self.rms = torch.zeros(4, dtype=torch.float64, device=self.device)
         self.work = K.reward_norm_workspace(self.T, self.n, self.device)
-        self.stats = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self.norm_scope = self.msg.get('norm_scope', 'global')
+        if self.norm_scope not in ('global', 'rank'):
+            raise ValueError(f"VecPPO2: norm_scope {self.norm_scope!r} (global | rank)")
+        self.global_norm = self.norm_scope == 'global' and self.world > 1
+        self.adv_parts = K.adv_stats_parts(self.n)
+        self.stats = K.adv_stats_buffer(self.n, self.world if self.global_norm else 1, self.device)
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(self.seed + 7919 * (self.env_id0 + 1))
         self.total_steps = 0
@@ -226,16 +235,33 @@ class VecPPO2:
         self.step0 += self.T
         self.total_steps += self.T * self.n * self.world
 
+    def _gather(self, local):
+        """Every rank's `local` (same size) in rank order, on every rank: each rank fills its slot
+        of a zero buffer and one all-reduce sums them (x + 0 is exact, so this is a gather)."""
+        rank = torch.distributed.get_rank(self.learner.pg)
+        out = torch.zeros(self.world * local.numel(), dtype=local.dtype, device=local.device)
+        out[rank * local.numel():(rank + 1) * local.numel()] = local.reshape(-1)
+        torch.distributed.all_reduce(out, group=self.learner.pg)
+        return out
+
     def advantages(self):
         b = self.bufs
         K.value_fixup(self.gpu_critic.desc, self.gpu_critic.packed, b["obs_next"], b["done"],
                       b["success"], b["value_next"])
-        K.reward_norm(b["reward"], self.rms, self.work, out=self.rnorm)
-        self.stats.zero_()
+        if self.global_norm:
+            parts = self._gather(K.reward_norm_stats(b["reward"], self.work))
+            K.reward_norm_finish(b["reward"], self.rms, self.work, parts, self.world, out=self.rnorm)
+        else:
+            K.reward_norm(b["reward"], self.rms, self.work, out=self.rnorm)
         K.gae(self.rnorm, b["value"], b["value_next"], b["done"], b["success"], self.msg['gamma'],
               self.msg['lmd'], adv=self.adv, v_target=self.v_target, stats=self.stats)
         if self.msg['use_adv_norm']:
-            K.adv_normalize(self.adv, self.stats)
+            parts = self.adv_parts
+            if self.global_norm:
+                local = self.stats[:3 * parts].clone()
+                self.stats[:3 * parts * self.world] = self._gather(local)
+                parts *= self.world
+            K.adv_normalize(self.adv, self.stats, parts)
 
     def update(self):
         b = self.bufs

@@ -27,6 +27,36 @@ __device__ __forceinline__ double block_sum(double v, double *red) {
     return s;
 }
 
+// (count, mean, M2) of two disjoint sets, Chan et al.'s pairwise combine
+struct Moments {
+    double c, m, q;
+};
+__device__ __forceinline__ Moments chan(Moments a, Moments b) {
+    if (b.c == 0) return a;
+    if (a.c == 0) return b;
+    const double nn = a.c + b.c, d = b.m - a.m;
+    return {nn, a.m + d * (b.c / nn), a.q + b.q + d * d * (a.c * b.c / nn)};
+}
+
+// fixed-order block combine: xor butterfly inside each wave (every lane's operands are fixed by
+// the data, so lane 0's result is run-independent), then waves 0, 1, 2, 3 in order
+template <int BS>
+__device__ __forceinline__ Moments block_moments(Moments v, Moments *red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        Moments u{__shfl_xor(v.c, o), __shfl_xor(v.m, o), __shfl_xor(v.q, o)};
+        v = (threadIdx.x & o) ? chan(u, v) : chan(v, u);
+    }
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    Moments s = red[0];
+#pragma unroll
+    for (int i = 1; i < BS / 64; ++i) s = chan(s, red[i]);
+    __syncthreads();
+    return s;
+}
+
 // ---- reward normalisation -----------------------------------------------------------------
 // Three launches: (1) chunk statistics — a [P x T] grid of 256-thread blocks, each two-pass over
 // a 4096-reward chunk of one time step held in registers (16 per lane, one HBM read, fp64
@@ -68,25 +98,37 @@ __global__ void __launch_bounds__(256) reward_stats_kernel(const float *__restri
     }
 }
 
-// sequential merge over t (RunningMeanStd.update, utils/classes.py:626-645): Welford for n == 1
-// (the reference exactly, first-call std = x quirk included), Chan's parallel merge otherwise
+// sequential merge over t (RunningMeanStd.update, utils/classes.py:626-645): Welford for a
+// single env (the reference exactly, first-call std = x quirk included), Chan's parallel merge
+// otherwise. `parts` holds the chunk statistics of `world` ranks of n envs each, rank-major
+// ([world][T][P][2]); per time step the world * P chunks are combined in global env order, so W
+// ranks of n envs reproduce one rank of W * n envs bit for bit (when n is a multiple of the chunk).
 __global__ void __launch_bounds__(256) reward_merge_kernel(const float *__restrict__ r, int T, int n,
+                                                           int world, const double *parts,
                                                            double *rms, double *work) {
     __shared__ double sa[kRsTile], sb[kRsTile], sw1[kRsTile], sw2[kRsTile];
     __shared__ double carry[4];
     const int P = rs_chunks(n);
-    double *part = work, *agg = work + (size_t)T * P * 2, *out = agg + (size_t)T * 2;
+    double *agg = work + (size_t)T * P * 2, *out = agg + (size_t)T * 2;
+    const double ntot = (double)n * world;
+    const bool single = ntot == 1;
     if (threadIdx.x == 0)
         for (int k = 0; k < 4; ++k) carry[k] = rms[k];
-    if (n > 1) {  // per time step: combine the chunks in chunk order
+    if (!single) {  // per time step: combine the chunks in global env order
         for (int t = threadIdx.x; t < T; t += 256) {
-            const double *pp = part + (size_t)t * P * 2;
-            double c = min(kRsChunk, n), mean = pp[0], m2 = pp[1];
-            for (int p = 1; p < P; ++p) {
-                const double cb = min(kRsChunk, n - p * kRsChunk), nn = c + cb;
-                const double dl = pp[2 * p] - mean;
+            double c = 0, mean = 0, m2 = 0;
+            for (int q = 0; q < world * P; ++q) {
+                const int rk = q / P, p = q - rk * P;
+                const double *pp = parts + (((size_t)rk * T + t) * P + p) * 2;
+                const double cb = min(kRsChunk, n - p * kRsChunk);
+                if (q == 0) {
+                    c = cb; mean = pp[0]; m2 = pp[1];
+                    continue;
+                }
+                const double nn = c + cb;
+                const double dl = pp[0] - mean;
                 mean = mean + dl * (cb / nn);
-                m2 = m2 + pp[2 * p + 1] + dl * dl * (c * cb / nn);
+                m2 = m2 + pp[1] + dl * dl * (c * cb / nn);
                 c = nn;
             }
             agg[2 * t] = mean;
@@ -99,21 +141,21 @@ __global__ void __launch_bounds__(256) reward_merge_kernel(const float *__restri
         const double cnt0 = carry[0];
         for (int j = threadIdx.x; j < tn; j += 256) {
             const int t = t0 + j;
-            if (n == 1) {
+            if (single) {
                 sa[j] = (double)r[t];
-            } else {  // the merge weights need only the running count (cnt0 + j n)
+            } else {  // the merge weights need only the running count (cnt0 + j ntot)
                 sa[j] = agg[2 * t];
                 sb[j] = agg[2 * t + 1];
-                const double cnt = cnt0 + (double)j * n, nn = cnt + n;
-                sw1[j] = (double)n / nn;
-                sw2[j] = cnt * (double)n / nn;
+                const double cnt = cnt0 + (double)j * ntot, nn = cnt + ntot;
+                sw1[j] = ntot / nn;
+                sw2[j] = cnt * ntot / nn;
             }
         }
         __syncthreads();
         if (threadIdx.x == 0) {
             double cnt = carry[0], mean = carry[1], S = carry[2], sd = carry[3];
             for (int j = 0; j < tn; ++j) {
-                if (n == 1) {
+                if (single) {
                     const double x = sa[j];
                     cnt += 1;
                     if (cnt == 1) {
@@ -134,19 +176,19 @@ __global__ void __launch_bounds__(256) reward_merge_kernel(const float *__restri
                         mean = mean + dl * sw1[j];
                         S = S + sb[j] + dl * dl * sw2[j];
                     }
-                    cnt += n;
+                    cnt += ntot;
                     sb[j] = S;
                 }
                 sa[j] = mean;
             }
-            if (n > 1 && tn > 0) sd = sqrt(S / cnt);
+            if (!single && tn > 0) sd = sqrt(S / cnt);
             carry[0] = cnt; carry[1] = mean; carry[2] = S; carry[3] = sd;
         }
         __syncthreads();
         for (int j = threadIdx.x; j < tn; j += 256) {
             const int t = t0 + j;
             out[2 * t] = sa[j];
-            out[2 * t + 1] = n == 1 ? sb[j] : sqrt(sb[j] / (cnt0 + (double)(j + 1) * n));
+            out[2 * t + 1] = single ? sb[j] : sqrt(sb[j] / (cnt0 + (double)(j + 1) * ntot));
         }
         __syncthreads();
     }
@@ -175,9 +217,9 @@ __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
                                                   const uint8_t *__restrict__ success, float g32,
                                                   float c, int T, int n, float *__restrict__ adv,
                                                   float *__restrict__ vt, double *stats) {
-    __shared__ double red[4];
+    __shared__ Moments red[4];
     const int i = blockIdx.x * 256 + threadIdx.x;
-    double s1 = 0, s2 = 0;
+    double s1 = 0, s2 = 0, k0 = 0;  // sums of (adv - k0), k0 = the lane's first advantage
     if (i < n) {
         float gae = 0.f;
         for (int t1 = T; t1 > 0; t1 -= kGaeU) {
@@ -203,29 +245,47 @@ __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
                     gae = delta + tt;
                     adv[k] = gae;
                     vt[k] = gae + vv[j];
-                    s1 += (double)gae;
-                    s2 += (double)gae * (double)gae;
+                    if (t1 == T && j == 0) k0 = (double)gae;
+                    const double d = (double)gae - k0;
+                    s1 += d;
+                    s2 += d * d;
                 }
             }
         }
     }
-    if (stats) {
-        s1 = block_sum<256>(s1, red);
-        s2 = block_sum<256>(s2, red);
+    if (stats) {  // this block's (count, mean, M2): shifted sums per lane, Chan across lanes
+        Moments mo{0, 0, 0};
+        if (i < n) {
+            const double c = (double)T;
+            mo = {c, k0 + s1 / c, fmax(s2 - s1 * (s1 / c), 0.0)};
+        }
+        mo = block_moments<256>(mo, red);
         if (threadIdx.x == 0) {
-            atomicAdd(&stats[0], s1);
-            atomicAdd(&stats[1], s2);
+            stats[3 * blockIdx.x + 0] = mo.c;
+            stats[3 * blockIdx.x + 1] = mo.m;
+            stats[3 * blockIdx.x + 2] = mo.q;
         }
     }
 }
 
+// the partials combined in a fixed order: thread j folds parts [j*per, (j+1)*per) left to right,
+// then the block combine above; writes (mean, unbiased std) after the partials
+__global__ void __launch_bounds__(256) adv_stats_merge_kernel(double *stats, int parts) {
+    __shared__ Moments red[4];
+    const int per = (parts + 255) / 256, lo = threadIdx.x * per, hi = min(parts, lo + per);
+    Moments a{0, 0, 0};
+    for (int j = lo; j < hi; ++j) a = chan(a, Moments{stats[3 * j], stats[3 * j + 1], stats[3 * j + 2]});
+    a = block_moments<256>(a, red);
+    if (threadIdx.x == 0) {
+        stats[3 * parts] = a.m;
+        stats[3 * parts + 1] = a.c > 1 ? sqrt(a.q / (a.c - 1)) : 0.0;
+    }
+}
+
 __global__ void __launch_bounds__(256) adv_norm_kernel(float *adv, int64_t count,
-                                                       const double *stats) {
-    const double N = (double)count;
-    const double mean = stats[0] / N;
-    const double var = (stats[1] - stats[0] * stats[0] / N) / (N - 1);
-    const float m32 = (float)mean;
-    const float den = (float)sqrt(var > 0 ? var : 0) + 1e-5f;
+                                                       const double *mean_std) {
+    const float m32 = (float)mean_std[0];
+    const float den = (float)mean_std[1] + 1e-5f;
     for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256)
         adv[i] = (adv[i] - m32) / den;
 }
@@ -241,21 +301,48 @@ int64_t rlp_reward_norm_workspace(int T, int n) {
     return (int64_t)T * (2 * (int64_t)rs_chunks(n > 0 ? n : 1) + 4);
 }
 
+int64_t rlp_reward_norm_parts(int T, int n) {
+    if (T < 0 || n < 0) return RLP_EINVAL;
+    return (int64_t)T * 2 * rs_chunks(n > 0 ? n : 1);
+}
+
+int rlp_reward_norm_stats(const float *reward_in, int T, int n, double *work, rlp_stream_t stream) {
+    RLP_REQUIRE(reward_in && work, "rlp_reward_norm_stats: null argument");
+    RLP_REQUIRE(T >= 0 && n >= 0, "rlp_reward_norm_stats: T=%d n=%d", T, n);
+    if (T == 0 || n == 0) return RLP_OK;
+    reward_stats_kernel<<<dim3(rs_chunks(n), T), 256, 0, as_stream(stream)>>>(reward_in, n, work);
+    RLP_CHECK_LAUNCH("rlp_reward_norm_stats");
+    return RLP_OK;
+}
+
+int rlp_reward_norm_finish(const float *reward_in, int T, int n, int world, const double *parts,
+                           double *rms, double *work, float *reward_out, rlp_stream_t stream) {
+    RLP_REQUIRE(reward_in && rms && work && reward_out, "rlp_reward_norm_finish: null argument");
+    RLP_REQUIRE(T >= 0 && n >= 0 && world >= 1, "rlp_reward_norm_finish: T=%d n=%d world=%d", T, n,
+                world);
+    RLP_REQUIRE(parts || (world == 1 && n == 1), "rlp_reward_norm_finish: null parts");
+    if (T == 0 || n == 0) return RLP_OK;
+    hipStream_t s = as_stream(stream);
+    const int P = rs_chunks(n);
+    reward_merge_kernel<<<1, 256, 0, s>>>(reward_in, T, n, world, parts, rms, work);
+    const size_t total = (size_t)T * n;
+    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    reward_apply_kernel<<<blocks, 256, 0, s>>>(reward_in, T, n, work + (size_t)T * P * 2 + (size_t)T * 2,
+                                               reward_out);
+    RLP_CHECK_LAUNCH("rlp_reward_norm_finish");
+    return RLP_OK;
+}
+
 int rlp_reward_norm(const float *reward_in, int T, int n, double *rms, double *work,
                     float *reward_out, rlp_stream_t stream) {
     RLP_REQUIRE(reward_in && rms && work && reward_out, "rlp_reward_norm: null argument");
     RLP_REQUIRE(T >= 0 && n >= 0, "rlp_reward_norm: T=%d n=%d", T, n);
     if (T == 0 || n == 0) return RLP_OK;
-    hipStream_t s = as_stream(stream);
-    const int P = rs_chunks(n);
-    if (n > 1) reward_stats_kernel<<<dim3(P, T), 256, 0, s>>>(reward_in, n, work);
-    reward_merge_kernel<<<1, 256, 0, s>>>(reward_in, T, n, rms, work);
-    const size_t total = (size_t)T * n;
-    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    reward_apply_kernel<<<blocks, 256, 0, s>>>(reward_in, T, n, work + (size_t)T * P * 2 + (size_t)T * 2,
-                                               reward_out);
-    RLP_CHECK_LAUNCH("rlp_reward_norm");
-    return RLP_OK;
+    if (n > 1) {
+        const int rc = rlp_reward_norm_stats(reward_in, T, n, work, stream);
+        if (rc != RLP_OK) return rc;
+    }
+    return rlp_reward_norm_finish(reward_in, T, n, 1, work, rms, work, reward_out, stream);
 }
 
 int rlp_gae(const float *reward, const float *value, const float *value_next, const uint8_t *done,
@@ -274,11 +361,17 @@ int rlp_gae(const float *reward, const float *value, const float *value_next, co
     return RLP_OK;
 }
 
-int rlp_adv_normalize(float *adv, int64_t count, const double *adv_stats, rlp_stream_t stream) {
+int rlp_adv_stats_parts(int n) { return n < 0 ? RLP_EINVAL : (n + 255) / 256; }
+
+int rlp_adv_normalize(float *adv, int64_t count, double *adv_stats, int parts,
+                      rlp_stream_t stream) {
     RLP_REQUIRE(adv && adv_stats, "rlp_adv_normalize: null argument");
+    RLP_REQUIRE(parts >= 1, "rlp_adv_normalize: parts=%d", parts);
     if (count <= 1) return RLP_OK;
+    hipStream_t s = as_stream(stream);
+    adv_stats_merge_kernel<<<1, 256, 0, s>>>(adv_stats, parts);
     const int64_t b = (count + 255) / 256;
-    adv_norm_kernel<<<(int)(b < 4096 ? b : 4096), 256, 0, as_stream(stream)>>>(adv, count, adv_stats);
+    adv_norm_kernel<<<(int)(b < 4096 ? b : 4096), 256, 0, s>>>(adv, count, adv_stats + 3 * (size_t)parts);
     RLP_CHECK_LAUNCH("rlp_adv_normalize");
     return RLP_OK;
 }

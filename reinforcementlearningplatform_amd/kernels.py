@@ -189,7 +189,35 @@ def reward_norm(reward, rms, work=None, out=None):
     return out
 
 
+def reward_norm_stats(reward, work):
+    """Stage 1 of a cross-rank reward normaliser: this rank's chunk statistics into work[:parts]
+    (include/rlp.h rlp_reward_norm_stats); returns that view for the all-gather."""
+    T, n = reward.shape
+    check(lib().rlp_reward_norm_stats(ptr(reward), T, n, ptr(work), stream_ptr()),
+          "rlp_reward_norm_stats")
+    return work[:int(lib().rlp_reward_norm_parts(T, n))]
+
+
+def reward_norm_finish(reward, rms, work, parts, world, out=None):
+    """Stage 2: merge every rank's chunk statistics (`parts`, rank-major) and normalise."""
+    T, n = reward.shape
+    out = out if out is not None else torch.empty_like(reward)
+    check(lib().rlp_reward_norm_finish(ptr(reward), T, n, int(world), ptr(parts), ptr(rms),
+                                       ptr(work), ptr(out), stream_ptr()), "rlp_reward_norm_finish")
+    return out
+
+
+def adv_stats_parts(n):
+    return int(lib().rlp_adv_stats_parts(int(n)))
+
+
+def adv_stats_buffer(n, world=1, device=None):
+    """f64 buffer for rlp_gae's per-block (count, mean, M2) partials of `world` ranks + (mean, std)."""
+    return torch.zeros(3 * adv_stats_parts(n) * world + 2, dtype=torch.float64, device=_dev(device))
+
+
 def gae(reward, value, value_next, done, success, gamma, lmd, adv=None, v_target=None, stats=None):
+    """stats (nullable): adv_stats_buffer(n), receives the per-block advantage partials."""
     T, n = reward.shape
     adv = adv if adv is not None else torch.empty_like(reward)
     v_target = v_target if v_target is not None else torch.empty_like(reward)
@@ -199,8 +227,11 @@ def gae(reward, value, value_next, done, success, gamma, lmd, adv=None, v_target
     return adv, v_target
 
 
-def adv_normalize(adv, stats):
-    check(lib().rlp_adv_normalize(ptr(adv), adv.numel(), ptr(stats), stream_ptr()),
+def adv_normalize(adv, stats, parts=None):
+    """Normalise adv with the first `parts` partials of stats (default: one rank's, from the
+    buffer's size); (mean, std) land at stats[3 * parts:3 * parts + 2]."""
+    parts = (stats.numel() - 2) // 3 if parts is None else int(parts)
+    check(lib().rlp_adv_normalize(ptr(adv), adv.numel(), ptr(stats), parts, stream_ptr()),
           "rlp_adv_normalize")
     return adv
 

@@ -871,6 +871,19 @@ def gen_ppo2_learn():
         rec = {}
         real = ppo2_mod.torch
         ppo2_mod.torch = _TorchProbe(rec)
+        grads = {}
+
+        def _tap(name, opt, params):   # the .grad each optimiser step consumes (post-clip)
+            step = opt.step
+
+            def wrapped(*a, **k):
+                if name not in grads:
+                    grads[name] = np.concatenate([p.grad.detach().reshape(-1).numpy().copy()
+                                                  for p in params])
+                return step(*a, **k)
+            opt.step = wrapped
+        _tap("actor", agent.optimizer_actor, list(actor.parameters()))
+        _tap("critic", agent.optimizer_critic, list(critic.parameters()))
         try:
             with _RandpermTape() as tape:
                 agent.learn(0, buf_num=1)
@@ -883,7 +896,9 @@ def gen_ppo2_learn():
                     f"{mode}_s_": s2, f"{mode}_done": done, f"{mode}_success": success,
                     f"{mode}_before_actor": before_a, f"{mode}_before_critic": before_c,
                     f"{mode}_after_actor": _flat(actor), f"{mode}_after_critic": _flat(critic),
-                    f"{mode}_adv_norm": adv_n.numpy()[:, 0], f"{mode}_v_target": v_target.numpy()[:, 0]})
+                    f"{mode}_adv_norm": adv_n.numpy()[:, 0], f"{mode}_v_target": v_target.numpy()[:, 0],
+                    # the reference's own first-step gradients (first epoch; mini: first batch)
+                    f"{mode}_grad_actor": grads["actor"], f"{mode}_grad_critic": grads["critic"]})
         if mode == "mini":
             out["mini_perms"] = np.stack([p.numpy() for p in tape.perms])
         print("ppo2_learn", mode, "max |dW| actor %.3e critic %.3e" % (

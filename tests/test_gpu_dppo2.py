@@ -7,7 +7,11 @@ ids r*n .. r*n+n-1 and draw from the Philox stream keyed by those ids, so
   (1) the union of the ranks' rollout buffers equals a single rank's buffers on 2n envs, bit for
       bit, and
   (2) after the synchronous update (one gradient all-reduce, the Worker.learn() rule) the replicas
-      are bit-identical, and stay so for the next iteration's rollout.
+      are bit-identical, and stay so for the next iteration's rollout;
+  (3) with the default global normalisation (ppo_msg norm_scope 'global', SURVEY §8e: reward
+      chunk statistics and advantage partials gathered across ranks) the update equals the single
+      rank's on 2n envs to f32 rounding of the gradient sums (1e-5), for CartPole (the DPPO2-CartPole
+      copy) and the UavRobust hover outer loop (config 4's sharded PPO2).
 """
 import os
 
@@ -18,6 +22,8 @@ import torch
 from reinforcementlearningplatform_amd.algorithm.policy_base.Distributed_PPO2 import (
     DPPO2_COPY, Distributed_PPO2, dppo2_std_schedule)
 from reinforcementlearningplatform_amd.environment.CartPole.CartPole import CartPole
+from reinforcementlearningplatform_amd.environment.UavRobust.UavHoverOuterLoop import \
+    uav_hover_outer_loop
 from reinforcementlearningplatform_amd.utils.classes import PPOActor_Gaussian, PPOCritic
 from reinforcementlearningplatform_amd import _abi
 
@@ -28,14 +34,20 @@ KEYS = ("obs", "obs_next", "action", "logp", "reward", "value", "value_next", "d
         "flag")
 
 
-def _agent(n, env_id0):
+def _agent(n, env_id0, env="cartpole", scope="global"):
     torch.manual_seed(0)   # the same initial nets on every rank (rank 0's are broadcast anyway)
-    env = CartPole(n_envs=n, seed=5, env_id0=env_id0, variant="dppo2")
-    actor = PPOActor_Gaussian(4, 1, np.array([-8.]), np.array([8.]), init_std=1.2)
-    critic = PPOCritic(4)
+    if env == "cartpole":
+        e = CartPole(n_envs=n, seed=5, env_id0=env_id0, variant="dppo2")
+    else:
+        e = uav_hover_outer_loop(n_envs=n, seed=5, env_id0=env_id0)
+        e.reset(random=True)
+    ar = np.array(e.action_range, dtype=np.float64)
+    actor = PPOActor_Gaussian(e.state_dim, e.action_dim, ar[:, 0], ar[:, 1], init_std=1.2)
+    critic = PPOCritic(e.state_dim)
     P = 20   # train.py:136-140
-    return Distributed_PPO2(env, actor_lr=1e-4 / min(P, 5), critic_lr=1e-3 / min(P, 5),
-                            num_of_pro=P, ppo_msg={'k_epo': int(30 / min(P, 5)), 'gamma': 0.99},
+    return Distributed_PPO2(e, actor_lr=1e-4 / min(P, 5), critic_lr=1e-3 / min(P, 5),
+                            num_of_pro=P, ppo_msg={'k_epo': int(30 / min(P, 5)), 'gamma': 0.99,
+                                                   'norm_scope': scope},
                             T=T, actor=actor, critic=critic, seed=3407)
 
 
@@ -71,10 +83,17 @@ def _rank(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
-    ag = _agent(N, rank * N)
-    assert ag.world == world and ag.worker.learner.distributed
-    out[rank] = _run(ag)
+    res = {}
+    for case in CASES:
+        ag = _agent(N, rank * N, *case)
+        assert ag.world == world and ag.worker.learner.distributed
+        assert ag.worker.global_norm == (case[1] == "global")
+        res[case] = _run(ag)
+    out[rank] = res
     torch.distributed.destroy_process_group()
+
+
+CASES = [("cartpole", "global"), ("uav", "global"), ("cartpole", "rank")]
 
 
 def test_dppo2_two_ranks_union_and_replicas():
@@ -82,21 +101,27 @@ def test_dppo2_two_ranks_union_and_replicas():
     mgr = mp.Manager()
     out = mgr.dict()
     mp.start_processes(_rank, args=(2, _free_port(), out), nprocs=2, start_method="spawn")
-    r0, r1 = out[0], out[1]
     for key in ("WORLD_SIZE", "RANK"):
         os.environ.pop(key, None)
-    single = _run(_agent(2 * N, 0))
-    # (1) the first iteration's rollouts: the union is the 2n-env run, bit for bit
-    b0, b1, bs = r0[0][0], r1[0][0], single[0][0]
-    for k in KEYS:
-        np.testing.assert_array_equal(np.concatenate([b0[k], b1[k]], axis=1), bs[k], err_msg=k)
-    assert bs["done"].any()
-    # (2) replicas identical after each synchronous update, and the second rollout too
-    for it in range(2):
-        np.testing.assert_array_equal(r0[it][1], r1[it][1])
-    assert np.abs(r0[0][1] - single[0][1]).max() < 1e-2      # same objective, per-rank adv-norm
-    for k in ("action", "value"):
-        assert not np.array_equal(r0[1][0][k], r0[0][0][k])   # the second rollout used new nets
+    for case in CASES:
+        r0, r1 = out[0][case], out[1][case]
+        single = _run(_agent(2 * N, 0, *case))
+        # (1) the first iteration's rollouts: the union is the 2n-env run, bit for bit
+        b0, b1, bs = r0[0][0], r1[0][0], single[0][0]
+        for k in KEYS:
+            np.testing.assert_array_equal(np.concatenate([b0[k], b1[k]], axis=1), bs[k],
+                                          err_msg=f"{case} {k}")
+        assert bs["done"].any() or case[0] == "uav"
+        # (2) replicas identical after each synchronous update, and the second rollout too
+        for it in range(2):
+            np.testing.assert_array_equal(r0[it][1], r1[it][1])
+        err = np.abs(r0[0][1] - single[0][1]).max()
+        if case[1] == "global":   # (3) the same update as one rank on 2n envs
+            assert err <= 1e-5, (case, err)
+        else:                     # per-rank normalisers: the same objective up to the statistics
+            assert err < 1e-2, (case, err)
+        for k in ("action", "value"):
+            assert not np.array_equal(r0[1][0][k], r0[0][0][k])   # the second rollout used new nets
 
 
 def test_dppo2_copy_semantics_selected():

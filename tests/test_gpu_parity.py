@@ -86,6 +86,7 @@ def test_env_step_vs_oracle_large(kind):
     rng = np.random.default_rng(kind)
     n = 1 << 16
     p, st, act = _random_states(kind, n, rng)
+    st0 = st.copy()
     g = dev(st)
     oc, on, r, f, d = K.env_step(kind, p, g, dev(act))
     o_oc, o_on, o_r, o_f, o_d = oracle.env_step(kind, p, st, act)
@@ -94,9 +95,24 @@ def test_env_step_vs_oracle_large(kind):
     close(host(oc), o_oc, 1e-6, 1e-7, "obs_cur")
     close(host(on), o_on, 1e-6, 1e-7, "obs_next")
     close(host(r), o_r, 1e-8, 1e-9, "reward")
-    # flags may only differ where a threshold is straddled within float64 rounding
-    assert (host(f) != o_f).mean() < 1e-4
-    assert (host(d) != o_d).mean() < 1e-4
+    # flags and done exact; a row is exempt only when the oracle's own flag flips under a 1e-12
+    # relative perturbation of its input state (a threshold straddled within float64 rounding of
+    # libm ulps), and such rows are listed
+    hf, hd = host(f), host(d)
+    bad = np.nonzero((hf != o_f) | (hd != o_d))[0]
+    exempt = []
+    for i in bad:
+        flips = set()
+        for eps in (-2e-12, -1e-12, 1e-12, 2e-12):
+            sp = np.ascontiguousarray(st0[:, i:i + 1] * (1 + eps))
+            _, _, _, pf_, pd_ = oracle.env_step(kind, p, sp, act[i:i + 1])
+            flips.add((int(pf_[0]), int(pd_[0])))
+        assert (int(hf[i]), int(hd[i])) in flips, \
+            f"env {i}: flag/done {hf[i]}/{hd[i]} vs oracle {o_f[i]}/{o_d[i]} with margin > 1e-12"
+        exempt.append(int(i))
+    if exempt:
+        print(f"kind {kind}: rows within 1e-12 of a threshold (exempt): {exempt}")
+    assert len(exempt) <= 2, exempt
 
 
 @pytest.mark.parametrize("kind", sorted(A.ENV_DIMS))
@@ -180,7 +196,7 @@ def test_gae_bit_exact_vs_reference(golden):
         k = lambda s: g[f"c{c}_{s}"]
         T = len(k("r"))
         col = lambda x, dt: dev(x.reshape(T, 1), dt)
-        stats = torch.zeros(2, dtype=torch.float64, device="cuda")
+        stats = K.adv_stats_buffer(1, device="cuda")
         adv, vt = K.gae(col(k("r"), torch.float32), col(k("v"), torch.float32),
                         col(k("vn"), torch.float32), col(k("done"), torch.uint8),
                         col(k("success"), torch.uint8), float(g["gamma"]), float(g["lmd"]),
@@ -219,3 +235,70 @@ def test_reward_norm_vs_oracle(golden, T, n):
         rms = torch.zeros(4, dtype=torch.float64, device="cuda")
         out = host(K.reward_norm(dev(gg["x"].astype(np.float32).reshape(-1, 1)), rms)).ravel()
         close(out, gg["y"], 1e-5, 1e-6, "vs reference Normalization")
+
+
+@pytest.mark.parametrize("T,n", [(64, 8192), (5, 4096 * 3)])
+def test_reward_norm_cross_rank_merge_bit_exact(T, n):
+    """SURVEY §8e's Welford/Chan merge across ranks: W "ranks" of n envs (chunk statistics
+    gathered rank-major, merged in global env order) reproduce one rank of W*n envs bit for bit,
+    and every rank ends with the same running statistics."""
+    rng = np.random.default_rng(n)
+    W = 2
+    r = rng.normal(-1, 2, (T, W * n)).astype(np.float32)
+    rms1 = torch.zeros(4, dtype=torch.float64, device="cuda")
+    whole = host(K.reward_norm(dev(r), rms1))
+    parts, halves = [], []
+    for k in range(W):
+        rk = dev(r[:, k * n:(k + 1) * n])
+        work = K.reward_norm_workspace(T, n, "cuda")
+        parts.append(K.reward_norm_stats(rk, work).clone())
+        halves.append((rk, work))
+    allp = torch.cat(parts)
+    for k, (rk, work) in enumerate(halves):
+        rms = torch.zeros(4, dtype=torch.float64, device="cuda")
+        out = host(K.reward_norm_finish(rk, rms, work, allp, W))
+        np.testing.assert_array_equal(out, whole[:, k * n:(k + 1) * n])
+        np.testing.assert_array_equal(host(rms), host(rms1))
+
+
+@pytest.mark.parametrize("T,n", [(128, 65536), (7, 1000)])
+def test_adv_stats_deterministic_two_pass_and_cross_rank(T, n):
+    """rlp_gae's advantage partials: run-to-run identical (no atomics), the normalised advantages
+    match a float64 two-pass mean / unbiased std (torch .std()), and the partials of two half
+    batches, gathered, give the whole batch's normalisation bit for bit (n a multiple of 256)."""
+    rng = np.random.default_rng(T)
+    r = rng.normal(0, 1, (T, n)).astype(np.float32)
+    v = rng.normal(30, 5, (T, n)).astype(np.float32)
+    vn = rng.normal(30, 5, (T, n)).astype(np.float32)
+    done = (rng.uniform(0, 1, (T, n)) < 0.01).astype(np.uint8)
+    succ = (done * (rng.uniform(0, 1, (T, n)) < 0.6)).astype(np.uint8)
+    outs = []
+    for _ in range(2):
+        st = K.adv_stats_buffer(n, device="cuda")
+        adv, _ = K.gae(dev(r), dev(v), dev(vn), dev(done), dev(succ), 0.999, 0.95, stats=st)
+        raw = host(adv).astype(np.float64)
+        K.adv_normalize(adv, st)
+        outs.append((host(adv), host(st)))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    m, sd = raw.mean(), raw.std(ddof=1)
+    P = K.adv_stats_parts(n)
+    assert abs(outs[0][1][3 * P] - m) <= 1e-12 * (abs(m) + sd)
+    assert abs(outs[0][1][3 * P + 1] - sd) <= 1e-12 * sd
+    ref = (raw.astype(np.float32) - np.float32(m)) / (np.float32(sd) + np.float32(1e-5))
+    close(outs[0][0], ref, 1e-6, 1e-6, "normalised advantages")
+    if n % 512 == 0:
+        h = n // 2
+        stp = []
+        advs = []
+        for k in range(2):
+            sl = slice(k * h, (k + 1) * h)
+            st = K.adv_stats_buffer(h, device="cuda")
+            a, _ = K.gae(dev(r[:, sl]), dev(v[:, sl]), dev(vn[:, sl]), dev(done[:, sl]),
+                         dev(succ[:, sl]), 0.999, 0.95, stats=st)
+            stp.append(st[:3 * K.adv_stats_parts(h)])
+            advs.append(a)
+        allp = torch.cat(stp + [torch.zeros(2, dtype=torch.float64, device="cuda")])
+        for k in range(2):
+            K.adv_normalize(advs[k], allp, 2 * K.adv_stats_parts(h))
+            np.testing.assert_array_equal(host(advs[k]), outs[0][0][:, k * h:(k + 1) * h])

@@ -169,3 +169,48 @@ def test_native_update_data_parallel_two_ranks():
     nl.update(dev(s), dev(a), dev(lp), dev(adv), dev(vt))
     ref = torch.cat([nl.net_a.flat, nl.net_c.flat]).cpu().numpy()
     np.testing.assert_allclose(r0, ref, rtol=1e-5, atol=2e-6)
+
+
+DUP_CASES = [("ppo2", False), ("ppo2", True), ("dppo2", False), ("dppo2", True)]
+
+
+def _dup_msg(rule, clip):
+    return dict(DEFAULT_PPO_MSG, K_epochs=3, use_grad_clip=clip, update_rule=rule,
+                grad_clip_norm=0.2 if rule == "dppo2" else 0.5)
+
+
+def _dp_dup_worker(rank, world, port, out):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    res = []
+    for rule, clip in DUP_CASES:
+        actor, critic, s, a, lp, adv, vt = make_case(4, 1, 1536, seed=33)
+        nl = NativePPO2Learner(actor, critic, _dup_msg(rule, clip), device="cuda")
+        dev = lambda t: t.cuda().contiguous()
+        nl.update(dev(s), dev(a), dev(lp), dev(adv), dev(vt))   # the SAME batch on both ranks
+        nl.update(dev(s), dev(a), dev(lp), dev(adv), dev(vt))
+        res.append(torch.cat([nl.net_a.flat, nl.net_c.flat]).cpu().numpy().copy())
+    out[rank] = res
+    torch.distributed.destroy_process_group()
+
+
+def test_native_update_data_parallel_duplicated_batch_bit_exact():
+    """with the same batch on both ranks the gradient average is the identity
+    ((g + g) / 2 == g exactly in f32), so a missing or doubled `/ world` in the all-reduce, or an
+    all-reduce applied at the wrong point of the update rule, shows as a bit difference against a
+    single-rank learner. Both update rules, clipping off and on, two learn() calls."""
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_dp_dup_worker, args=(2, _free_port(), out), nprocs=2, start_method="spawn")
+    for i, (rule, clip) in enumerate(DUP_CASES):
+        actor, critic, s, a, lp, adv, vt = make_case(4, 1, 1536, seed=33)
+        nl = NativePPO2Learner(actor, critic, _dup_msg(rule, clip), device="cuda")
+        dev = lambda t: t.cuda().contiguous()
+        nl.update(dev(s), dev(a), dev(lp), dev(adv), dev(vt))
+        nl.update(dev(s), dev(a), dev(lp), dev(adv), dev(vt))
+        ref = torch.cat([nl.net_a.flat, nl.net_c.flat]).cpu().numpy()
+        for r in (0, 1):
+            np.testing.assert_array_equal(out[r][i], ref, err_msg=f"rank {r} {rule} clip={clip}")
