@@ -103,6 +103,17 @@ def pmc_traffic(workload, n, T, kernel=None):
     return e["hbm_bytes_per_launch"]
 
 
+def pmc_kernel_traffic(name):
+    """HBM bytes per launch of an hbm_legs kernel from the committed PMC pass
+    (profiles/pmc_traffic.json "hbm_kernels"), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        e = json.load(f).get("hbm_kernels", {}).get(name)
+    return None if e is None else e.get("hbm_bytes_per_launch")
+
+
 class Segment:
     """Device-resident state + buffers of one rank's env batch."""
 
@@ -154,7 +165,7 @@ class Segment:
         self.learn_side()
 
 
-def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
+def e2e_iterations(seg, iters, k_epochs=6, learner="native", fd_streams=False):
     """Whole PPO2 iterations: rollout + advantages + K full-batch epochs of the clipped-surrogate /
     MSE update (torch autograd + Adam on this GPU; the DPPO2 CartPole drivers' k_epo = 6,
     demonstration/DPPO2/DPPO2-4-CartPole/train.py:161). Returns env-steps/s of this rank."""
@@ -171,7 +182,8 @@ def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
                 p.copy_(flat[off:off + p.numel()].view_as(p).cpu())
                 off += p.numel()
     cls = NativePPO2Learner if learner == "native" else PPO2Learner
-    learner = cls(actor, critic, dict(DEFAULT_PPO_MSG, K_epochs=k_epochs), device="cuda")
+    learner = cls(actor, critic, dict(DEFAULT_PPO_MSG, K_epochs=k_epochs, fd_streams=fd_streams),
+                  device="cuda")
     b = seg.bufs
 
     def one():
@@ -345,6 +357,75 @@ def ugvoa_sac_leg(rank, n=16384, steps=20, warmup=3, batch=4096, capacity=1 << 2
                       "per update (sample, gather, update, soft update, actor refresh)"}
 
 
+def hbm_legs(seg, n_env=1 << 22, iters=10, warmup=2):
+    """BASELINE.md §3 / SURVEY §8(d): the HBM-bound kernels priced against the HBM roof (8 TB/s),
+    with algorithmic bytes per launch (the minimal reads + writes of the kernel's contract):
+      gae_kernel           r, V, V' f32 + done, success u8 read; adv, v_target f32 written
+      reward_norm          stats pass reads r; apply reads r and writes the normalised reward
+      adv_normalize        reads and writes adv
+      env_step_kernel<K>   f64 state read (D) and written (DW, the components step() changes) +
+                           f32 action read; f32 obs_next, f64 reward, i32 flag, u8 done written
+    GAE / normaliser on the bench segment (n x T); env steps at n_env envs (SOI, UGV, UAV kinds)."""
+    out = {}
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(iters)]
+        for a, b in ev:
+            a.record()
+            fn()
+            b.record()
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    def put(name, kernel, nbytes, ms, extra=None):
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out[name] = dict({"kernel": kernel, "bytes_per_launch": int(nbytes), "avg_launch_ms": ms,
+                          "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                          "frac": gbs / PEAK_HBM_GBS}, **(extra or {}))
+
+    b, smp = seg.bufs, seg.n * seg.T
+    ms = timed(lambda: K.gae(seg.rnorm, b["value"], b["value_next"], b["done"], b["success"], 0.999,
+                             0.95, adv=seg.adv, v_target=seg.vt, stats=seg.stats))
+    put("gae", "rlp::gae_kernel", smp * (3 * 4 + 2 + 2 * 4), ms, {"samples": smp})
+    rms = torch.zeros(4, dtype=torch.float64, device="cuda")
+    ms = timed(lambda: K.reward_norm(b["reward"], rms, seg.work, out=seg.rnorm))
+    put("reward_norm", "rlp::reward_stats_kernel + reward_merge_kernel + reward_apply_kernel",
+        smp * 12, ms, {"samples": smp})
+    ms = timed(lambda: K.adv_normalize(seg.adv, seg.stats))
+    put("adv_normalize", "rlp::adv_stats_merge_kernel + adv_norm_kernel", smp * 8, ms,
+        {"samples": smp})
+    for env, kind, pf, dw in (("soi", A.RLP_ENV_SOI, lambda: A.soi_params("env"), 5),
+                              ("ugv", A.RLP_ENV_UGV_FORWARD,
+                               lambda: A.ugv_params(A.RLP_ENV_UGV_FORWARD, "ppo2"), 6),
+                              ("uav", A.RLP_ENV_UAV_HOVER_OUTER_LOOP, A.uav_hover_params, 22)):
+        D, S, Ad = A.ENV_DIMS[kind]
+        p = pf()
+        st = K.new_state(kind, n_env)
+        K.env_reset(kind, p, st, seed=7, counter=1)
+        lo, hi = A.action_bounds(kind, p)
+        g = torch.Generator(device="cuda").manual_seed(3)
+        act = (torch.tensor(lo, device="cuda") + (torch.tensor(hi, device="cuda") - torch.tensor(lo, device="cuda"))
+               * torch.rand(n_env, Ad, device="cuda", generator=g)).float().contiguous()
+        on = torch.empty((n_env, S), dtype=torch.float32, device="cuda")
+        r = torch.empty(n_env, dtype=torch.float64, device="cuda")
+        f = torch.empty(n_env, dtype=torch.int32, device="cuda")
+        d = torch.empty(n_env, dtype=torch.uint8, device="cuda")
+        lib = _native.lib()
+
+        def step():
+            K.check(lib.rlp_env_step(kind, K.C.byref(p), K.ptr(st), n_env, K.ptr(act), None,
+                                     K.ptr(on), K.ptr(r), K.ptr(f), K.ptr(d), K.stream_ptr()),
+                    "rlp_env_step")
+        ms = timed(step)
+        nbytes = n_env * (D * 8 + Ad * 4 + dw * 8 + S * 4 + 8 + 4 + 1)
+        put(f"env_step_{env}", f"rlp::env_step_kernel<{kind}>", nbytes, ms, {"envs": n_env})
+        del st, act, on, r, f, d
+    return out
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -388,17 +469,73 @@ def cpu_baseline(env, seconds=10.0):
         dt = run(n, T)
         return n * T / dt, n, T, dt
 
+    def env_only(threads, secs):   # the env step alone, random actions
+        oracle.set_threads(threads)
+        n = 4096 * threads
+        st = np.zeros((D, n))
+        oracle.env_reset(kind, p, st, seed=3, counter=1)
+        act = np.random.default_rng(0).uniform(lo, hi, (n, Ad)).astype(np.float32)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            oracle.env_step(kind, p, st, act, want_obs_cur=False)
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= secs:
+                return n * reps / dt, n * reps, dt
+
+    def learn(threads, B=1000, K=30):
+        """the PPO2-CartPole driver's update (K=30 full-batch epochs on its
+        1000-row buffer, Proximal_Policy_Optimization2.py:102-163) with the reference's own
+        arithmetic: torch-autograd + Adam on the CPU (vec_ppo2.PPO2Learner, pinned to the
+        reference's learn() by tests/test_learn_golden.py)."""
+        from reinforcementlearningplatform_amd.algorithm.policy_base.vec_ppo2 import (
+            DEFAULT_PPO_MSG, PPO2Learner)
+        from reinforcementlearningplatform_amd.utils.classes import PPOActor_Gaussian, PPOCritic
+        old = torch.get_num_threads()
+        torch.set_num_threads(threads)
+        torch.manual_seed(0)
+        actor = PPOActor_Gaussian(S, Ad, np.array(lo), np.array(hi), init_std=std[0])
+        lrn = PPO2Learner(actor, PPOCritic(S), dict(DEFAULT_PPO_MSG, K_epochs=K), device="cpu")
+        g = torch.Generator().manual_seed(1)
+        x = [torch.randn(B, S, generator=g), torch.randn(B, Ad, generator=g),
+             -torch.rand(B, Ad, generator=g), torch.randn(B, 1, generator=g),
+             torch.randn(B, 1, generator=g)]
+        lrn.update(*x)   # warm-up
+        t0 = time.perf_counter()
+        lrn.update(*x)
+        dt = time.perf_counter() - t0
+        torch.set_num_threads(old)
+        return B / dt, dt
+
     P = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
     v1, n1, T1, dt1 = sample(1, seconds / 2)
     vp, n_p, Tp, dtp = sample(P, seconds / 2)
+    e1, en1, edt1 = env_only(1, 1.5)
+    ep, enp, edtp = env_only(P, 1.5)
+    l1, ldt1 = learn(1)
+    lp, ldtp = learn(P)
     oracle.set_threads(P)
     return {"value": vp, "unit": "env-steps/s", "cores": P, "kind": "port",
             "cpu_model": _cpu_model(), "cpus_visible": os.cpu_count(),
+            "cores_note": "the GPU box grants one GPU's job 16 host CPUs (OMP_NUM_THREADS=16); the "
+                          "other visible CPUs serve the other GPUs' jobs",
             "single_thread": {"value": v1, "cores": 1, "env_steps": n1 * T1, "seconds": dt1},
             "sample": f"oracle/rlp_oracle.c rollout (actor+critic 256x256 fp32 MLP with double "
                       f"accumulation, Philox sample, f64 RK4 {env} step): {n_p} envs x {Tp} steps = "
                       f"{n_p * Tp} env-steps in {dtp:.1f} s on {P} host threads (OpenMP over envs); "
-                      f"1 thread: {n1} x {T1} in {dt1:.1f} s"}
+                      f"1 thread: {n1} x {T1} in {dt1:.1f} s",
+            "env_only": {"value": ep, "unit": "env-steps/s", "cores": P,
+                         "single_thread": e1, "env_steps": enp, "seconds": edtp,
+                         "sample": f"oracle env_step ({env}, f64 RK4, uniform actions): "
+                                   f"{4096 * P} envs x repeats on {P} threads, {4096} on 1"},
+            "learn": {"value": lp, "unit": "rows/s (K=30 epochs each)", "cores": P,
+                      "single_thread": l1, "seconds": ldtp, "single_thread_seconds": ldt1,
+                      "sample": "torch CPU autograd + Adam (the reference's learn() arithmetic), "
+                                "K=30 full-batch epochs on a 1000-row buffer, [S,256,256,A] nets"},
+            "e2e": {"value": 1.0 / (1.0 / vp + 1.0 / lp), "unit": "env-steps/s", "cores": P,
+                    "single_thread": 1.0 / (1.0 / v1 + 1.0 / l1),
+                    "note": "rollout + K=30 update per collected row (the PPO2-CartPole driver's "
+                            "learn() after each 1000-row buffer)"}}
 
 
 def main():
@@ -427,8 +564,12 @@ def main():
     ap.add_argument("--uav-envs", type=int, default=32768, help="UavRobust leg's envs per GPU (config 4: 262144 / 8)")
     ap.add_argument("--uav-physics", default=None, choices=list(PHYSICS_MODES),
                     help="rollout kernel of the UavRobust leg (default: --physics)")
+    ap.add_argument("--hbm", type=int, default=1, help="also time the HBM-bound kernels (GAE, reward / "
+                    "advantage normalisation, SOI / UGV / UAV env steps) against the HBM roof")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
+    ap.add_argument("--fd-streams", type=int, default=0, help="e2e: actor and critic gradient "
+                    "kernels concurrently on two streams (NativePPO2Learner fd_streams)")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="rollout hidden-layer arithmetic (include/rlp.h rlp_set_mlp_precision)")
     args = ap.parse_args()
@@ -566,6 +707,10 @@ def main():
                          "avg_launch_ms": ums, "flop_per_launch": uflop}}
         del useg
         _native.set_rollout_physics(PHYSICS_MODES[args.physics])
+    if args.hbm:
+        out["hbm_kernels"] = hbm_legs(seg)
+        for k, v in out["hbm_kernels"].items():
+            v["traffic"] = pmc_kernel_traffic(k)
     if args.ddpg and args.env == "cartpole":
         d = soi_ddpg_leg(rank)
         if dist is not None:
@@ -590,12 +735,13 @@ def main():
     if args.e2e:
         upd = ("librlp rlp_ppo2_grad + rlp_adam_step" if args.learner == "native"
                else "torch autograd + Adam (fp32)")
-        v, it_s = e2e_iterations(seg, args.e2e, learner=args.learner)
+        v, it_s = e2e_iterations(seg, args.e2e, learner=args.learner, fd_streams=bool(args.fd_streams))
         out["e2e"] = {"value": v * world, "unit": "env-steps/s", "s_per_iteration": it_s,
                       "update": f"K=6 full-batch epochs per iteration (DPPO2 drivers' k_epo), {upd}",
                       "note": "rollout + GAE + PPO update; `value` above is the rollout hot path"}
         if args.e2e_k30:
-            v30, it30 = e2e_iterations(seg, max(1, args.e2e // 2), k_epochs=30, learner=args.learner)
+            v30, it30 = e2e_iterations(seg, max(1, args.e2e // 2), k_epochs=30, learner=args.learner,
+                                       fd_streams=bool(args.fd_streams))
             out["e2e"]["k30"] = {
                 "value": v30 * world, "unit": "env-steps/s", "s_per_iteration": it30,
                 "update": f"K=30 full-batch epochs per iteration (PPO2-4-CartPole/train.py:146), {upd}"}

@@ -423,6 +423,15 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
                   const float *s, const float *a, const float *a_logprob, const float *adv,
                   const float *v_target, const int64_t *index, int64_t rows, float *grad,
                   double *loss_sum, float *workspace, rlp_stream_t stream);
+
+/* Block shape of rlp_ppo2_grad's forward/backward (FD) kernel, library-wide: 0 one 8-wave block
+ * per CU (default), 1 two 4-wave blocks per CU, 2 one 4-wave block per CU — for running the
+ * actor's and the critic's rlp_ppo2_grad concurrently on two streams (each with its own workspace):
+ * every CU then holds one wave of each net per SIMD, and the two independent instruction streams
+ * overlap one net's VALU phases with the other's MFMA phases. */
+int rlp_set_fd_mode(int mode);
+int rlp_get_fd_mode(void);
+
 /* out[0] += sum(grad^2) (torch.nn.utils.clip_grad_norm_'s total norm, squared), accumulated in
  * double in a fixed order: bit-identical on every run and every data-parallel rank. */
 int rlp_grad_sqnorm(const float *grad, int64_t n, double *out, rlp_stream_t stream);

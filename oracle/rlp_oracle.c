@@ -894,8 +894,10 @@ int oracle_env_step(int kind, const void *params, double *state, int n, const fl
                     float *obs_cur, float *obs_next, double *reward, int32_t *flag, uint8_t *done) {
     int D, S, A;
     if (oracle_env_dims(kind, &D, &S, &A)) return -1;
-    double s[64];
+    /* independent envs: OpenMP over them (oracle_set_threads), each env's arithmetic unchanged */
+#pragma omp parallel for schedule(static) if (n > 256)
     for (int i = 0; i < n; ++i) {
+        double s[64];
         gather(state, D, n, i, s);
         env_step1(kind, params, s, action + (size_t)i * A, obs_cur ? obs_cur + (size_t)i * S : NULL,
                   obs_next + (size_t)i * S, reward + i, flag + i, done + i);

@@ -88,6 +88,92 @@ __device__ __forceinline__ double div_nr(double num, double den) {
     return fma(fma(-den, q, num), y, q);
 }
 
+// Reciprocal of a finite, normal den (rcp + two Newton steps, <= 1 ulp) and the quotient from it
+// with one residual correction (Markstein): for denominators shared by several quotients in a step
+// (inertias, mass, cos theta), 3 VALU ops per quotient after the reciprocal's 5.
+__device__ __forceinline__ double recip_nr(double den) {
+    double y = __builtin_amdgcn_rcp(den);
+    y = fma(y, fma(-den, y, 1.0), y);
+    return fma(y, fma(-den, y, 1.0), y);
+}
+__device__ __forceinline__ double div_r(double num, double den, double y) {
+    const double q = num * y;
+    return fma(fma(-den, q, num), y, q);
+}
+
+// exp / log / tanh for the UAV controller and reward (FNTSMC.py:96-106, UavHoverOuterLoop.py:93-110):
+// ~20-40 VALU ops each instead of ocml's 42 / 98 / 165 (whose double-double paths buy the last
+// half ulp): <= 2-3 ulp, far inside the 1e-9 state parity (tests/test_gpu_rollout_parity.py).
+// exp: Cody-Waite by ln 2 (hi / lo), Taylor to r^13 on |r| <= ln2/2 (truncation < 1e-17), ldexp;
+// the argument clamped to [-746, 709.7] (exp(-inf) = 0, as pow(0, a > 0) = 0).
+__device__ __forceinline__ double exp_fast(double x) {
+    x = fmin(fmax(x, -746.0), 709.78);
+    const double k = rint(x * 1.4426950408889634074);
+    double r = fma(-k, 6.93147180369123816490e-01, x);
+    r = fma(-k, 1.90821492927058770002e-10, r);
+    double q = 1.6059043836821614599e-10;                 // 1/13!
+    q = fma(q, r, 2.0876756987868098979e-09);             // 1/12!
+    q = fma(q, r, 2.5052108385441718775e-08);             // 1/11!
+    q = fma(q, r, 2.7557319223985890653e-07);             // 1/10!
+    q = fma(q, r, 2.7557319223985890653e-06);             // 1/9!
+    q = fma(q, r, 2.4801587301587301587e-05);             // 1/8!
+    q = fma(q, r, 1.9841269841269841270e-04);             // 1/7!
+    q = fma(q, r, 1.3888888888888888889e-03);             // 1/6!
+    q = fma(q, r, 8.3333333333333333333e-03);             // 1/5!
+    q = fma(q, r, 4.1666666666666666667e-02);             // 1/4!
+    q = fma(q, r, 1.6666666666666666667e-01);             // 1/3!
+    q = fma(q, r, 0.5);
+    q = fma(q, r, 1.0);
+    q = fma(q, r, 1.0);
+    return __builtin_amdgcn_ldexp(q, (int)k);
+}
+// log: x = m 2^e with m in [sqrt(1/2), sqrt(2)), f = m - 1 exact, s = f / (2 + f), and fdlibm's
+// __ieee754_log reduction and minimax coefficients Lg1..Lg7 (< 1 ulp there); log(0) = -inf.
+__device__ __forceinline__ double log_fast(double x) {
+    double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
+    int e = __builtin_amdgcn_frexp_exp(x);
+    const bool lo = m < 0.70710678118654752440;
+    m = lo ? m + m : m;
+    e = lo ? e - 1 : e;
+    const double f = m - 1.0, dk = (double)e;
+    const double s = div_nr(f, 2.0 + f);
+    const double z = s * s, w = z * z;
+    const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01),
+                              3.999999999940941908e-01);
+    const double t2 = z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01),
+                                     2.857142874366239149e-01), 6.666666666666735130e-01);
+    const double R = t2 + t1, hfsq = 0.5 * f * f;
+    const double r = dk * 6.93147180369123816490e-01 -
+                     ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
+    return x == 0.0 ? -__builtin_inf() : r;
+}
+// tanh(x) = sign(x) em / (em + 2), em = expm1(2|x|) = 2^k (1 + q) - 1 with q = expm1(r) (Taylor to
+// r^14 on |r| <= ln2/2): relative accuracy for tiny |x| (k = 0: em = q), |x| clamped to 22
+// (tanh = 1 in f64 beyond 19.1).
+__device__ __forceinline__ double tanh_fast(double x) {
+    const double y = 2.0 * fmin(fabs(x), 22.0);
+    const double k = rint(y * 1.4426950408889634074);
+    double r = fma(-k, 6.93147180369123816490e-01, y);
+    r = fma(-k, 1.90821492927058770002e-10, r);
+    double q = 1.1470745597729724714e-11;                 // 1/14!
+    q = fma(q, r, 1.6059043836821614599e-10);
+    q = fma(q, r, 2.0876756987868098979e-09);
+    q = fma(q, r, 2.5052108385441718775e-08);
+    q = fma(q, r, 2.7557319223985890653e-07);
+    q = fma(q, r, 2.7557319223985890653e-06);
+    q = fma(q, r, 2.4801587301587301587e-05);
+    q = fma(q, r, 1.9841269841269841270e-04);
+    q = fma(q, r, 1.3888888888888888889e-03);
+    q = fma(q, r, 8.3333333333333333333e-03);
+    q = fma(q, r, 4.1666666666666666667e-02);
+    q = fma(q, r, 1.6666666666666666667e-01);
+    q = fma(q, r, 0.5);
+    q = r * fma(q, r, 1.0);                               // expm1(r)
+    const int ki = (int)k;
+    const double em = __builtin_amdgcn_ldexp(q, ki) + (__builtin_amdgcn_ldexp(1.0, ki) - 1.0);
+    return copysign(div_nr(em, em + 2.0), x);
+}
+
 template <int KIND> struct Env;
 
 // components of the physics state step() may change (E::DW when the kind declares it, else D):
@@ -310,6 +396,7 @@ template <> struct Env<RLP_ENV_CARTPOLE_ANGLEONLY> {
 template <> struct Env<RLP_ENV_SOI> {
     using P = rlp_soi_params;
     static constexpr int D = RLP_SOI_D, S = 4, A = 2;
+    static constexpr int DW = 5;  // step() changes x y vx vy time (the target is fixed per episode)
 
     __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
         const double ex = s[5] - s[0], ey = s[6] - s[1];  // get_state :211-219
@@ -382,6 +469,7 @@ template <> struct Env<RLP_ENV_SOI> {
 template <bool BIDIR> struct UGV {
     using P = rlp_ugv_params;
     static constexpr int D = RLP_UGV_D, S = 4, A = 2;
+    static constexpr int DW = 6;  // step() changes x y vel phi omega time (not the target)
 
     __device__ static __forceinline__ double get_e(const double *s, double c, double sn) {
         const double ex = s[6] - s[0], ey = s[7] - s[1];
@@ -509,29 +597,38 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
     static constexpr int D = RLP_UAV_D, S = 6, A = 3;
     enum { X = 0, VX = 3, PHI = 6, THE = 7, PSI = 8, PP = 9, T = 12, REF = 13, S1 = 16, AREF = 19 };
 
-    // UAV.ode uav.py:429-460 (J0 = 0, ideal: dis = 0)
-    __device__ static __forceinline__ void ode(const P &p, double thr, const double tq[3],
-                                               const double *x, double *d) {
-        const double vx = x[3], vy = x[4], vz = x[5], phi = x[6], th = x[7], psi = x[8];
+    // reciprocals of the step's constant denominators (inertias, mass), shared by the 4 ODE stages
+    struct Rc {
+        double J[3], m;
+    };
+    // UAV.ode uav.py:429-460 (J0 = 0, ideal: dis = 0); sc = sin / cos of phi, theta, psi of x
+    __device__ static __forceinline__ void ode(const P &p, const Rc &rc, double thr, const double tq[3],
+                                               const double *x, const double sc[6], double *d) {
+        const double vx = x[3], vy = x[4], vz = x[5];
         const double pp = x[9], q = x[10], r = x[11];
-        const double dp = div_nr(-p.kr * pp - q * r * (p.J[2] - p.J[1]) + tq[0], p.J[0]);
-        const double dq = div_nr(-p.kr * q - pp * r * (p.J[0] - p.J[2]) + tq[1], p.J[1]);
-        const double dr = div_nr(-p.kr * r - pp * q * (p.J[1] - p.J[0]) + tq[2], p.J[2]);
-        double sphi, cphi, sth, cth, spsi, cpsi;
-        sincos_fast(phi, &sphi, &cphi);
-        sincos_fast(th, &sth, &cth);
-        sincos_fast(psi, &spsi, &cpsi);
-        const double tth = div_nr(sth, cth);
+        const double dp = div_r(-p.kr * pp - q * r * (p.J[2] - p.J[1]) + tq[0], p.J[0], rc.J[0]);
+        const double dq = div_r(-p.kr * q - pp * r * (p.J[0] - p.J[2]) + tq[1], p.J[1], rc.J[1]);
+        const double dr = div_r(-p.kr * r - pp * q * (p.J[1] - p.J[0]) + tq[2], p.J[2], rc.J[2]);
+        const double sphi = sc[0], cphi = sc[1], sth = sc[2], cth = sc[3], spsi = sc[4], cpsi = sc[5];
+        const double ic = recip_nr(cth);
+        const double tth = div_r(sth, cth, ic);
         const double R01 = tth * sphi, R02 = tth * cphi, R11 = cphi, R12 = -sphi;
-        const double R21 = div_nr(sphi, cth), R22 = div_nr(cphi, cth);
+        const double R21 = div_r(sphi, cth, ic), R22 = div_r(cphi, cth, ic);
         d[6] = 1 * pp + R01 * q + R02 * r;
         d[7] = 0 * pp + R11 * q + R12 * r;
         d[8] = 0 * pp + R21 * q + R22 * r;
         d[0] = vx; d[1] = vy; d[2] = vz;
-        d[3] = div_nr(thr * (cpsi * sth * cphi + spsi * sphi) - p.kt * vx + 0.0, p.m);
-        d[4] = div_nr(thr * (spsi * sth * cphi - cpsi * sphi) - p.kt * vy + 0.0, p.m);
-        d[5] = -p.g + div_nr(thr * cphi * cth - p.kt * vz + 0.0, p.m);
+        d[3] = div_r(thr * (cpsi * sth * cphi + spsi * sphi) - p.kt * vx + 0.0, p.m, rc.m);
+        d[4] = div_r(thr * (spsi * sth * cphi - cpsi * sphi) - p.kt * vy + 0.0, p.m, rc.m);
+        d[5] = -p.g + div_r(thr * cphi * cth - p.kt * vz + 0.0, p.m, rc.m);
         d[9] = dp; d[10] = dq; d[11] = dr;
+    }
+    // the stage's angles' sin / cos from the base point's by angle addition (sincos_step)
+    __device__ static __forceinline__ void stage_sc(const double sc0[6], const double *s,
+                                                    const double *t, double sc[6]) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            sincos_step(sc0[2 * i], sc0[2 * i + 1], t[PHI + i] - s[PHI + i], &sc[2 * i], &sc[2 * i + 1]);
     }
     __device__ static __forceinline__ void observe(const P &p, const double *s, float *o) {
 #pragma unroll
@@ -552,39 +649,45 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
         // uo_2_ref_angle_throttle uav_pos_ctrl.py:67-76; (uz + g) * m in float32 (NEP 50)
         const double ux = (double)a[0], uy = (double)a[1];
         const float uzg = (a[2] + (float)p.g) * (float)p.m;
-        const double uf = (double)uzg / (cphi * cth);
-        const double phi_d0 = asin(clipd((ux * spsi - uy * cpsi) * p.m / uf, -1, 1));
-        const double th_d0 = asin(clipd((ux * cpsi + uy * spsi) * p.m / (uf * cos(phi_d0)), -1, 1));
+        const double uf = div_nr((double)uzg, cphi * cth);
+        const double u0 = clipd(div_nr((ux * spsi - uy * cpsi) * p.m, uf), -1, 1);
+        const double phi_d0 = asin(u0);
+        double spd, cpd;  // cos(phi_d0) as the reference evaluates it (not sqrt(1 - u0^2))
+        sincos_fast(phi_d0, &spd, &cpd);
+        const double th_d0 = asin(clipd(div_nr((ux * cpsi + uy * spsi) * p.m, uf * cpd), -1, 1));
         const double phi_d = clipd(phi_d0, p.att_zone[0][0], p.att_zone[0][1]);  // :126-127
         const double th_d = clipd(th_d0, p.att_zone[1][0], p.att_zone[1][1]);
         const double aref_new[3] = {phi_d, th_d, 0.0};
         double daref[3], aref[3];
+        const double idt = recip_nr(p.dt);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {  // attitude-reference rate limit :130-134
             const double old = s[AREF + i];
-            daref[i] = clipd((aref_new[i] - old) / p.dt, p.dot_att_min[i], p.dot_att_max[i]);
+            daref[i] = clipd(div_r(aref_new[i] - old, p.dt, idt), p.dot_att_min[i], p.dot_att_max[i]);
             aref[i] = daref[i] * p.dt + old;
         }
         // att_control uav_pos_ctrl.py:46-65 -> fntsmc_att.control_update FNTSMC.py:80-106
-        const double tth = div_nr(sth, cth);
+        const Rc rc = {{recip_nr(p.J[0]), recip_nr(p.J[1]), recip_nr(p.J[2])}, recip_nr(p.m)};
+        const double icth = recip_nr(cth);
+        const double tth = div_r(sth, cth, icth);
         const double f1[3][3] = {{1., sphi * tth, cphi * tth}, {0., cphi, -sphi},
-                                 {0., sphi / cth, cphi / cth}};
+                                 {0., div_r(sphi, cth, icth), div_r(cphi, cth, icth)}};
         const double rho2[3] = {pp, q, r};
         double drho1[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i)
             drho1[i] = f1[i][0] * rho2[0] + f1[i][1] * rho2[1] + f1[i][2] * rho2[2];
-        const double f2[3] = {(p.kr * pp + q * r * (p.J[1] - p.J[2])) / p.J[0],  // uav.py:630-641
-                              (p.kr * q + pp * r * (p.J[2] - p.J[0])) / p.J[1],
-                              (p.kr * r + pp * q * (p.J[0] - p.J[1])) / p.J[2]};
-        const double c2 = cth * cth;  // F uav.py:668-686
+        const double f2[3] = {div_r(p.kr * pp + q * r * (p.J[1] - p.J[2]), p.J[0], rc.J[0]),  // uav.py:630-641
+                              div_r(p.kr * q + pp * r * (p.J[2] - p.J[0]), p.J[1], rc.J[1]),
+                              div_r(p.kr * r + pp * q * (p.J[0] - p.J[1]), p.J[2], rc.J[2])};
+        const double c2 = cth * cth, ic2 = recip_nr(c2);  // F uav.py:668-686
         double dF[3][3] = {{0., 0., 0.}, {0., 0., 0.}, {0., 0., 0.}};
-        dF[0][1] = drho1[0] * tth * cphi + drho1[1] * sphi / c2;
-        dF[0][2] = -drho1[0] * tth * sphi + drho1[1] * cphi / c2;
+        dF[0][1] = drho1[0] * tth * cphi + div_r(drho1[1] * sphi, c2, ic2);
+        dF[0][2] = -drho1[0] * tth * sphi + div_r(drho1[1] * cphi, c2, ic2);
         dF[1][1] = -drho1[0] * sphi;
         dF[1][2] = -drho1[0] * cphi;
-        dF[2][1] = (drho1[0] * cphi * cth + drho1[1] * sphi * sth) / c2;
-        dF[2][2] = (-drho1[0] * sphi * cth + drho1[1] * cphi * sth) / c2;
+        dF[2][1] = div_r(drho1[0] * cphi * cth + drho1[1] * sphi * sth, c2, ic2);
+        dF[2][2] = div_r(-drho1[0] * sphi * cth + drho1[1] * cphi * sth, c2, ic2);
         const double rho1[3] = {phi, th, psi};
         double u12[3];
 #pragma unroll
@@ -596,16 +699,16 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
             // |e|^alpha and |e|^(alpha-1) from one log: exp(a log|e|) instead of two f64 pow
             // (ocml's pow carries a double-double log for a 1-ulp result; this is within a few
             // ulps, far inside the 1e-9 state parity; pow(0, a) = exp(a * -inf) as pow's)
-            const double le = log(fabs(e));
-            const double pe = exp(p.att_alpha[i] * le), pe1 = exp((p.att_alpha[i] - 1) * le);
-            const double ss = 1 * de + p.att_k1[i] * e + p.att_gamma[i] * pe * tanh(5 * e);
-            const double ds1 = exp(p.att_beta[i] * log(fabs(ss))) * tanh(5 * ss);
+            const double le = log_fast(fabs(e));
+            const double pe = exp_fast(p.att_alpha[i] * le), pe1 = exp_fast((p.att_alpha[i] - 1) * le);
+            const double ss = 1 * de + p.att_k1[i] * e + p.att_gamma[i] * pe * tanh_fast(5 * e);
+            const double ds1 = exp_fast(p.att_beta[i] * log_fast(fabs(ss))) * tanh_fast(5 * ss);
             s[S1 + i] += ds1 * p.att_ctrl_dt;
             const double sigma = ss + p.att_lmd[i] * s[S1 + i];
             const double u1 = sec + 0.0 + p.att_k1[i] * de +
                               p.att_gamma[i] * p.att_alpha[i] * pe1 * de +
                               p.att_lmd[i] * ds1;
-            const double u2 = -p.att_k2[i] * tanh(10 * sigma);
+            const double u2 = -p.att_k2[i] * tanh_fast(10 * sigma);
             u12[i] = u1 + u2;
         }
         // -inv(f1 diag(1/J)) (u1+u2) = -diag(J) f1^-1 (u1+u2); f1^-1 of the Euler-rate matrix
@@ -622,17 +725,23 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
         const double h = p.dt / 1;
         // s[0..11] is the RK4 base point (unchanged until the end); running sum of
         // (K1 + 2*K2 + 2*K3 + K4), bit-identical to the left-to-right expression
+        // stage angles' sin / cos: the step's own (stage 1) and angle addition from them (2-4)
         double sum[12], t[12], d[12];
-        ode(p, uf, tq, s, d);
+        const double sc0[6] = {sphi, cphi, sth, cth, spsi, cpsi};
+        double sc[6];
+        ode(p, rc, uf, tq, s, sc0, d);
 #pragma unroll
         for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = k; t[i] = fma(k, 0.5, s[i]); }
-        ode(p, uf, tq, t, d);
+        stage_sc(sc0, s, t, sc);
+        ode(p, rc, uf, tq, t, sc, d);
 #pragma unroll
         for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = fma(k, 2.0, sum[i]); t[i] = fma(k, 0.5, s[i]); }
-        ode(p, uf, tq, t, d);
+        stage_sc(sc0, s, t, sc);
+        ode(p, rc, uf, tq, t, sc, d);
 #pragma unroll
         for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = fma(k, 2.0, sum[i]); t[i] = s[i] + k; }
-        ode(p, uf, tq, t, d);
+        stage_sc(sc0, s, t, sc);
+        ode(p, rc, uf, tq, t, sc, d);
 #pragma unroll
         for (int i = 0; i < 12; ++i) s[i] = s[i] + div6(sum[i] + h * d[i]);
         s[T] += p.dt;
@@ -649,22 +758,23 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
         if (po) f = 2;
         if (ao) f = 3;
         observe(p, s, on);
-        double nte = 0, ne = 0, ntv = 0, nv = 0;  // get_reward :93-110
+        // get_reward :93-110; ||x||^2 as the sum of squares (numpy's sqrt-then-square is within
+        // 1 ulp of it)
+        double nte2 = 0, ne2 = 0, ntv2 = 0, nv2 = 0;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const double e = s[X + i] - s[REF + i], v = s[VX + i];
-            const double te = tanh(10 * e), tv = tanh(10 * v);
-            nte += te * te; ne += e * e; ntv += tv * tv; nv += v * v;
+            const double te = tanh_fast(10 * e), tv = tanh_fast(10 * v);
+            nte2 += te * te; ne2 += e * e; ntv2 += tv * tv; nv2 += v * v;
         }
-        nte = sqrt(nte); ne = sqrt(ne); ntv = sqrt(ntv); nv = sqrt(nv);
         const float na = sqrtf(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);  // float32 action norm
-        const double r1 = -(nte * nte) * 0.5 * p.Qx - ne * ne * 0.5 * p.Qx;
-        const double r2 = -(ntv * ntv) * 0.5 * p.Qx - nv * nv * 0.5 * p.Qv;
+        const double r1 = -nte2 * 0.5 * p.Qx - ne2 * 0.5 * p.Qx;
+        const double r2 = -ntv2 * 0.5 * p.Qx - nv2 * 0.5 * p.Qv;
         const double r3 = (double)(-(na * na) * (float)p.R);
         double r4 = 0;
         if (po || ao)
-            r4 = -(p.time_max - s[T]) / p.dt *
-                 (p.Qx * (ne * ne) + p.Qv * (nv * nv) + (double)((float)p.R * (na * na)));
+            r4 = -div_r(p.time_max - s[T], p.dt, idt) *
+                 (p.Qx * ne2 + p.Qv * nv2 + (double)((float)p.R * (na * na)));
         reward = r1 + r2 + r3 + r4;
         flag = f;
         done = f != 0;

@@ -66,11 +66,14 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
 #pragma unroll
         for (int cc = 0; cc < CPB; ++cc) {
             float *slot = my_part + ((sc % kX3Ring) * CPB + cc) * kX3ChunkFloats;
-            gptr<float> src = Xw + (sc * CPB + cc) * kX3ChunkFloats;
-            // opaque: the unrolled loop would otherwise materialise all 64 piece addresses up front
-            asm volatile("" : "+v"(src));
+            // scalar chunk base (opaque: the unrolled loop would otherwise materialise all 64 piece
+            // addresses up front) + the lane's 16 B: saddr DMA, no per-piece VALU address math
 #pragma unroll
-            for (int q = 0; q < NPW; ++q) lds_dma_1k(src + q * 256, slot + q * 256);
+            for (int q = 0; q < NPW; ++q) {
+                gptr<float> src = Xw + (sc * CPB + cc) * kX3ChunkFloats + q * 256;
+                asm volatile("" : "+s"(src));
+                lds_dma_1k(src + lane * 4, slot + q * 256);
+            }
         }
     };
     lds_barrier();  // every wave is done with the ring
@@ -197,18 +200,24 @@ constexpr int kFdCpb = RLP_FD_CPB;
 constexpr int kFdRegion = kX3RingFloats * kFdCpb;
 
 
-template <int KS1, int A, int LOSS>
-__global__ void __launch_bounds__(64 * kFdWaves, 8 / kFdWaves) ppo2_fd_kernel(Ppo2Args g) {
+// W: waves per block (kFdWaves by default; 4 with one block per CU when the actor's and the
+// critic's FD kernels run concurrently on two streams, rlp_set_fd_mode)
+template <int KS1, int A, int LOSS, int W = kFdWaves>
+__global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
+    constexpr int kFdWaves = W, kFdRows = 16 * W;
     constexpr int H = kUpdH, SMALL = mlp_small_floats<H, KS1, A>();
     constexpr int NC = 4 * KS1 + 1;  // dW1 columns per neuron: s features | bias
     __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + kFdWaves * 16 * 8];
     float *ring = lds, *small = lds + kFdRegion;
-    float *const srw = lds + kFdRegion + SMALL + (threadIdx.x >> 6) * 128;  // [16 rows][8]
+    // the wave index as a scalar (readfirstlane): every wave-derived offset, the G2 tile and its
+    // store guard become SGPR values (no per-lane 64-bit address arithmetic, no exec-masked stores)
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float *const srw = lds + kFdRegion + SMALL + wv * 128;  // [16 rows][8]
     const MfmaNet &net = g.net;
     mlp_small_to_lds(g.packed, net, small, true);  // small_r: W1, b1 x 2/ln 2, b2 x 2^(sw+SH)
     __syncthreads();
 
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, gq = lane >> 4, e = lane & 15;
+    const int lane = threadIdx.x & 63, gq = lane >> 4, e = lane & 15;
     const int S = net.S;
     const float *info = small + (net.off_info - net.off_w1);
     const float sw = info[0];
@@ -236,8 +245,8 @@ __global__ void __launch_bounds__(64 * kFdWaves, 8 / kFdWaves) ppo2_fd_kernel(Pp
         // opaque per iteration: keeps the 2 x 64 chunk addresses from being hoisted (and spilled)
         const float *Pg = g.packed;
         asm volatile("" : "+s"(Pg));
-        const gptr<float> Xf = as_global(Pg) + net.off_x3 + wv * (16 / kFdWaves) * 256 + lane * 4;
-        const gptr<float> Xb = as_global(Pg) + net.off_x3t + wv * (16 / kFdWaves) * 256 + lane * 4;
+        const gptr<float> Xf = as_global(Pg) + net.off_x3 + wv * (16 / kFdWaves) * 256;
+        const gptr<float> Xb = as_global(Pg) + net.off_x3t + wv * (16 / kFdWaves) * 256;
         auto *g2base = (__attribute__((address_space(1))) float *)g.g2t;
         asm volatile("" : "+s"(g2base));
         // the small weights are re-read from LDS per use, not hoisted into registers
@@ -387,8 +396,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 8 / kFdWaves) ppo2_fd_kernel(Pp
         // ---- g2 = (W3^T g3) * (1 - h2^2) in place, to HBM in G2's [tile][neuron][64 rows] layout
         // straight from the registers (lane (gq, e): rows 16 wv + e of neurons 16 j + 4 gq + q;
         // each store instruction writes four 64-B row runs)
-        auto *g2row = g2base + tile * kUpdTileFloats + (4 * gq) * kUpdRows + 16 * (wv & 3) + e;
-        const bool tile_ok = tile * kUpdRows < g.rows;  // (8-wave blocks: the last pair's 2nd tile)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             floatx4 w3[A];
@@ -401,7 +408,19 @@ __global__ void __launch_bounds__(64 * kFdWaves, 8 / kFdWaves) ppo2_fd_kernel(Pp
 #pragma unroll
                 for (int a = 0; a < A; ++a) dh = __builtin_fmaf(w3[a][q], g3[a], dh);
                 acc[j][q] = dh * (1.f - h * h);
-                if (tile_ok) g2row[(16 * j + q) * kUpdRows] = acc[j][q];
+            }
+        }
+        // one wave-uniform guard (8-wave blocks: the last pair's 2nd tile); a scalar tile base
+        // advanced per j plus the lane's 32-bit offset (saddr stores, no 64-bit VALU addresses)
+        if (tile * kUpdRows < g.rows) {
+            auto *tb = g2base + tile * kUpdTileFloats;
+            const int lofs = (4 * gq) * kUpdRows + 16 * (wv & 3) + e;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                auto *tbj = tb + (16 * j) * kUpdRows;
+                asm volatile("" : "+s"(tbj));  // keep the per-j base scalar
+#pragma unroll
+                for (int q = 0; q < 4; ++q) tbj[lofs + q * kUpdRows] = acc[j][q];
             }
         }
 
@@ -794,6 +813,8 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
     }
 }
 
+static int g_fd_mode = 0;  // rlp_set_fd_mode
+
 static int ppo2_grid() {  // CUs of the device (cached: device properties are slow)
     static int cus = 0;
     if (cus == 0) {
@@ -843,8 +864,11 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     hipStream_t st = as_stream(stream);
     const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
     const int grid = (int)(tiles < ppo2_grid() ? tiles : ppo2_grid());         // wgrad: 1 per CU
-    const int64_t fd_tiles = (rows + kFdRows - 1) / kFdRows;
-    const int fd_per_cu = 8 / kFdWaves;  // 2 waves per SIMD
+    // FD block shape (rlp_set_fd_mode): 0 one 8-wave block per CU (default), 1 two 4-wave blocks
+    // per CU, 2 one 4-wave block per CU (the other net's FD kernel co-resident from another stream)
+    const int fdw = g_fd_mode == 0 ? kFdWaves : 4;
+    const int64_t fd_tiles = (rows + 16 * fdw - 1) / (16 * fdw);
+    const int fd_per_cu = g_fd_mode == 2 ? 1 : 8 / fdw;
     const int gfd = (int)(fd_tiles < fd_per_cu * ppo2_grid() ? fd_tiles : fd_per_cu * ppo2_grid());
     const int gfull = ppo2_grid();
     Ppo2Args g{};
@@ -869,7 +893,11 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     if (hipMemsetAsync(g.g2max, 0, sizeof(unsigned), st) != hipSuccess)
         return fail(RLP_EINVAL, "rlp_ppo2_grad: memset");
     g.loss_sum = loss_sum;
-#define RLP_FD(KS1, A_, L) ppo2_fd_kernel<KS1, A_, L><<<gfd, 64 * kFdWaves, 0, st>>>(g)
+#define RLP_FD(KS1, A_, L)                                                                      \
+    do {                                                                                        \
+        if (fdw == 8) ppo2_fd_kernel<KS1, A_, L, 8><<<gfd, 512, 0, st>>>(g);                    \
+        else ppo2_fd_kernel<KS1, A_, L, 4><<<gfd, 256, 0, st>>>(g);                             \
+    } while (0)
     if (actor) {
         if (net.ks1 == 1) {
             if (net.A == 1) RLP_FD(1, 1, 0); else if (net.A == 2) RLP_FD(1, 2, 0); else if (net.A == 3) RLP_FD(1, 3, 0); else RLP_FD(1, 4, 0);
@@ -890,10 +918,18 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     const int64_t total = (int64_t)net.H * net.S + net.H + (int64_t)net.H * net.H + net.H +
                           (int64_t)net.A * net.H + net.A;
     ppo2_reduce_kernel<<<(int)((total + 63) / 64), 64 * kRedSplit, 0, st>>>(net, partw, grid,
-                                                                          g.part3, gfd * kFdWaves, grad);
+                                                                          g.part3, gfd * fdw, grad);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (reduce)");
     return RLP_OK;
 }
+
+int rlp_set_fd_mode(int mode) {
+    if (mode < 0 || mode > 2) return fail(RLP_EINVAL, "rlp_set_fd_mode: %d", mode);
+    g_fd_mode = mode;
+    return RLP_OK;
+}
+
+int rlp_get_fd_mode(void) { return g_fd_mode; }
 
 int rlp_grad_sqnorm(const float *grad, int64_t n, double *out, rlp_stream_t stream) {
     RLP_REQUIRE(grad && out && n >= 0, "rlp_grad_sqnorm: bad argument");

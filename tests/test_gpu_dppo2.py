@@ -58,15 +58,21 @@ def _flat(ag):
 
 
 def _run(ag):
-    """Two iterations; per iteration the rollout buffers, then the params after learn()."""
+    """Two iterations; per iteration the rollout buffers (+ the normalised rewards / advantages
+    and value targets learn() consumes), then the params after learn() and the (all-reduced)
+    gradient the learner stepped with."""
     rec = []
     for _ in range(2):
         w = ag.worker
         w.rollout()
         bufs = {k: w.bufs[k].cpu().numpy().copy() for k in KEYS}
         w.advantages()
+        for k, t in (("rnorm", w.rnorm), ("adv", w.adv), ("v_target", w.v_target)):
+            bufs[k] = t.cpu().numpy().copy()
         w.update()
-        rec.append((bufs, _flat(ag)))
+        lr = w.learner
+        grad = torch.cat([lr.net_a.grad, lr.net_c.grad]).cpu().numpy().copy()
+        rec.append((bufs, _flat(ag), grad))
     return rec
 
 
@@ -116,7 +122,14 @@ def test_dppo2_two_ranks_union_and_replicas():
         for it in range(2):
             np.testing.assert_array_equal(r0[it][1], r1[it][1])
         err = np.abs(r0[0][1] - single[0][1]).max()
-        if case[1] == "global":   # (3) the same update as one rank on 2n envs
+        gs = single[0][2]
+        gerr = np.abs(r0[0][2] - gs).max() / np.abs(gs).max()
+        print(f"{case}: max |param diff| {err:.3e}, gradient diff {gerr:.3e} of max|g|")
+        if case[1] == "global":   # (3) the same learn() inputs and update as one rank on 2n envs
+            for k in ("rnorm", "adv", "v_target"):
+                u = np.concatenate([r0[0][0][k], r1[0][0][k]], axis=1)
+                np.testing.assert_allclose(u, bs[k], rtol=1e-6, atol=1e-6, err_msg=f"{case} {k}")
+            assert gerr <= 1e-5, (case, gerr)
             assert err <= 1e-5, (case, err)
         else:                     # per-rank normalisers: the same objective up to the statistics
             assert err < 1e-2, (case, err)

@@ -214,3 +214,24 @@ def test_native_update_data_parallel_duplicated_batch_bit_exact():
         ref = torch.cat([nl.net_a.flat, nl.net_c.flat]).cpu().numpy()
         for r in (0, 1):
             np.testing.assert_array_equal(out[r][i], ref, err_msg=f"rank {r} {rule} clip={clip}")
+
+
+@pytest.mark.parametrize("A", [1, 3])
+def test_native_grads_concurrent_streams_match(A):
+    """fd_streams (actor and critic gradient kernels on two streams, one 4-wave FD block per CU)
+    against one stream with 8-wave FD blocks: per-row arithmetic is the same (16-row wave tiles in
+    both shapes); only the grouping of the per-wave dW1 / dW3 partials differs, so the gradients
+    agree to f32 summation rounding, and each shape is run-to-run deterministic."""
+    actor, critic, s, a, lp, adv, vt = make_case(4, A, 5000, seed=41)
+    dev = lambda t: t.cuda().contiguous()
+    out = []
+    for fs in (False, True, True):
+        msg = dict(DEFAULT_PPO_MSG, K_epochs=1, fd_streams=fs)
+        nl = NativePPO2Learner(copy.deepcopy(actor), copy.deepcopy(critic), msg, device="cuda")
+        nl.grads(dev(s), dev(a), dev(lp), dev(adv), dev(vt))
+        torch.cuda.synchronize()
+        out.append(torch.cat([nl.net_a.grad, nl.net_c.grad]).cpu().double())
+    assert torch.equal(out[1], out[2])
+    for g0, g1 in ((out[0], out[1]),):
+        scale = float(g0.abs().max())
+        assert float((g0 - g1).abs().max()) <= 1e-6 * scale
