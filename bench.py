@@ -165,7 +165,7 @@ class Segment:
         self.learn_side()
 
 
-def e2e_iterations(seg, iters, k_epochs=6, learner="native", fd_streams=False):
+def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
     """Whole PPO2 iterations: rollout + advantages + K full-batch epochs of the clipped-surrogate /
     MSE update (torch autograd + Adam on this GPU; the DPPO2 CartPole drivers' k_epo = 6,
     demonstration/DPPO2/DPPO2-4-CartPole/train.py:161). Returns env-steps/s of this rank."""
@@ -182,8 +182,7 @@ def e2e_iterations(seg, iters, k_epochs=6, learner="native", fd_streams=False):
                 p.copy_(flat[off:off + p.numel()].view_as(p).cpu())
                 off += p.numel()
     cls = NativePPO2Learner if learner == "native" else PPO2Learner
-    learner = cls(actor, critic, dict(DEFAULT_PPO_MSG, K_epochs=k_epochs, fd_streams=fd_streams),
-                  device="cuda")
+    learner = cls(actor, critic, dict(DEFAULT_PPO_MSG, K_epochs=k_epochs), device="cuda")
     b = seg.bufs
 
     def one():
@@ -568,8 +567,8 @@ def main():
                     "advantage normalisation, SOI / UGV / UAV env steps) against the HBM roof")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
-    ap.add_argument("--fd-streams", type=int, default=0, help="e2e: actor and critic gradient "
-                    "kernels concurrently on two streams (NativePPO2Learner fd_streams)")
+    ap.add_argument("--wgrad-waves", type=int, default=0, choices=[0, 4, 8],
+                    help="PPO2 update's weight-gradient kernel block shape (0: library default)")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="rollout hidden-layer arithmetic (include/rlp.h rlp_set_mlp_precision)")
     args = ap.parse_args()
@@ -592,6 +591,8 @@ def main():
             dist.init_process_group(backend)
     if args.sub:
         _native.set_rollout_sub(args.sub)
+    if args.wgrad_waves:
+        _native.lib().rlp_set_wgrad_waves(args.wgrad_waves)
     _native.set_rollout_physics(PHYSICS_MODES[args.physics])
     prec = _native.MLP_F16X3 if args.precision == "f16x3" else _native.MLP_FP32
     _native.set_mlp_precision(prec)
@@ -735,13 +736,12 @@ def main():
     if args.e2e:
         upd = ("librlp rlp_ppo2_grad + rlp_adam_step" if args.learner == "native"
                else "torch autograd + Adam (fp32)")
-        v, it_s = e2e_iterations(seg, args.e2e, learner=args.learner, fd_streams=bool(args.fd_streams))
+        v, it_s = e2e_iterations(seg, args.e2e, learner=args.learner)
         out["e2e"] = {"value": v * world, "unit": "env-steps/s", "s_per_iteration": it_s,
                       "update": f"K=6 full-batch epochs per iteration (DPPO2 drivers' k_epo), {upd}",
                       "note": "rollout + GAE + PPO update; `value` above is the rollout hot path"}
         if args.e2e_k30:
-            v30, it30 = e2e_iterations(seg, max(1, args.e2e // 2), k_epochs=30, learner=args.learner,
-                                       fd_streams=bool(args.fd_streams))
+            v30, it30 = e2e_iterations(seg, max(1, args.e2e // 2), k_epochs=30, learner=args.learner)
             out["e2e"]["k30"] = {
                 "value": v30 * world, "unit": "env-steps/s", "s_per_iteration": it30,
                 "update": f"K=30 full-batch epochs per iteration (PPO2-4-CartPole/train.py:146), {upd}"}

@@ -425,12 +425,18 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
                   double *loss_sum, float *workspace, rlp_stream_t stream);
 
 /* Block shape of rlp_ppo2_grad's forward/backward (FD) kernel, library-wide: 0 one 8-wave block
- * per CU (default), 1 two 4-wave blocks per CU, 2 one 4-wave block per CU — for running the
- * actor's and the critic's rlp_ppo2_grad concurrently on two streams (each with its own workspace):
- * every CU then holds one wave of each net per SIMD, and the two independent instruction streams
- * overlap one net's VALU phases with the other's MFMA phases. */
+ * per CU (default), 1 two 4-wave blocks per CU, 2 one 4-wave block per CU (so that the actor's and
+ * the critic's rlp_ppo2_grad, launched on two streams with their own workspaces, can share every
+ * CU; measured no faster than mode 0 on one stream: e2e K=30 0.749 vs 0.733 s). */
 int rlp_set_fd_mode(int mode);
 int rlp_get_fd_mode(void);
+
+/* Block shape of rlp_ppo2_grad's weight-gradient (dW2 = sum_rows g2 h1^T) kernel, library-wide:
+ * 8 (default) one 8-wave block per CU, each wave 32 output rows (2 waves per SIMD); 4 one 4-wave
+ * block per CU, each wave 64 output rows with the VGPR + AGPR budget (1 wave per SIMD: half the
+ * LDS fragment reads per tile, fragments read one step ahead). Same partial-sum order. */
+int rlp_set_wgrad_waves(int waves);
+int rlp_get_wgrad_waves(void);
 
 /* out[0] += sum(grad^2) (torch.nn.utils.clip_grad_norm_'s total norm, squared), accumulated in
  * double in a fixed order: bit-identical on every run and every data-parallel rank. */

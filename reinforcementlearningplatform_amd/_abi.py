@@ -35,9 +35,10 @@ ENV_DIMS = {
     RLP_ENV_UAV_HOVER_OUTER_LOOP: (22, 6, 3),
     RLP_ENV_UGV_OBSTACLE_AVOIDANCE: (RLP_UGVOA_D, 4 + RLP_UGVOA_NLASER, 2),
 }
-# kinds the fused PPO2 rollout (rlp_rollout, [S<=8 -> H -> H -> A<=4] nets) runs; the lidar env
-# (S = 41) steps through rlp_env_step + the generic MLP kernels (SAC / VecEnv paths)
-ROLLOUT_KINDS = tuple(k for k in ENV_DIMS if k != RLP_ENV_UGV_OBSTACLE_AVOIDANCE)
+# kinds rlp_rollout runs: the fused one-kernel rollout ([S<=8 -> 256 -> 256 -> A<=4] nets), and the
+# lidar env (S = 41: 4 + 37 beams) as a per-step kernel sequence inside the same call
+FUSED_ROLLOUT_KINDS = tuple(k for k in ENV_DIMS if k != RLP_ENV_UGV_OBSTACLE_AVOIDANCE)
+ROLLOUT_KINDS = tuple(ENV_DIMS)
 
 RLP_ACT_NONE, RLP_ACT_TANH, RLP_ACT_RELU = 0, 1, 2
 RLP_MLP_MAX_LAYERS = 8

@@ -60,6 +60,8 @@ def _declare(lib):
         "rlp_grad_sqnorm": (i32, [vp, i64, vp, vp]),
         "rlp_set_fd_mode": (i32, [i32]),
         "rlp_get_fd_mode": (i32, []),
+        "rlp_set_wgrad_waves": (i32, [i32]),
+        "rlp_get_wgrad_waves": (i32, []),
         "rlp_grad_clip": (i32, [vp, i64, vp, C.c_float, vp]),
         "rlp_adam_step": (i32, [vp, vp, vp, vp, i64, vp, vp, vp]),
         "rlp_replay_store": (i32, [vp, i64, vp, vp, vp, vp, vp, i64, vp]),

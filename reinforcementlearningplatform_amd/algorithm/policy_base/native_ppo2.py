@@ -22,15 +22,6 @@ msg keys beyond the reference's ppo_msg (all optional):
   grad_clip_norm  clip_grad_norm_'s max_norm (PPO2 0.5, :150; DPPO2 CartPole/SOI copies 0.2)
   adam_betas      (0.9, 0.999) for torch.optim.Adam; SharedAdam's default is (0.9, 0.99)
                   (utils/classes.py:676-679), which every DPPO2 driver uses
-  fd_streams      False (default): one stream, one 8-wave FD block per CU; True: the actor's and
-                  the critic's gradient kernels run
-                  concurrently, the critic's on a second stream with its own workspace, FD kernels
-                  in one 4-wave block per CU each (rlp_set_fd_mode(2)): every SIMD then holds one
-                  wave of each net, whose VALU and MFMA phases could overlap (measured: e2e K=30
-                  0.749 s against 0.733 s for one stream, r3b — kept selectable, not the default).
-                  Per-row arithmetic is identical either way (16-row
-                  wave tiles); the dW1 / dW3 partials are grouped per wave, so the two shapes
-                  agree to f32 summation rounding (each deterministic run to run).
 """
 import numpy as np
 import torch
@@ -40,19 +31,18 @@ from ... import _abi
 from ... import kernels as K
 
 
-class _nullctx:
-    def __enter__(self):
-        return None
-
-    def __exit__(self, *a):
-        return False
+def native_fits(module):
+    """True when librlp's update kernels take the net: a [S<=8 -> 256 -> 256 -> A<=4] Linear stack."""
+    lin = [m for m in module.modules() if isinstance(m, nn.Linear)]
+    dims = [lin[0].in_features] + [l.out_features for l in lin] if lin else []
+    return len(lin) == 3 and dims[1] == 256 and dims[2] == 256 and dims[0] <= 8 and dims[3] <= 4
 
 
 class _Net:
     def __init__(self, module, is_actor, device):
         lin = [m for m in module.modules() if isinstance(m, nn.Linear)]
         dims = [lin[0].in_features] + [l.out_features for l in lin] if lin else []
-        if len(lin) != 3 or dims[1] != 256 or dims[2] != 256 or dims[0] > 8 or dims[3] > 4:
+        if not native_fits(module):
             raise ValueError(f"NativePPO2Learner: needs a [S<=8 -> 256 -> 256 -> A<=4] Linear/Tanh "
                              f"stack (got {dims})")
         acts = [_abi.RLP_ACT_TANH, _abi.RLP_ACT_TANH,
@@ -102,9 +92,7 @@ class NativePPO2Learner:
         if self.rule not in ('ppo2', 'dppo2'):
             raise ValueError(f"NativePPO2Learner: update_rule {self.rule!r} (ppo2 | dppo2)")
         self.loss = torch.zeros(2, dtype=torch.float64, device=self.device)
-        self.ws = {}
-        self.fd_streams = bool(msg.get('fd_streams', False)) and self.device.type == "cuda"
-        self.side = torch.cuda.Stream(device=self.device) if self.fd_streams else None
+        self.ws = None
         self.total_steps = 0
 
     # same accessors as PPO2Learner
@@ -129,35 +117,26 @@ class NativePPO2Learner:
         return K.ppo2_loss_cfg(_abi.RLP_LOSS_ACTOR, self.msg['eps_clip'], self.msg['entropy_coef'],
                                std, lo, hi)
 
-    def _workspace(self, which, net, rows):
-        need = K.lib().rlp_ppo2_workspace_floats(__import__("ctypes").byref(net.desc), rows)
-        ws = self.ws.get(which)
-        if ws is None or ws.numel() < need:
-            ws = self.ws[which] = torch.empty(int(need), dtype=torch.float32, device=self.device)
-        return ws
+    def _workspace(self, rows):
+        need = max(K.lib().rlp_ppo2_workspace_floats(__import__("ctypes").byref(n.desc), rows)
+                   for n in (self.net_a, self.net_c))
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(int(need), dtype=torch.float32, device=self.device)
+        return self.ws
 
     def grads(self, s, a, a_lp, adv, vt, index=None):
-        """Gradients of one step's actor and critic losses into net.grad (no optimiser step);
-        with fd_streams the critic's kernels run on the side stream, joined before returning."""
+        """Gradients of one step's actor and critic losses into net.grad (no optimiser step)."""
         rows = int(index.shape[0]) if index is not None else int(s.shape[0])
+        ws = self._workspace(rows)
         self.loss.zero_()
         adv, vt = adv.reshape(-1), vt.reshape(-1)
         na, nc = self.net_a, self.net_c
-        ws_a = self._workspace("a", na, rows)
-        ws_c = self._workspace("c" if self.fd_streams else "a", nc, rows)
-        K.lib().rlp_set_fd_mode(2 if self.fd_streams else 0)
-        main = torch.cuda.current_stream(self.device) if self.fd_streams else None
-        if self.fd_streams:
-            self.side.wait_stream(main)
         K.mfma_pack(na.desc, na.flat, out=na.packed)
         K.ppo2_grad(na.desc, na.packed, self._actor_cfg(), s, a=a, a_logprob=a_lp, adv=adv,
-                    index=index, grad=na.grad, loss_sum=self.loss[0:1], workspace=ws_a)
-        with torch.cuda.stream(self.side) if self.fd_streams else _nullctx():
-            K.mfma_pack(nc.desc, nc.flat, out=nc.packed)
-            K.ppo2_grad(nc.desc, nc.packed, K.ppo2_loss_cfg(_abi.RLP_LOSS_CRITIC), s, v_target=vt,
-                        index=index, grad=nc.grad, loss_sum=self.loss[1:2], workspace=ws_c)
-        if self.fd_streams:
-            main.wait_stream(self.side)
+                    index=index, grad=na.grad, loss_sum=self.loss[0:1], workspace=ws)
+        K.mfma_pack(nc.desc, nc.flat, out=nc.packed)
+        K.ppo2_grad(nc.desc, nc.packed, K.ppo2_loss_cfg(_abi.RLP_LOSS_CRITIC), s, v_target=vt,
+                    index=index, grad=nc.grad, loss_sum=self.loss[1:2], workspace=ws)
         return rows
 
     def _allreduce_grads(self):

@@ -177,7 +177,7 @@ class PPO2Learner:
 
 class VecPPO2:
     def __init__(self, env, actor, critic, ppo_msg=None, T=128, success_rule=None, seed=None,
-                 process_group=None, device=None, learner="native"):
+                 process_group=None, device=None, learner="auto"):
         self.env = env
         self.kind, self.params = env.KIND, env.params
         self.n, self.T = env.n_envs, int(T)
@@ -185,9 +185,12 @@ class VecPPO2:
         self.msg = dict(DEFAULT_PPO_MSG, **(ppo_msg or {}))
         if 'k_epo' in self.msg:                       # DPPO2 drivers name it k_epo
             self.msg['K_epochs'] = self.msg['k_epo']
-        if learner not in ("native", "torch"):
-            raise ValueError(f"VecPPO2: learner {learner!r} (native | torch)")
-        from .native_ppo2 import NativePPO2Learner
+        if learner not in ("auto", "native", "torch"):
+            raise ValueError(f"VecPPO2: learner {learner!r} (auto | native | torch)")
+        from .native_ppo2 import NativePPO2Learner, native_fits
+        if learner == "auto":  # librlp's update covers [S<=8 -> 256 -> 256 -> A<=4]; the lidar
+            # env's 41-input nets take the torch-autograd learner (on the same device)
+            learner = "native" if native_fits(actor) and native_fits(critic) else "torch"
         cls = NativePPO2Learner if learner == "native" else PPO2Learner
         self.learner = cls(actor, critic, self.msg, process_group, self.device)
         self.actor, self.critic = self.learner.actor, self.learner.critic
@@ -196,7 +199,7 @@ class VecPPO2:
         self.gpu_critic = GPUNet(self.critic, False, self.device)
         if not (self.gpu_actor.mfma_ok and self.gpu_critic.mfma_ok):
             raise ValueError("VecPPO2 needs [S->256->256->A] actor / [S->256->256->1] critic nets "
-                             "for the fused rollout kernel")
+                             "(S <= 8, or 41-44) for rlp_rollout")
         rule, flag = success_rule or (_abi.RLP_SUCCESS_DONE_AND_FLAG_NE, _abi.timeout_flag(self.kind))
         self.rule, self.flag = rule, flag
         lo, hi = _abi.action_bounds(self.kind, self.params)

@@ -54,7 +54,11 @@ __global__ void __launch_bounds__(256) env_step_kernel(typename Env<KIND>::P p, 
     double r;
     int f;
     bool dn;
-    E::step(p, s, a, on, r, f, dn);
+    // p as the kernarg segment's first argument (not the by-value copy): Env steps that re-read
+    // their parameters per phase (phase_ref) then load them from there instead of a stack copy
+    const auto &pk = *(const typename E::P *)(const __attribute__((address_space(4))) typename E::P *)
+        __builtin_amdgcn_kernarg_segment_ptr();
+    E::step(pk, s, a, on, r, f, dn);
 #pragma unroll
     for (int d = 0; d < EnvDW<E>::value; ++d) state[(size_t)d * n + i] = s[d];
 #pragma unroll

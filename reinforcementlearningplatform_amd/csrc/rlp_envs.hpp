@@ -174,6 +174,18 @@ __device__ __forceinline__ double tanh_fast(double x) {
     return copysign(div_nr(em, em + 2.0), x);
 }
 
+// The same object behind an opaque (scalar) pointer: loads of its fields after this point cannot
+// reuse values loaded before it, so a long step re-reads its parameters phase by phase (short
+// SGPR live ranges) instead of holding them all at once — the UAV step's ~60 uniform doubles
+// otherwise spill to VGPR lanes (a v_readlane per use). Only for objects in memory (the rollout
+// kernel's kernarg segment), never a by-value copy.
+template <class T>
+__device__ __forceinline__ const T &phase_ref(const T &x) {
+    const T *q = &x;
+    asm volatile("" : "+s"(q));
+    return *q;
+}
+
 template <int KIND> struct Env;
 
 // components of the physics state step() may change (E::DW when the kind declares it, else D):
@@ -638,7 +650,7 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
             o[3 + i] = (float)(2 * s[VX + i] / (p.vel_max[i] - p.vel_min[i]) * p.static_gain);
         }
     }
-    __device__ static __forceinline__ void step(const P &p, double *s, const float *a, float *on,
+    __device__ static __forceinline__ void step(const P &p0, double *s, const float *a, float *on,
                                                 double &reward, int &flag, bool &done) {
         const double phi = s[PHI], th = s[THE], psi = s[PSI];
         const double pp = s[PP], q = s[PP + 1], r = s[PP + 2];
@@ -648,25 +660,26 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
         sincos_fast(psi, &spsi, &cpsi);
         // uo_2_ref_angle_throttle uav_pos_ctrl.py:67-76; (uz + g) * m in float32 (NEP 50)
         const double ux = (double)a[0], uy = (double)a[1];
-        const float uzg = (a[2] + (float)p.g) * (float)p.m;
+        const float uzg = (a[2] + (float)p0.g) * (float)p0.m;
         const double uf = div_nr((double)uzg, cphi * cth);
-        const double u0 = clipd(div_nr((ux * spsi - uy * cpsi) * p.m, uf), -1, 1);
+        const double u0 = clipd(div_nr((ux * spsi - uy * cpsi) * p0.m, uf), -1, 1);
         const double phi_d0 = asin(u0);
         double spd, cpd;  // cos(phi_d0) as the reference evaluates it (not sqrt(1 - u0^2))
         sincos_fast(phi_d0, &spd, &cpd);
-        const double th_d0 = asin(clipd(div_nr((ux * cpsi + uy * spsi) * p.m, uf * cpd), -1, 1));
-        const double phi_d = clipd(phi_d0, p.att_zone[0][0], p.att_zone[0][1]);  // :126-127
-        const double th_d = clipd(th_d0, p.att_zone[1][0], p.att_zone[1][1]);
+        const double th_d0 = asin(clipd(div_nr((ux * cpsi + uy * spsi) * p0.m, uf * cpd), -1, 1));
+        const double phi_d = clipd(phi_d0, p0.att_zone[0][0], p0.att_zone[0][1]);  // :126-127
+        const double th_d = clipd(th_d0, p0.att_zone[1][0], p0.att_zone[1][1]);
         const double aref_new[3] = {phi_d, th_d, 0.0};
         double daref[3], aref[3];
-        const double idt = recip_nr(p.dt);
+        const double idt = recip_nr(p0.dt);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {  // attitude-reference rate limit :130-134
             const double old = s[AREF + i];
-            daref[i] = clipd(div_r(aref_new[i] - old, p.dt, idt), p.dot_att_min[i], p.dot_att_max[i]);
-            aref[i] = daref[i] * p.dt + old;
+            daref[i] = clipd(div_r(aref_new[i] - old, p0.dt, idt), p0.dot_att_min[i], p0.dot_att_max[i]);
+            aref[i] = daref[i] * p0.dt + old;
         }
         // att_control uav_pos_ctrl.py:46-65 -> fntsmc_att.control_update FNTSMC.py:80-106
+        const P &p = phase_ref(p0);
         const Rc rc = {{recip_nr(p.J[0]), recip_nr(p.J[1]), recip_nr(p.J[2])}, recip_nr(p.m)};
         const double icth = recip_nr(cth);
         const double tth = div_r(sth, cth, icth);
@@ -729,31 +742,32 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
         double sum[12], t[12], d[12];
         const double sc0[6] = {sphi, cphi, sth, cth, spsi, cpsi};
         double sc[6];
-        ode(p, rc, uf, tq, s, sc0, d);
+        ode(phase_ref(p0), rc, uf, tq, s, sc0, d);
 #pragma unroll
         for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = k; t[i] = fma(k, 0.5, s[i]); }
         stage_sc(sc0, s, t, sc);
-        ode(p, rc, uf, tq, t, sc, d);
+        ode(phase_ref(p0), rc, uf, tq, t, sc, d);
 #pragma unroll
         for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = fma(k, 2.0, sum[i]); t[i] = fma(k, 0.5, s[i]); }
         stage_sc(sc0, s, t, sc);
-        ode(p, rc, uf, tq, t, sc, d);
+        ode(phase_ref(p0), rc, uf, tq, t, sc, d);
 #pragma unroll
         for (int i = 0; i < 12; ++i) { const double k = h * d[i]; sum[i] = fma(k, 2.0, sum[i]); t[i] = s[i] + k; }
         stage_sc(sc0, s, t, sc);
-        ode(p, rc, uf, tq, t, sc, d);
+        ode(phase_ref(p0), rc, uf, tq, t, sc, d);
 #pragma unroll
         for (int i = 0; i < 12; ++i) s[i] = s[i] + div6(sum[i] + h * d[i]);
-        s[T] += p.dt;
+        const P &pr = phase_ref(p0);  // is_episode_Terminal / reward parameters
+        s[T] += pr.dt;
         if (s[PSI] > kPi) s[PSI] -= 2 * kPi;
         if (s[PSI] < -kPi) s[PSI] += 2 * kPi;
         int f = 0;  // is_episode_Terminal uav.py:543-560
-        if (s[T] > p.time_max - p.dt / 2) f = 1;
+        if (s[T] > pr.time_max - pr.dt / 2) f = 1;
         bool po = false, ao = false;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            po |= (s[X + i] < p.pos_zone[i][0]) || (s[X + i] > p.pos_zone[i][1]);
-            ao |= (s[PHI + i] < p.att_zone[i][0]) || (s[PHI + i] > p.att_zone[i][1]);
+            po |= (s[X + i] < pr.pos_zone[i][0]) || (s[X + i] > pr.pos_zone[i][1]);
+            ao |= (s[PHI + i] < pr.att_zone[i][0]) || (s[PHI + i] > pr.att_zone[i][1]);
         }
         if (po) f = 2;
         if (ao) f = 3;
@@ -768,13 +782,13 @@ template <> struct Env<RLP_ENV_UAV_HOVER_OUTER_LOOP> {
             nte2 += te * te; ne2 += e * e; ntv2 += tv * tv; nv2 += v * v;
         }
         const float na = sqrtf(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);  // float32 action norm
-        const double r1 = -nte2 * 0.5 * p.Qx - ne2 * 0.5 * p.Qx;
-        const double r2 = -ntv2 * 0.5 * p.Qx - nv2 * 0.5 * p.Qv;
-        const double r3 = (double)(-(na * na) * (float)p.R);
+        const double r1 = -nte2 * 0.5 * pr.Qx - ne2 * 0.5 * pr.Qx;
+        const double r2 = -ntv2 * 0.5 * pr.Qx - nv2 * 0.5 * pr.Qv;
+        const double r3 = (double)(-(na * na) * (float)pr.R);
         double r4 = 0;
         if (po || ao)
-            r4 = -div_r(p.time_max - s[T], p.dt, idt) *
-                 (p.Qx * ne2 + p.Qv * nv2 + (double)((float)p.R * (na * na)));
+            r4 = -div_r(pr.time_max - s[T], pr.dt, idt) *
+                 (pr.Qx * ne2 + pr.Qv * nv2 + (double)((float)pr.R * (na * na)));
         reward = r1 + r2 + r3 + r4;
         flag = f;
         done = f != 0;

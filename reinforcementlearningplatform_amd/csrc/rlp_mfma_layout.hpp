@@ -47,7 +47,9 @@ inline bool mfma_net_from_desc(const rlp_mlp_desc &d, MfmaNet *net) {
     if (d.n_layers != 3) return false;
     const int S = d.dims[0], H = d.dims[1], A = d.dims[3];
     if (d.dims[2] != H || !(H == 64 || H == 128 || H == 256)) return false;
-    if (S < 1 || S > 8 || A < 1 || A > 4) return false;
+    // inputs: the drivers' 1-8 (CartPole, AngleOnly, SOI, UGV, UAV) or 41-44 (the UGV obstacle-
+    // avoidance demos' 4 + 37 lidar beams: layer 1 as KS1 = 11 K-steps of the 16x16x4 MFMA)
+    if (!((S >= 1 && S <= 8) || (S >= 41 && S <= 44)) || A < 1 || A > 4) return false;
     if (d.act[0] != RLP_ACT_TANH || d.act[1] != RLP_ACT_TANH) return false;
     if (d.act[2] != RLP_ACT_TANH && d.act[2] != RLP_ACT_NONE) return false;
     const int KS1 = (S + 3) / 4;

@@ -302,7 +302,7 @@ int64_t rlp_mfma_packed_count(const rlp_mlp_desc *desc) {
     MfmaNet net;
     if (!desc || !mfma_net_from_desc(*desc, &net))
         return fail(RLP_EUNSUPPORTED,
-                    "rlp_mfma_packed_count: need [S<=8 -> H -> H -> A<=4], H in {64,128,256}");
+                    "rlp_mfma_packed_count: need [S<=8 or 41<=S<=44 -> H -> H -> A<=4], H in {64,128,256}");
     return net.count;
 }
 
@@ -311,7 +311,8 @@ int rlp_mfma_pack(const rlp_mlp_desc *desc, const float *params, float *packed,
     RLP_REQUIRE(desc && params && packed, "rlp_mfma_pack: null argument");
     MfmaNet net;
     if (!mfma_net_from_desc(*desc, &net))
-        return fail(RLP_EUNSUPPORTED, "rlp_mfma_pack: need [S<=8 -> H -> H -> A<=4], H in {64,128,256}");
+        return fail(RLP_EUNSUPPORTED,
+                    "rlp_mfma_pack: need [S<=8 or 41<=S<=44 -> H -> H -> A<=4], H in {64,128,256}");
     const int blocks = (int)((net.count + 255) / 256);
     mfma_scale_kernel<<<1, 256, 0, as_stream(stream)>>>(net, params, packed);
     mfma_pack_kernel<<<blocks < 1024 ? blocks : 1024, 256, 0, as_stream(stream)>>>(net, params,

@@ -15,6 +15,16 @@
 
 namespace rlp {
 
+// UGVForwardObstacleAvoidance lidar step / observe / reset (rlp_lidar.hip)
+int launch_ugvoa_step(const rlp_ugv_oa_params &p, double *state, int n, const float *action,
+                      float *obs_cur, float *obs_next, double *reward, int32_t *flag,
+                      uint8_t *done, hipStream_t st);
+int launch_ugvoa_observe(const rlp_ugv_oa_params &p, const double *state, int n, float *obs,
+                         hipStream_t st);
+int launch_ugvoa_reset(const rlp_ugv_oa_params &p, double *state, int n, const uint8_t *mask,
+                       const double *init, uint64_t seed, uint64_t counter, uint64_t env_id0,
+                       hipStream_t st);
+
 // Each wave stages only its own envs' observations in LDS, so a wave-level fence suffices; no
 // block barrier keeps the two waves of a SIMD in lockstep (one's f64 physics overlaps the other's
 // MFMAs).
@@ -261,11 +271,35 @@ constexpr bool rollout_sp_fits() { return SUB <= 2 && rollout_sp_ring<KIND, SUB>
 // oldest-first issue arbitration lets one run ahead (measured: half the blocks finish their
 // segment in 12.0M cycles, the other half in 16.9M, and the launch waits for the slow half); in
 // one block the barriers keep all eight waves in step.
+// The launch's arguments as ONE kernel parameter, so that the kernel can address them in the
+// kernarg segment (__builtin_amdgcn_kernarg_segment_ptr) and re-read the env params, launch
+// constants and buffer pointers per step with scalar loads instead of holding them in SGPRs across
+// the MLP passes (which spilled them to VGPR lanes: a v_readlane per use, 248 in the CartPole
+// kernel, 901 in the UAV kernel).
+template <int KIND>
+struct SpArgs {
+    typename Env<KIND>::P p;
+    double *state;
+    uint8_t *need_reset;
+    const float *actor;
+    MfmaNet an;
+    const float *critic;
+    MfmaNet cn;
+    RolloutArgs ra;
+    rlp_rollout_bufs b;
+};
+
 template <int KIND, int H, int SUB, int W = 4, int WPS = rollout_sp_default_wps<SUB, W>()>
 __global__ void __launch_bounds__(64 * W, WPS)  // (HIP's second argument: waves per SIMD)
-rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *__restrict__ need_reset,
-                  const float *__restrict__ actor, MfmaNet an, const float *__restrict__ critic,
-                  MfmaNet cn, RolloutArgs ra, rlp_rollout_bufs b) {
+rollout_sp_kernel(SpArgs<KIND> args) {
+    const typename Env<KIND>::P &p = args.p;
+    double *__restrict__ state = args.state;
+    uint8_t *__restrict__ need_reset = args.need_reset;
+    const float *__restrict__ actor = args.actor;
+    const float *__restrict__ critic = args.critic;
+    const MfmaNet &an = args.an, &cn = args.cn;
+    const RolloutArgs &ra = args.ra;
+    const rlp_rollout_bufs &b = args.b;
     using E = Env<KIND>;
     constexpr int S = E::S, A = E::A, D = E::D, KS1 = (S + 3) / 4, WENV = 16 * SUB;
     // physics lanes per physics wave: 64 (full waves; RLP_SP_UAV_PHL can give the UAV half waves)
@@ -318,6 +352,12 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
     __syncthreads();
 
     auto mlp_pass = [&](bool both) {
+        // the nets' pointers and layouts re-read from the kernarg segment (scalar loads) per pass
+        auto ak = (const __attribute__((address_space(4))) SpArgs<KIND> *)
+            __builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ak));
+        const float *actor = ak->actor, *critic = ak->critic;
+        const MfmaNet &an = *(const MfmaNet *)&ak->an, &cn = *(const MfmaNet *)&ak->cn;
         float bobs[SUB][KS1];
 #pragma unroll
         for (int sb = 0; sb < SUB; ++sb)
@@ -355,6 +395,15 @@ rollout_sp_kernel(typename Env<KIND>::P p, double *__restrict__ state, uint8_t *
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // (mean, V) of every env
         if (wave / PW == t % ROT && lane < PHL) {  // this step's physics waves
             const int le = PHL * (wave % PW) + lane, env = base + le;
+            // the env params, launch constants and buffer pointers are read through opaque
+            // pointers into the kernarg segment here (s_load per step) instead of being held in
+            // SGPRs across the MLP passes, which spilled them to VGPR lanes (a v_readlane per use)
+            auto ak = (const __attribute__((address_space(4))) SpArgs<KIND> *)
+                __builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(ak));
+            const typename E::P &p = *(const typename E::P *)&ak->p;
+            const RolloutArgs &ra = *(const RolloutArgs *)&ak->ra;
+            const rlp_rollout_bufs &b = *(const rlp_rollout_bufs *)&ak->b;
             if (env < n) {
                 const uint64_t eid = ra.env_id0 + (uint64_t)env;
                 const int k = t * n + env;  // 32-bit: T * n * 8 < 2^31 (rlp_rollout)
@@ -496,8 +545,11 @@ static int launch_packed_forward(const MfmaNet &net, const float *P, const float
         P, net, x, y, rows, done, success, apply_out_act)
     if (net.ks1 == 1) {
         if (net.A == 1) RLP_PF(1, 1); else if (net.A == 2) RLP_PF(1, 2); else if (net.A == 3) RLP_PF(1, 3); else RLP_PF(1, 4);
-    } else {
+    } else if (net.ks1 == 2) {
         if (net.A == 1) RLP_PF(2, 1); else if (net.A == 2) RLP_PF(2, 2); else if (net.A == 3) RLP_PF(2, 3); else RLP_PF(2, 4);
+    } else {  // 41-44 inputs (the lidar env's nets: actor A = 2, critic A = 1)
+        if (net.A == 1) RLP_PF(11, 1); else if (net.A == 2) RLP_PF(11, 2);
+        else return fail(RLP_EUNSUPPORTED, "packed forward: %d inputs with %d outputs", net.S, net.A);
     }
 #undef RLP_PF
     RLP_CHECK_LAUNCH("packed forward");
@@ -518,8 +570,7 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     if constexpr (X3 && SUB == 1 && rollout_sp_ring<KIND, 1, 8>() != 0) {
         if (physics == 2) {  // 8-wave blocks, 16 envs per wave
             const int blocks8 = (ra.n + 127) / 128;
-            rollout_sp_kernel<KIND, H, 1, 8><<<blocks8, 512, 0, stream>>>(p, state, need_reset, actor,
-                                                                         an, critic, cn, ra, b);
+            rollout_sp_kernel<KIND, H, 1, 8><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
@@ -527,8 +578,7 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     if constexpr (X3 && SUB == 1 && rollout_sp_ring<KIND, 1, 8, 2>() != 0) {
         if (physics == 4) {  // one 8-wave block of 16-env waves per CU (2 waves per SIMD)
             const int blocks8 = (ra.n + 127) / 128;
-            rollout_sp_kernel<KIND, H, 1, 8, 2><<<blocks8, 512, 0, stream>>>(p, state, need_reset,
-                                                                            actor, an, critic, cn, ra, b);
+            rollout_sp_kernel<KIND, H, 1, 8, 2><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
@@ -536,8 +586,7 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     if constexpr (X3 && SUB == 2 && rollout_sp_ring<KIND, 2, 8>() != 0) {
         if (physics == 3) {  // one 8-wave block per CU, 32 envs per wave
             const int blocks8 = (ra.n + 255) / 256;
-            rollout_sp_kernel<KIND, H, 2, 8><<<blocks8, 512, 0, stream>>>(p, state, need_reset, actor,
-                                                                         an, critic, cn, ra, b);
+            rollout_sp_kernel<KIND, H, 2, 8><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
@@ -545,8 +594,7 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     if constexpr (X3 && SUB == 2 && rollout_sp_ring<KIND, 2, 4, 1>() != 0) {
         if (physics == 5) {  // one 4-wave block of 32-env waves per CU (1 wave per SIMD, 512 registers)
             const int blocks4 = (ra.n + 127) / 128;
-            rollout_sp_kernel<KIND, H, 2, 4, 1><<<blocks4, 256, 0, stream>>>(p, state, need_reset,
-                                                                            actor, an, critic, cn, ra, b);
+            rollout_sp_kernel<KIND, H, 2, 4, 1><<<blocks4, 256, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
@@ -554,16 +602,14 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     if constexpr (X3 && SUB == 4 && rollout_sp_ring<KIND, 4, 4, 1>() != 0) {
         if (physics == 6) {  // one 4-wave block of 64-env waves per CU (1 wave per SIMD, 512 registers)
             const int blocks4 = (ra.n + 255) / 256;
-            rollout_sp_kernel<KIND, H, 4, 4, 1><<<blocks4, 256, 0, stream>>>(p, state, need_reset,
-                                                                            actor, an, critic, cn, ra, b);
+            rollout_sp_kernel<KIND, H, 4, 4, 1><<<blocks4, 256, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
     }
     if constexpr (X3 && rollout_sp_fits<KIND, SUB>()) {
         if (physics)
-            rollout_sp_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor,
-                                                                          an, critic, cn, ra, b);
+            rollout_sp_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
         else
             rollout_kernel<KIND, H, SUB, X3><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor,
                                                                          an, critic, cn, ra, b);
@@ -630,6 +676,113 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
                                                    ra, b, physics, stream);
     return launch_rollout<KIND, 256, 4, false>(params, state, need_reset, actor, an, critic, cn, ra,
                                                b, physics, stream);
+}
+
+// ------------------------------------------------------------------------------------------
+// UGVForwardObstacleAvoidance PPO2 / DPPO2 rollout (demonstration/PPO2/PPO2-4-UGVForward
+// ObstacleAvoidance/train.py:48-50,95-97: 41 -> 256 -> 256 -> 2 actor, 41 -> 256 -> 256 -> 1
+// critic, tanh; DPPO2 copy likewise). The 41 inputs (4 + 37 lidar beams), the lidar scan and the
+// 38-double env state (10 obstacle circles travel with the env) do not fit the fused kernel's LDS,
+// so ONE rlp_rollout call runs the same driver loop as a sequence of kernels per step on the
+// caller's stream (no host round trip, no synchronisation):
+//   critic V(s_t), actor z_t            packed forward (layer 1 as 11 K-steps of 16x16x4 f32 MFMA)
+//   oa_sample_kernel                    mean = tanh(z) gain + off, Philox eps (the fused kernel's
+//                                       stream), clamp, log-prob; V(s'_{t-1}) = V(s_t) where the env
+//                                       did not end at t-1
+//   lidar env step (oa_kernel)          obs_next, reward, flag, done
+//   oa_post_kernel                      f32 reward, i8 flag, success rule
+//   reset of ended envs (map generator, counter step0 + t + 1) and the next observation (lidar)
+// and after the segment the bootstrap V(s'_{T-1}) of the envs still running. Same semantics, same
+// random draws and same buffers as the fused kernel; the MLPs run on the exact f32 MFMA path.
+using OA = Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE>;
+
+__global__ void __launch_bounds__(256) oa_sample_kernel(RolloutArgs ra, int t, int out_tanh,
+                                                        rlp_rollout_bufs b) {
+    const int i = blockIdx.x * 256 + threadIdx.x, n = ra.n;
+    if (i >= n) return;
+    constexpr int A = OA::A;
+    const int k = t * n + i;
+    float eps[A];
+    philox_normal_f32<A>(ra.seed, ra.step0 + (uint64_t)t, ra.env_id0 + (uint64_t)i, eps);
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        const float mr = b.action[k * A + a];  // the actor's pre-activation, written in place
+        const float m = (out_tanh ? tanhf(mr) : mr) * ra.gain[a] + ra.off[a];
+        float x = m + ra.std_[a] * eps[a];
+        x = fmaxf(fminf(x, ra.a_max[a]), ra.a_min[a]);
+        b.action[k * A + a] = x;
+        b.logp[k * A + a] = normal_logp_c(x, m, ra.half_inv_var[a], ra.log_std[a]);
+    }
+    if (t > 0 && !b.done[k - n]) b.value_next[k - n] = b.value[k];  // V(s'_{t-1}) == V(s_t)
+}
+
+__global__ void __launch_bounds__(256) oa_post_kernel(RolloutArgs ra, int t, const double *r64,
+                                                      const int32_t *f32, rlp_rollout_bufs b,
+                                                      uint8_t *need_reset) {
+    const int i = blockIdx.x * 256 + threadIdx.x, n = ra.n;
+    if (i >= n) return;
+    const int k = t * n + i;
+    const bool dn = b.done[k] != 0;
+    b.reward[k] = (float)r64[i];
+    b.flag[k] = (int8_t)f32[i];
+    b.success[k] = success_of(ra.success_rule, ra.success_flag, dn, f32[i]);
+    if (t == ra.T - 1) need_reset[i] = dn;  // ended envs of the last step reset next segment
+}
+
+__global__ void __launch_bounds__(256) oa_boot_kernel(int T, int n, const float *v, rlp_rollout_bufs b) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int k = (T - 1) * n + i;
+    if (!b.done[k]) b.value_next[k] = v[i];
+}
+
+static int rollout_oa(const void *params, double *state, uint8_t *need_reset, const float *actor,
+                      const MfmaNet &an, const float *critic, const MfmaNet &cn,
+                      const RolloutArgs &ra, const rlp_rollout_bufs &b, hipStream_t s) {
+    const auto &p = *static_cast<const OA::P *>(params);
+    if (an.S != OA::S || cn.S != OA::S || an.A != OA::A || cn.A != 1)
+        return fail(RLP_EINVAL, "rlp_rollout: net dims (S=%d,A=%d / S=%d,A=%d) != env (S=%d,A=%d)",
+                    an.S, an.A, cn.S, cn.A, OA::S, OA::A);
+    if (an.H != 256 || cn.H != 256)
+        return fail(RLP_EUNSUPPORTED, "rlp_rollout: hidden width %d/%d (built for 256)", an.H, cn.H);
+    const int n = ra.n, T = ra.T, nb = (n + 255) / 256;
+    // per-call scratch (stream-ordered): the step's f64 reward, i32 flag, the bootstrap V
+    void *ws = nullptr;
+    const size_t wsz = (size_t)n * (sizeof(double) + sizeof(int32_t) + sizeof(float));
+    if (hipMallocAsync(&ws, wsz, s) != hipSuccess) return fail(RLP_EINVAL, "rlp_rollout: scratch");
+    double *r64 = static_cast<double *>(ws);
+    int32_t *f32 = reinterpret_cast<int32_t *>(r64 + n);
+    float *vb = reinterpret_cast<float *>(f32 + n);
+    int rc = launch_ugvoa_reset(p, state, n, need_reset, nullptr, ra.seed, ra.step0, ra.env_id0, s);
+    if (rc == RLP_OK) rc = launch_ugvoa_observe(p, state, n, b.obs, s);
+    for (int t = 0; t < T && rc == RLP_OK; ++t) {
+        const size_t k0 = (size_t)t * n;
+        float *obs_t = b.obs + k0 * OA::S;
+        rc = launch_packed_forward<0>(cn, critic, obs_t, b.value + k0, n, nullptr, nullptr, 0, s);
+        if (rc == RLP_OK)
+            rc = launch_packed_forward<0>(an, actor, obs_t, b.action + k0 * OA::A, n, nullptr,
+                                          nullptr, 0, s);
+        if (rc != RLP_OK) break;
+        oa_sample_kernel<<<nb, 256, 0, s>>>(ra, t, an.out_tanh, b);
+        rc = launch_ugvoa_step(p, state, n, b.action + k0 * OA::A, nullptr, b.obs_next + k0 * OA::S,
+                               r64, f32, b.done + k0, s);
+        if (rc != RLP_OK) break;
+        oa_post_kernel<<<nb, 256, 0, s>>>(ra, t, r64, f32, b, need_reset);
+        if (t + 1 < T) {  // the ended envs' reset with the next step's counter, then obs_{t+1}
+            rc = launch_ugvoa_reset(p, state, n, b.done + k0, nullptr, ra.seed, ra.step0 + t + 1,
+                                    ra.env_id0, s);
+            if (rc == RLP_OK) rc = launch_ugvoa_observe(p, state, n, b.obs + (k0 + n) * OA::S, s);
+        }
+    }
+    if (rc == RLP_OK) {  // V(s'_{T-1}) of the envs still running
+        rc = launch_packed_forward<0>(cn, critic, b.obs_next + (size_t)(T - 1) * n * OA::S, vb, n,
+                                      nullptr, nullptr, 0, s);
+        if (rc == RLP_OK) oa_boot_kernel<<<nb, 256, 0, s>>>(T, n, vb, b);
+    }
+    (void)hipFreeAsync(ws, s);
+    if (rc != RLP_OK) return rc;
+    RLP_CHECK_LAUNCH("rlp_rollout (UGVForwardObstacleAvoidance)");
+    return RLP_OK;
 }
 
 static int g_rollout_sub = 0;  // 0: auto
@@ -752,6 +905,8 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
         return rollout_kind<RLP_ENV_UAV_HOVER_OUTER_LOOP>(env_params, state, need_reset,
                                                           actor_packed, an, critic_packed, cn, ra,
                                                           b, sub, prec, physics, s);
+    case RLP_ENV_UGV_OBSTACLE_AVOIDANCE:
+        return rollout_oa(env_params, state, need_reset, actor_packed, an, critic_packed, cn, ra, b, s);
     }
     return fail(RLP_EINVAL, "rlp_rollout: unknown env kind %d", kind);
 }

@@ -543,15 +543,18 @@ struct WArgs {
 // lane (g, e) of MFMA step ks holds h1(row, neuron 16 nt + e) * 2^SH for rows 32 ks + 4 g + i and
 // 32 ks + 16 + 4 g + i (i < 4): the C layout of two layer-1 MFMA tiles (rows on the lane groups),
 // with the A operands (g2 rows) loaded in the same K order.
-// 8 waves (2 per SIMD): wave wv owns output rows j in [32 wv, 32 wv + 32) of dW2 (128 accumulator
-// registers), all waves share the tile's h1 fragments.
+// W waves per block, one block per CU; wave wv owns the JT = 16 / W output-row tiles j in
+// [16 JT wv, 16 JT wv + 16 JT) of dW2 (64 JT accumulator registers); all waves share the tile's
+// h1 fragments. W = 8: 2 waves per SIMD (256 registers, JT = 2). W = 4: 1 wave per SIMD with the
+// VGPR + AGPR budget (JT = 4): every fragment read from LDS feeds 12 MFMAs instead of 6, so the
+// CU reads half the LDS bytes per tile, and the next fragment pair is read one step ahead.
 constexpr int kWgWaves = 8;
-template <int KS1>
-__global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
-    constexpr int H = kUpdH, SP = 4 * KS1, NT = 64 * kWgWaves;
+template <int KS1, int W = kWgWaves>
+__global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
+    constexpr int H = kUpdH, SP = 4 * KS1, NT = 64 * W, JT = 16 / W;
     constexpr int SV = (kUpdRows * SP + NT - 1) / NT;
     constexpr int FRAG = 2 * 16 * 2 * 64 * 8;  // halfs of one tile's h1 fragments (64 KiB)
-    constexpr int FPW = 32 / kWgWaves;         // fragments (ks, nt) built per wave and tile
+    constexpr int FPW = 32 / W;                // fragments (ks, nt) built per wave and tile
     // double-buffered: tile i's MFMAs read hfrag[i & 1] while its waves build tile i + step's
     // fragments into hfrag[(i + 1) & 1] from srow[(i + 1) & 1]
     __shared__ float srow[2][kUpdRows][SP];
@@ -560,7 +563,8 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
     __shared__ __attribute__((aligned(16))) _Float16 hfrag[2][FRAG];
     const MfmaNet &net = w.net;
     const int S = net.S;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, gq = lane >> 4, e = lane & 15;
+    const int lane = threadIdx.x & 63, gq = lane >> 4, e = lane & 15;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     {
         // small_r: W1, b1 x 2/ln 2 (h1 as in the FD forward)
         const float *W1c = w.packed + net.off_small_r;
@@ -577,9 +581,9 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
     half8 ones;
 #pragma unroll
     for (int i = 0; i < 8; ++i) ones[i] = (_Float16)1.0f;
-    floatx4 acc2[2][16], accb[2];
+    floatx4 acc2[JT][16], accb[JT];
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
+    for (int jt = 0; jt < JT; ++jt) {
         accb[jt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int nt = 0; nt < 16; ++nt) acc2[jt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -628,19 +632,20 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
     };
     const float *g2base = w.g2t;
     asm volatile("" : "+s"(g2base));
-    auto load_g2 = [&](int64_t tile, floatx4 (&gv)[2][2][2]) {
+    // A operands of one K step: g2(rows 32 ks + 4 gq + i and 32 ks + 16 + 4 gq + i,
+    // j = 16 JT wv + 16 jt + e) (the fragments' K order); loaded one K step ahead
+    auto load_g2 = [&](int64_t tile, int ks, floatx4 (&gv)[JT][2]) {
         const int64_t t = tile < ntiles ? tile : ntiles - 1;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int jt = 0; jt < 2; ++jt) {
-                // A operands: g2(rows 32 ks + 4 gq + i and 32 ks + 16 + 4 gq + i, j = 32 wv + 16 jt + e)
-                // (the fragments' K order)
-                const gptr<float> src = as_global(g2base + t * kUpdTileFloats +
-                                                  (32 * wv + 16 * jt + e) * kUpdRows + 32 * ks + 4 * gq);
-                gv[ks][jt][0] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src);
-                gv[ks][jt][1] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 16);
-            }
+        for (int jt = 0; jt < JT; ++jt) {
+            const gptr<float> src = as_global(g2base + t * kUpdTileFloats +
+                                              (16 * JT * wv + 16 * jt + e) * kUpdRows + 32 * ks + 4 * gq);
+            gv[jt][0] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src);
+            gv[jt][1] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 16);
+        }
+    };
+    auto frag = [&](int buf, int F, int hl) {
+        return *reinterpret_cast<const half8 *>(&hfrag[buf][((F * 2 + hl) * 64 + lane) * 8]);
     };
 
     // prologue: the first tile's s rows and fragments
@@ -655,8 +660,8 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
     for (int u = 0; u < FPW; ++u) build_frag(0, FPW * wv + u);
     float svn[SV];
     load_s(tile + gridDim.x, svn);
-    floatx4 gv[2][2][2];
-    load_g2(tile, gv);
+    floatx4 gv[JT][2];
+    load_g2(tile, 0, gv);
     lds_barrier();
     for (int i = 0; tile < ntiles; tile += gridDim.x, ++i) {
         const int cur = i & 1, nxt = cur ^ 1;
@@ -665,28 +670,35 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
         store_s(nxt, svn);
         lds_barrier();
         load_s(tile + 2 * (int64_t)gridDim.x, svn);
-        floatx4 gvn[2][2][2];
-        load_g2(tile + gridDim.x, gvn);
+        half8 bh = frag(cur, 0, 0), bl = frag(cur, 0, 1);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             // A operands scaled by 2^sg and split
-            half8 ah[2], al[2];
+            half8 ah[JT], al[JT];
 #pragma unroll
-            for (int jt = 0; jt < 2; ++jt) {
+            for (int jt = 0; jt < JT; ++jt) {
                 float x[8];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    x[u] = gv[ks][jt][0][u] * sg;
-                    x[u + 4] = gv[ks][jt][1][u] * sg;
+                    x[u] = gv[jt][0][u] * sg;
+                    x[u + 4] = gv[jt][1][u] * sg;
                 }
                 split8(x, ah[jt], al[jt]);
             }
+            // the next K step's g2 (this tile's second, or the next tile's first), in flight
+            // under this step's MFMAs
+            if (ks == 0) load_g2(tile, 1, gv);
+            else load_g2(tile + gridDim.x, 0, gv);
 #pragma unroll
             for (int nt = 0; nt < 16; ++nt) {
-                const half8 bh = *reinterpret_cast<const half8 *>(&hfrag[cur][(((ks * 16 + nt) * 2 + 0) * 64 + lane) * 8]);
-                const half8 bl = *reinterpret_cast<const half8 *>(&hfrag[cur][(((ks * 16 + nt) * 2 + 1) * 64 + lane) * 8]);
+                const int F = ks * 16 + nt;
+                half8 nbh, nbl;  // the next fragment pair, read one step ahead
+                if (F + 1 < 32) {
+                    nbh = frag(cur, F + 1, 0);
+                    nbl = frag(cur, F + 1, 1);
+                }
 #pragma unroll
-                for (int jt = 0; jt < 2; ++jt) {
+                for (int jt = 0; jt < JT; ++jt) {
                     floatx4 v = acc2[jt][nt];
                     v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jt], bh, v, 0, 0, 0);
                     v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jt], bl, v, 0, 0, 0);
@@ -694,30 +706,28 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
                     acc2[jt][nt] = v;
                 }
                 // the next tile's fragments, spread over this tile's MFMAs (FPW per wave)
-                if ((ks * 16 + nt) % (32 / FPW) == (32 / FPW) - 1)
-                    build_frag(nxt, FPW * wv + (ks * 16 + nt) / (32 / FPW));
+                if (F % (32 / FPW) == (32 / FPW) - 1)
+                    build_frag(nxt, FPW * wv + F / (32 / FPW));
+                if (F + 1 < 32) {
+                    bh = nbh;
+                    bl = nbl;
+                }
             }
 #pragma unroll
-            for (int jt = 0; jt < 2; ++jt) {  // db2: g2 against a ones column
+            for (int jt = 0; jt < JT; ++jt) {  // db2: g2 against a ones column
                 accb[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[jt], ones, accb[jt], 0, 0, 0);
                 accb[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jt], ones, accb[jt], 0, 0, 0);
             }
         }
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int c = 0; c < 2; ++c) gv[a][b][c] = gvn[a][b][c];
         lds_barrier();  // the next tile's fragments are complete; this tile's buffer is free
     }
-    // C layout: lane holds rows m = 4 gq + q (j = 32 wv + 16 jt + m), column e (n = 16 nt + e)
+    // C layout: lane holds rows m = 4 gq + q (j = 16 JT wv + 16 jt + m), column e (n = 16 nt + e)
     float *out = w.part + (size_t)blockIdx.x * (H * H + H);
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
+    for (int jt = 0; jt < JT; ++jt)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int j = 32 * wv + 16 * jt + 4 * gq + q;
+            const int j = 16 * JT * wv + 16 * jt + 4 * gq + q;
 #pragma unroll
             for (int nt = 0; nt < 16; ++nt) out[j * H + 16 * nt + e] = acc2[jt][nt][q] * un2;
             if (e == 0) out[H * H + j] = accb[jt][q] * unb;
@@ -813,7 +823,8 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
     }
 }
 
-static int g_fd_mode = 0;  // rlp_set_fd_mode
+static int g_fd_mode = 0;      // rlp_set_fd_mode
+static int g_wgrad_waves = 8;  // rlp_set_wgrad_waves
 
 static int ppo2_grid() {  // CUs of the device (cached: device properties are slow)
     static int cus = 0;
@@ -836,7 +847,8 @@ extern "C" {
 
 int64_t rlp_ppo2_workspace_floats(const rlp_mlp_desc *desc, int64_t rows) {
     MfmaNet net;
-    if (!desc || !mfma_net_from_desc(*desc, &net) || net.H != kUpdH || rows < 0) return RLP_EINVAL;
+    if (!desc || !mfma_net_from_desc(*desc, &net) || net.H != kUpdH || net.ks1 > 2 || rows < 0)
+        return RLP_EINVAL;
     const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
     const int64_t grid = ppo2_grid();  // wgrad: one block per CU; FD: two
     return tiles * kUpdTileFloats + grid * (kUpdH * kUpdH + kUpdH) +
@@ -849,8 +861,8 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
                   double *loss_sum, float *workspace, rlp_stream_t stream) {
     RLP_REQUIRE(desc && packed && cfg && s && grad && workspace, "rlp_ppo2_grad: null argument");
     MfmaNet net;
-    if (!mfma_net_from_desc(*desc, &net) || net.H != kUpdH)
-        return fail(RLP_EUNSUPPORTED, "rlp_ppo2_grad: need a [S->256->256->A] tanh net");
+    if (!mfma_net_from_desc(*desc, &net) || net.H != kUpdH || net.ks1 > 2)
+        return fail(RLP_EUNSUPPORTED, "rlp_ppo2_grad: need a [S<=8 -> 256 -> 256 -> A] tanh net");
     const bool actor = cfg->kind == RLP_LOSS_ACTOR;
     RLP_REQUIRE(actor || cfg->kind == RLP_LOSS_CRITIC, "rlp_ppo2_grad: loss kind %d", cfg->kind);
     if (actor) {
@@ -912,8 +924,13 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     WArgs w{};
     w.packed = packed; w.net = net; w.s = s; w.index = index; w.rows = rows;
     w.g2t = g.g2t; w.g2max = g.g2max; w.part = partw;
-    if (net.ks1 == 1) ppo2_wgrad_kernel<1><<<grid, 64 * kWgWaves, 0, st>>>(w);
-    else ppo2_wgrad_kernel<2><<<grid, 64 * kWgWaves, 0, st>>>(w);
+    if (g_wgrad_waves == 4) {
+        if (net.ks1 == 1) ppo2_wgrad_kernel<1, 4><<<grid, 256, 0, st>>>(w);
+        else ppo2_wgrad_kernel<2, 4><<<grid, 256, 0, st>>>(w);
+    } else {
+        if (net.ks1 == 1) ppo2_wgrad_kernel<1, 8><<<grid, 512, 0, st>>>(w);
+        else ppo2_wgrad_kernel<2, 8><<<grid, 512, 0, st>>>(w);
+    }
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (wgrad)");
     const int64_t total = (int64_t)net.H * net.S + net.H + (int64_t)net.H * net.H + net.H +
                           (int64_t)net.A * net.H + net.A;
@@ -930,6 +947,14 @@ int rlp_set_fd_mode(int mode) {
 }
 
 int rlp_get_fd_mode(void) { return g_fd_mode; }
+
+int rlp_set_wgrad_waves(int waves) {
+    if (waves != 4 && waves != 8) return fail(RLP_EINVAL, "rlp_set_wgrad_waves: %d", waves);
+    g_wgrad_waves = waves;
+    return RLP_OK;
+}
+
+int rlp_get_wgrad_waves(void) { return g_wgrad_waves; }
 
 int rlp_grad_sqnorm(const float *grad, int64_t n, double *out, rlp_stream_t stream) {
     RLP_REQUIRE(grad && out && n >= 0, "rlp_grad_sqnorm: bad argument");

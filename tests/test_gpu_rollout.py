@@ -42,13 +42,25 @@ def nets(S, Ad, seed, H=256):
     return ad, init(ad, 1.0), cd, init(cd, 1.0)
 
 
-def test_rollout_rejects_lidar_env():
-    """The 41-input lidar env is outside the fused kernel's net shapes: a clean error, no launch."""
+def test_lidar_env_nets_pack_and_forward_but_update_rejects():
+    """41-input nets (the lidar env's PPO2 demos) pack for the MFMA forward (layer 1 on 11
+    K-steps), which matches the oracle's double-accumulated MLP; the native PPO2 update, built for
+    <= 8 inputs, rejects them with a clean error (their update runs on the torch learner)."""
+    from oracle import oracle
     kind = A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE
     D, S, Ad = A.ENV_DIMS[kind]
     ad, ap, cd, cp = nets(S, Ad, seed=1)
+    x = np.random.default_rng(3).uniform(-1, 1, (3001, S)).astype(np.float32)
+    for d, prm in ((ad, ap), (cd, cp)):
+        pk = K.mfma_pack(d, dev(prm))
+        y = K.mfma_forward(d, pk, dev(x)).cpu().numpy()
+        ref = oracle.mlp_forward(d, prm, x)
+        np.testing.assert_allclose(y, ref, rtol=1e-5, atol=2e-6)
+    pk = K.mfma_pack(cd, dev(cp))
+    ws = torch.empty(1 << 20, device="cuda")
     with pytest.raises(_native.RLPError, match="S<=8"):
-        K.mfma_pack(ad, dev(ap))
+        K.ppo2_grad(cd, pk, K.ppo2_loss_cfg(A.RLP_LOSS_CRITIC), dev(x), v_target=dev(x[:, 0].copy()),
+                    grad=torch.empty(cd.param_count(), device="cuda"), workspace=ws)
 
 
 def test_rollout_invariants_at_bench_size():

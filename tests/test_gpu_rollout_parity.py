@@ -264,7 +264,7 @@ def _nets(S, Ad, seed):
     return ad, orthogonal(ad, [1, 1, 1.0], seed), cd, orthogonal(cd, [1, 1, 1], seed + 1)
 
 
-@pytest.mark.parametrize("kind", sorted(A.ROLLOUT_KINDS))
+@pytest.mark.parametrize("kind", sorted(A.FUSED_ROLLOUT_KINDS))
 @pytest.mark.parametrize("sub", [1, 2, 4])
 def test_rollout_teacher_forced_vs_oracle(kind, sub):
     """All kinds x envs-per-wave: physics replayed with the kernel's actions, the oracle's own
@@ -334,3 +334,34 @@ def test_rollout_env_copies_teacher_forced(kind, variant):
         a_tol, _ = policy_bounds(ad, ap, gb["obs"], ob["action"], lo, hi, std)
         bound_rows(gb["action"], ob["action"], 1e-5, a_tol, "action")
         bound(gb["value"], ob["value"], 1e-5, 2e-6, "V(s)")
+
+
+@pytest.mark.parametrize("variant", ["env", "ppo2"])
+def test_rollout_lidar_env_teacher_forced(variant):
+    """UGVForwardObstacleAvoidance through rlp_rollout (the per-step kernel sequence: packed
+    forward with the 41-input layer 1 on 11 K-steps of f32 MFMA, Philox sample, lidar env step,
+    map-generator resets), the PPO2 demo's 41 -> 256 -> 256 -> 2 / -> 1 nets
+    (demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97), two chained
+    segments with resets inside: physics teacher-forced against the oracle (flags / done exact,
+    state 1e-9, observations 2 ulps), the oracle's own policy and critic on the kernel's
+    observations (action, log-prob, V(s), V(s'))."""
+    kind = A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE
+    D, S, Ad = A.ENV_DIMS[kind]
+    p = A.default_params(kind, variant)
+    ad, ap, cd, cp = _nets(S, Ad, 90)
+    lo, hi = A.action_bounds(kind, p)
+    std = [(h - l) / 6 for l, h in zip(lo, hi)]
+    n, T = 1024 + 37, 40
+    cfg = K.make_rollout_cfg(T, n, 3407, 0, 0, std, lo, hi, A.RLP_SUCCESS_DONE_AND_FLAG_NE,
+                             A.timeout_flag(kind))
+    g, gst, gneed = _gpu_segment(kind, p, n, T, ad, ap, cd, cp, cfg, segments=2)
+    assert g[0]["done"].any() or g[1]["done"].any()
+    o, ost, oneed = _oracle_forced(kind, p, n, T, cfg, g, ad, ap, cd, cp)
+    _check_physics(kind, g, o, gst, ost, gneed, oneed, f"lidar env {variant}")
+    for gb, ob in zip(g, o):
+        a_tol, lp_tol = policy_bounds(ad, ap, gb["obs"], ob["action"], lo, hi, std)
+        bound_rows(gb["action"], ob["action"], 1e-5, a_tol, "action")
+        bound_rows(gb["logp"], ob["logp"], 1e-5, lp_tol, "log-prob")
+        bound(gb["value"], ob["value"], 1e-5, 2e-6, "V(s)")
+        nd = gb["done"] == 0
+        bound(gb["value_next"][nd], ob["value_next"][nd], 1e-5, 2e-6, "V(s')")
