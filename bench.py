@@ -318,6 +318,43 @@ def ugvoa_leg(rank, n=16384, steps=30, warmup=3, seed=5):
                       "circles + GPU map generator on reset, random actions"}
 
 
+def ugvoa_ppo2_leg(rank, n=16384, T=64, iters=3, seed=17):
+    """UGVForwardObstacleAvoidance PPO2 rollout (the PPO2 demo's 41 -> 256 -> 256 -> 2 / -> 1 tanh
+    nets, demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97) through
+    rlp_rollout: per step packed actor / critic forward (layer 1 on 11 K-steps of f32 MFMA),
+    Philox sample, lidar env step, map-generator resets; n envs per GPU (config 5: 131 072 / 8)."""
+    kind = A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE
+    p = A.default_params(kind, "ppo2")
+    D, S, Ad = A.ENV_DIMS[kind]
+    ad = A.MLPDesc.make([S, 256, 256, Ad], [A.RLP_ACT_TANH] * 3)
+    cd = A.MLPDesc.make([S, 256, 256, 1], [A.RLP_ACT_TANH, A.RLP_ACT_TANH, A.RLP_ACT_NONE])
+    apk = K.mfma_pack(ad, orthogonal_params(ad, [1.0, 1.0, 0.01], seed).cuda())
+    cpk = K.mfma_pack(cd, orthogonal_params(cd, [1.0, 1.0, 1.0], seed + 1).cuda())
+    lo, hi = A.action_bounds(kind, p)
+    std = [(h - l) / 6 for l, h in zip(lo, hi)]
+    st = K.new_state(kind, n)
+    need = torch.ones(n, dtype=torch.uint8, device="cuda")
+    bufs = K.rollout_buffers(kind, T, n)
+    step0 = [0]
+
+    def seg():
+        cfg = K.make_rollout_cfg(T, n, seed, step0[0], rank * n, std, lo, hi,
+                                 A.RLP_SUCCESS_DONE_AND_FLAG_NE, A.timeout_flag(kind))
+        K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs)
+        step0[0] += T
+    seg()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        seg()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"value": n * T * iters / dt, "unit": "env-steps/s", "envs_per_gpu": n, "T": T,
+            "ms_per_segment": dt / iters * 1e3, "episodes_per_segment": int(bufs["done"].sum()),
+            "config": "UGVForwardObstacleAvoidance (PPO2 copy, 37-beam lidar, 10 circles) PPO2 "
+                      "rollout, nets [41,256,256,2] / [41,256,256,1] tanh (rlp_rollout)"}
+
+
 def ugvoa_sac_leg(rank, n=16384, steps=20, warmup=3, batch=4096, capacity=1 << 20, seed=13):
     """BASELINE config 5 shard: UGVForwardObstacleAvoidance SAC, n envs per GPU (131 072 / 8),
     replay in HBM. One step = actor trunk + squashed-Gaussian sample (librlp) + env step with the
@@ -726,6 +763,13 @@ def main():
             dist.all_reduce(t)
             d["value"] = float(t[0])
         out["ugvoa_lidar"] = d
+    if args.oa and args.env == "cartpole":
+        d = ugvoa_ppo2_leg(rank)
+        if dist is not None:
+            t = torch.tensor([d["value"]], device="cuda", dtype=torch.float64)
+            dist.all_reduce(t)
+            d["value"] = float(t[0])
+        out["ugvoa_ppo2_rollout"] = d
     if args.sac and args.env == "cartpole":
         d = ugvoa_sac_leg(rank)
         if dist is not None:

@@ -59,103 +59,89 @@ __device__ __forceinline__ Moments block_moments(Moments v, Moments *red) {
 
 // ---- reward normalisation -----------------------------------------------------------------
 // Three launches: (1) chunk statistics — a [P x T] grid of 256-thread blocks, each two-pass over
-// a 4096-reward chunk of one time step held in registers (16 per lane, one HBM read, fp64
-// sums); (2) one block: per time step the chunks' (mean, M2) combined in chunk order (Chan),
-// then the running-statistics recurrence over t (the merge weights n/(cnt+n), cnt*n/(cnt+n)
-// depend only on the count and are computed in parallel; the serial chain is a few fp64 ops per
-// step, staged through LDS), then std_t = sqrt(S_t / cnt_t) in parallel; (3) the elementwise
-// normalisation. Workspace layout (rlp_reward_norm_workspace): part [T][P][2] | agg [T][2] |
-// out [T][2] (mean_t, std_t after step t's merge).
+// a 4096-reward chunk of one time step held in registers (16 per lane as four 16-byte loads when
+// the rows are 16-byte aligned, one HBM read, fp64 sums); (2) one block: per time step the
+// chunks' (mean, M2) combined in chunk order (Chan), then the running statistics over t as a
+// block-wide inclusive scan of Chan merges (each thread folds two time steps, a shuffle scan in
+// each wave, the four wave totals through LDS; fixed order, so run-independent), 512 steps per
+// tile with the carry between tiles; the single-env case keeps the reference's serial Welford
+// recurrence (first-call std = x quirk); (3) the elementwise normalisation on a [chunks x T] grid
+// (the time step is the block row: no per-element index division). Workspace layout
+// (rlp_reward_norm_workspace): part [T][P][2] | agg [T][2] | out [T][2] (mean_t, std_t after
+// step t's merge).
+__host__ inline bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
 constexpr int kRsChunk = 4096, kRsPer = kRsChunk / 256, kRsTile = 512;
 
 __host__ __device__ inline int rs_chunks(int n) { return (n + kRsChunk - 1) / kRsChunk; }
 
-__global__ void __launch_bounds__(256) reward_stats_kernel(const float *__restrict__ r, int n,
+template <bool VEC>
+__global__ void __launch_bounds__(256) reward_stats_kernel(const float *__restrict__ r, int T, int n,
                                                            double *__restrict__ part) {
     __shared__ double red[4];
-    const int p = blockIdx.x, t = blockIdx.y, P = gridDim.x;
+    const int p = blockIdx.x, P = gridDim.x;
     const int lo = p * kRsChunk, cnt = min(kRsChunk, n - lo);
-    const float *x = r + (size_t)t * n + lo;
-    float v[kRsPer];
-    double s = 0;
+    for (int t = blockIdx.y; t < T; t += gridDim.y) {
+        const float *x = r + (size_t)t * n + lo;
+        float v[kRsPer];
+        if (VEC) {  // lane owns 4 consecutive rewards per 1024-reward slice; cnt % 4 == 0
 #pragma unroll
-    for (int j = 0; j < kRsPer; ++j) {
-        const int i = j * 256 + threadIdx.x;
-        v[j] = i < cnt ? x[i] : 0.f;
-        s += (double)v[j];
-    }
-    const double mean = block_sum<256>(s, red) / cnt;
-    double q = 0;
+            for (int j = 0; j < kRsPer / 4; ++j) {
+                const int i = (j * 256 + (int)threadIdx.x) * 4;
+                const float4 q = i < cnt ? *(const float4 *)(x + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[4 * j] = q.x; v[4 * j + 1] = q.y; v[4 * j + 2] = q.z; v[4 * j + 3] = q.w;
+            }
+        } else {
 #pragma unroll
-    for (int j = 0; j < kRsPer; ++j) {
-        const double d = (double)v[j] - mean;
-        if (j * 256 + (int)threadIdx.x < cnt) q += d * d;
-    }
-    const double m2 = block_sum<256>(q, red);
-    if (threadIdx.x == 0) {
-        part[((size_t)t * P + p) * 2 + 0] = mean;
-        part[((size_t)t * P + p) * 2 + 1] = m2;
+            for (int j = 0; j < kRsPer; ++j) {
+                const int i = j * 256 + threadIdx.x;
+                v[j] = i < cnt ? x[i] : 0.f;
+            }
+        }
+        double s = 0;
+#pragma unroll
+        for (int j = 0; j < kRsPer; ++j) s += (double)v[j];
+        const double mean = block_sum<256>(s, red) / cnt;
+        double q = 0;
+#pragma unroll
+        for (int j = 0; j < kRsPer; ++j) {
+            const int i = VEC ? (j / 4 * 256 + (int)threadIdx.x) * 4 + (j & 3) : j * 256 + threadIdx.x;
+            const double d = (double)v[j] - mean;
+            if (i < cnt) q += d * d;
+        }
+        const double m2 = block_sum<256>(q, red);
+        if (threadIdx.x == 0) {
+            part[((size_t)t * P + p) * 2 + 0] = mean;
+            part[((size_t)t * P + p) * 2 + 1] = m2;
+        }
     }
 }
 
-// sequential merge over t (RunningMeanStd.update, utils/classes.py:626-645): Welford for a
-// single env (the reference exactly, first-call std = x quirk included), Chan's parallel merge
-// otherwise. `parts` holds the chunk statistics of `world` ranks of n envs each, rank-major
-// ([world][T][P][2]); per time step the world * P chunks are combined in global env order, so W
-// ranks of n envs reproduce one rank of W * n envs bit for bit (when n is a multiple of the chunk).
+// Welford for a single env (the reference exactly, first-call std = x quirk included, serial),
+// Chan's parallel merge otherwise (utils/classes.py:626-645 RunningMeanStd.update). `parts` holds
+// the chunk statistics of `world` ranks of n envs each, rank-major ([world][T][P][2]); per time
+// step the world * P chunks are combined in global env order, so W ranks of n envs reproduce one
+// rank of W * n envs bit for bit (when n is a multiple of the chunk).
 __global__ void __launch_bounds__(256) reward_merge_kernel(const float *__restrict__ r, int T, int n,
                                                            int world, const double *parts,
                                                            double *rms, double *work) {
-    __shared__ double sa[kRsTile], sb[kRsTile], sw1[kRsTile], sw2[kRsTile];
+    __shared__ double sa[kRsTile], sb[kRsTile];
+    __shared__ Moments wred[4];
     __shared__ double carry[4];
     const int P = rs_chunks(n);
     double *agg = work + (size_t)T * P * 2, *out = agg + (size_t)T * 2;
     const double ntot = (double)n * world;
-    const bool single = ntot == 1;
     if (threadIdx.x == 0)
         for (int k = 0; k < 4; ++k) carry[k] = rms[k];
-    if (!single) {  // per time step: combine the chunks in global env order
-        for (int t = threadIdx.x; t < T; t += 256) {
-            double c = 0, mean = 0, m2 = 0;
-            for (int q = 0; q < world * P; ++q) {
-                const int rk = q / P, p = q - rk * P;
-                const double *pp = parts + (((size_t)rk * T + t) * P + p) * 2;
-                const double cb = min(kRsChunk, n - p * kRsChunk);
-                if (q == 0) {
-                    c = cb; mean = pp[0]; m2 = pp[1];
-                    continue;
-                }
-                const double nn = c + cb;
-                const double dl = pp[0] - mean;
-                mean = mean + dl * (cb / nn);
-                m2 = m2 + pp[1] + dl * dl * (c * cb / nn);
-                c = nn;
-            }
-            agg[2 * t] = mean;
-            agg[2 * t + 1] = m2;
-        }
-    }
-    __syncthreads();
-    for (int t0 = 0; t0 < T; t0 += kRsTile) {
-        const int tn = min(kRsTile, T - t0);
-        const double cnt0 = carry[0];
-        for (int j = threadIdx.x; j < tn; j += 256) {
-            const int t = t0 + j;
-            if (single) {
-                sa[j] = (double)r[t];
-            } else {  // the merge weights need only the running count (cnt0 + j ntot)
-                sa[j] = agg[2 * t];
-                sb[j] = agg[2 * t + 1];
-                const double cnt = cnt0 + (double)j * ntot, nn = cnt + ntot;
-                sw1[j] = ntot / nn;
-                sw2[j] = cnt * ntot / nn;
-            }
-        }
+    if (ntot == 1) {  // the reference's own shape: one reward per step, serial Welford
         __syncthreads();
-        if (threadIdx.x == 0) {
-            double cnt = carry[0], mean = carry[1], S = carry[2], sd = carry[3];
-            for (int j = 0; j < tn; ++j) {
-                if (single) {
+        for (int t0 = 0; t0 < T; t0 += kRsTile) {
+            const int tn = min(kRsTile, T - t0);
+            for (int j = threadIdx.x; j < tn; j += 256) sa[j] = (double)r[t0 + j];
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double cnt = carry[0], mean = carry[1], S = carry[2], sd = carry[3];
+                for (int j = 0; j < tn; ++j) {
                     const double x = sa[j];
                     cnt += 1;
                     if (cnt == 1) {
@@ -167,42 +153,107 @@ __global__ void __launch_bounds__(256) reward_merge_kernel(const float *__restri
                         S = S + (x - old) * (x - mean);
                         sd = sqrt(S / cnt);
                     }
+                    sa[j] = mean;
                     sb[j] = sd;
-                } else {
-                    if (cnt == 0) {
-                        mean = sa[j]; S = sb[j];
-                    } else {
-                        const double dl = sa[j] - mean;
-                        mean = mean + dl * sw1[j];
-                        S = S + sb[j] + dl * dl * sw2[j];
-                    }
-                    cnt += ntot;
-                    sb[j] = S;
                 }
-                sa[j] = mean;
+                carry[0] = cnt; carry[1] = mean; carry[2] = S; carry[3] = sd;
             }
-            if (!single && tn > 0) sd = sqrt(S / cnt);
-            carry[0] = cnt; carry[1] = mean; carry[2] = S; carry[3] = sd;
+            __syncthreads();
+            for (int j = threadIdx.x; j < tn; j += 256) {
+                out[2 * (t0 + j)] = sa[j];
+                out[2 * (t0 + j) + 1] = sb[j];
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        for (int j = threadIdx.x; j < tn; j += 256) {
-            const int t = t0 + j;
-            out[2 * t] = sa[j];
-            out[2 * t + 1] = single ? sb[j] : sqrt(sb[j] / (cnt0 + (double)(j + 1) * ntot));
-        }
-        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 4; ++k) rms[k] = carry[k];
+        return;
     }
-    if (threadIdx.x == 0)
-        for (int k = 0; k < 4; ++k) rms[k] = carry[k];
+    // per time step: combine the chunks in global env order
+    for (int t = threadIdx.x; t < T; t += 256) {
+        double c = 0, mean = 0, m2 = 0;
+        for (int q = 0; q < world * P; ++q) {
+            const int rk = q / P, p = q - rk * P;
+            const double *pp = parts + (((size_t)rk * T + t) * P + p) * 2;
+            const double cb = min(kRsChunk, n - p * kRsChunk);
+            if (q == 0) {
+                c = cb; mean = pp[0]; m2 = pp[1];
+                continue;
+            }
+            const double nn = c + cb;
+            const double dl = pp[0] - mean;
+            mean = mean + dl * (cb / nn);
+            m2 = m2 + pp[1] + dl * dl * (c * cb / nn);
+            c = nn;
+        }
+        agg[2 * t] = mean;
+        agg[2 * t + 1] = m2;
+    }
+    __syncthreads();
+    Moments cr{carry[0], carry[1], carry[2]};
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int t0 = 0; t0 < T; t0 += kRsTile) {
+        const int ta = t0 + 2 * (int)threadIdx.x, tb = ta + 1;
+        const Moments e0 = ta < T ? Moments{ntot, agg[2 * ta], agg[2 * ta + 1]} : Moments{0, 0, 0};
+        const Moments e1 = tb < T ? Moments{ntot, agg[2 * tb], agg[2 * tb + 1]} : Moments{0, 0, 0};
+        Moments v = chan(e0, e1);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive scan inside the wave
+            const Moments u{__shfl_up(v.c, o), __shfl_up(v.m, o), __shfl_up(v.q, o)};
+            if (l >= o) v = chan(u, v);
+        }
+        Moments ex{__shfl_up(v.c, 1), __shfl_up(v.m, 1), __shfl_up(v.q, 1)};
+        if (l == 0) ex = Moments{0, 0, 0};
+        if (l == 63) wred[w] = v;
+        __syncthreads();
+        Moments base = cr;
+        for (int i = 0; i < w; ++i) base = chan(base, wred[i]);
+        base = chan(base, ex);
+        Moments tot = cr;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tot = chan(tot, wred[i]);
+        __syncthreads();
+        const Moments s0 = chan(base, e0), s1 = chan(s0, e1);
+        if (ta < T) {
+            out[2 * ta] = s0.m;
+            out[2 * ta + 1] = sqrt(s0.q / s0.c);
+        }
+        if (tb < T) {
+            out[2 * tb] = s1.m;
+            out[2 * tb + 1] = sqrt(s1.q / s1.c);
+        }
+        cr = tot;
+    }
+    if (threadIdx.x == 0) {
+        rms[0] = cr.c; rms[1] = cr.m; rms[2] = cr.q;
+        rms[3] = T > 0 ? sqrt(cr.q / cr.c) : carry[3];
+    }
 }
 
+// [chunks x T] grid: the block row is the time step, so the per-step (mean, std) are two scalar
+// loads and no element index is divided; 4 rewards per lane as 16-byte accesses when aligned
+template <bool VEC>
 __global__ void __launch_bounds__(256) reward_apply_kernel(const float *__restrict__ r, int T,
                                                            int n, const double *__restrict__ out_t,
                                                            float *__restrict__ out) {
-    const size_t total = (size_t)T * n;
-    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
-        const int t = (int)(i / n);
-        out[i] = (float)(((double)r[i] - out_t[2 * t]) / (out_t[2 * t + 1] + 1e-8));
+    for (int t = blockIdx.y; t < T; t += gridDim.y) {
+        const double m = out_t[2 * t], den = out_t[2 * t + 1] + 1e-8;
+        const float *x = r + (size_t)t * n;
+        float *y = out + (size_t)t * n;
+        if (VEC) {
+            for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += gridDim.x * 1024) {
+                const float4 q = *(const float4 *)(x + i);
+                float4 o;
+                o.x = (float)(((double)q.x - m) / den);
+                o.y = (float)(((double)q.y - m) / den);
+                o.z = (float)(((double)q.z - m) / den);
+                o.w = (float)(((double)q.w - m) / den);
+                *(float4 *)(y + i) = o;
+            }
+        } else {
+            for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+                y[i] = (float)(((double)x[i] - m) / den);
+        }
     }
 }
 
@@ -282,12 +333,30 @@ __global__ void __launch_bounds__(256) adv_stats_merge_kernel(double *stats, int
     }
 }
 
+// 4 advantages per lane as one 16-byte access (the tail of count % 4 by the first lanes) when
+// adv is 16-byte aligned
+template <bool VEC>
 __global__ void __launch_bounds__(256) adv_norm_kernel(float *adv, int64_t count,
                                                        const double *mean_std) {
     const float m32 = (float)mean_std[0];
     const float den = (float)mean_std[1] + 1e-5f;
-    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256)
-        adv[i] = (adv[i] - m32) / den;
+    if (VEC) {
+        const int64_t c4 = count >> 2;
+        float4 *a4 = (float4 *)adv;
+        for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < c4; i += (int64_t)gridDim.x * 256) {
+            float4 q = a4[i];
+            q.x = (q.x - m32) / den;
+            q.y = (q.y - m32) / den;
+            q.z = (q.z - m32) / den;
+            q.w = (q.w - m32) / den;
+            a4[i] = q;
+        }
+        const int64_t i = 4 * c4 + blockIdx.x * 256 + threadIdx.x;
+        if (i < count) adv[i] = (adv[i] - m32) / den;
+    } else {
+        for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256)
+            adv[i] = (adv[i] - m32) / den;
+    }
 }
 
 }  // namespace rlp
@@ -310,7 +379,11 @@ int rlp_reward_norm_stats(const float *reward_in, int T, int n, double *work, rl
     RLP_REQUIRE(reward_in && work, "rlp_reward_norm_stats: null argument");
     RLP_REQUIRE(T >= 0 && n >= 0, "rlp_reward_norm_stats: T=%d n=%d", T, n);
     if (T == 0 || n == 0) return RLP_OK;
-    reward_stats_kernel<<<dim3(rs_chunks(n), T), 256, 0, as_stream(stream)>>>(reward_in, n, work);
+    const dim3 grid(rs_chunks(n), T < 65535 ? T : 65535);
+    if (n % 4 == 0 && aligned16(reward_in))
+        reward_stats_kernel<true><<<grid, 256, 0, as_stream(stream)>>>(reward_in, T, n, work);
+    else
+        reward_stats_kernel<false><<<grid, 256, 0, as_stream(stream)>>>(reward_in, T, n, work);
     RLP_CHECK_LAUNCH("rlp_reward_norm_stats");
     return RLP_OK;
 }
@@ -325,10 +398,15 @@ int rlp_reward_norm_finish(const float *reward_in, int T, int n, int world, cons
     hipStream_t s = as_stream(stream);
     const int P = rs_chunks(n);
     reward_merge_kernel<<<1, 256, 0, s>>>(reward_in, T, n, world, parts, rms, work);
-    const size_t total = (size_t)T * n;
-    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    reward_apply_kernel<<<blocks, 256, 0, s>>>(reward_in, T, n, work + (size_t)T * P * 2 + (size_t)T * 2,
-                                               reward_out);
+    const double *out_t = work + (size_t)T * P * 2 + (size_t)T * 2;
+    const bool vec = n % 4 == 0 && aligned16(reward_in) && aligned16(reward_out);
+    const int per = vec ? 1024 : 256, bx = (n + per - 1) / per;
+    const int cap = T >= 256 ? 64 : 16384 / (T > 0 ? T : 1);  // >= 16k blocks in flight
+    const dim3 grid(bx < cap ? bx : cap, T < 65535 ? T : 65535);
+    if (vec)
+        reward_apply_kernel<true><<<grid, 256, 0, s>>>(reward_in, T, n, out_t, reward_out);
+    else
+        reward_apply_kernel<false><<<grid, 256, 0, s>>>(reward_in, T, n, out_t, reward_out);
     RLP_CHECK_LAUNCH("rlp_reward_norm_finish");
     return RLP_OK;
 }
@@ -370,8 +448,14 @@ int rlp_adv_normalize(float *adv, int64_t count, double *adv_stats, int parts,
     if (count <= 1) return RLP_OK;
     hipStream_t s = as_stream(stream);
     adv_stats_merge_kernel<<<1, 256, 0, s>>>(adv_stats, parts);
-    const int64_t b = (count + 255) / 256;
-    adv_norm_kernel<<<(int)(b < 4096 ? b : 4096), 256, 0, s>>>(adv, count, adv_stats + 3 * (size_t)parts);
+    const double *ms = adv_stats + 3 * (size_t)parts;
+    if (aligned16(adv)) {
+        const int64_t b = (count / 4 + 255) / 256;
+        adv_norm_kernel<true><<<(int)(b < 1 ? 1 : b < 8192 ? b : 8192), 256, 0, s>>>(adv, count, ms);
+    } else {
+        const int64_t b = (count + 255) / 256;
+        adv_norm_kernel<false><<<(int)(b < 8192 ? b : 8192), 256, 0, s>>>(adv, count, ms);
+    }
     RLP_CHECK_LAUNCH("rlp_adv_normalize");
     return RLP_OK;
 }

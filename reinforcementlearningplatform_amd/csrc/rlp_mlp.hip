@@ -83,19 +83,28 @@ __global__ void __launch_bounds__(64) mlp_forward_kernel(MlpArgs args, const flo
 // ------------------------------------------------------------------------------------------
 // info[] = {2^sw, 2^sw * 2^SH, 2^-(sw + SH), 0}: 2^sw puts max|W2| in [2^13, 2^14), far inside f16
 // range, so the hi and lo f16 halves of every weight that matters stay normal (rlp_mfma_x3.hpp).
-__global__ void __launch_bounds__(256) mfma_scale_kernel(MfmaNet net, const float *__restrict__ P,
-                                                         float *out) {
+// (one 1024-thread block; each thread keeps 8 independent loads in flight, so the 256 KB of W2
+// stream at once instead of one dependent load per thread and step: 83 -> a few us per call)
+__global__ void __launch_bounds__(1024) mfma_scale_kernel(MfmaNet net, const float *__restrict__ P,
+                                                          float *out) {
     const int S = net.S, H = net.H;
     const float *W2 = P + S * H + H;
-    float m = 0.f;
-    for (int i = threadIdx.x; i < H * H; i += blockDim.x) m = fmaxf(m, fabsf(W2[i]));
-    __shared__ float red[256];
-    red[threadIdx.x] = m;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
-        __syncthreads();
+    float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i0 = threadIdx.x; i0 < H * H; i0 += 8 * 1024) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 1024;
+            if (i < H * H) m[u] = fmaxf(m[u], fabsf(W2[i]));
+        }
     }
+    float mm = fmaxf(fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3])), fmaxf(fmaxf(m[4], m[5]), fmaxf(m[6], m[7])));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mm = fmaxf(mm, __shfl_xor(mm, o));
+    __shared__ float red[16];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mm;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int w = 1; w < 16; ++w) red[0] = fmaxf(red[0], red[w]);
     if (threadIdx.x == 0) {
         int e = 0;
         if (red[0] > 0.f) frexpf(red[0], &e);  // max = f * 2^e, f in [0.5, 1)
@@ -314,7 +323,7 @@ int rlp_mfma_pack(const rlp_mlp_desc *desc, const float *params, float *packed,
         return fail(RLP_EUNSUPPORTED,
                     "rlp_mfma_pack: need [S<=8 or 41<=S<=44 -> H -> H -> A<=4], H in {64,128,256}");
     const int blocks = (int)((net.count + 255) / 256);
-    mfma_scale_kernel<<<1, 256, 0, as_stream(stream)>>>(net, params, packed);
+    mfma_scale_kernel<<<1, 1024, 0, as_stream(stream)>>>(net, params, packed);
     mfma_pack_kernel<<<blocks < 1024 ? blocks : 1024, 256, 0, as_stream(stream)>>>(net, params,
                                                                                   packed);
     RLP_CHECK_LAUNCH("rlp_mfma_pack");

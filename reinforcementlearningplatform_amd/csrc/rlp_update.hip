@@ -407,7 +407,7 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
                 float dh = 0.f;
 #pragma unroll
                 for (int a = 0; a < A; ++a) dh = __builtin_fmaf(w3[a][q], g3[a], dh);
-                acc[j][q] = dh * (1.f - h * h);
+                acc[j][q] = dh * __builtin_fmaf(-h, h, 1.f);  // tanh' = 1 - h^2, one rounding
             }
         }
         // one wave-uniform guard (8-wave blocks: the last pair's 2nd tile); a scalar tile base

@@ -23,6 +23,17 @@ WORKLOADS = {  # workload -> (kernel name prefix, envs per GPU, T, algorithmic b
 }
 
 
+# bench.py hbm_legs kernels -> the kernel-name prefixes whose FETCH / WRITE add up to one launch
+HBM_KERNELS = {
+    "gae": ["rlp::gae_kernel"],
+    "reward_norm": ["rlp::reward_stats_kernel", "rlp::reward_merge_kernel", "rlp::reward_apply_kernel"],
+    "adv_normalize": ["rlp::adv_stats_merge_kernel", "rlp::adv_norm_kernel"],
+    "env_step_soi": ["rlp::env_step_kernel<3>"],
+    "env_step_ugv": ["rlp::env_step_kernel<4>"],
+    "env_step_uav": ["rlp::env_step_kernel<6>"],
+}
+
+
 def main(run_dir, profile):
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(run_dir, "p*", "**", "*counter_collection.csv"), recursive=True):
@@ -48,6 +59,26 @@ def main(run_dir, profile):
                   "algorithmic_bytes_per_launch": alg, "profile": profile, "kernel": prefix})
         d[wl] = e
         print(f"{wl}: {e['hbm_bytes_per_launch'] / 1e6:.1f} MB per launch vs {alg / 1e6:.1f} MB algorithmic")
+    hk = d.setdefault("hbm_kernels", {})
+    for leg, prefixes in HBM_KERNELS.items():
+        fetch = write = 0.0
+        found = True
+        for pre in prefixes:
+            hit = [k for k in vals if k.startswith(pre) and "FETCH_SIZE" in vals[k] and "WRITE_SIZE" in vals[k]]
+            if not hit:
+                found = False
+                break
+            c = vals[hit[0]]
+            fetch += sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"])
+            write += sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
+        if not found:
+            print(f"{leg}: no FETCH_SIZE/WRITE_SIZE")
+            continue
+        # FETCH_SIZE doubled as for the rollout (128-B requests tallied at 64 B,
+        # MI355X_MICROARCH.md §HBM)
+        hk[leg] = {"kernels": prefixes, "FETCH_SIZE_KB": round(fetch, 1), "WRITE_SIZE_KB": round(write, 1),
+                   "hbm_bytes_per_launch": int((2 * fetch + write) * 1024), "profile": profile}
+        print(f"{leg}: {hk[leg]['hbm_bytes_per_launch'] / 1e6:.1f} MB per launch")
     with open(path, "w") as f:
         json.dump(d, f, indent=1)
         f.write("\n")
