@@ -251,26 +251,42 @@ def soi_ddpg_leg(rank, n=65536, steps=20, warmup=3, batch=4096, capacity=1 << 20
     env = SecondOrderIntegration(n_envs=n, variant="ddpg", seed=seed, env_id0=rank * n)
     env.reset(random=True)
     lo, hi = env.action_range[:, 0], env.action_range[:, 1]
-    nets = [Actor(1e-4, 4, 2, lo, hi), Actor(1e-4, 4, 2, lo, hi), Critic(3e-4, 4, 2), Critic(3e-4, 4, 2)]
     msg = {'state_dim': 4, 'action_dim': 2, 'action_range': env.action_range, 'name': env.name}
-    agent = DDPG(msg, 0.99, 0.005, 0.005, capacity, batch, *nets, device="cuda", seed=seed,
-                 graph=True)
-    loop = VecDDPG(env, agent, learn_iters=1)
     out = {}
-    for learn in (False, True):
-        for _ in range(warmup):
-            loop.step(learn=learn)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            loop.step(learn=learn)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        out["with_learn" if learn else "env_only"] = n * steps / dt
+    for native in (True, False):
+        torch.manual_seed(seed)
+        nets = [Actor(1e-4, 4, 2, lo, hi), Actor(1e-4, 4, 2, lo, hi), Critic(3e-4, 4, 2),
+                Critic(3e-4, 4, 2)]
+        agent = DDPG(msg, 0.99, 0.005, 0.005, capacity, batch, *nets, device="cuda", seed=seed,
+                     graph=True, native=native)
+        assert (agent._native is not None) == native
+        loop = VecDDPG(env, agent, learn_iters=1)
+        for learn in ((False, True) if native else (True,)):
+            for _ in range(warmup):
+                loop.step(learn=learn)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                loop.step(learn=learn)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            key = "env_only" if not learn else "with_learn" if native else "with_learn_torch_update"
+            out[key] = n * steps / dt
+        if native:   # the update alone: one captured learn() (gather + rlp_ddpg_update + refresh)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(steps):
+                agent.learn(is_reward_ascent=False)
+            ev[1].record()
+            torch.cuda.synchronize()
+            out["learn_ms"] = ev[0].elapsed_time(ev[1]) / steps
     return {"value": out["with_learn"], "unit": "env-steps/s", "env_only": out["env_only"],
+            "with_learn_torch_update": out["with_learn_torch_update"], "learn_ms": out["learn_ms"],
             "envs_per_gpu": n, "replay_capacity": capacity, "batch": batch, "learn_iters_per_step": 1,
             "config": "SecondOrderIntegration (DDPG copy) DDPG, replay in HBM, nets [4,256,256,2] "
-                      "relu / Q [6,256,256,1] relu; DDPG update in torch on the device, one HIP graph per update"}
+                      "relu / Q [6,256,256,1] relu; native DDPG update (rlp_ddpg_update, f32 MFMA) "
+                      "in one HIP graph per learn(); with_learn_torch_update = the same loop with "
+                      "the reference's torch update"}
 
 
 def ugvoa_leg(rank, n=16384, steps=30, warmup=3, seed=5):
@@ -371,26 +387,41 @@ def ugvoa_sac_leg(rank, n=16384, steps=20, warmup=3, batch=4096, capacity=1 << 2
     S, Ad = env.state_dim, env.action_dim
     lo, hi = env.action_range[:, 0], env.action_range[:, 1]
     msg = {'state_dim': S, 'action_dim': Ad, 'action_range': env.action_range, 'name': env.name}
-    agent = SAC(msg, 0.99, 0.005, capacity, batch, SACActor(S, Ad, lo, hi, std_min=0.05, std_scale=1.),
-                SACCritic(S, Ad), SACCritic(S, Ad), 1e-4, 1e-4, 1e-4, True, device="cuda", seed=seed,
-                graph=True)
-    loop = VecSAC(env, agent)
     out = {}
-    for learn in (False, True):
-        for _ in range(warmup):
-            loop.step(learn=learn)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            loop.step(learn=learn)
-        torch.cuda.synchronize()
-        out["with_learn" if learn else "env_only"] = n * steps / (time.perf_counter() - t0)
+    for native in (True, False):
+        torch.manual_seed(seed)
+        agent = SAC(msg, 0.99, 0.005, capacity, batch,
+                    SACActor(S, Ad, lo, hi, std_min=0.05, std_scale=1.), SACCritic(S, Ad),
+                    SACCritic(S, Ad), 1e-4, 1e-4, 1e-4, True, device="cuda", seed=seed, graph=True,
+                    native=native)
+        assert (agent._native is not None) == native
+        loop = VecSAC(env, agent)
+        for learn in ((False, True) if native else (True,)):
+            for _ in range(warmup):
+                loop.step(learn=learn)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                loop.step(learn=learn)
+            torch.cuda.synchronize()
+            key = "env_only" if not learn else "with_learn" if native else "with_learn_torch_update"
+            out[key] = n * steps / (time.perf_counter() - t0)
+        if native:   # the update alone: one captured learn()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(steps):
+                agent.learn()
+            ev[1].record()
+            torch.cuda.synchronize()
+            out["learn_ms"] = ev[0].elapsed_time(ev[1]) / steps
     return {"value": out["with_learn"], "unit": "env-steps/s", "env_only": out["env_only"],
+            "with_learn_torch_update": out["with_learn_torch_update"], "learn_ms": out["learn_ms"],
             "envs_per_gpu": n, "replay_capacity": capacity, "batch": batch,
             "learn_iters_per_step": 1,
             "config": "UGVForwardObstacleAvoidance (env-dir copy, 37-beam lidar, 10 circles) SAC, "
-                      "replay in HBM, demo nets; SAC update in torch on the device, one HIP graph "
-                      "per update (sample, gather, update, soft update, actor refresh)"}
+                      "replay in HBM, demo nets; native SAC update (rlp_sac_update, f32 MFMA) in one "
+                      "HIP graph per learn() (sample, gather, update, actor refresh); "
+                      "with_learn_torch_update = the same loop with the reference's torch update"}
 
 
 def hbm_legs(seg, n_env=1 << 22, iters=10, warmup=2):

@@ -486,11 +486,94 @@ int rlp_replay_gather(const rlp_replay *rb, const int64_t *index, int64_t batch,
                       float *a, float *r, float *s_next, float *end, rlp_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
+/* Native DDPG update (algorithm/actor_critic/DDPG.py:72-109 learn() body, :111-118 soft update)
+ * for the drivers' ReLU nets (demonstration/DDPG/DDPG-4-{SecondOrderIntegration,...}/train.py:26-100): actor
+ * S -> ... -> A with relu hidden layers and a = gain * tanh(z) + off; critic cat(s, a) -> ... -> 1
+ * with relu hidden layers. Replaces the torch autograd + torch.optim.Adam sequence of one learn()
+ * iteration on a sampled batch (s, a, r, s', end = 1 - done):
+ *   y = r + gamma * end * Q'(s', mu'(s'));  critic: MSE(y, Q(s, a)) -> grad -> Adam;
+ *   actor: -mean(Q(s, mu(s))) with the UPDATED critic -> grad -> Adam;  soft target updates.
+ * Every product runs on v_mfma_f32_16x16x4_f32 (f32 products and accumulation); weight gradients
+ * are reduced in a fixed order (run-to-run identical). A net is a flat fp32 parameter buffer in
+ * module.parameters() order: layer l's W [out][in] at offset[l], its b [out] right after it;
+ * parameters the chain does not use (e.g. the drivers' critic.action_value) may sit in between —
+ * their gradient entries must be zero (Adam then leaves them unchanged, as torch skips them) and
+ * the soft update still blends them, as torch does. */
+#define RLP_DENSE_MAX_LAYERS 4
+typedef struct rlp_dense_net {
+    int32_t n_layers;                          /* Linear layers in the forward chain */
+    int32_t dims[RLP_DENSE_MAX_LAYERS + 1];    /* dims[0] inputs ... dims[n_layers] outputs */
+    int64_t offset[RLP_DENSE_MAX_LAYERS];      /* of layer l's W in params (floats) */
+    int64_t n_params;                          /* length of params (and of its grad / Adam state) */
+    float *params;
+} rlp_dense_net;
+typedef struct rlp_ddpg_nets {
+    rlp_dense_net actor, target_actor, critic, target_critic;  /* targets: the nets' layouts */
+    float *actor_grad, *actor_m, *actor_v;      /* [actor.n_params]: gradient, Adam exp_avg(_sq) */
+    float *critic_grad, *critic_m, *critic_v;   /* [critic.n_params] */
+    int32_t *steps;            /* device [2]: Adam step counts (actor, critic), +1 per update */
+    const float *gain, *off;   /* device [A]: the actor's output affine */
+} rlp_ddpg_nets;
+typedef struct rlp_ddpg_cfg {
+    int32_t batch;
+    float gamma, actor_tau, critic_tau;
+    rlp_adam_cfg actor_adam, critic_adam;   /* lr, beta1, beta2, eps (max_norm and step unused) */
+} rlp_ddpg_cfg;
+/* device workspace (floats) of rlp_ddpg_update for this net shape and batch */
+int64_t rlp_ddpg_workspace(const rlp_ddpg_nets *nets, int batch);
+/* one update; s [B][S], a [B][A], r [B], s_next [B][S], end [B] device fp32 (the replay gather's
+ * output); losses (device [2]) = critic MSE, actor loss. Graph-capturable (all state on the
+ * device). */
+int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const float *s,
+                    const float *a, const float *r, const float *s_next, const float *end,
+                    float *work, float *losses, rlp_stream_t stream);
+
+/* Native SAC update (algorithm/actor_critic/Soft_Actor_Critic.py:70-129 learn() body) for the
+ * SAC drivers' nets (utils/classes.py SACActor / SACCritic): actor trunk S -> ... -> H with relu
+ * after every layer, heads mean [A][H] and log_std [A][H] (log_std clamped to [ls_lo, ls_hi],
+ * std = exp, a = tanh(mean + std * eps) * gain + off, log_pi with the tanh-squash correction);
+ * twin critic chains cat(s, a) -> ... -> 1 (relu hidden layers) in ONE parameter buffer, and the
+ * target critic in the same layout. One iteration on a sampled batch (s, a, r, s', dw):
+ *   target_Q = r + gamma * (1 - dw) * (min(Q1', Q2')(s', a') - alpha * log_pi')  (a' ~ pi(s'))
+ *   actor: mean(alpha * log_pi - min(Q1, Q2)(s, a~pi(s))) -> grad -> Adam
+ *   critic: MSE(Q1(s, a), target_Q) + MSE(Q2(s, a), target_Q) -> grad -> Adam
+ *   alpha (adaptive): -mean(exp(log_alpha) * (log_pi + target_entropy)) -> grad -> Adam
+ *   soft update target = tau * critic + (1 - tau) * target.
+ * Noise: `noise` [2][B][A] (eps for s', then for s: the reference's two rsample calls in order) or
+ * NULL for Philox draws keyed by (seed, *counter, row), *counter advanced per update on the device
+ * (graph-capturable). */
+typedef struct rlp_sac_nets {
+    rlp_dense_net actor;       /* the trunk layers (relu after each); params = the actor's buffer */
+    int64_t mean_offset;       /* mean head W [A][H] (b follows) in actor.params */
+    int64_t log_std_offset;    /* log_std head W [A][H] (b follows) */
+    int32_t action_dim;
+    rlp_dense_net q1, q2;      /* critic chains; params = the critic's buffer (n_params = its length) */
+    float *target_critic;      /* target critic params, the critic's layout */
+    float *actor_grad, *actor_m, *actor_v;     /* [actor.n_params] */
+    float *critic_grad, *critic_m, *critic_v;  /* [q1.n_params] */
+    float *log_alpha, *alpha_grad, *alpha_m, *alpha_v;   /* device [1] each */
+    int32_t *steps;            /* device [3]: Adam step counts (actor, critic, alpha), +1 per update */
+    uint64_t *counter;         /* device [1]: Philox counter of the noise, +1 per update */
+    const float *gain, *off, *ls_lo, *ls_hi;   /* device [A] */
+} rlp_sac_nets;
+typedef struct rlp_sac_cfg {
+    int32_t batch, adaptive_alpha;
+    float gamma, tau, target_entropy, alpha;   /* alpha: the fixed temperature when not adaptive */
+    uint64_t seed;
+    rlp_adam_cfg actor_adam, critic_adam, alpha_adam;
+} rlp_sac_cfg;
+int64_t rlp_sac_workspace(const rlp_sac_nets *nets, int batch);
+/* losses (device [2]) = critic loss, actor loss */
+int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float *s, const float *a,
+                   const float *r, const float *s_next, const float *dw, const float *noise,
+                   float *work, float *losses, rlp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------ */
 const char *rlp_last_error_string(void);
 int rlp_abi_version(void);
 /* sizeof of the ABI structs as compiled into the library (0 cartpole, 1 angleonly, 2 soi, 3 ugv,
  * 4 uav, 5 mlp_desc, 6 rollout_cfg, 7 rollout_bufs, 8 ppo2_loss_cfg, 9 adam_cfg, 10 replay,
- * 11 ugv_oa): FFI bindings
+ * 11 ugv_oa, 12 dense_net, 13 ddpg_nets, 14 ddpg_cfg, 15 sac_nets, 16 sac_cfg): FFI bindings
  * verify their mirrors with it. */
 int64_t rlp_struct_size(int which);
 /* Tuning knob of rlp_rollout: 16-env sub-blocks per wave: 0 = auto (default; the f16x3 path

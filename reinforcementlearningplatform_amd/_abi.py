@@ -166,6 +166,45 @@ class Replay(C.Structure):
                 ("end", C.c_void_p), ("capacity", C.c_int64), ("S", C.c_int32), ("A", C.c_int32)]
 
 
+RLP_DENSE_MAX_LAYERS = 4
+
+
+class DenseNet(C.Structure):
+    """rlp_dense_net: a Linear chain inside a flat fp32 parameter buffer (module.parameters()
+    order; layer l's W [out][in] at offset[l], b right after it)."""
+    _fields_ = [("n_layers", C.c_int32), ("dims", C.c_int32 * (RLP_DENSE_MAX_LAYERS + 1)),
+                ("offset", C.c_int64 * RLP_DENSE_MAX_LAYERS), ("n_params", C.c_int64),
+                ("params", C.c_void_p)]
+
+
+class DDPGNets(C.Structure):
+    _fields_ = [("actor", DenseNet), ("target_actor", DenseNet), ("critic", DenseNet),
+                ("target_critic", DenseNet)] + [(n, C.c_void_p) for n in (
+        "actor_grad", "actor_m", "actor_v", "critic_grad", "critic_m", "critic_v", "steps", "gain",
+        "off")]
+
+
+class DDPGCfg(C.Structure):
+    _fields_ = [("batch", C.c_int32), ("gamma", C.c_float), ("actor_tau", C.c_float),
+                ("critic_tau", C.c_float), ("actor_adam", AdamCfg), ("critic_adam", AdamCfg)]
+
+
+class SACNets(C.Structure):
+    _fields_ = [("actor", DenseNet), ("mean_offset", C.c_int64), ("log_std_offset", C.c_int64),
+                ("action_dim", C.c_int32), ("q1", DenseNet), ("q2", DenseNet)] + [
+        (n, C.c_void_p) for n in (
+            "target_critic", "actor_grad", "actor_m", "actor_v", "critic_grad", "critic_m",
+            "critic_v", "log_alpha", "alpha_grad", "alpha_m", "alpha_v", "steps", "counter", "gain",
+            "off", "ls_lo", "ls_hi")]
+
+
+class SACCfg(C.Structure):
+    _fields_ = [("batch", C.c_int32), ("adaptive_alpha", C.c_int32), ("gamma", C.c_float),
+                ("tau", C.c_float), ("target_entropy", C.c_float), ("alpha", C.c_float),
+                ("seed", C.c_uint64), ("actor_adam", AdamCfg), ("critic_adam", AdamCfg),
+                ("alpha_adam", AdamCfg)]
+
+
 PARAM_TYPES = {
     RLP_ENV_CARTPOLE: CartPoleParams,
     RLP_ENV_CARTPOLE_ANGLEONLY: AngleOnlyParams,
@@ -382,7 +421,10 @@ def check_struct_sizes():
             "uav": C.sizeof(UAVHoverParams), "mlp_desc": C.sizeof(MLPDesc),
             "rollout_cfg": C.sizeof(RolloutCfg), "rollout_bufs": C.sizeof(RolloutBufs),
             "ppo2_loss_cfg": C.sizeof(PPO2LossCfg), "adam_cfg": C.sizeof(AdamCfg),
-            "replay": C.sizeof(Replay), "ugv_oa": C.sizeof(UGVOAParams)}
+            "replay": C.sizeof(Replay), "ugv_oa": C.sizeof(UGVOAParams),
+            "dense_net": C.sizeof(DenseNet), "ddpg_nets": C.sizeof(DDPGNets),
+            "ddpg_cfg": C.sizeof(DDPGCfg), "sac_nets": C.sizeof(SACNets),
+            "sac_cfg": C.sizeof(SACCfg)}
 
 
 _ = math  # keep import for callers doing deg arithmetic

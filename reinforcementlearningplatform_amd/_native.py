@@ -69,6 +69,10 @@ def _declare(lib):
         "rlp_replay_workspace_bytes": (i64, [i64]),
         "rlp_replay_sample_reward_top": (i32, [vp, i64, i64, u64, u64, vp, vp, vp, i64, vp]),
         "rlp_replay_gather": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, vp]),
+        "rlp_ddpg_workspace": (i64, [vp, i32]),
+        "rlp_ddpg_update": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "rlp_sac_workspace": (i64, [vp, i32]),
+        "rlp_sac_update": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

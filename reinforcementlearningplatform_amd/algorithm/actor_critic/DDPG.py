@@ -7,8 +7,11 @@ Same constructor, attributes and methods as the reference. Differences that matt
     forward then runs through librlp (GPUNet; the drivers' ReLU nets go through the generic MLP
     kernel) and the N(0, sigma^2) exploration noise + clip through rlp_policy_sample (Philox),
     returning a device tensor;
-  * the update itself is the reference's torch code on the device (critic MSE to the target
-    r + gamma * (1 - done) * Q'(s', mu'(s')), actor loss -Q(s, mu(s)), soft target updates);
+  * the update (critic MSE to the target r + gamma * (1 - done) * Q'(s', mu'(s')), actor loss
+    -Q(s, mu(s)), Adam, soft target updates) runs natively — ONE rlp_ddpg_update call
+    (native_ddpg.py) — for the drivers' relu nets (native="auto" checks the nets' forward on a
+    probe batch; native=True requires it; native=False or any other net: the reference's torch
+    code on the device);
   * graph=True captures one whole learn iteration (uniform batch indices from torch's generator,
     the replay gather, the update with the nets' Adam switched to capturable, the soft updates
     and the GPU actor's weight refresh) in a HIP graph and replays it.
@@ -25,7 +28,7 @@ class DDPG:
     def __init__(self, env_msg: dict, gamma: float = 0.99, actor_soft_update: float = 1e-2,
                  critic_soft_update: float = 1e-2, memory_capacity: int = 5000,
                  batch_size: int = 512, actor=None, target_actor=None, critic=None,
-                 target_critic=None, device=None, seed=None, graph=False):
+                 target_critic=None, device=None, seed=None, graph=False, native="auto"):
         if actor is None or target_actor is None or critic is None or target_critic is None:
             raise ValueError("DDPG: pass the driver's actor/target_actor/critic/target_critic "
                              "(the reference's default-argument placeholder nets have no forward)")
@@ -54,6 +57,11 @@ class DDPG:
         self.noise_counter = 0
         self.graph = bool(graph)
         self._graph = None
+        self._native = None
+        if native:
+            from .native_ddpg import DDPGNativeUpdate
+            if native != "auto" or DDPGNativeUpdate.fits(self):
+                self._native = DDPGNativeUpdate(self)
 
     def choose_action_random(self, n=None):
         if n is None:
@@ -130,7 +138,8 @@ class DDPG:
             self._gmax.fill_(float(min(mem.mem_counter, mem.mem_size)))
             self._graph = _capture(self._graph_body, self.device,
                                    [self.actor, self.target_actor, self.critic, self.target_critic],
-                                   [self.critic.optimizer, self.actor.optimizer])
+                                   [self.critic.optimizer, self.actor.optimizer],
+                                   self._native.state_tensors() if self._native else ())
         for _ in range(iters):
             self._gmax.fill_(float(min(mem.mem_counter, mem.mem_size)))
             self._graph.replay()
@@ -144,6 +153,8 @@ class DDPG:
         return out
 
     def _update_core(self, s, a, r, s_, done):
+        if self._native is not None:
+            return self._native.update(s, a, r, s_, done)
         with torch.no_grad():
             Q_ = self.target_critic(s_, self.target_actor(s_))
             target_Q = r.unsqueeze(1) + self.gamma * done.unsqueeze(1) * Q_

@@ -6,9 +6,12 @@ Same constructor, attributes and methods as the reference. What a driver sees di
   * choose_action also takes a batch of states ([n][S], one row per env of a VecEnv): the actor
     trunk then runs through rlp_mlp_forward and the squashed-Gaussian sample + clamp through
     rlp_sac_sample (Philox noise), returning a device tensor [n][A];
-  * learn() is the reference's torch code on the device: twin-Q target with the entropy term,
-    actor loss alpha * log_pi - min(Q1, Q2), critic MSE on both heads, adaptive temperature,
-    soft target update;
+  * learn() (twin-Q target with the entropy term, actor loss alpha * log_pi - min(Q1, Q2), critic
+    MSE on both heads, adaptive temperature, soft target update) runs natively — ONE
+    rlp_sac_update call (native_sac.py) — for the drivers' SACActor / SACCritic structure
+    (native="auto" checks it on a probe batch; native=True requires it; otherwise, or with
+    native=False, the reference's torch code on the device). The native path draws its Gaussian
+    noise from Philox (seed, device counter, row) instead of torch's generator;
   * graph=True captures one whole learn iteration — uniform batch indices (torch Philox), the
     replay gather, the update with capturable Adam, the soft update and the GPU actor's weight
     refresh — in a HIP graph (torch.cuda.CUDAGraph) and replays it: one launch instead of
@@ -78,7 +81,7 @@ class SAC:
                  memory_capacity: int = 5000, batch_size: int = 256, actor=None, critic=None,
                  target_critic=None, a_lr: float = 3e-4, c_lr: float = 1e-4,
                  alpha_lr: float = 3e-4, adaptive_alpha: bool = True, device=None, seed=None,
-                 graph: bool = False):
+                 graph: bool = False, native="auto"):
         if actor is None or critic is None or target_critic is None:
             raise ValueError("SAC: pass actor / critic / target_critic (utils.classes.SACActor, "
                              "SACCritic or the driver's own)")
@@ -114,6 +117,11 @@ class SAC:
         self.gpu_actor = None
         self.noise_counter = 0
         self._graph = None
+        self._native = None
+        if native:
+            from .native_sac import SACNativeUpdate
+            if native != "auto" or SACNativeUpdate.fits(self):
+                self._native = SACNativeUpdate(self)
 
     def choose_action(self, s, deterministic=False):
         batched = (torch.is_tensor(s) and s.dim() == 2) or (not torch.is_tensor(s) and np.ndim(s) == 2)
@@ -179,9 +187,10 @@ class SAC:
             self._gmax.fill_(float(min(mem.mem_counter, mem.mem_size)))
             opts = [self.actor_optimizer, self.critic_optimizer] + (
                 [self.alpha_optimizer] if self.adaptive_alpha else [])
+            extra = ([self.log_alpha] if self.adaptive_alpha else []) + (
+                self._native.state_tensors() if self._native else [])
             self._graph = _capture(self._graph_body, self.device,
-                                   [self.actor, self.critic, self.target_critic], opts,
-                                   [self.log_alpha] if self.adaptive_alpha else [])
+                                   [self.actor, self.critic, self.target_critic], opts, extra)
         for _ in range(iters):
             self._gmax.fill_(float(min(mem.mem_counter, mem.mem_size)))
             self._graph.replay()
@@ -189,9 +198,16 @@ class SAC:
             self.alpha = self.log_alpha.detach().exp()
         return self._gloss[0], self._gloss[1]
 
-    def update(self, batch_s, batch_a, batch_r, batch_s_, batch_dw):
-        """One SAC update (:73-124); batch_dw is the buffer's fifth column, as in the reference."""
-        out = self._update_core(batch_s, batch_a, batch_r, batch_s_, batch_dw, self.alpha)
+    def update(self, batch_s, batch_a, batch_r, batch_s_, batch_dw, noise=None):
+        """One SAC update (:73-124); batch_dw is the buffer's fifth column, as in the reference.
+        noise ([2][B][A]: eps of the s' draw, then of the s draw) replays a recorded tape on the
+        native path."""
+        if self._native is not None:
+            out = self._native.update(batch_s, batch_a, batch_r, batch_s_, batch_dw, noise)
+        else:
+            if noise is not None:
+                raise ValueError("SAC.update: noise is a native-path argument")
+            out = self._update_core(batch_s, batch_a, batch_r, batch_s_, batch_dw, self.alpha)
         if self.adaptive_alpha:
             self.alpha = self.log_alpha.exp()
         if self.gpu_actor is not None:
@@ -199,6 +215,8 @@ class SAC:
         return out
 
     def _update_core(self, batch_s, batch_a, batch_r, batch_s_, batch_dw, alpha):
+        if self._native is not None:
+            return self._native.update(batch_s, batch_a, batch_r, batch_s_, batch_dw)
         batch_r = batch_r.reshape(-1, 1)
         batch_dw = batch_dw.reshape(-1, 1)
         with torch.no_grad():

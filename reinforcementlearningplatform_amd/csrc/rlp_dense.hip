@@ -1,0 +1,920 @@
+// rlp_dense.hip — batched dense layers and the native DDPG update (algorithm/actor_critic/
+// DDPG.py:72-109 learn, :111-118 update_network_parameters) for the drivers' ReLU nets
+// (demonstration/DDPG/DDPG-4-*/train.py:26-100: actor S -> 256 -> 256 -> A, relu, relu,
+// gain * tanh + off; critic cat(s, a) -> 256 -> 256 -> 1, relu, relu, identity).
+//
+// Every matrix product of the update — the forward passes (x W^T + b), the backward data passes
+// (dY W, masked by the activation's derivative) and the weight gradients (dY^T X, the bias as an
+// extra all-ones column of X) — runs through ONE tiled GEMM on v_mfma_f32_16x16x4_f32 (exact f32
+// products, f32 accumulation, like torch's f32 GEMMs): 64 x 64 output tiles per 4-wave block,
+// each wave a 32 x 32 quarter (2 x 2 MFMA tiles), the reduction staged through LDS 16 deep. The
+// operands are strided views (row / column strides, an optional column split for torch.cat and
+// an all-ones column), so transposes and concatenations are never materialised. Weight
+// gradients split the batch over gridDim.z into partials summed in fixed order by a second
+// kernel (deterministic, no atomics). Fused epilogues: + bias, relu, gain * tanh + off (keeping
+// tanh for the backward), relu' mask, (. * gain) * (1 - t^2). Adam (torch.optim.Adam's
+// non-capturable arithmetic, step count read from device memory so a captured HIP graph can be
+// replayed) and the soft target update are elementwise kernels.
+#include "rlp_common.hpp"
+
+namespace rlp {
+
+// element (i, j) of a rows x cols matrix: columns (rows, with split_rows) [0, split) from p0, the
+// rest from p1 (indexed from the split); column `ones` reads 1 (the bias column of a weight
+// gradient); out of range reads 0
+struct Opnd {
+    const float *p0, *p1;
+    int64_t rs0, cs0, rs1, cs1;
+    int rows, cols, split, ones, split_rows;
+};
+
+__device__ __forceinline__ float opnd_ld(const Opnd &o, int i, int j) {
+    if (i >= o.rows || j >= o.cols) return 0.f;
+    if (j == o.ones) return 1.f;
+    if (o.split_rows)
+        return i < o.split ? o.p0[i * o.rs0 + j * o.cs0] : o.p1[(i - o.split) * o.rs1 + j * o.cs1];
+    return j < o.split ? o.p0[i * o.rs0 + j * o.cs0] : o.p1[i * o.rs1 + (j - o.split) * o.cs1];
+}
+
+enum : int { kEpiNone = 0, kEpiRelu, kEpiTanhAff, kEpiReluBack, kEpiTanhAffBack, kEpiPartial };
+
+struct Epi {
+    float *y;
+    int64_t ldy;
+    const float *bias;                 // + bias[n] (forward kinds)
+    const float *gain, *off;           // kEpiTanhAff: y = gain * tanh(z) + off; kEpiTanhAffBack: gain
+    float *aux;                        // kEpiTanhAff: tanh(z) stored here (ldaux)
+    int64_t ldaux;
+    const float *mask;                 // kEpiReluBack: y = acc where mask > 0 (relu output), else 0
+    int64_t ldm;                       // kEpiTanhAffBack: mask holds t = tanh(z)
+    int kind, M, N;
+};
+
+constexpr int kDT = 64;            // output tile (M and N)
+constexpr int kDRc = 256;          // reduction rows one block stages at once
+constexpr int kDLd = kDRc + 4;     // LDS row: operand row-major along r, 4 banks apart per row
+
+// C[M x N] = sum_r A(m, r) B(r, n) over r in [z * rchunk, min(R, (z + 1) * rchunk)), rchunk <= 256.
+// The block stages its whole reduction slice of both operands at once (all global loads in
+// flight together, 128 registers per lane, then one barrier): these GEMMs have <= 256-deep
+// slices, so one memory latency per launch instead of one per 16-deep tile. LDS holds A as
+// [m][r] and B as [n][r] (row stride 260 floats: the 16 x 4 fragment reads hit 64 distinct banks);
+// the reduction order is permuted so that each lane's operands for four consecutive MFMA steps
+// are contiguous (one 16-byte LDS read): step s, lane group g reads r = g * Q + s.
+__global__ void __launch_bounds__(256) dense_gemm_kernel(Opnd A, Opnd B, int R, int rchunk, Epi e) {
+    extern __shared__ float lds[];
+    float *As = lds, *Bs = lds + kDT * kDLd;
+    const int m0 = blockIdx.y * kDT, n0 = blockIdx.x * kDT;
+    const int r_lo = blockIdx.z * rchunk, rc = min(R, r_lo + rchunk) - r_lo;
+    const int Q = (rc + 15) / 16 * 4;  // MFMA steps (multiple of 4); rows g * Q + s, s < Q
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+    const bool a_rfast = A.cs0 == 1;  // A(m, r) contiguous along r: lanes walk r
+    const bool b_rfast = B.rs0 == 1;  // B(r, n) contiguous along r
+    const int span = 4 * Q;           // staged rows (zero beyond rc)
+    float ra[64], rb[64];
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+        const int x = t + 256 * q;
+        const int am = a_rfast ? x >> 8 : x & 63, ar = a_rfast ? x & 255 : x >> 6;
+        ra[q] = ar < rc ? opnd_ld(A, m0 + am, r_lo + ar) : 0.f;
+        const int bn = b_rfast ? x >> 8 : x & 63, br = b_rfast ? x & 255 : x >> 6;
+        rb[q] = br < rc ? opnd_ld(B, r_lo + br, n0 + bn) : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+        const int x = t + 256 * q;
+        const int am = a_rfast ? x >> 8 : x & 63, ar = a_rfast ? x & 255 : x >> 6;
+        if (ar < span) As[am * kDLd + ar] = ra[q];
+        const int bn = b_rfast ? x >> 8 : x & 63, br = b_rfast ? x & 255 : x >> 6;
+        if (br < span) Bs[bn * kDLd + br] = rb[q];
+    }
+    __syncthreads();
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int g = l >> 4, c = l & 15;
+    for (int s = 0; s < Q; s += 4) {
+        floatx4 af[2], bf[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = *(const floatx4 *)&As[(wm + 16 * i + c) * kDLd + g * Q + s];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bf[j] = *(const floatx4 *)&Bs[(wn + 16 * j + c) * kDLd + g * Q + s];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][u], bf[j][u], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int m = m0 + wm + 16 * i + 4 * (l >> 4) + q, n = n0 + wn + 16 * j + (l & 15);
+                if (m >= e.M || n >= e.N) continue;
+                float v = acc[i][j][q];
+                switch (e.kind) {
+                case kEpiPartial:
+                    e.y[(size_t)blockIdx.z * e.M * e.N + (size_t)m * e.N + n] = v;
+                    continue;
+                case kEpiReluBack:
+                    v = e.mask[m * e.ldm + n] > 0.f ? v : 0.f;
+                    break;
+                case kEpiTanhAffBack: {  // torch: grad_t = da * gain; grad_z = grad_t * (1 - t*t)
+                    const float tt = e.mask[m * e.ldm + n];
+                    v = (v * e.gain[n]) * (1.f - tt * tt);
+                    break;
+                }
+                default:
+                    if (e.bias) v = v + e.bias[n];
+                    if (e.kind == kEpiRelu) {
+                        v = fmaxf(v, 0.f);
+                    } else if (e.kind == kEpiTanhAff) {
+                        const float tt = tanhf(v);
+                        e.aux[m * e.ldaux + n] = tt;
+                        v = e.gain[n] * tt + e.off[n];
+                    }
+                }
+                e.y[m * e.ldy + n] = v;
+            }
+}
+
+// grad[m][n] = sum over the splits of the partials, in split order; column N-1 is the bias
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float *__restrict__ part, int splits,
+                                                           int M, int N, float *__restrict__ gW,
+                                                           float *__restrict__ gb) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= M * N) return;
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += part[(size_t)z * M * N + i];
+    const int m = i / N, n = i - m * N;
+    if (n < N - 1)
+        gW[(size_t)m * (N - 1) + n] = s;
+    else
+        gb[m] = s;
+}
+
+// TD target + critic MSE gradient (DDPG.py:83-89): y = r + (gamma * end) * Q'; dQ = d/dQ of
+// mse_loss(y, Q) = -((2 / B) * (y - Q)); loss = mean((y - Q)^2). One block; also advances the
+// two Adam step counters (actor, critic) the update's optimizer steps read.
+__global__ void __launch_bounds__(1024) ddpg_td_kernel(const float *__restrict__ r,
+                                                       const float *__restrict__ end,
+                                                       const float *__restrict__ q_next,
+                                                       const float *__restrict__ q, int B, float gamma,
+                                                       float *__restrict__ dq, float *loss,
+                                                       int32_t *steps) {
+    __shared__ double red[16];
+    double s = 0;
+    const float two_b = 2.f / (float)B;
+    for (int i = threadIdx.x; i < B; i += 1024) {
+        const float y = r[i] + (gamma * end[i]) * q_next[i];
+        const float d = y - q[i];
+        dq[i] = -(two_b * d);
+        s += (double)d * (double)d;
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double tot = 0;
+        for (int k = 0; k < 16; ++k) tot += red[k];
+        loss[0] = (float)(tot / B);
+        steps[0] += 1;
+        steps[1] += 1;
+    }
+}
+
+// actor loss -mean(Q(s, mu(s))) and its gradient dQ = -(1 / B) per row (DDPG.py:97)
+__global__ void __launch_bounds__(1024) ddpg_actor_loss_kernel(const float *__restrict__ q, int B,
+                                                               float *__restrict__ dq, float *loss) {
+    __shared__ double red[16];
+    double s = 0;
+    const float g = -(1.f / (float)B);
+    for (int i = threadIdx.x; i < B; i += 1024) {
+        s += (double)q[i];
+        dq[i] = g;
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double tot = 0;
+        for (int k = 0; k < 16; ++k) tot += red[k];
+        loss[1] = (float)(-(tot / B));
+    }
+}
+
+// torch.optim.Adam step (non-capturable arithmetic) with the step count read from the device
+__global__ void __launch_bounds__(256) adam_dev_kernel(float *__restrict__ p, const float *__restrict__ g,
+                                                       float *__restrict__ m, float *__restrict__ v,
+                                                       int64_t n, float lr, float beta1, float beta2,
+                                                       float eps, const int32_t *step) {
+    const float st = (float)*step;
+    const float bc1 = 1.f - powf(beta1, st);
+    const float bc2 = 1.f - powf(beta2, st);
+    const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const float gi = g[i];
+        float mi = m[i];
+        mi = mi + (1.f - beta1) * (gi - mi);
+        const float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        p[i] = p[i] + (-step_size) * (mi / denom);
+    }
+}
+
+// target = target * keep + param * take (DDPG.py:116-118: tp * (1 - tau) + p * tau, fp32)
+__global__ void __launch_bounds__(256) soft_update_kernel(float *__restrict__ tp, const float *__restrict__ p,
+                                                          int64_t n, float keep, float take) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        tp[i] = tp[i] * keep + p[i] * take;
+}
+
+// ---- SAC (algorithm/actor_critic/Soft_Actor_Critic.py:70-129) --------------------------------
+__device__ __forceinline__ float softplus_t(float x) {  // torch softplus(beta=1, threshold=20)
+    return x > 20.f ? x : log1pf(expf(x));
+}
+
+// the actor's squashed-Gaussian head on z = [mean | log_std] pre-bias (utils/classes.py SACActor
+// forward): ls = clamp(z + b, lo, hi), std = exp(ls), u = mean + eps * std (Normal.rsample),
+// log_pi = sum log_prob(u) - sum 2 (log 2 - u - softplus(-2u)), a = tanh(u) * gain + off. TRAIN
+// keeps u, std, eps, tanh(u) and the clamp's pass mask for the backward.
+template <int A, bool TRAIN>
+__global__ void __launch_bounds__(256) sac_head_kernel(const float *__restrict__ z, int B,
+                                                       const float *bm, const float *bl,
+                                                       const float *ls_lo, const float *ls_hi,
+                                                       const float *gain, const float *off,
+                                                       const float *noise, uint64_t seed,
+                                                       const uint64_t *counter, uint64_t draw,
+                                                       float *__restrict__ act, float *__restrict__ lp,
+                                                       float *__restrict__ save) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= B) return;
+    float eps[A];
+    if (noise) {
+#pragma unroll
+        for (int j = 0; j < A; ++j) eps[j] = noise[(size_t)i * A + j];
+    } else {
+        philox_normal_f32<A>(seed, *counter, (uint64_t)i + (draw << 40), eps);
+    }
+    const float kHalfLog2Pi = 0.918938533204672742f, kLog2 = 0.693147180559945309f;
+    float l = 0.f, corr = 0.f;
+#pragma unroll
+    for (int j = 0; j < A; ++j) {
+        const float mean = z[(size_t)i * 2 * A + j] + bm[j];
+        const float x = z[(size_t)i * 2 * A + A + j] + bl[j];
+        const float ls = fminf(fmaxf(x, ls_lo[j]), ls_hi[j]);
+        const float sd = expf(ls);
+        const float u = mean + eps[j] * sd;
+        const float d = u - mean;
+        const float lpj = -(d * d) / (2.f * (sd * sd)) - logf(sd) - kHalfLog2Pi;
+        l = j == 0 ? lpj : l + lpj;
+        const float cj = 2.f * ((kLog2 - u) - softplus_t(-2.f * u));
+        corr = j == 0 ? cj : corr + cj;
+        const float t = tanhf(u);
+        act[(size_t)i * A + j] = t * gain[j] + off[j];
+        if (TRAIN) {  // [6][B][A]: u, std, eps, tanh(u), clamp pass, u - mean
+            const size_t o = (size_t)i * A + j, st = (size_t)B * A;
+            save[o] = u;
+            save[st + o] = sd;
+            save[2 * st + o] = eps[j];
+            save[3 * st + o] = t;
+            save[4 * st + o] = (x >= ls_lo[j] && x <= ls_hi[j]) ? 1.f : 0.f;
+            save[5 * st + o] = d;
+        }
+    }
+    lp[i] = l - corr;
+}
+
+__device__ __forceinline__ float sac_alpha(const float *log_alpha, int adaptive, float alpha) {
+    return adaptive ? expf(*log_alpha) : alpha;
+}
+
+// target_Q = r + (gamma * (1 - dw)) * (min(Q1', Q2') - alpha * log_pi')  (:75-78)
+__global__ void __launch_bounds__(256) sac_target_kernel(const float *__restrict__ r,
+                                                         const float *__restrict__ dw,
+                                                         const float *__restrict__ q1,
+                                                         const float *__restrict__ q2,
+                                                         const float *__restrict__ lp, int B,
+                                                         float gamma, const float *log_alpha,
+                                                         int adaptive, float alpha_fixed,
+                                                         float *__restrict__ tq) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= B) return;
+    const float al = sac_alpha(log_alpha, adaptive, alpha_fixed);
+    const float m = fminf(q1[i], q2[i]) - al * lp[i];
+    tq[i] = r[i] + (gamma * (1.f - dw[i])) * m;
+}
+
+// actor loss mean(alpha * log_pi - min(Q1, Q2)) and d/dQ1, d/dQ2 (torch.minimum's backward: ties
+// split the gradient in half); the temperature's gradient exp(log_alpha) * sum(-(log_pi + H)/B);
+// advances the Adam step counts and the noise counter (both samples of this update are drawn).
+__global__ void __launch_bounds__(1024) sac_actor_loss_kernel(const float *__restrict__ q1,
+                                                              const float *__restrict__ q2,
+                                                              const float *__restrict__ lp, int B,
+                                                              const float *log_alpha, int adaptive,
+                                                              float alpha_fixed, float target_entropy,
+                                                              float *__restrict__ g1,
+                                                              float *__restrict__ g2, float *losses,
+                                                              float *alpha_grad, int32_t *steps,
+                                                              uint64_t *counter) {
+    __shared__ double red[2][16];
+    const float al = sac_alpha(log_alpha, adaptive, alpha_fixed);
+    const float g = -(1.f / (float)B), h = g / 2.f;
+    double sl = 0, sa = 0;
+    for (int i = threadIdx.x; i < B; i += 1024) {
+        const float a = q1[i], b = q2[i];
+        g1[i] = a == b ? h : a < b ? g : 0.f;
+        g2[i] = a == b ? h : a > b ? g : 0.f;
+        sl += (double)(al * lp[i] - fminf(a, b));
+        sa += (double)(g * (lp[i] + target_entropy));
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sl += __shfl_xor(sl, o);
+        sa += __shfl_xor(sa, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = sl;
+        red[1][threadIdx.x >> 6] = sa;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double tl = 0, ta = 0;
+        for (int k = 0; k < 16; ++k) {
+            tl += red[0][k];
+            ta += red[1][k];
+        }
+        losses[1] = (float)(tl / B);
+        if (adaptive) alpha_grad[0] = (float)ta * expf(*log_alpha);
+        steps[0] += 1;
+        steps[1] += 1;
+        steps[2] += 1;
+        counter[0] += 1;
+    }
+}
+
+// d(actor loss)/d[mean | log_std pre-clamp] per row from da (both critic chains' input
+// gradients at a) and the log-prob terms (G = alpha / B per row's log_pi)
+template <int A>
+__global__ void __launch_bounds__(256) sac_head_back_kernel(const float *__restrict__ save,
+                                                            const float *__restrict__ da1,
+                                                            const float *__restrict__ da2, int B,
+                                                            const float *gain, const float *log_alpha,
+                                                            int adaptive, float alpha_fixed,
+                                                            float *__restrict__ gz) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= B) return;
+    const float G = (1.f / (float)B) * sac_alpha(log_alpha, adaptive, alpha_fixed);
+    const size_t st = (size_t)B * A;
+#pragma unroll
+    for (int j = 0; j < A; ++j) {
+        const size_t o = (size_t)i * A + j;
+        const float u = save[o], sd = save[st + o], eps = save[2 * st + o], t = save[3 * st + o];
+        const float pass = save[4 * st + o];
+        const float da = da1[o] + da2[o];
+        const float d = save[5 * st + o];  // u - mean
+        const float var = sd * sd;
+        const float sig = 1.f / (1.f + expf(2.f * u));  // sigmoid(-2u) (softplus' at -2u)
+        const float dsq = -2.f * u > 20.f ? 1.f : sig;
+        const float gu = (da * gain[j]) * (1.f - t * t) + G * (-(d / var) + (2.f - 4.f * dsq));
+        const float gmean = gu + G * (d / var);
+        const float gsd = gu * eps + G * ((d * d) / (var * sd) - 1.f / sd);
+        gz[(size_t)i * 2 * A + j] = gmean;
+        gz[(size_t)i * 2 * A + A + j] = pass != 0.f ? gsd * sd : 0.f;
+    }
+}
+
+// critic loss MSE(Q1, y) + MSE(Q2, y) and its gradients (2 / B) (Qk - y)  (:110-113)
+__global__ void __launch_bounds__(1024) sac_critic_loss_kernel(const float *__restrict__ q1,
+                                                               const float *__restrict__ q2,
+                                                               const float *__restrict__ tq, int B,
+                                                               float *__restrict__ g1,
+                                                               float *__restrict__ g2, float *losses) {
+    __shared__ double red[2][16];
+    const float nb = 2.f / (float)B;
+    double s1 = 0, s2 = 0;
+    for (int i = threadIdx.x; i < B; i += 1024) {
+        const float d1 = q1[i] - tq[i], d2 = q2[i] - tq[i];
+        g1[i] = nb * d1;
+        g2[i] = nb * d2;
+        s1 += (double)d1 * d1;
+        s2 += (double)d2 * d2;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = s1;
+        red[1][threadIdx.x >> 6] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t1 = 0, t2 = 0;
+        for (int k = 0; k < 16; ++k) {
+            t1 += red[0][k];
+            t2 += red[1][k];
+        }
+        losses[0] = (float)(t1 / B) + (float)(t2 / B);
+    }
+}
+
+// target = tau * p + (1 - tau) * target (:126-127)
+__global__ void __launch_bounds__(256) soft_update_sac_kernel(float *__restrict__ tp,
+                                                              const float *__restrict__ p, int64_t n,
+                                                              float tau, float keep) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        tp[i] = tau * p[i] + keep * tp[i];
+}
+
+// ---- host side ------------------------------------------------------------------------------
+
+inline Opnd mat(const float *p, int rows, int cols, int64_t ld) {  // row-major rows x cols
+    return Opnd{p, p, ld, 1, ld, 1, rows, cols, cols, -1, 0};
+}
+inline Opnd cat2(const float *p0, int c0, int64_t ld0, const float *p1, int c1, int64_t ld1, int rows) {
+    return Opnd{p0, p1, ld0, 1, ld1, 1, rows, c0 + c1, c0, -1, 0};
+}
+inline Opnd transposed(const float *p, int rows, int cols, int64_t ld) {  // (i, j) = p[j * ld + i]
+    return Opnd{p, p, 1, ld, 1, ld, rows, cols, cols, -1, 0};
+}
+
+constexpr size_t kDenseLds = 2 * kDT * kDLd * sizeof(float);  // 133 120 B
+
+// splits >= ceil(R / 256) slices of the reduction (each <= 256 rows); returns the slice count
+int gemm(const Opnd &A, const Opnd &B, int M, int N, int R, int splits, const Epi &e, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void *)dense_gemm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kDenseLds);
+        attr = true;
+    }
+    const int need = (R + kDRc - 1) / kDRc;
+    const int sp = splits > need ? splits : need;
+    const int rchunk = ((R + sp - 1) / sp + 15) / 16 * 16;
+    const int z = (R + rchunk - 1) / rchunk;
+    dim3 grid((N + kDT - 1) / kDT, (M + kDT - 1) / kDT, z > 0 ? z : 1);
+    dense_gemm_kernel<<<grid, 256, kDenseLds, s>>>(A, B, R, rchunk, e);
+    return z > 0 ? z : 1;
+}
+
+struct Layer {
+    const float *W, *b;
+    int in, out;
+};
+inline Layer layer_of(const rlp_dense_net &n, const float *params, int l) {
+    const float *W = params + n.offset[l];
+    return Layer{W, W + (int64_t)n.dims[l] * n.dims[l + 1], n.dims[l], n.dims[l + 1]};
+}
+
+// y = act(x W^T + b); x is [B][in] (or the concatenation of two row-major sources)
+void dense_fwd(const Opnd &x, const Layer &L, int B, int act, float *y, const float *gain,
+               const float *off, float *aux, hipStream_t s) {
+    Epi e{};
+    e.y = y; e.ldy = L.out; e.bias = L.b; e.kind = act; e.M = B; e.N = L.out;
+    e.gain = gain; e.off = off; e.aux = aux; e.ldaux = L.out;
+    // B(r, n) = W[n][r]: column stride in, row stride 1
+    gemm(x, Opnd{L.W, L.W, 1, L.in, 1, L.in, L.in, L.out, L.out, -1, 0}, B, L.out, L.in, 1, e, s);
+}
+
+// dX[:, c0:c0+nc] = (dY W[:, c0:c0+nc]) with the epilogue (relu' mask or tanh-affine backward)
+void dense_bwd_data(const float *dy, const Layer &L, int B, int c0, int nc, int kind,
+                    const float *mask, int64_t ldm, const float *gain, float *dx, hipStream_t s) {
+    Epi e{};
+    e.y = dx; e.ldy = nc; e.kind = kind; e.M = B; e.N = nc; e.mask = mask; e.ldm = ldm; e.gain = gain;
+    gemm(mat(dy, B, L.out, L.out), mat(L.W + c0, L.out, nc, L.in), B, nc, L.out, 1, e, s);
+}
+
+// gW = dY^T X, gb = column sums of dY: split over the batch, partials reduced in fixed order
+void dense_wgrad(const float *dy, const Opnd &x, const Layer &L, int B, float *part, int splits,
+                 float *gW, float *gb, hipStream_t s, int64_t ldy = -1) {
+    Epi e{};
+    e.y = part; e.kind = kEpiPartial; e.M = L.out; e.N = L.in + 1;
+    Opnd xo = x;
+    xo.cols = L.in + 1;
+    xo.ones = L.in;
+    const int z = gemm(transposed(dy, L.out, B, ldy < 0 ? L.out : ldy), xo, L.out, L.in + 1, B, splits,
+                       e, s);
+    const int tot = L.out * (L.in + 1);
+    wgrad_reduce_kernel<<<(tot + 255) / 256, 256, 0, s>>>(part, z, L.out, L.in + 1, gW, gb);
+}
+
+void adam_dev(float *p, const float *g, float *m, float *v, int64_t n, const rlp_adam_cfg &c,
+              const int32_t *step, hipStream_t s) {
+    const int64_t b = (n + 255) / 256;
+    adam_dev_kernel<<<(int)(b < 2048 ? b : 2048), 256, 0, s>>>(p, g, m, v, n, c.lr, c.beta1, c.beta2,
+                                                              c.eps, step);
+}
+
+void soft_update(float *tp, const float *p, int64_t n, float tau, hipStream_t s) {
+    const int64_t b = (n + 255) / 256;
+    soft_update_kernel<<<(int)(b < 2048 ? b : 2048), 256, 0, s>>>(tp, p, n, (float)(1.0 - (double)tau),
+                                                                 tau);
+}
+
+bool net_ok(const rlp_dense_net &n) {
+    if (n.n_layers < 1 || n.n_layers > RLP_DENSE_MAX_LAYERS || !n.params) return false;
+    for (int l = 0; l <= n.n_layers; ++l)
+        if (n.dims[l] < 1 || n.dims[l] > 4096) return false;
+    for (int l = 0; l < n.n_layers; ++l) {
+        const int64_t sz = (int64_t)n.dims[l] * n.dims[l + 1] + n.dims[l + 1];
+        if (n.offset[l] < 0 || n.offset[l] + sz > n.n_params) return false;
+    }
+    return true;
+}
+bool same_shape(const rlp_dense_net &a, const rlp_dense_net &b) {
+    if (a.n_layers != b.n_layers || a.n_params != b.n_params) return false;
+    for (int l = 0; l <= a.n_layers; ++l)
+        if (a.dims[l] != b.dims[l]) return false;
+    for (int l = 0; l < a.n_layers; ++l)
+        if (a.offset[l] != b.offset[l]) return false;
+    return true;
+}
+
+int max_width(const rlp_dense_net &n) {
+    int w = 0;
+    for (int l = 0; l <= n.n_layers; ++l) w = w > n.dims[l] ? w : n.dims[l];
+    return w;
+}
+int64_t hidden_sum(const rlp_dense_net &n) {
+    int64_t s = 0;
+    for (int l = 1; l <= n.n_layers; ++l) s += n.dims[l];
+    return s;
+}
+constexpr int kWgradRows = 256;  // batch rows per weight-gradient split
+
+struct DdpgWs {  // float offsets into the workspace
+    int64_t ta, tc, c, pa, pc, ta_t, pa_t, g0, g1, dq, part, total;
+};
+DdpgWs ddpg_ws(const rlp_ddpg_nets &n, int B) {
+    DdpgWs w{};
+    int64_t o = 0;
+    auto take = [&](int64_t k) { int64_t r = o; o += (k + 63) / 64 * 64; return r; };
+    w.ta = take(B * hidden_sum(n.actor));
+    w.ta_t = take((int64_t)B * n.actor.dims[n.actor.n_layers]);
+    w.tc = take(B * hidden_sum(n.critic));
+    w.c = take(B * hidden_sum(n.critic));
+    w.pa = take(B * hidden_sum(n.actor));
+    w.pa_t = take((int64_t)B * n.actor.dims[n.actor.n_layers]);
+    w.pc = take(B * hidden_sum(n.critic));
+    const int mw = max_width(n.actor) > max_width(n.critic) ? max_width(n.actor) : max_width(n.critic);
+    w.g0 = take((int64_t)B * mw);
+    w.g1 = take((int64_t)B * mw);
+    w.dq = take((int64_t)B * n.actor.dims[n.actor.n_layers]);
+    const int splits = (B + kWgradRows - 1) / kWgradRows;
+    w.part = take((int64_t)splits * mw * (mw + 1));
+    w.total = o;
+    return w;
+}
+
+// forward of a whole net: layer l's output at act + off_l (row-major [B][dims[l+1]]); the first
+// layer reads x (a strided / concatenated view)
+void net_fwd(const rlp_dense_net &n, const float *params, const Opnd &x, int B, float *act,
+             bool actor_head, const float *gain, const float *off, float *tanh_out, hipStream_t s) {
+    int64_t o = 0;
+    Opnd in = x;
+    for (int l = 0; l < n.n_layers; ++l) {
+        const Layer L = layer_of(n, params, l);
+        const bool last = l == n.n_layers - 1;
+        const int kind = !last ? kEpiRelu : actor_head ? kEpiTanhAff : kEpiNone;
+        dense_fwd(in, L, B, kind, act + o, gain, off, tanh_out, s);
+        in = mat(act + o, B, L.out, L.out);
+        o += (int64_t)B * L.out;
+    }
+}
+const float *layer_out(const rlp_dense_net &n, const float *act, int B, int l) {
+    int64_t o = 0;
+    for (int k = 0; k < l; ++k) o += (int64_t)B * n.dims[k + 1];
+    return act + o;
+}
+
+// backward of a relu net from dY of its last layer (in g[0]); weight gradients into grad (same
+// layout as params) when grad != NULL; optionally the input gradient of columns [c0, c0 + nc)
+// with the tanh-affine backward of the layer that produced them (the actor's head) into dx
+void net_bwd(const rlp_dense_net &n, const float *params, float *grad, const Opnd &x, int B,
+             const float *act, float *g0, float *g1, float *part, int splits, int c0, int nc,
+             const float *t_in, const float *gain, float *dx, hipStream_t s) {
+    float *dy = g0, *dn = g1;
+    for (int l = n.n_layers - 1; l >= 0; --l) {
+        const Layer L = layer_of(n, params, l);
+        const Opnd xin = l == 0 ? x : mat(layer_out(n, act, B, l - 1), B, L.in, L.in);
+        if (grad)
+            dense_wgrad(dy, xin, L, B, part, splits, grad + n.offset[l],
+                        grad + n.offset[l] + (int64_t)L.in * L.out, s);
+        if (l > 0) {
+            const float *h = layer_out(n, act, B, l - 1);
+            dense_bwd_data(dy, L, B, 0, L.in, kEpiReluBack, h, L.in, nullptr, dn, s);
+            float *tmp = dy; dy = dn; dn = tmp;
+        } else if (dx) {
+            dense_bwd_data(dy, L, B, c0, nc, t_in ? kEpiTanhAffBack : kEpiNone, t_in, nc, gain, dx, s);
+        }
+    }
+}
+
+}  // namespace rlp
+
+using namespace rlp;
+
+extern "C" {
+
+int64_t rlp_ddpg_workspace(const rlp_ddpg_nets *nets, int batch) {
+    if (!nets || batch < 1 || !net_ok(nets->actor) || !net_ok(nets->critic)) return RLP_EINVAL;
+    return ddpg_ws(*nets, batch).total;
+}
+
+int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const float *s, const float *a,
+                    const float *r, const float *s_next, const float *end, float *work,
+                    float *losses, rlp_stream_t stream) {
+    RLP_REQUIRE(nets && cfg && s && a && r && s_next && end && work && losses,
+                "rlp_ddpg_update: null argument");
+    const rlp_ddpg_nets &n = *nets;
+    RLP_REQUIRE(net_ok(n.actor) && net_ok(n.critic), "rlp_ddpg_update: bad net description");
+    RLP_REQUIRE(same_shape(n.actor, n.target_actor) && same_shape(n.critic, n.target_critic),
+                "rlp_ddpg_update: target nets must have their nets' layout");
+    RLP_REQUIRE(n.target_actor.params && n.target_critic.params && n.actor_grad && n.actor_m &&
+                    n.actor_v && n.critic_grad && n.critic_m && n.critic_v && n.steps && n.gain && n.off,
+                "rlp_ddpg_update: null buffer in the net state");
+    const int S = n.actor.dims[0], A = n.actor.dims[n.actor.n_layers];
+    RLP_REQUIRE(n.critic.dims[0] == S + A && n.critic.dims[n.critic.n_layers] == 1,
+                "rlp_ddpg_update: critic must map cat(s, a) (%d inputs) to 1 output, has %d -> %d",
+                S + A, n.critic.dims[0], n.critic.dims[n.critic.n_layers]);
+    const int B = cfg->batch;
+    RLP_REQUIRE(B >= 1, "rlp_ddpg_update: batch=%d", B);
+    hipStream_t st = as_stream(stream);
+    const DdpgWs w = ddpg_ws(n, B);
+    float *ta = work + w.ta, *tc = work + w.tc, *c = work + w.c, *pa = work + w.pa, *pc = work + w.pc;
+    float *ta_t = work + w.ta_t, *pa_t = work + w.pa_t, *g0 = work + w.g0, *g1 = work + w.g1;
+    float *dq = work + w.dq, *part = work + w.part;
+    const int splits = (B + kWgradRows - 1) / kWgradRows;
+    const int La = n.actor.n_layers, Lc = n.critic.n_layers;
+
+    // target: Q' = target_critic(s', target_actor(s'))
+    net_fwd(n.target_actor, n.target_actor.params, mat(s_next, B, S, S), B, ta, true, n.gain, n.off,
+            ta_t, st);
+    const float *a_next = layer_out(n.target_actor, ta, B, La - 1);
+    net_fwd(n.target_critic, n.target_critic.params, cat2(s_next, S, S, a_next, A, A, B), B, tc, false,
+            nullptr, nullptr, nullptr, st);
+    // critic: Q(s, a), TD target, MSE gradient, backward, Adam
+    const Opnd sa = cat2(s, S, S, a, A, A, B);
+    net_fwd(n.critic, n.critic.params, sa, B, c, false, nullptr, nullptr, nullptr, st);
+    ddpg_td_kernel<<<1, 1024, 0, st>>>(r, end, layer_out(n.target_critic, tc, B, Lc - 1),
+                                       layer_out(n.critic, c, B, Lc - 1), B, cfg->gamma, g0, losses,
+                                       n.steps);
+    net_bwd(n.critic, n.critic.params, n.critic_grad, sa, B, c, g0, g1, part, splits, 0, 0, nullptr,
+            nullptr, nullptr, st);
+    adam_dev(n.critic.params, n.critic_grad, n.critic_m, n.critic_v, n.critic.n_params, cfg->critic_adam,
+             n.steps + 1, st);
+    // actor: a = mu(s), Q(s, a) with the updated critic (no critic gradients), -mean(Q) backward
+    net_fwd(n.actor, n.actor.params, mat(s, B, S, S), B, pa, true, n.gain, n.off, pa_t, st);
+    const float *a_pi = layer_out(n.actor, pa, B, La - 1);
+    const Opnd sp = cat2(s, S, S, a_pi, A, A, B);
+    net_fwd(n.critic, n.critic.params, sp, B, pc, false, nullptr, nullptr, nullptr, st);
+    ddpg_actor_loss_kernel<<<1, 1024, 0, st>>>(layer_out(n.critic, pc, B, Lc - 1), B, g0, losses);
+    net_bwd(n.critic, n.critic.params, nullptr, sp, B, pc, g0, g1, part, splits, S, A, pa_t, n.gain, dq,
+            st);
+    // dq now holds dL/dz of the actor's head ([B][A]); back through the actor
+    const Opnd s_in = mat(s, B, S, S);
+    {
+        float *dy = dq, *d0 = g0, *d1 = g1;
+        for (int l = La - 1; l >= 0; --l) {
+            const Layer L = layer_of(n.actor, n.actor.params, l);
+            const Opnd xin = l == 0 ? s_in : mat(layer_out(n.actor, pa, B, l - 1), B, L.in, L.in);
+            dense_wgrad(dy, xin, L, B, part, splits, n.actor_grad + n.actor.offset[l],
+                        n.actor_grad + n.actor.offset[l] + (int64_t)L.in * L.out, st);
+            if (l > 0) {
+                dense_bwd_data(dy, L, B, 0, L.in, kEpiReluBack, layer_out(n.actor, pa, B, l - 1), L.in,
+                               nullptr, d0, st);
+                dy = d0;
+                float *tmp = d0; d0 = d1; d1 = tmp;
+            }
+        }
+    }
+    adam_dev(n.actor.params, n.actor_grad, n.actor_m, n.actor_v, n.actor.n_params, cfg->actor_adam,
+             n.steps, st);
+    // soft target updates (critic first, DDPG.py:113-118)
+    soft_update(n.target_critic.params, n.critic.params, n.critic.n_params, cfg->critic_tau, st);
+    soft_update(n.target_actor.params, n.actor.params, n.actor.n_params, cfg->actor_tau, st);
+    RLP_CHECK_LAUNCH("rlp_ddpg_update");
+    return RLP_OK;
+}
+
+}  // extern "C"
+
+// ---- SAC host side ----------------------------------------------------------------------------
+namespace rlp {
+
+struct SacWs {
+    int64_t tn_act, tn_z, tn_a, tn_lp, tq1, tq2, ta, tz, ta_a, ta_lp, save, p1, p2, c1, c2, y, g1,
+        g2, da1, da2, gz, d0, d1, part, total;
+};
+SacWs sac_ws(const rlp_sac_nets &n, int B) {
+    SacWs w{};
+    int64_t o = 0;
+    auto take = [&](int64_t k) { int64_t r = o; o += (k + 63) / 64 * 64; return r; };
+    const int A = n.action_dim;
+    const int64_t ha = B * hidden_sum(n.actor), hq1 = B * hidden_sum(n.q1), hq2 = B * hidden_sum(n.q2);
+    w.tn_act = take(ha); w.tn_z = take((int64_t)B * 2 * A); w.tn_a = take((int64_t)B * A); w.tn_lp = take(B);
+    w.tq1 = take(hq1); w.tq2 = take(hq2);
+    w.ta = take(ha); w.tz = take((int64_t)B * 2 * A); w.ta_a = take((int64_t)B * A); w.ta_lp = take(B);
+    w.save = take((int64_t)6 * B * A);
+    w.p1 = take(hq1); w.p2 = take(hq2); w.c1 = take(hq1); w.c2 = take(hq2);
+    w.y = take(B); w.g1 = take(B); w.g2 = take(B);
+    w.da1 = take((int64_t)B * A); w.da2 = take((int64_t)B * A); w.gz = take((int64_t)B * 2 * A);
+    int mw = max_width(n.actor);
+    mw = max_width(n.q1) > mw ? max_width(n.q1) : mw;
+    mw = max_width(n.q2) > mw ? max_width(n.q2) : mw;
+    mw = 2 * A > mw ? 2 * A : mw;
+    w.d0 = take((int64_t)B * mw); w.d1 = take((int64_t)B * mw);
+    const int splits = (B + kWgradRows - 1) / kWgradRows;
+    w.part = take((int64_t)splits * mw * (mw + 1));
+    w.total = o;
+    return w;
+}
+
+// trunk (relu after every layer) then the head GEMM z = h [Wm; Wl]^T (biases added by the head kernel)
+void sac_actor_fwd(const rlp_sac_nets &n, const float *x, int B, float *act, float *z, hipStream_t s) {
+    Opnd in = mat(x, B, n.actor.dims[0], n.actor.dims[0]);
+    int64_t o = 0;
+    for (int l = 0; l < n.actor.n_layers; ++l) {
+        const Layer L = layer_of(n.actor, n.actor.params, l);
+        dense_fwd(in, L, B, kEpiRelu, act + o, nullptr, nullptr, nullptr, s);
+        in = mat(act + o, B, L.out, L.out);
+        o += (int64_t)B * L.out;
+    }
+    const int H = n.actor.dims[n.actor.n_layers], A = n.action_dim;
+    Epi e{};
+    e.y = z; e.ldy = 2 * A; e.kind = kEpiNone; e.M = B; e.N = 2 * A;
+    const float *Wm = n.actor.params + n.mean_offset, *Wl = n.actor.params + n.log_std_offset;
+    gemm(in, Opnd{Wm, Wl, 1, H, 1, H, H, 2 * A, A, -1, 0}, B, 2 * A, H, 1, e, s);
+}
+
+int sac_head(const rlp_sac_nets &n, const rlp_sac_cfg &c, const float *z, int B, const float *noise,
+             uint64_t draw, float *act, float *lp, float *save, hipStream_t s) {
+    const float *P = n.actor.params;
+    const int H = n.actor.dims[n.actor.n_layers], A = n.action_dim;
+    const float *bm = P + n.mean_offset + (int64_t)A * H, *bl = P + n.log_std_offset + (int64_t)A * H;
+    const int g = (B + 255) / 256;
+#define RLP_SAC_HEAD(AA)                                                                                  \
+    if (save)                                                                                             \
+        sac_head_kernel<AA, true><<<g, 256, 0, s>>>(z, B, bm, bl, n.ls_lo, n.ls_hi, n.gain, n.off, noise, \
+                                                    c.seed, n.counter, draw, act, lp, save);              \
+    else                                                                                                  \
+        sac_head_kernel<AA, false><<<g, 256, 0, s>>>(z, B, bm, bl, n.ls_lo, n.ls_hi, n.gain, n.off,       \
+                                                     noise, c.seed, n.counter, draw, act, lp, nullptr);
+    switch (A) {
+    case 1: RLP_SAC_HEAD(1) break;
+    case 2: RLP_SAC_HEAD(2) break;
+    case 3: RLP_SAC_HEAD(3) break;
+    case 4: RLP_SAC_HEAD(4) break;
+    default: return RLP_EINVAL;
+    }
+#undef RLP_SAC_HEAD
+    return RLP_OK;
+}
+
+bool chain_ok(const rlp_dense_net &q, int S, int A) {
+    return net_ok(q) && q.dims[0] == S + A && q.dims[q.n_layers] == 1;
+}
+
+}  // namespace rlp
+
+extern "C" {
+
+int64_t rlp_sac_workspace(const rlp_sac_nets *nets, int batch) {
+    if (!nets || batch < 1 || !net_ok(nets->actor) || !net_ok(nets->q1) || !net_ok(nets->q2) ||
+        nets->action_dim < 1 || nets->action_dim > 4)
+        return RLP_EINVAL;
+    return sac_ws(*nets, batch).total;
+}
+
+int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float *s, const float *a,
+                   const float *r, const float *s_next, const float *dw, const float *noise,
+                   float *work, float *losses, rlp_stream_t stream) {
+    RLP_REQUIRE(nets && cfg && s && a && r && s_next && dw && work && losses,
+                "rlp_sac_update: null argument");
+    const rlp_sac_nets &n = *nets;
+    const int A = n.action_dim, S = n.actor.dims[0], H = n.actor.dims[n.actor.n_layers];
+    RLP_REQUIRE(A >= 1 && A <= 4, "rlp_sac_update: action_dim=%d (1..4)", A);
+    RLP_REQUIRE(net_ok(n.actor) && chain_ok(n.q1, S, A) && chain_ok(n.q2, S, A) &&
+                    n.q1.params == n.q2.params && n.q1.n_params == n.q2.n_params,
+                "rlp_sac_update: bad net description (two critic chains cat(s, a) -> 1 in one buffer)");
+    RLP_REQUIRE(n.mean_offset >= 0 && n.log_std_offset >= 0 &&
+                    n.mean_offset + (int64_t)A * (H + 1) <= n.actor.n_params &&
+                    n.log_std_offset + (int64_t)A * (H + 1) <= n.actor.n_params,
+                "rlp_sac_update: head offsets outside the actor's parameters");
+    RLP_REQUIRE(n.target_critic && n.actor_grad && n.actor_m && n.actor_v && n.critic_grad &&
+                    n.critic_m && n.critic_v && n.log_alpha && n.alpha_grad && n.alpha_m &&
+                    n.alpha_v && n.steps && n.counter && n.gain && n.off && n.ls_lo && n.ls_hi,
+                "rlp_sac_update: null buffer in the net state");
+    const int B = cfg->batch;
+    RLP_REQUIRE(B >= 1, "rlp_sac_update: batch=%d", B);
+    hipStream_t st = as_stream(stream);
+    const SacWs w = sac_ws(n, B);
+    auto W = [&](int64_t off) { return work + off; };
+    const int splits = (B + kWgradRows - 1) / kWgradRows;
+    const int Lq1 = n.q1.n_layers, Lq2 = n.q2.n_layers;
+    const int g = (B + 255) / 256;
+    const int ad = cfg->adaptive_alpha;
+
+    // target: a' ~ pi(s'), Q1', Q2' of the target critic, target_Q
+    sac_actor_fwd(n, s_next, B, W(w.tn_act), W(w.tn_z), st);
+    int rc = sac_head(n, *cfg, W(w.tn_z), B, noise, 0, W(w.tn_a), W(w.tn_lp), nullptr, st);
+    if (rc != RLP_OK) return fail(rc, "rlp_sac_update: action_dim %d", A);
+    const Opnd tx = cat2(s_next, S, S, W(w.tn_a), A, A, B);
+    net_fwd(n.q1, n.target_critic, tx, B, W(w.tq1), false, nullptr, nullptr, nullptr, st);
+    net_fwd(n.q2, n.target_critic, tx, B, W(w.tq2), false, nullptr, nullptr, nullptr, st);
+    sac_target_kernel<<<g, 256, 0, st>>>(r, dw, layer_out(n.q1, W(w.tq1), B, Lq1 - 1),
+                                         layer_out(n.q2, W(w.tq2), B, Lq2 - 1), W(w.tn_lp), B,
+                                         cfg->gamma, n.log_alpha, ad, cfg->alpha, W(w.y));
+    // actor: a ~ pi(s), Q1, Q2 of the critic, loss, backward through the critic into a
+    sac_actor_fwd(n, s, B, W(w.ta), W(w.tz), st);
+    sac_head(n, *cfg, W(w.tz), B, noise ? noise + (size_t)B * A : nullptr, 1, W(w.ta_a), W(w.ta_lp),
+             W(w.save), st);
+    const Opnd px = cat2(s, S, S, W(w.ta_a), A, A, B);
+    net_fwd(n.q1, n.q1.params, px, B, W(w.p1), false, nullptr, nullptr, nullptr, st);
+    net_fwd(n.q2, n.q2.params, px, B, W(w.p2), false, nullptr, nullptr, nullptr, st);
+    sac_actor_loss_kernel<<<1, 1024, 0, st>>>(layer_out(n.q1, W(w.p1), B, Lq1 - 1),
+                                              layer_out(n.q2, W(w.p2), B, Lq2 - 1), W(w.ta_lp), B,
+                                              n.log_alpha, ad, cfg->alpha, cfg->target_entropy,
+                                              W(w.g1), W(w.g2), losses, n.alpha_grad, n.steps,
+                                              n.counter);
+    // (net_bwd's ping-pong buffers start with dY in the first one)
+    hipMemcpyAsync(W(w.d0), W(w.g1), sizeof(float) * B, hipMemcpyDeviceToDevice, st);
+    net_bwd(n.q1, n.q1.params, nullptr, px, B, W(w.p1), W(w.d0), W(w.d1), W(w.part), splits, S, A,
+            nullptr, nullptr, W(w.da1), st);
+    hipMemcpyAsync(W(w.d0), W(w.g2), sizeof(float) * B, hipMemcpyDeviceToDevice, st);
+    net_bwd(n.q2, n.q2.params, nullptr, px, B, W(w.p2), W(w.d0), W(w.d1), W(w.part), splits, S, A,
+            nullptr, nullptr, W(w.da2), st);
+    switch (A) {
+    case 1: sac_head_back_kernel<1><<<g, 256, 0, st>>>(W(w.save), W(w.da1), W(w.da2), B, n.gain, n.log_alpha, ad, cfg->alpha, W(w.gz)); break;
+    case 2: sac_head_back_kernel<2><<<g, 256, 0, st>>>(W(w.save), W(w.da1), W(w.da2), B, n.gain, n.log_alpha, ad, cfg->alpha, W(w.gz)); break;
+    case 3: sac_head_back_kernel<3><<<g, 256, 0, st>>>(W(w.save), W(w.da1), W(w.da2), B, n.gain, n.log_alpha, ad, cfg->alpha, W(w.gz)); break;
+    default: sac_head_back_kernel<4><<<g, 256, 0, st>>>(W(w.save), W(w.da1), W(w.da2), B, n.gain, n.log_alpha, ad, cfg->alpha, W(w.gz)); break;
+    }
+    // actor backward: heads' weight gradients, then the trunk
+    {
+        const int Lt = n.actor.n_layers;
+        float *P = n.actor.params, *G = n.actor_grad;
+        const float *h_last = layer_out(n.actor, W(w.ta), B, Lt - 1);
+        const Opnd hx = mat(h_last, B, H, H);
+        const Layer Lm{P + n.mean_offset, P + n.mean_offset + (int64_t)A * H, H, A};
+        const Layer Ll{P + n.log_std_offset, P + n.log_std_offset + (int64_t)A * H, H, A};
+        dense_wgrad(W(w.gz), hx, Lm, B, W(w.part), splits, G + n.mean_offset,
+                    G + n.mean_offset + (int64_t)A * H, st, 2 * A);
+        dense_wgrad(W(w.gz) + A, hx, Ll, B, W(w.part), splits, G + n.log_std_offset,
+                    G + n.log_std_offset + (int64_t)A * H, st, 2 * A);
+        // dh = (gz [Wm; Wl]) * relu'(h)
+        Epi e{};
+        e.y = W(w.d0); e.ldy = H; e.kind = kEpiReluBack; e.M = B; e.N = H; e.mask = h_last; e.ldm = H;
+        gemm(mat(W(w.gz), B, 2 * A, 2 * A), Opnd{Lm.W, Ll.W, H, 1, H, 1, 2 * A, H, A, -1, 1}, B, H,
+             2 * A, 1, e, st);
+        float *dy = W(w.d0), *dn = W(w.d1);
+        for (int l = Lt - 1; l >= 0; --l) {
+            const Layer L = layer_of(n.actor, P, l);
+            const Opnd xin = l == 0 ? mat(s, B, S, S) : mat(layer_out(n.actor, W(w.ta), B, l - 1), B, L.in, L.in);
+            dense_wgrad(dy, xin, L, B, W(w.part), splits, G + n.actor.offset[l],
+                        G + n.actor.offset[l] + (int64_t)L.in * L.out, st);
+            if (l > 0) {
+                dense_bwd_data(dy, L, B, 0, L.in, kEpiReluBack, layer_out(n.actor, W(w.ta), B, l - 1),
+                               L.in, nullptr, dn, st);
+                float *tmp = dy; dy = dn; dn = tmp;
+            }
+        }
+    }
+    // critic: Q1, Q2 on the batch's actions, MSE to target_Q, backward into the critic's gradient
+    const Opnd bx = cat2(s, S, S, a, A, A, B);
+    net_fwd(n.q1, n.q1.params, bx, B, W(w.c1), false, nullptr, nullptr, nullptr, st);
+    net_fwd(n.q2, n.q2.params, bx, B, W(w.c2), false, nullptr, nullptr, nullptr, st);
+    sac_critic_loss_kernel<<<1, 1024, 0, st>>>(layer_out(n.q1, W(w.c1), B, Lq1 - 1),
+                                               layer_out(n.q2, W(w.c2), B, Lq2 - 1), W(w.y), B,
+                                               W(w.g1), W(w.g2), losses);
+    hipMemcpyAsync(W(w.d0), W(w.g1), sizeof(float) * B, hipMemcpyDeviceToDevice, st);
+    net_bwd(n.q1, n.q1.params, n.critic_grad, bx, B, W(w.c1), W(w.d0), W(w.d1), W(w.part), splits, 0,
+            0, nullptr, nullptr, nullptr, st);
+    hipMemcpyAsync(W(w.d0), W(w.g2), sizeof(float) * B, hipMemcpyDeviceToDevice, st);
+    net_bwd(n.q2, n.q2.params, n.critic_grad, bx, B, W(w.c2), W(w.d0), W(w.d1), W(w.part), splits, 0,
+            0, nullptr, nullptr, nullptr, st);
+    // optimizer steps (actor, critic, temperature), then the soft target update
+    adam_dev(n.actor.params, n.actor_grad, n.actor_m, n.actor_v, n.actor.n_params, cfg->actor_adam,
+             n.steps, st);
+    adam_dev(n.q1.params, n.critic_grad, n.critic_m, n.critic_v, n.q1.n_params, cfg->critic_adam,
+             n.steps + 1, st);
+    if (ad) adam_dev(n.log_alpha, n.alpha_grad, n.alpha_m, n.alpha_v, 1, cfg->alpha_adam, n.steps + 2, st);
+    {
+        const int64_t nn = n.q1.n_params, b = (nn + 255) / 256;
+        soft_update_sac_kernel<<<(int)(b < 2048 ? b : 2048), 256, 0, st>>>(
+            n.target_critic, n.q1.params, nn, cfg->tau, (float)(1.0 - (double)cfg->tau));
+    }
+    RLP_CHECK_LAUNCH("rlp_sac_update");
+    return RLP_OK;
+}
+
+}  // extern "C"

@@ -164,6 +164,11 @@ int64_t rlp_struct_size(int which) {
     case 9: return sizeof(rlp_adam_cfg);
     case 10: return sizeof(rlp_replay);
     case 11: return sizeof(rlp_ugv_oa_params);
+    case 12: return sizeof(rlp_dense_net);
+    case 13: return sizeof(rlp_ddpg_nets);
+    case 14: return sizeof(rlp_ddpg_cfg);
+    case 15: return sizeof(rlp_sac_nets);
+    case 16: return sizeof(rlp_sac_cfg);
     }
     return -1;
 }

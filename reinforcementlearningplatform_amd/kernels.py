@@ -357,3 +357,48 @@ def replay_gather(rb, index, out=None):
     check(lib().rlp_replay_gather(C.byref(rb), ptr(index_), B, ptr(s), ptr(a), ptr(r),
                                   ptr(s2), ptr(e), stream_ptr()), "rlp_replay_gather")
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Native DDPG update (include/rlp.h: rlp_ddpg_workspace, rlp_ddpg_update)
+# ---------------------------------------------------------------------------------------------
+def dense_net(flat, dims, offsets):
+    """rlp_dense_net over a flat fp32 parameter tensor: dims [in, h..., out], offsets of each
+    layer's W (floats; its b follows it)."""
+    n = _abi.DenseNet()
+    n.n_layers = len(dims) - 1
+    if not 1 <= n.n_layers <= _abi.RLP_DENSE_MAX_LAYERS or len(offsets) != n.n_layers:
+        raise ValueError(f"dense_net: {len(dims) - 1} layers (1..{_abi.RLP_DENSE_MAX_LAYERS})")
+    for i, d in enumerate(dims):
+        n.dims[i] = int(d)
+    for i, o in enumerate(offsets):
+        n.offset[i] = int(o)
+    n.n_params, n.params = flat.numel(), flat.data_ptr()
+    return n
+
+
+def ddpg_workspace(nets, batch, device=None):
+    nf = lib().rlp_ddpg_workspace(C.byref(nets), int(batch))
+    check(nf if nf < 0 else 0, "rlp_ddpg_workspace")
+    return torch.empty(int(nf), dtype=torch.float32, device=_dev(device))
+
+
+def ddpg_update(nets, cfg, s, a, r, s_next, end, work, losses):
+    """One DDPG learn() iteration on a sampled batch (all device fp32, contiguous); losses [2]."""
+    check(lib().rlp_ddpg_update(C.byref(nets), C.byref(cfg), ptr(s), ptr(a), ptr(r), ptr(s_next),
+                                ptr(end), ptr(work), ptr(losses), stream_ptr()), "rlp_ddpg_update")
+    return losses
+
+
+def sac_workspace(nets, batch, device=None):
+    nf = lib().rlp_sac_workspace(C.byref(nets), int(batch))
+    check(nf if nf < 0 else 0, "rlp_sac_workspace")
+    return torch.empty(int(nf), dtype=torch.float32, device=_dev(device))
+
+
+def sac_update(nets, cfg, s, a, r, s_next, dw, noise, work, losses):
+    """One SAC learn() iteration (include/rlp.h rlp_sac_update); noise None or [2][B][A]."""
+    check(lib().rlp_sac_update(C.byref(nets), C.byref(cfg), ptr(s), ptr(a), ptr(r), ptr(s_next),
+                               ptr(dw), ptr(noise), ptr(work), ptr(losses), stream_ptr()),
+          "rlp_sac_update")
+    return losses

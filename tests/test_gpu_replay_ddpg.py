@@ -112,7 +112,7 @@ def load_flat(m, flat):
             off += p.numel()
 
 
-def make_agent(g=None, memory=10000, batch=64, seed=0, graph=False):
+def make_agent(g=None, memory=10000, batch=64, seed=0, graph=False, native="auto"):
     lo, hi = np.array([-3., -3.]), np.array([3., 3.])
     nets = [Actor(1e-4, 4, 2, lo, hi), Actor(1e-4, 4, 2, lo, hi), Critic(3e-4, 4, 2),
             Critic(3e-4, 4, 2)]
@@ -123,12 +123,17 @@ def make_agent(g=None, memory=10000, batch=64, seed=0, graph=False):
                'name': 'SecondOrderIntegration'}
     return DDPG(env_msg, gamma=0.99, actor_soft_update=0.005, critic_soft_update=0.005,
                 memory_capacity=memory, batch_size=batch, actor=nets[0], target_actor=nets[1],
-                critic=nets[2], target_critic=nets[3], device="cuda", seed=seed, graph=graph)
+                critic=nets[2], target_critic=nets[3], device="cuda", seed=seed, graph=graph,
+                native=native)
 
 
-def test_ddpg_update_matches_reference(golden):
+@pytest.mark.parametrize("native", [True, False])
+def test_ddpg_update_matches_reference(golden, native):
+    """One learn() iteration from the reference's before-weights on its sampled batch: the
+    after-weights of all four nets (native rlp_ddpg_update and the torch path)."""
     g = golden("ddpg_soi_learn")
-    agent = make_agent(g)
+    agent = make_agent(g, native=native)
+    assert (agent._native is not None) == native
     dev = lambda k: torch.as_tensor(np.asarray(g[k]), dtype=torch.float32, device="cuda")
     agent.update(dev("s"), dev("a"), dev("r"), dev("s2"), dev("end"))
     for k, m in (("actor", agent.actor), ("target_actor", agent.target_actor),
@@ -201,3 +206,75 @@ def test_ddpg_graphed_update_is_one_adam_step():
     for _ in range(5):
         g_agent.learn(is_reward_ascent=False, iter=2)
     assert all(torch.isfinite(p).all() for p in g_agent.actor.parameters())
+
+
+def _flat(m):
+    return torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+
+
+def _batch(B, seed):
+    rng = np.random.default_rng(seed)
+    dev = lambda x: torch.as_tensor(x, dtype=torch.float32, device="cuda")
+    return (dev(rng.uniform(-2, 2, (B, 4))), dev(rng.uniform(-3, 3, (B, 2))), dev(rng.normal(size=B)),
+            dev(rng.uniform(-2, 2, (B, 4))), dev((rng.uniform(size=B) > 0.1).astype(np.float32)))
+
+
+@pytest.mark.parametrize("B", [4096, 1000])
+def test_native_ddpg_tracks_torch_update(B):
+    """rlp_ddpg_update against the torch autograd + Adam path from the same weights over 5
+    updates on fresh batches (bench batch 4096, and a batch that is not a multiple of the
+    256-row weight-gradient split): per-step losses and all four nets agree to f32 GEMM noise;
+    the drivers' unused critic.action_value stays put (no gradient), its target copy is blended."""
+    torch.manual_seed(3)
+    t_agent, n_agent = make_agent(native=False), make_agent(native=True)
+    for k in ("actor", "target_actor", "critic", "target_critic"):
+        getattr(n_agent, k).load_state_dict(getattr(t_agent, k).state_dict())
+    av0 = n_agent.critic.action_value.weight.detach().clone()
+    tav0 = n_agent.target_critic.action_value.weight.detach().clone()
+    for it in range(5):
+        batch = _batch(B, it)
+        lt = t_agent.update(*batch)
+        ln = n_agent.update(*batch)
+        for x, y in zip(lt, ln):
+            torch.testing.assert_close(y, x, rtol=2e-4, atol=1e-6)
+    for k in ("actor", "target_actor", "critic", "target_critic"):
+        torch.testing.assert_close(_flat(getattr(n_agent, k)), _flat(getattr(t_agent, k)),
+                                   rtol=1e-4, atol=2e-6, msg=k)
+    assert torch.equal(n_agent.critic.action_value.weight, av0)
+    tav = n_agent.target_critic.action_value.weight
+    assert not torch.equal(tav, tav0)
+    torch.testing.assert_close(tav, t_agent.target_critic.action_value.weight, rtol=0, atol=1e-7)
+
+
+def test_native_ddpg_deterministic_and_state_dict_views():
+    """Two runs from the same weights on the same batches are bit-identical (fixed-order weight
+    gradient reduction, no atomics), and the modules' state_dict() sees the native steps."""
+    out = []
+    for _ in range(2):
+        torch.manual_seed(5)
+        agent = make_agent(native=True)
+        sd0 = {k: v.clone() for k, v in agent.actor.state_dict().items()}
+        for it in range(3):
+            agent.update(*_batch(4096, 10 + it))
+        sd = agent.actor.state_dict()
+        assert any(not torch.equal(sd[k], sd0[k]) for k in sd)
+        out.append(torch.cat([_flat(getattr(agent, k)) for k in
+                              ("actor", "target_actor", "critic", "target_critic")]))
+    assert torch.equal(out[0], out[1])
+
+
+def test_native_ddpg_rejects_other_nets():
+    """A critic whose forward is not relu(Linear(cat(s, a))) ... Linear stays on the torch path
+    under native='auto' and is refused under native=True."""
+    class TanhCritic(Critic):
+        def forward(self, s, a):
+            return self.q(torch.tanh(self.fc2(torch.tanh(self.fc1(torch.cat([s, a], 1))))))
+
+    lo, hi = np.array([-3., -3.]), np.array([3., 3.])
+    env_msg = {'state_dim': 4, 'action_dim': 2, 'action_range': np.stack([lo, hi], 1), 'name': 'x'}
+    mk = lambda native: DDPG(env_msg, actor=Actor(1e-4, 4, 2, lo, hi), target_actor=Actor(1e-4, 4, 2, lo, hi),
+                             critic=TanhCritic(3e-4, 4, 2), target_critic=TanhCritic(3e-4, 4, 2),
+                             device="cuda", native=native)
+    assert mk("auto")._native is None
+    with pytest.raises(ValueError):
+        mk(True)

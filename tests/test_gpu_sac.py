@@ -90,7 +90,7 @@ class _Replay:
         torch.distributions.Normal.rsample = self.orig
 
 
-def make_agent(g=None, capacity=10000, batch=64, seed=0, graph=False):
+def make_agent(g=None, capacity=10000, batch=64, seed=0, graph=False, native="auto"):
     actor, critic, target = demo_actor(), SACCritic(S, A), SACCritic(S, A)
     if g is not None:
         load_flat(actor, g["before_actor"])
@@ -99,17 +99,29 @@ def make_agent(g=None, capacity=10000, batch=64, seed=0, graph=False):
     env_msg = {'state_dim': S, 'action_dim': A, 'action_range': np.stack([LO, HI], 1), 'name': 'OA'}
     return SAC(env_msg, gamma=0.99, critic_tau=0.005, memory_capacity=capacity, batch_size=batch,
                actor=actor, critic=critic, target_critic=target, a_lr=1e-4, c_lr=1e-4,
-               alpha_lr=1e-4, adaptive_alpha=True, device="cuda", seed=seed, graph=graph)
+               alpha_lr=1e-4, adaptive_alpha=True, device="cuda", seed=seed, graph=graph,
+               native=native)
 
 
-def test_sac_update_vs_reference(golden):
+@pytest.mark.parametrize("native", [True, False])
+def test_sac_update_vs_reference(golden, native):
+    """Two learn() iterations from the reference's before-weights on its sampled batches with its
+    recorded Normal.rsample noise (native rlp_sac_update, and the torch path): all three nets and
+    log_alpha after the updates."""
     g = golden("sac")
-    agent = make_agent(g)
+    agent = make_agent(g, native=native)
+    assert (agent._native is not None) == native
     dev = lambda k: torch.as_tensor(np.asarray(g[k]), dtype=torch.float32, device="cuda")
-    with _Replay(list(g["learn_eps"])):
+    eps = [torch.from_numpy(np.asarray(e, np.float32)).cuda() for e in g["learn_eps"]]
+    if native:
         for i in range(2):
             agent.update(dev(f"b{i}_s"), dev(f"b{i}_a"), dev(f"b{i}_r"), dev(f"b{i}_s2"),
-                         dev(f"b{i}_dw"))
+                         dev(f"b{i}_dw"), noise=torch.stack(eps[2 * i:2 * i + 2]))
+    else:
+        with _Replay(list(g["learn_eps"])):
+            for i in range(2):
+                agent.update(dev(f"b{i}_s"), dev(f"b{i}_a"), dev(f"b{i}_r"), dev(f"b{i}_s2"),
+                             dev(f"b{i}_dw"))
     for k, m in (("actor", agent.actor), ("critic", agent.critic),
                  ("target_critic", agent.target_critic)):
         got = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
@@ -176,3 +188,48 @@ def test_sac_graphed_learn_tracks_eager():
     for _ in range(5):
         g_agent.learn(iter=2)
     assert torch.isfinite(g_agent.log_alpha).all()
+
+
+def _sac_batch(B, seed):
+    rng = np.random.default_rng(seed)
+    d = lambda x: torch.as_tensor(x, dtype=torch.float32, device="cuda")
+    return (d(rng.uniform(-1, 1, (B, S))), d(rng.uniform(LO, HI, (B, A))), d(rng.normal(size=B)),
+            d(rng.uniform(-1, 1, (B, S))), d((rng.uniform(size=B) < 0.1).astype(np.float32)))
+
+
+@pytest.mark.parametrize("B", [4096, 1000])
+def test_native_sac_tracks_torch_update(B):
+    """rlp_sac_update against the torch path from the same weights, the same batches and the same
+    noise over 4 updates (the bench batch, and one that is not a multiple of 256): losses, the
+    three nets and log_alpha agree to f32 GEMM noise."""
+    torch.manual_seed(7)
+    t_agent, n_agent = make_agent(native=False), make_agent(native=True)
+    for k in ("actor", "critic", "target_critic"):
+        getattr(n_agent, k).load_state_dict(getattr(t_agent, k).state_dict())
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for it in range(4):
+        batch = _sac_batch(B, it)
+        eps = torch.randn(2, B, A, device="cuda", generator=g)
+        with _Replay([eps[0].cpu().numpy(), eps[1].cpu().numpy()]):
+            lt = t_agent.update(*batch)
+        ln = n_agent.update(*batch, noise=eps)
+        for x, y in zip(lt, ln):
+            torch.testing.assert_close(y, x, rtol=5e-4, atol=1e-5)
+    for k in ("actor", "critic", "target_critic"):
+        a = torch.cat([p.detach().reshape(-1) for p in getattr(n_agent, k).parameters()])
+        b = torch.cat([p.detach().reshape(-1) for p in getattr(t_agent, k).parameters()])
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=2e-6, msg=k)
+    torch.testing.assert_close(n_agent.log_alpha.detach(), t_agent.log_alpha.detach(), rtol=1e-5, atol=1e-8)
+
+
+def test_native_sac_philox_noise_deterministic():
+    """Without a tape the native update draws Philox noise keyed by (seed, device counter, row):
+    two agents from the same weights and seed take bit-identical steps; a different seed does not."""
+    outs = []
+    for seed in (2, 2, 3):
+        torch.manual_seed(11)
+        ag = make_agent(native=True, seed=seed)
+        for it in range(3):
+            ag.update(*_sac_batch(512, 20 + it))
+        outs.append(torch.cat([p.detach().reshape(-1) for p in ag.actor.parameters()]))
+    assert torch.equal(outs[0], outs[1]) and not torch.equal(outs[0], outs[2])
