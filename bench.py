@@ -44,14 +44,21 @@ ROLLOUT_KERNEL = {"shared": "rlp::rollout_sp_kernel<KIND,256,SUB,4>",
 PHYSICS_MODES = {"auto": -1, "lanes": 0, "shared": 1, "shared8": 2, "cu": 3, "cu16": 4, "cu4": 5, "cu64": 6}
 
 
-def rollout_kernel_name(physics, n, env="cartpole"):
-    """The kernel rlp_rollout runs for `physics` (auto: one 8-wave block per CU when n fills every
-    CU with a 256-env block, else — and always for the UAV — one 4-wave block of 32-env waves per
-    CU; include/rlp.h rlp_set_rollout_physics)."""
+def rollout_kernel_name(physics, n, env="cartpole", sub=0):
+    """The kernel rlp_rollout runs for `physics` and the --sub knob, mirroring rlp_rollout's own
+    selection (rlp_rollout.hip rollout_kind): auto = one 8-wave block per CU when n fills every CU
+    with a 256-env block (not the UAV), else one 4-wave block of 32-env waves per CU — both only
+    for sub 0 / 2; any other sub falls back to the shared-physics kernel (mode 1)."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
     if physics == "auto":
-        cus = torch.cuda.get_device_properties(0).multi_processor_count
-        physics = "cu" if env != "uav" and (n + 255) // 256 >= cus else "cu4"
-    return ROLLOUT_KERNEL[physics]
+        if sub in (0, 2):
+            physics = "cu" if env != "uav" and (n + 255) // 256 >= cus else "cu4"
+        else:
+            physics = "shared"
+    if sub == 0:   # the library's auto sub for the modes that take it
+        sub = 1 if (n + 127) // 128 < 2 * cus else 2
+    return ROLLOUT_KERNEL[physics].replace("SUB", str(sub))
+
 
 ENVS = {
     "cartpole": (A.RLP_ENV_CARTPOLE, lambda: A.cartpole_params("ppo2"), 3),
@@ -635,6 +642,10 @@ def main():
                     "advantage normalisation, SOI / UGV / UAV env steps) against the HBM roof")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
+    ap.add_argument("--rollout-prio", type=int, default=-1, choices=[-1, 0, 1],
+                    help="rlp_set_rollout_prio (-1: library default)")
+    ap.add_argument("--update-prio", type=int, default=-1, choices=[-1, 0, 1],
+                    help="rlp_set_update_prio for the PPO2 update kernels (-1: library default)")
     ap.add_argument("--wgrad-waves", type=int, default=0, choices=[0, 4, 8],
                     help="PPO2 update's weight-gradient kernel block shape (0: library default)")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
@@ -661,6 +672,10 @@ def main():
         _native.set_rollout_sub(args.sub)
     if args.wgrad_waves:
         _native.lib().rlp_set_wgrad_waves(args.wgrad_waves)
+    if args.update_prio >= 0:
+        _native.lib().rlp_set_update_prio(args.update_prio)
+    if args.rollout_prio >= 0:
+        _native.lib().rlp_set_rollout_prio(args.rollout_prio)
     _native.set_rollout_physics(PHYSICS_MODES[args.physics])
     prec = _native.MLP_F16X3 if args.precision == "f16x3" else _native.MLP_FP32
     _native.set_mlp_precision(prec)
@@ -718,7 +733,7 @@ def main():
                    "nets": "actor [S,256,256,A] tanh, critic [S,256,256,1]",
                    "parallelism": f"dp{world} (env shards, no data-path collective)",
                    "physics": "f64", "mlp": mlp},
-        "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(args.physics, n, args.env) if args.precision == "f16x3"
+        "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(args.physics, n, args.env, args.sub) if args.precision == "f16x3"
                                                 else "rlp::rollout_kernel<KIND,256,SUB,false>"), "achieved": achieved,
                      "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                      "peak_basis": basis, "avg_launch_ms": rollout_ms, "flop_per_launch": flop_launch},
@@ -767,12 +782,12 @@ def main():
             "value": un * uT * usteps * world / uel, "unit": "env-steps/s", "envs_per_gpu": un,
             "global_envs": un * world, "T": uT,
             "config": "UavRobust hover outer loop (6-DoF + FNTSMC), PPO2 [6,256,256,3]",
-            "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(uphys, un, "uav")
+            "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(uphys, un, "uav", args.sub)
                                                      if args.precision == "f16x3"
                                                      else "rlp::rollout_kernel<KIND,256,SUB,false>"),
                          "achieved": uach, "peak": upeak, "unit": "TFLOP/s", "frac": uach / upeak,
                          "traffic": pmc_traffic("uav_ppo2_rollout", un, uT,
-                                                rollout_kernel_name(uphys, un, "uav")),
+                                                rollout_kernel_name(uphys, un, "uav", args.sub)),
                          "avg_launch_ms": ums, "flop_per_launch": uflop}}
         del useg
         _native.set_rollout_physics(PHYSICS_MODES[args.physics])

@@ -318,7 +318,7 @@ typedef struct rlp_rollout_cfg {
      * rlp_set_rollout_physics / rlp_set_rollout_sub, else value + 1 (mlp_precision: 1 RLP_MLP_FP32,
      * 2 RLP_MLP_F16X3; physics: 1 register-resident, 2 shared, 3 shared 8-wave, 4 shared
      * one-block-per-CU, 5 shared one-block-per-CU of 16-env waves, 6 / 7 one 4-wave block of 32- /
-     * 64-env waves per CU); sub: 0 default,
+     * 64-env waves per CU, 8 auto — the knob's -1); sub: 0 default,
      * 1, 2, 4 */
     int32_t mlp_precision, physics, sub, reserved;
 } rlp_rollout_cfg;
@@ -435,6 +435,11 @@ int rlp_get_fd_mode(void);
  * 8 (default) one 8-wave block per CU, each wave 32 output rows (2 waves per SIMD); 4 one 4-wave
  * block per CU, each wave 64 output rows with the VGPR + AGPR budget (1 wave per SIMD: half the
  * LDS fragment reads per tile, fragments read one step ahead). Same partial-sum order. */
+/* Tuning knob of rlp_ppo2_grad: 1 = the second half of each FD / wgrad block's waves (the younger
+ * wave of every SIMD pair) runs at s_setprio 1, 0 = all waves at priority 0 (default). Same
+ * results. */
+int rlp_set_update_prio(int mode);
+int rlp_get_update_prio(void);
 int rlp_set_wgrad_waves(int waves);
 int rlp_get_wgrad_waves(void);
 
@@ -590,6 +595,10 @@ int rlp_set_rollout_sub(int sub);
  * (2 waves per SIMD), 0 = the register-resident kernel (physics on the 16*sub lanes of each env's
  * own wave). Same results. */
 int rlp_set_rollout_physics(int shared);
+/* Tuning knob of the fused rollout (rollout_sp_kernel): 1 = the younger half of each block's waves
+ * (the second wave of every SIMD pair in the 8-wave variants) runs at s_setprio 1; 0 (default) =
+ * all at priority 0. Same results. */
+int rlp_set_rollout_prio(int mode);
 /* Arithmetic of rlp_rollout's hidden layer (the [256 x 256] GEMM, 99 % of its FLOPs):
  *   RLP_MLP_F16X3 (default): error-compensated split, w*x = wh*xh + wh*xl + wl*xh on f16 MFMA with
  *     f32 accumulation — fp32-class accuracy (see tests/test_gpu_rollout.py) at 16/3 x the f32

@@ -378,8 +378,8 @@ def ugv_oa_params(variant="env"):
 def default_params(kind, variant=None):
     if kind == RLP_ENV_CARTPOLE:
         return cartpole_params(variant or "ppo2")
-    if kind == RLP_ENV_CARTPOLE_ANGLEONLY:
-        return angleonly_params(variant or "ppo2")
+    if kind == RLP_ENV_CARTPOLE_ANGLEONLY:   # the same default as CartPoleAngleOnly(variant=)
+        return angleonly_params(variant or "env")
     if kind == RLP_ENV_SOI:
         return soi_params(variant or "env")
     if kind in (RLP_ENV_UGV_FORWARD, RLP_ENV_UGV_BIDIRECTIONAL):

@@ -18,8 +18,10 @@ copy's clip norm and success rule, no lr decay (the Worker stores use_lr_decay a
 it, Distributed_PPO2.py:50), and the copy's exploration-std schedule after every learn().
 """
 import os
+import warnings
 
 import numpy as np
+
 import torch
 
 from ... import _abi
@@ -108,6 +110,10 @@ class Distributed_PPO2:
             state_dim=env.state_dim, use_orthogonal_init=True)
         self.eval_actor = self.global_actor
         self.copy = DPPO2_COPY[env.KIND]
+        if env.KIND == _abi.RLP_ENV_CARTPOLE_ANGLEONLY and getattr(env, "variant", "dppo2") == "env":
+            warnings.warn("Distributed_PPO2: CartPoleAngleOnly(variant='env') is the env-dir file; "
+                          "the DPPO2 demos train the demo copy, CartPoleAngleOnly(variant='dppo2')",
+                          stacklevel=2)
         msg = dict(ppo_msg or {})
         msg.setdefault('a_lr', actor_lr)
         msg.setdefault('c_lr', critic_lr)

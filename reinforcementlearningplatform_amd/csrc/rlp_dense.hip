@@ -24,16 +24,23 @@ namespace rlp {
 // gradient); out of range reads 0
 struct Opnd {
     const float *p0, *p1;
-    int64_t rs0, cs0, rs1, cs1;
+    int rs0, cs0, rs1, cs1;  // element strides (every operand here has < 2^31 elements)
     int rows, cols, split, ones, split_rows;
 };
 
+// branch-free: one unconditional load (index 0 of the chosen source when out of range), then
+// selects — so a thread's many staged loads issue back to back instead of one per branch
 __device__ __forceinline__ float opnd_ld(const Opnd &o, int i, int j) {
-    if (i >= o.rows || j >= o.cols) return 0.f;
-    if (j == o.ones) return 1.f;
-    if (o.split_rows)
-        return i < o.split ? o.p0[i * o.rs0 + j * o.cs0] : o.p1[(i - o.split) * o.rs1 + j * o.cs1];
-    return j < o.split ? o.p0[i * o.rs0 + j * o.cs0] : o.p1[i * o.rs1 + (j - o.split) * o.cs1];
+    const bool in = i < o.rows && j < o.cols;
+    const bool ld = in && j != o.ones;
+    const bool second = o.split_rows ? i >= o.split : j >= o.split;
+    const int ii = (o.split_rows && second) ? i - o.split : i;
+    const int jj = (!o.split_rows && second) ? j - o.split : j;
+    const int idx = second ? ii * o.rs1 + jj * o.cs1 : ii * o.rs0 + jj * o.cs0;
+    const float v = (second ? o.p1 : o.p0)[ld ? idx : 0];
+    // arithmetic, not a select on the loaded value: the backend turns "c ? load : k" into a branch
+    // around the load, which serialises the staged loads (v is finite operand data)
+    return __builtin_fmaf(v, ld ? 1.f : 0.f, (in && j == o.ones) ? 1.f : 0.f);
 }
 
 enum : int { kEpiNone = 0, kEpiRelu, kEpiTanhAff, kEpiReluBack, kEpiTanhAffBack, kEpiPartial };
@@ -54,6 +61,104 @@ constexpr int kDT = 64;            // output tile (M and N)
 constexpr int kDRc = 256;          // reduction rows one block stages at once
 constexpr int kDLd = kDRc + 4;     // LDS row: operand row-major along r, 4 banks apart per row
 
+// extent of the panel's outer index u (A: rows m; B: columns n)
+__device__ __forceinline__ int e_rows(const Opnd &o, bool is_a) { return is_a ? o.rows : o.cols; }
+
+// Stage this block's panel of an operand into LDS as L[u][r] (row stride kDLd): u in [0, 64) the
+// outer index (A: m0 + u; B: n0 + u), r in [0, 256) the reduction index (r_lo + r; zero past rc).
+// Fast path (the panel lies inside one source, off the ones column, fully in range, and is
+// contiguous along r or along u with 16-byte alignment): 16 float4 loads per thread, all in
+// flight together. Otherwise the generic element loader in groups of 16.
+__device__ __forceinline__ void stage_panel(const Opnd &o, bool is_a, int u0, int ubound, int r_lo,
+                                            int rc, int nr, float *L) {
+    const int t = threadIdx.x;
+    // (i, j) of panel element (u, r)
+    auto ij = [&](int u, int r, int &i, int &j) {
+        i = is_a ? u0 + u : r_lo + r;
+        j = is_a ? r_lo + r : u0 + u;
+    };
+    const int i_lo = is_a ? u0 : r_lo, i_hi = is_a ? u0 + 64 : r_lo + rc;  // [lo, hi)
+    const int j_lo = is_a ? r_lo : u0, j_hi = is_a ? r_lo + rc : u0 + 64;
+    const int s_lo = o.split_rows ? i_lo : j_lo, s_hi = o.split_rows ? i_hi : j_hi;
+    const bool one_src = s_hi <= o.split || s_lo >= o.split;
+    const bool second = s_lo >= o.split;
+    const bool no_ones = o.ones < j_lo || o.ones >= j_hi;
+    const bool inrange = u0 + 64 <= ubound && (rc & 3) == 0;
+    const float *p = second ? o.p1 : o.p0;
+    const int rs = second ? o.rs1 : o.rs0, cs = second ? o.cs1 : o.cs0;
+    const int ioff = (o.split_rows && second) ? o.split : 0, joff = (!o.split_rows && second) ? o.split : 0;
+    // contiguity along r or u
+    const int r_stride = is_a ? cs : rs, u_stride = is_a ? rs : cs;
+    const bool rfast = r_stride == 1 && (u_stride & 3) == 0;
+    const bool ufast = u_stride == 1 && (r_stride & 3) == 0;
+    const bool aligned = ((uintptr_t)p & 15) == 0 &&
+                         (((is_a ? (u0 - ioff) * rs + (r_lo - joff) * cs : (r_lo - ioff) * rs + (u0 - joff) * cs)) & 3) == 0;
+    if (one_src && no_ones && inrange && aligned && (rfast || ufast)) {
+        const float *base = p + (int64_t)((is_a ? u0 : r_lo) - ioff) * rs + (int64_t)((is_a ? r_lo : u0) - joff) * cs;
+        floatx4 v[16];
+        if (rfast) {  // thread: r4 = 4 (t & 63), u = (t >> 6) + 4 q
+            const int r4 = 4 * (t & 63);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int u = (t >> 6) + 4 * q;
+                v[q] = r4 < rc ? *(const floatx4 *)(base + (int64_t)u * u_stride + r4) : floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) *(floatx4 *)&L[((t >> 6) + 4 * q) * kDLd + r4] = v[q];
+        } else {      // thread: u4 = 4 (t & 15), r = (t >> 4) + 16 q
+            const int u4 = 4 * (t & 15);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int r = (t >> 4) + 16 * q;
+                v[q] = r < rc ? *(const floatx4 *)(base + (int64_t)r * r_stride + u4) : floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) L[(u4 + k) * kDLd + (t >> 4) + 16 * q] = v[q][k];
+        }
+        return;
+    }
+    // generic element loader. Rows u past ubound are left as they are (their outputs are never
+    // stored); columns r in [rc, nr) are zeroed (they meet valid outputs in the MFMAs).
+    const int nu = ubound - u0 < 64 ? ubound - u0 : 64;
+    if (nu <= 16) {  // few valid u (a last layer's W, an edge tile): thread = r, loop over u
+        const int r = t;
+        if (r < nr) {
+            float v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                int i, j;
+                ij(u, r, i, j);
+                const bool ok = u < nu && r < rc;
+                v[u] = opnd_ld(o, ok ? i : 0x7fffffff, ok ? j : 0x7fffffff);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (u < nu) L[u * kDLd + r] = v[u];
+        }
+        return;
+    }
+    // thread = u (t & 63) and every 4th r from t >> 6, 8 loads in flight per step
+    const int u = t & 63;
+    if (u >= nu) return;
+#pragma unroll 1
+    for (int r0 = t >> 6; r0 < nr; r0 += 32) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int r = r0 + 4 * k;
+            int i, j;
+            ij(u, r, i, j);
+            const bool ok = r < rc;
+            v[k] = opnd_ld(o, ok ? i : 0x7fffffff, ok ? j : 0x7fffffff);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (r0 + 4 * k < nr) L[u * kDLd + r0 + 4 * k] = v[k];
+    }
+}
+
 // C[M x N] = sum_r A(m, r) B(r, n) over r in [z * rchunk, min(R, (z + 1) * rchunk)), rchunk <= 256.
 // The block stages its whole reduction slice of both operands at once (all global loads in
 // flight together, 128 registers per lane, then one barrier): these GEMMs have <= 256-deep
@@ -69,26 +174,8 @@ __global__ void __launch_bounds__(256) dense_gemm_kernel(Opnd A, Opnd B, int R, 
     const int Q = (rc + 15) / 16 * 4;  // MFMA steps (multiple of 4); rows g * Q + s, s < Q
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
     const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
-    const bool a_rfast = A.cs0 == 1;  // A(m, r) contiguous along r: lanes walk r
-    const bool b_rfast = B.rs0 == 1;  // B(r, n) contiguous along r
-    const int span = 4 * Q;           // staged rows (zero beyond rc)
-    float ra[64], rb[64];
-#pragma unroll
-    for (int q = 0; q < 64; ++q) {
-        const int x = t + 256 * q;
-        const int am = a_rfast ? x >> 8 : x & 63, ar = a_rfast ? x & 255 : x >> 6;
-        ra[q] = ar < rc ? opnd_ld(A, m0 + am, r_lo + ar) : 0.f;
-        const int bn = b_rfast ? x >> 8 : x & 63, br = b_rfast ? x & 255 : x >> 6;
-        rb[q] = br < rc ? opnd_ld(B, r_lo + br, n0 + bn) : 0.f;
-    }
-#pragma unroll
-    for (int q = 0; q < 64; ++q) {
-        const int x = t + 256 * q;
-        const int am = a_rfast ? x >> 8 : x & 63, ar = a_rfast ? x & 255 : x >> 6;
-        if (ar < span) As[am * kDLd + ar] = ra[q];
-        const int bn = b_rfast ? x >> 8 : x & 63, br = b_rfast ? x & 255 : x >> 6;
-        if (br < span) Bs[bn * kDLd + br] = rb[q];
-    }
+    stage_panel(A, true, m0, e_rows(A, true), r_lo, rc, 4 * Q, As);
+    stage_panel(B, false, n0, e_rows(B, false), r_lo, rc, 4 * Q, Bs);
     __syncthreads();
     floatx4 acc[2][2];
 #pragma unroll
@@ -437,13 +524,13 @@ __global__ void __launch_bounds__(256) soft_update_sac_kernel(float *__restrict_
 
 // ---- host side ------------------------------------------------------------------------------
 
-inline Opnd mat(const float *p, int rows, int cols, int64_t ld) {  // row-major rows x cols
+inline Opnd mat(const float *p, int rows, int cols, int ld) {  // row-major rows x cols
     return Opnd{p, p, ld, 1, ld, 1, rows, cols, cols, -1, 0};
 }
-inline Opnd cat2(const float *p0, int c0, int64_t ld0, const float *p1, int c1, int64_t ld1, int rows) {
+inline Opnd cat2(const float *p0, int c0, int ld0, const float *p1, int c1, int ld1, int rows) {
     return Opnd{p0, p1, ld0, 1, ld1, 1, rows, c0 + c1, c0, -1, 0};
 }
-inline Opnd transposed(const float *p, int rows, int cols, int64_t ld) {  // (i, j) = p[j * ld + i]
+inline Opnd transposed(const float *p, int rows, int cols, int ld) {  // (i, j) = p[j * ld + i]
     return Opnd{p, p, 1, ld, 1, ld, rows, cols, cols, -1, 0};
 }
 
@@ -501,7 +588,7 @@ void dense_wgrad(const float *dy, const Opnd &x, const Layer &L, int B, float *p
     Opnd xo = x;
     xo.cols = L.in + 1;
     xo.ones = L.in;
-    const int z = gemm(transposed(dy, L.out, B, ldy < 0 ? L.out : ldy), xo, L.out, L.in + 1, B, splits,
+    const int z = gemm(transposed(dy, L.out, B, (int)(ldy < 0 ? L.out : ldy)), xo, L.out, L.in + 1, B, splits,
                        e, s);
     const int tot = L.out * (L.in + 1);
     wgrad_reduce_kernel<<<(tot + 255) / 256, 256, 0, s>>>(part, z, L.out, L.in + 1, gW, gb);

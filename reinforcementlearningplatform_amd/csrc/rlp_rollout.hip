@@ -287,6 +287,7 @@ struct SpArgs {
     MfmaNet cn;
     RolloutArgs ra;
     rlp_rollout_bufs b;
+    int prio;  // rlp_set_rollout_prio: the block's younger half of waves at s_setprio 1
 };
 
 template <int KIND, int H, int SUB, int W = 4, int WPS = rollout_sp_default_wps<SUB, W>()>
@@ -350,6 +351,8 @@ rollout_sp_kernel(SpArgs<KIND> args) {
         s_pdone[le] = 1;  // no value_next write before step 0
     }
     __syncthreads();
+    if (args.prio && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= W / 2)
+        __builtin_amdgcn_s_setprio(1);
 
     auto mlp_pass = [&](bool both) {
         // the nets' pointers and layouts re-read from the kernarg segment (scalar loads) per pass
@@ -557,6 +560,7 @@ static int launch_packed_forward(const MfmaNet &net, const float *P, const float
 }
 
 static int g_rollout_shared_physics = -1;  // rlp_set_rollout_physics (-1: auto)
+static int g_rollout_prio = 0;             // rlp_set_rollout_prio
 
 template <int KIND, int H, int SUB, bool X3>
 static int launch_rollout(const void *params, double *state, uint8_t *need_reset,
@@ -570,7 +574,7 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     if constexpr (X3 && SUB == 1 && rollout_sp_ring<KIND, 1, 8>() != 0) {
         if (physics == 2) {  // 8-wave blocks, 16 envs per wave
             const int blocks8 = (ra.n + 127) / 128;
-            rollout_sp_kernel<KIND, H, 1, 8><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
+            rollout_sp_kernel<KIND, H, 1, 8><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
@@ -578,7 +582,7 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     if constexpr (X3 && SUB == 1 && rollout_sp_ring<KIND, 1, 8, 2>() != 0) {
         if (physics == 4) {  // one 8-wave block of 16-env waves per CU (2 waves per SIMD)
             const int blocks8 = (ra.n + 127) / 128;
-            rollout_sp_kernel<KIND, H, 1, 8, 2><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
+            rollout_sp_kernel<KIND, H, 1, 8, 2><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
@@ -586,7 +590,7 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     if constexpr (X3 && SUB == 2 && rollout_sp_ring<KIND, 2, 8>() != 0) {
         if (physics == 3) {  // one 8-wave block per CU, 32 envs per wave
             const int blocks8 = (ra.n + 255) / 256;
-            rollout_sp_kernel<KIND, H, 2, 8><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
+            rollout_sp_kernel<KIND, H, 2, 8><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
@@ -594,7 +598,7 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     if constexpr (X3 && SUB == 2 && rollout_sp_ring<KIND, 2, 4, 1>() != 0) {
         if (physics == 5) {  // one 4-wave block of 32-env waves per CU (1 wave per SIMD, 512 registers)
             const int blocks4 = (ra.n + 127) / 128;
-            rollout_sp_kernel<KIND, H, 2, 4, 1><<<blocks4, 256, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
+            rollout_sp_kernel<KIND, H, 2, 4, 1><<<blocks4, 256, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
@@ -602,14 +606,14 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     if constexpr (X3 && SUB == 4 && rollout_sp_ring<KIND, 4, 4, 1>() != 0) {
         if (physics == 6) {  // one 4-wave block of 64-env waves per CU (1 wave per SIMD, 512 registers)
             const int blocks4 = (ra.n + 255) / 256;
-            rollout_sp_kernel<KIND, H, 4, 4, 1><<<blocks4, 256, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
+            rollout_sp_kernel<KIND, H, 4, 4, 1><<<blocks4, 256, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
     }
     if constexpr (X3 && rollout_sp_fits<KIND, SUB>()) {
         if (physics)
-            rollout_sp_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
+            rollout_sp_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
         else
             rollout_kernel<KIND, H, SUB, X3><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor,
                                                                          an, critic, cn, ra, b);
@@ -806,11 +810,17 @@ int rlp_get_mlp_precision(void) { return g_mlp_precision; }
 // tuning knob (envs per wave = 16 * sub): 0 = auto (f16x3: 1 when 32-env waves would leave fewer
 // than 2 blocks per CU, else 2; f32: 2), 1 (f16x3 only), 2, 4
 
-// tuning knob: 1 (default) = the shared-physics f16x3 kernel where its LDS fits (full-lane
-// physics), 0 = the register-resident kernel
+// tuning knob (include/rlp.h): -1 (default) = auto (3 when the envs fill every CU with a 256-env
+// block, else — and always for the UAV — 5), 0-6 the kernel variants listed there
 int rlp_set_rollout_physics(int shared) {
     if (shared < -1 || shared > 6) return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
     g_rollout_shared_physics = shared;
+    return RLP_OK;
+}
+
+int rlp_set_rollout_prio(int mode) {
+    if (mode < 0 || mode > 1) return fail(RLP_EINVAL, "rlp_set_rollout_prio: %d", mode);
+    g_rollout_prio = mode;
     return RLP_OK;
 }
 
@@ -878,13 +888,13 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
     hipStream_t s = as_stream(stream);
     // per-call selections (cfg, 0 = the library-wide default of the rlp_set_* knobs)
     RLP_REQUIRE(cfg->mlp_precision >= 0 && cfg->mlp_precision <= 2 && cfg->physics >= 0 &&
-                    cfg->physics <= 7 && (cfg->sub == 0 || cfg->sub == 1 || cfg->sub == 2 ||
+                    cfg->physics <= 8 && (cfg->sub == 0 || cfg->sub == 1 || cfg->sub == 2 ||
                                           cfg->sub == 4),
                 "rlp_rollout: cfg mlp_precision=%d physics=%d sub=%d", cfg->mlp_precision,
                 cfg->physics, cfg->sub);
     const int sub = cfg->sub ? cfg->sub : g_rollout_sub;
     const int prec = cfg->mlp_precision ? cfg->mlp_precision - 1 : g_mlp_precision;
-    const int physics = cfg->physics ? cfg->physics - 1 : g_rollout_shared_physics;
+    const int physics = cfg->physics == 8 ? -1 : cfg->physics ? cfg->physics - 1 : g_rollout_shared_physics;
     switch (kind) {
     case RLP_ENV_CARTPOLE:
         return rollout_kind<RLP_ENV_CARTPOLE>(env_params, state, need_reset, actor_packed, an,

@@ -38,6 +38,7 @@ struct Ppo2Args {
     unsigned *g2max;    // bits of max|g2| (atomicMax)
     float *part3;       // [grid * 4][A*256 + A + 256*S + 256]: per-wave dW3 | db3 | dW1 | db1
     double *loss_sum;
+    int prio;           // rlp_set_update_prio: the second half of the block's waves at priority 1
 };
 
 // block barrier for LDS hand-offs only: drains this wave's LDS ops, not its global loads (HIP's
@@ -212,6 +213,9 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
     // the wave index as a scalar (readfirstlane): every wave-derived offset, the G2 tile and its
     // store guard become SGPR values (no per-lane 64-bit address arithmetic, no exec-masked stores)
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // (the younger half of the SIMD pairs loses VALU arbitration at every segment start otherwise;
+    // wv is wave-uniform, so this is a scalar branch around one s_setprio)
+    if (g.prio && wv >= kFdWaves / 2) __builtin_amdgcn_s_setprio(1);
     float *const srw = lds + kFdRegion + SMALL + wv * 128;  // [16 rows][8]
     const MfmaNet &net = g.net;
     mlp_small_to_lds(g.packed, net, small, true);  // small_r: W1, b1 x 2/ln 2, b2 x 2^(sw+SH)
@@ -537,6 +541,7 @@ struct WArgs {
     const float *g2t;
     const unsigned *g2max;
     float *part;  // [grid][H*H + H]: dW2 | db2
+    int prio;
 };
 
 // B fragments of h1 for one 64-row tile: [ks 2][nt 16][hi, lo][64 lanes][8 halfs] (64 KiB):
@@ -565,6 +570,7 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
     const int S = net.S;
     const int lane = threadIdx.x & 63, gq = lane >> 4, e = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (w.prio && wv >= W / 2) __builtin_amdgcn_s_setprio(1);
     {
         // small_r: W1, b1 x 2/ln 2 (h1 as in the FD forward)
         const float *W1c = w.packed + net.off_small_r;
@@ -825,6 +831,7 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
 
 static int g_fd_mode = 0;      // rlp_set_fd_mode
 static int g_wgrad_waves = 8;  // rlp_set_wgrad_waves
+static int g_update_prio = 0;  // rlp_set_update_prio
 
 static int ppo2_grid() {  // CUs of the device (cached: device properties are slow)
     static int cus = 0;
@@ -905,6 +912,7 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     if (hipMemsetAsync(g.g2max, 0, sizeof(unsigned), st) != hipSuccess)
         return fail(RLP_EINVAL, "rlp_ppo2_grad: memset");
     g.loss_sum = loss_sum;
+    g.prio = g_update_prio;
 #define RLP_FD(KS1, A_, L)                                                                      \
     do {                                                                                        \
         if (fdw == 8) ppo2_fd_kernel<KS1, A_, L, 8><<<gfd, 512, 0, st>>>(g);                    \
@@ -923,7 +931,7 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (fd)");
     WArgs w{};
     w.packed = packed; w.net = net; w.s = s; w.index = index; w.rows = rows;
-    w.g2t = g.g2t; w.g2max = g.g2max; w.part = partw;
+    w.g2t = g.g2t; w.g2max = g.g2max; w.part = partw; w.prio = g_update_prio;
     if (g_wgrad_waves == 4) {
         if (net.ks1 == 1) ppo2_wgrad_kernel<1, 4><<<grid, 256, 0, st>>>(w);
         else ppo2_wgrad_kernel<2, 4><<<grid, 256, 0, st>>>(w);
@@ -947,6 +955,14 @@ int rlp_set_fd_mode(int mode) {
 }
 
 int rlp_get_fd_mode(void) { return g_fd_mode; }
+
+int rlp_set_update_prio(int mode) {
+    if (mode < 0 || mode > 1) return fail(RLP_EINVAL, "rlp_set_update_prio: %d", mode);
+    g_update_prio = mode;
+    return RLP_OK;
+}
+
+int rlp_get_update_prio(void) { return g_update_prio; }
 
 int rlp_set_wgrad_waves(int waves) {
     if (waves != 4 && waves != 8) return fail(RLP_EINVAL, "rlp_set_wgrad_waves: %d", waves);

@@ -18,6 +18,7 @@ class CartPoleAngleOnly(VecEnv):
                  seed=None, env_id0=0):
         p = _abi.angleonly_params(variant)
         super().__init__(p, n_envs, device, seed, env_id0)
+        self.variant = variant
         self.name = 'CartPoleAngleOnly'
         self.initTheta = initTheta
         self.thetaMax, self.staticGain = p.theta_max, p.static_gain

@@ -153,14 +153,15 @@ def rollout(kind, params, state, need_reset, actor_desc, actor_packed, critic_de
 
 def make_rollout_cfg(T, n, seed, step0, env_id0, std, a_min, a_max, success_rule, success_flag,
                      mlp_precision=None, physics=None, sub=None):
-    """rlp_rollout_cfg. mlp_precision (RLP_MLP_FP32 | RLP_MLP_F16X3), physics (0 register-resident,
-    1 shared, 2 shared 8-wave, 3 / 4 shared one-block-per-CU of 32- / 16-env waves) and sub
-    (1 | 2 | 4) select the kernel for
-    this call only; None
-    keeps the library-wide defaults (rlp_set_*)."""
+    """rlp_rollout_cfg. mlp_precision (RLP_MLP_FP32 | RLP_MLP_F16X3), physics (-1 auto, 0
+    register-resident, 1 shared, 2 shared 8-wave, 3 / 4 shared one-block-per-CU of 32- / 16-env
+    waves, 5 / 6 one 4-wave block of 32- / 64-env waves per CU; include/rlp.h) and sub (1 | 2 | 4)
+    select the kernel for this call only; None keeps the library-wide defaults (rlp_set_*)."""
     cfg = _abi.RolloutCfg()
     cfg.mlp_precision = 0 if mlp_precision is None else int(mlp_precision) + 1
-    cfg.physics = 0 if physics is None else int(physics) + 1
+    if physics is not None and not -1 <= int(physics) <= 6:
+        raise ValueError(f"make_rollout_cfg: physics={physics} (-1 auto, 0..6)")
+    cfg.physics = 0 if physics is None else 8 if int(physics) == -1 else int(physics) + 1
     cfg.sub = 0 if sub is None else int(sub)
     cfg.T, cfg.n, cfg.seed, cfg.step0, cfg.env_id0 = T, n, seed, step0, env_id0
     cfg.success_rule, cfg.success_flag = success_rule, success_flag
