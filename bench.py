@@ -642,6 +642,8 @@ def main():
                     "advantage normalisation, SOI / UGV / UAV env steps) against the HBM roof")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
+    ap.add_argument("--fd-mode", type=int, default=-1, choices=[-1, 0, 1, 2],
+                    help="rlp_set_fd_mode for the PPO2 update's FD kernel (-1: library default)")
     ap.add_argument("--rollout-prio", type=int, default=-1, choices=[-1, 0, 1],
                     help="rlp_set_rollout_prio (-1: library default)")
     ap.add_argument("--update-prio", type=int, default=-1, choices=[-1, 0, 1],
@@ -676,6 +678,8 @@ def main():
         _native.lib().rlp_set_update_prio(args.update_prio)
     if args.rollout_prio >= 0:
         _native.lib().rlp_set_rollout_prio(args.rollout_prio)
+    if args.fd_mode >= 0:
+        _native.lib().rlp_set_fd_mode(args.fd_mode)
     _native.set_rollout_physics(PHYSICS_MODES[args.physics])
     prec = _native.MLP_F16X3 if args.precision == "f16x3" else _native.MLP_FP32
     _native.set_mlp_precision(prec)

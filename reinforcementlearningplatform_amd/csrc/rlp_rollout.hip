@@ -533,12 +533,22 @@ packed_forward_kernel(const float *__restrict__ P, MfmaNet net, const float *__r
     }
 }
 
-template <int MODE>
-static int launch_packed_forward(const MfmaNet &net, const float *P, const float *x, float *y,
-                                 int64_t rows, const uint8_t *done, const uint8_t *success,
-                                 int apply_out_act, hipStream_t s) {
-    if (net.H != 256) return fail(RLP_EUNSUPPORTED, "packed forward: hidden width %d", net.H);
-    constexpr int SUB = MODE == 0 ? 4 : 1;
+static int device_cus() {  // CUs of the current device (cached: device properties are slow)
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+    }
+    return cus;
+}
+
+template <int MODE, int SUB>
+static int launch_packed_forward_sub(const MfmaNet &net, const float *P, const float *x, float *y,
+                                     int64_t rows, const uint8_t *done, const uint8_t *success,
+                                     int apply_out_act, hipStream_t s) {
     const int64_t groups = (rows + 16 * SUB - 1) / (16 * SUB);
     int64_t blocks = (groups + 3) / 4;
     if (blocks > 2048) blocks = 2048;
@@ -557,6 +567,18 @@ static int launch_packed_forward(const MfmaNet &net, const float *P, const float
 #undef RLP_PF
     RLP_CHECK_LAUNCH("packed forward");
     return RLP_OK;
+}
+
+// 64 rows per wave for large batches (learn()'s V(s) over a whole segment), 16 when that would
+// leave CUs idle (the lidar rollout's per-step forwards over n envs; the value fix-up)
+template <int MODE>
+static int launch_packed_forward(const MfmaNet &net, const float *P, const float *x, float *y,
+                                 int64_t rows, const uint8_t *done, const uint8_t *success,
+                                 int apply_out_act, hipStream_t s) {
+    if (net.H != 256) return fail(RLP_EUNSUPPORTED, "packed forward: hidden width %d", net.H);
+    if (MODE == 0 && rows >= (int64_t)64 * 4 * 2 * device_cus())
+        return launch_packed_forward_sub<MODE, 4>(net, P, x, y, rows, done, success, apply_out_act, s);
+    return launch_packed_forward_sub<MODE, 1>(net, P, x, y, rows, done, success, apply_out_act, s);
 }
 
 static int g_rollout_shared_physics = -1;  // rlp_set_rollout_physics (-1: auto)
