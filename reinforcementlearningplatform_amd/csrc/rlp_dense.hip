@@ -686,10 +686,12 @@ const float *layer_out(const rlp_dense_net &n, const float *act, int B, int l) {
 // backward of a relu net from dY of its last layer (in g[0]); weight gradients into grad (same
 // layout as params) when grad != NULL; optionally the input gradient of columns [c0, c0 + nc)
 // with the tanh-affine backward of the layer that produced them (the actor's head) into dx
+// (dy_top: dY of the last layer; g0 / g1 ping-pong for the layers below, either may be dy_top)
 void net_bwd(const rlp_dense_net &n, const float *params, float *grad, const Opnd &x, int B,
-             const float *act, float *g0, float *g1, float *part, int splits, int c0, int nc,
-             const float *t_in, const float *gain, float *dx, hipStream_t s) {
-    float *dy = g0, *dn = g1;
+             const float *act, const float *dy_top, float *g0, float *g1, float *part, int splits,
+             int c0, int nc, const float *t_in, const float *gain, float *dx, hipStream_t s) {
+    const float *dy = dy_top;
+    float *dn = dy_top == g0 ? g1 : g0;
     for (int l = n.n_layers - 1; l >= 0; --l) {
         const Layer L = layer_of(n, params, l);
         const Opnd xin = l == 0 ? x : mat(layer_out(n, act, B, l - 1), B, L.in, L.in);
@@ -699,7 +701,9 @@ void net_bwd(const rlp_dense_net &n, const float *params, float *grad, const Opn
         if (l > 0) {
             const float *h = layer_out(n, act, B, l - 1);
             dense_bwd_data(dy, L, B, 0, L.in, kEpiReluBack, h, L.in, nullptr, dn, s);
-            float *tmp = dy; dy = dn; dn = tmp;
+            float *nxt = dn == g0 ? g1 : g0;
+            dy = dn;
+            dn = nxt;
         } else if (dx) {
             dense_bwd_data(dy, L, B, c0, nc, t_in ? kEpiTanhAffBack : kEpiNone, t_in, nc, gain, dx, s);
         }
@@ -755,7 +759,7 @@ int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const fl
     ddpg_td_kernel<<<1, 1024, 0, st>>>(r, end, layer_out(n.target_critic, tc, B, Lc - 1),
                                        layer_out(n.critic, c, B, Lc - 1), B, cfg->gamma, g0, losses,
                                        n.steps);
-    net_bwd(n.critic, n.critic.params, n.critic_grad, sa, B, c, g0, g1, part, splits, 0, 0, nullptr,
+    net_bwd(n.critic, n.critic.params, n.critic_grad, sa, B, c, g0, g0, g1, part, splits, 0, 0, nullptr,
             nullptr, nullptr, st);
     adam_dev(n.critic.params, n.critic_grad, n.critic_m, n.critic_v, n.critic.n_params, cfg->critic_adam,
              n.steps + 1, st);
@@ -765,8 +769,8 @@ int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const fl
     const Opnd sp = cat2(s, S, S, a_pi, A, A, B);
     net_fwd(n.critic, n.critic.params, sp, B, pc, false, nullptr, nullptr, nullptr, st);
     ddpg_actor_loss_kernel<<<1, 1024, 0, st>>>(layer_out(n.critic, pc, B, Lc - 1), B, g0, losses);
-    net_bwd(n.critic, n.critic.params, nullptr, sp, B, pc, g0, g1, part, splits, S, A, pa_t, n.gain, dq,
-            st);
+    net_bwd(n.critic, n.critic.params, nullptr, sp, B, pc, g0, g0, g1, part, splits, S, A, pa_t, n.gain,
+            dq, st);
     // dq now holds dL/dz of the actor's head ([B][A]); back through the actor
     const Opnd s_in = mat(s, B, S, S);
     {
@@ -933,13 +937,10 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
                                               n.log_alpha, ad, cfg->alpha, cfg->target_entropy,
                                               W(w.g1), W(w.g2), losses, n.alpha_grad, n.steps,
                                               n.counter);
-    // (net_bwd's ping-pong buffers start with dY in the first one)
-    hipMemcpyAsync(W(w.d0), W(w.g1), sizeof(float) * B, hipMemcpyDeviceToDevice, st);
-    net_bwd(n.q1, n.q1.params, nullptr, px, B, W(w.p1), W(w.d0), W(w.d1), W(w.part), splits, S, A,
-            nullptr, nullptr, W(w.da1), st);
-    hipMemcpyAsync(W(w.d0), W(w.g2), sizeof(float) * B, hipMemcpyDeviceToDevice, st);
-    net_bwd(n.q2, n.q2.params, nullptr, px, B, W(w.p2), W(w.d0), W(w.d1), W(w.part), splits, S, A,
-            nullptr, nullptr, W(w.da2), st);
+    net_bwd(n.q1, n.q1.params, nullptr, px, B, W(w.p1), W(w.g1), W(w.d0), W(w.d1), W(w.part), splits,
+            S, A, nullptr, nullptr, W(w.da1), st);
+    net_bwd(n.q2, n.q2.params, nullptr, px, B, W(w.p2), W(w.g2), W(w.d0), W(w.d1), W(w.part), splits,
+            S, A, nullptr, nullptr, W(w.da2), st);
     switch (A) {
     case 1: sac_head_back_kernel<1><<<g, 256, 0, st>>>(W(w.save), W(w.da1), W(w.da2), B, n.gain, n.log_alpha, ad, cfg->alpha, W(w.gz)); break;
     case 2: sac_head_back_kernel<2><<<g, 256, 0, st>>>(W(w.save), W(w.da1), W(w.da2), B, n.gain, n.log_alpha, ad, cfg->alpha, W(w.gz)); break;
@@ -983,12 +984,10 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
     sac_critic_loss_kernel<<<1, 1024, 0, st>>>(layer_out(n.q1, W(w.c1), B, Lq1 - 1),
                                                layer_out(n.q2, W(w.c2), B, Lq2 - 1), W(w.y), B,
                                                W(w.g1), W(w.g2), losses);
-    hipMemcpyAsync(W(w.d0), W(w.g1), sizeof(float) * B, hipMemcpyDeviceToDevice, st);
-    net_bwd(n.q1, n.q1.params, n.critic_grad, bx, B, W(w.c1), W(w.d0), W(w.d1), W(w.part), splits, 0,
-            0, nullptr, nullptr, nullptr, st);
-    hipMemcpyAsync(W(w.d0), W(w.g2), sizeof(float) * B, hipMemcpyDeviceToDevice, st);
-    net_bwd(n.q2, n.q2.params, n.critic_grad, bx, B, W(w.c2), W(w.d0), W(w.d1), W(w.part), splits, 0,
-            0, nullptr, nullptr, nullptr, st);
+    net_bwd(n.q1, n.q1.params, n.critic_grad, bx, B, W(w.c1), W(w.g1), W(w.d0), W(w.d1), W(w.part),
+            splits, 0, 0, nullptr, nullptr, nullptr, st);
+    net_bwd(n.q2, n.q2.params, n.critic_grad, bx, B, W(w.c2), W(w.g2), W(w.d0), W(w.d1), W(w.part),
+            splits, 0, 0, nullptr, nullptr, nullptr, st);
     // optimizer steps (actor, critic, temperature), then the soft target update
     adam_dev(n.actor.params, n.actor_grad, n.actor_m, n.actor_v, n.actor.n_params, cfg->actor_adam,
              n.steps, st);
