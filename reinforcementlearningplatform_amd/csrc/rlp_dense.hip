@@ -166,10 +166,16 @@ __device__ __forceinline__ void stage_panel(const Opnd &o, bool is_a, int u0, in
 // [m][r] and B as [n][r] (row stride 260 floats: the 16 x 4 fragment reads hit 64 distinct banks);
 // the reduction order is permuted so that each lane's operands for four consecutive MFMA steps
 // are contiguous (one 16-byte LDS read): step s, lane group g reads r = g * Q + s.
-__global__ void __launch_bounds__(256) dense_gemm_kernel(Opnd A, Opnd B, int R, int rchunk, Epi e) {
+// Two problems of the same shape in one launch (the twin critic's chains): row tiles
+// [0, mt0) of the grid run (A0, B0, e0), the rest (A1, B1, e1); one problem: mt0 = gridDim.y.
+__global__ void __launch_bounds__(256) dense_gemm_kernel(Opnd A0, Opnd B0, Epi e0, Opnd A1, Opnd B1,
+                                                         Epi e1, int mt0, int R, int rchunk) {
     extern __shared__ float lds[];
     float *As = lds, *Bs = lds + kDT * kDLd;
-    const int m0 = blockIdx.y * kDT, n0 = blockIdx.x * kDT;
+    const bool second = (int)blockIdx.y >= mt0;  // block-uniform
+    const Opnd A = second ? A1 : A0, B = second ? B1 : B0;
+    const Epi e = second ? e1 : e0;
+    const int m0 = ((int)blockIdx.y - (second ? mt0 : 0)) * kDT, n0 = blockIdx.x * kDT;
     const int r_lo = blockIdx.z * rchunk, rc = min(R, r_lo + rchunk) - r_lo;
     const int Q = (rc + 15) / 16 * 4;  // MFMA steps (multiple of 4); rows g * Q + s, s < Q
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
@@ -232,10 +238,16 @@ __global__ void __launch_bounds__(256) dense_gemm_kernel(Opnd A, Opnd B, int R, 
             }
 }
 
-// grad[m][n] = sum over the splits of the partials, in split order; column N-1 is the bias
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float *__restrict__ part, int splits,
-                                                           int M, int N, float *__restrict__ gW,
-                                                           float *__restrict__ gb) {
+// grad[m][n] = sum over the splits of the partials, in split order; column N-1 is the bias.
+// blockIdx.y = 1: the second problem of a twin launch (part1 -> gW1, gb1)
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float *__restrict__ part0, int splits,
+                                                           int M, int N, float *__restrict__ gW0,
+                                                           float *__restrict__ gb0,
+                                                           const float *__restrict__ part1,
+                                                           float *__restrict__ gW1,
+                                                           float *__restrict__ gb1) {
+    const float *part = blockIdx.y ? part1 : part0;
+    float *gW = blockIdx.y ? gW1 : gW0, *gb = blockIdx.y ? gb1 : gb0;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= M * N) return;
     float s = 0.f;
@@ -537,20 +549,27 @@ inline Opnd transposed(const float *p, int rows, int cols, int ld) {  // (i, j) 
 constexpr size_t kDenseLds = 2 * kDT * kDLd * sizeof(float);  // 133 120 B
 
 // splits >= ceil(R / 256) slices of the reduction (each <= 256 rows); returns the slice count
-int gemm(const Opnd &A, const Opnd &B, int M, int N, int R, int splits, const Epi &e, hipStream_t s) {
+// one problem, or two of the same shape (A1 != nullptr) in one launch
+int gemm_impl(const Opnd &A, const Opnd &B, const Epi &e, const Opnd *A1, const Opnd *B1,
+              const Epi *e1, int M, int N, int R, int splits, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        hipFuncSetAttribute((const void *)dense_gemm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kDenseLds);
+        (void)hipFuncSetAttribute((const void *)dense_gemm_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDenseLds);
         attr = true;
     }
     const int need = (R + kDRc - 1) / kDRc;
     const int sp = splits > need ? splits : need;
     const int rchunk = ((R + sp - 1) / sp + 15) / 16 * 16;
     const int z = (R + rchunk - 1) / rchunk;
-    dim3 grid((N + kDT - 1) / kDT, (M + kDT - 1) / kDT, z > 0 ? z : 1);
-    dense_gemm_kernel<<<grid, 256, kDenseLds, s>>>(A, B, R, rchunk, e);
+    const int mt = (M + kDT - 1) / kDT;
+    dim3 grid((N + kDT - 1) / kDT, A1 ? 2 * mt : mt, z > 0 ? z : 1);
+    dense_gemm_kernel<<<grid, 256, kDenseLds, s>>>(A, B, e, A1 ? *A1 : A, B1 ? *B1 : B, e1 ? *e1 : e, mt,
+                                                   R, rchunk);
     return z > 0 ? z : 1;
+}
+int gemm(const Opnd &A, const Opnd &B, int M, int N, int R, int splits, const Epi &e, hipStream_t s) {
+    return gemm_impl(A, B, e, nullptr, nullptr, nullptr, M, N, R, splits, s);
 }
 
 struct Layer {
@@ -591,7 +610,7 @@ void dense_wgrad(const float *dy, const Opnd &x, const Layer &L, int B, float *p
     const int z = gemm(transposed(dy, L.out, B, (int)(ldy < 0 ? L.out : ldy)), xo, L.out, L.in + 1, B, splits,
                        e, s);
     const int tot = L.out * (L.in + 1);
-    wgrad_reduce_kernel<<<(tot + 255) / 256, 256, 0, s>>>(part, z, L.out, L.in + 1, gW, gb);
+    wgrad_reduce_kernel<<<(tot + 255) / 256, 256, 0, s>>>(part, z, L.out, L.in + 1, gW, gb, part, gW, gb);
 }
 
 void adam_dev(float *p, const float *g, float *m, float *v, int64_t n, const rlp_adam_cfg &c,
@@ -710,6 +729,87 @@ void net_bwd(const rlp_dense_net &n, const float *params, float *grad, const Opn
     }
 }
 
+// ---- twin chains (the SAC critic's Q1 / Q2: same shapes, one parameter buffer) in shared launches
+bool same_dims(const rlp_dense_net &a, const rlp_dense_net &b) {
+    if (a.n_layers != b.n_layers) return false;
+    for (int l = 0; l <= a.n_layers; ++l)
+        if (a.dims[l] != b.dims[l]) return false;
+    return true;
+}
+
+// two same-shaped chains, each with its own parameters and input (p2 / x2 default to p1 / x1)
+void twin_fwd(const rlp_dense_net &n1, const rlp_dense_net &n2, const float *params, const Opnd &x,
+              int B, float *act1, float *act2, hipStream_t s, const float *params2 = nullptr,
+              const Opnd *x2 = nullptr) {
+    int64_t o = 0;
+    Opnd in1 = x, in2 = x2 ? *x2 : x;
+    for (int l = 0; l < n1.n_layers; ++l) {
+        const Layer L1 = layer_of(n1, params, l), L2 = layer_of(n2, params2 ? params2 : params, l);
+        const int kind = l == n1.n_layers - 1 ? kEpiNone : kEpiRelu;
+        Epi e1{}, e2{};
+        e1.y = act1 + o; e1.ldy = L1.out; e1.bias = L1.b; e1.kind = kind; e1.M = B; e1.N = L1.out;
+        e2 = e1;
+        e2.y = act2 + o; e2.bias = L2.b;
+        const Opnd W1{L1.W, L1.W, 1, L1.in, 1, L1.in, L1.in, L1.out, L1.out, -1, 0};
+        const Opnd W2{L2.W, L2.W, 1, L2.in, 1, L2.in, L2.in, L2.out, L2.out, -1, 0};
+        gemm_impl(in1, W1, e1, &in2, &W2, &e2, B, L1.out, L1.in, 1, s);
+        in1 = mat(act1 + o, B, L1.out, L1.out);
+        in2 = mat(act2 + o, B, L2.out, L2.out);
+        o += (int64_t)B * L1.out;
+    }
+}
+
+// backward of both chains from their last layers' dY (dy1 / dy2): weight gradients into grad
+// (when non-null; part1 / part2 the two problems' partials), input gradients of columns
+// [c0, c0 + nc) into dx1 / dx2 (when non-null). d[0..3]: ping-pong buffers (two per chain).
+void twin_bwd(const rlp_dense_net &n1, const rlp_dense_net &n2, const float *params, float *grad,
+              const Opnd &x, int B, const float *act1, const float *act2, const float *dy1,
+              const float *dy2, float *const d[4], float *part1, float *part2, int splits, int c0,
+              int nc, float *dx1, float *dx2, hipStream_t s) {
+    const float *y1 = dy1, *y2 = dy2;
+    int pp = 0;
+    for (int l = n1.n_layers - 1; l >= 0; --l) {
+        const Layer L1 = layer_of(n1, params, l), L2 = layer_of(n2, params, l);
+        const Opnd x1 = l == 0 ? x : mat(layer_out(n1, act1, B, l - 1), B, L1.in, L1.in);
+        const Opnd x2 = l == 0 ? x : mat(layer_out(n2, act2, B, l - 1), B, L2.in, L2.in);
+        if (grad) {
+            Epi e1{}, e2{};
+            e1.y = part1; e1.kind = kEpiPartial; e1.M = L1.out; e1.N = L1.in + 1;
+            e2 = e1;
+            e2.y = part2;
+            Opnd xo1 = x1, xo2 = x2;
+            xo1.cols = xo2.cols = L1.in + 1;
+            xo1.ones = xo2.ones = L1.in;
+            const Opnd t1 = transposed(y1, L1.out, B, L1.out), t2 = transposed(y2, L2.out, B, L2.out);
+            const int z = gemm_impl(t1, xo1, e1, &t2, &xo2, &e2, L1.out, L1.in + 1, B, splits, s);
+            const int tot = L1.out * (L1.in + 1);
+            wgrad_reduce_kernel<<<dim3((tot + 255) / 256, 2), 256, 0, s>>>(
+                part1, z, L1.out, L1.in + 1, grad + n1.offset[l], grad + n1.offset[l] + (int64_t)L1.in * L1.out,
+                part2, grad + n2.offset[l], grad + n2.offset[l] + (int64_t)L2.in * L2.out);
+        }
+        if (l > 0 || dx1) {
+            const int cc = l > 0 ? 0 : c0, nn = l > 0 ? L1.in : nc;
+            float *o1 = l > 0 ? d[pp] : dx1, *o2 = l > 0 ? d[2 + pp] : dx2;
+            Epi e1{}, e2{};
+            e1.y = o1; e1.ldy = nn; e1.kind = l > 0 ? kEpiReluBack : kEpiNone; e1.M = B; e1.N = nn;
+            e2 = e1;
+            e2.y = o2;
+            if (l > 0) {
+                e1.mask = layer_out(n1, act1, B, l - 1); e1.ldm = L1.in;
+                e2.mask = layer_out(n2, act2, B, l - 1); e2.ldm = L2.in;
+            }
+            const Opnd a1 = mat(y1, B, L1.out, L1.out), a2 = mat(y2, B, L2.out, L2.out);
+            const Opnd w1 = mat(L1.W + cc, L1.out, nn, L1.in), w2 = mat(L2.W + cc, L2.out, nn, L2.in);
+            gemm_impl(a1, w1, e1, &a2, &w2, &e2, B, nn, L1.out, 1, s);
+            if (l > 0) {
+                y1 = o1;
+                y2 = o2;
+                pp ^= 1;
+            }
+        }
+    }
+}
+
 }  // namespace rlp
 
 using namespace rlp;
@@ -751,11 +851,9 @@ int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const fl
     net_fwd(n.target_actor, n.target_actor.params, mat(s_next, B, S, S), B, ta, true, n.gain, n.off,
             ta_t, st);
     const float *a_next = layer_out(n.target_actor, ta, B, La - 1);
-    net_fwd(n.target_critic, n.target_critic.params, cat2(s_next, S, S, a_next, A, A, B), B, tc, false,
-            nullptr, nullptr, nullptr, st);
-    // critic: Q(s, a), TD target, MSE gradient, backward, Adam
-    const Opnd sa = cat2(s, S, S, a, A, A, B);
-    net_fwd(n.critic, n.critic.params, sa, B, c, false, nullptr, nullptr, nullptr, st);
+    // Q'(s', a') of the target critic and Q(s, a) of the critic: same shapes, shared launches
+    const Opnd tx = cat2(s_next, S, S, a_next, A, A, B), sa = cat2(s, S, S, a, A, A, B);
+    twin_fwd(n.target_critic, n.critic, n.target_critic.params, tx, B, tc, c, st, n.critic.params, &sa);
     ddpg_td_kernel<<<1, 1024, 0, st>>>(r, end, layer_out(n.target_critic, tc, B, Lc - 1),
                                        layer_out(n.critic, c, B, Lc - 1), B, cfg->gamma, g0, losses,
                                        n.steps);
@@ -804,7 +902,7 @@ namespace rlp {
 
 struct SacWs {
     int64_t tn_act, tn_z, tn_a, tn_lp, tq1, tq2, ta, tz, ta_a, ta_lp, save, p1, p2, c1, c2, y, g1,
-        g2, da1, da2, gz, d0, d1, part, total;
+        g2, da1, da2, gz, d0, d1, d2, d3, part, part2, total;
 };
 SacWs sac_ws(const rlp_sac_nets &n, int B) {
     SacWs w{};
@@ -824,8 +922,10 @@ SacWs sac_ws(const rlp_sac_nets &n, int B) {
     mw = max_width(n.q2) > mw ? max_width(n.q2) : mw;
     mw = 2 * A > mw ? 2 * A : mw;
     w.d0 = take((int64_t)B * mw); w.d1 = take((int64_t)B * mw);
+    w.d2 = take((int64_t)B * mw); w.d3 = take((int64_t)B * mw);
     const int splits = (B + kWgradRows - 1) / kWgradRows;
     w.part = take((int64_t)splits * mw * (mw + 1));
+    w.part2 = take((int64_t)splits * mw * (mw + 1));
     w.total = o;
     return w;
 }
@@ -920,8 +1020,14 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
     int rc = sac_head(n, *cfg, W(w.tn_z), B, noise, 0, W(w.tn_a), W(w.tn_lp), nullptr, st);
     if (rc != RLP_OK) return fail(rc, "rlp_sac_update: action_dim %d", A);
     const Opnd tx = cat2(s_next, S, S, W(w.tn_a), A, A, B);
-    net_fwd(n.q1, n.target_critic, tx, B, W(w.tq1), false, nullptr, nullptr, nullptr, st);
-    net_fwd(n.q2, n.target_critic, tx, B, W(w.tq2), false, nullptr, nullptr, nullptr, st);
+    const bool twin = same_dims(n.q1, n.q2);  // Q1 / Q2 GEMMs share launches
+    float *const dd[4] = {W(w.d0), W(w.d1), W(w.d2), W(w.d3)};
+    if (twin) {
+        twin_fwd(n.q1, n.q2, n.target_critic, tx, B, W(w.tq1), W(w.tq2), st);
+    } else {
+        net_fwd(n.q1, n.target_critic, tx, B, W(w.tq1), false, nullptr, nullptr, nullptr, st);
+        net_fwd(n.q2, n.target_critic, tx, B, W(w.tq2), false, nullptr, nullptr, nullptr, st);
+    }
     sac_target_kernel<<<g, 256, 0, st>>>(r, dw, layer_out(n.q1, W(w.tq1), B, Lq1 - 1),
                                          layer_out(n.q2, W(w.tq2), B, Lq2 - 1), W(w.tn_lp), B,
                                          cfg->gamma, n.log_alpha, ad, cfg->alpha, W(w.y));
@@ -930,17 +1036,26 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
     sac_head(n, *cfg, W(w.tz), B, noise ? noise + (size_t)B * A : nullptr, 1, W(w.ta_a), W(w.ta_lp),
              W(w.save), st);
     const Opnd px = cat2(s, S, S, W(w.ta_a), A, A, B);
-    net_fwd(n.q1, n.q1.params, px, B, W(w.p1), false, nullptr, nullptr, nullptr, st);
-    net_fwd(n.q2, n.q2.params, px, B, W(w.p2), false, nullptr, nullptr, nullptr, st);
+    if (twin) {
+        twin_fwd(n.q1, n.q2, n.q1.params, px, B, W(w.p1), W(w.p2), st);
+    } else {
+        net_fwd(n.q1, n.q1.params, px, B, W(w.p1), false, nullptr, nullptr, nullptr, st);
+        net_fwd(n.q2, n.q2.params, px, B, W(w.p2), false, nullptr, nullptr, nullptr, st);
+    }
     sac_actor_loss_kernel<<<1, 1024, 0, st>>>(layer_out(n.q1, W(w.p1), B, Lq1 - 1),
                                               layer_out(n.q2, W(w.p2), B, Lq2 - 1), W(w.ta_lp), B,
                                               n.log_alpha, ad, cfg->alpha, cfg->target_entropy,
                                               W(w.g1), W(w.g2), losses, n.alpha_grad, n.steps,
                                               n.counter);
-    net_bwd(n.q1, n.q1.params, nullptr, px, B, W(w.p1), W(w.g1), W(w.d0), W(w.d1), W(w.part), splits,
-            S, A, nullptr, nullptr, W(w.da1), st);
-    net_bwd(n.q2, n.q2.params, nullptr, px, B, W(w.p2), W(w.g2), W(w.d0), W(w.d1), W(w.part), splits,
-            S, A, nullptr, nullptr, W(w.da2), st);
+    if (twin) {
+        twin_bwd(n.q1, n.q2, n.q1.params, nullptr, px, B, W(w.p1), W(w.p2), W(w.g1), W(w.g2), dd,
+                 W(w.part), W(w.part2), splits, S, A, W(w.da1), W(w.da2), st);
+    } else {
+        net_bwd(n.q1, n.q1.params, nullptr, px, B, W(w.p1), W(w.g1), W(w.d0), W(w.d1), W(w.part),
+                splits, S, A, nullptr, nullptr, W(w.da1), st);
+        net_bwd(n.q2, n.q2.params, nullptr, px, B, W(w.p2), W(w.g2), W(w.d0), W(w.d1), W(w.part),
+                splits, S, A, nullptr, nullptr, W(w.da2), st);
+    }
     switch (A) {
     case 1: sac_head_back_kernel<1><<<g, 256, 0, st>>>(W(w.save), W(w.da1), W(w.da2), B, n.gain, n.log_alpha, ad, cfg->alpha, W(w.gz)); break;
     case 2: sac_head_back_kernel<2><<<g, 256, 0, st>>>(W(w.save), W(w.da1), W(w.da2), B, n.gain, n.log_alpha, ad, cfg->alpha, W(w.gz)); break;
@@ -979,15 +1094,24 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
     }
     // critic: Q1, Q2 on the batch's actions, MSE to target_Q, backward into the critic's gradient
     const Opnd bx = cat2(s, S, S, a, A, A, B);
-    net_fwd(n.q1, n.q1.params, bx, B, W(w.c1), false, nullptr, nullptr, nullptr, st);
-    net_fwd(n.q2, n.q2.params, bx, B, W(w.c2), false, nullptr, nullptr, nullptr, st);
+    if (twin) {
+        twin_fwd(n.q1, n.q2, n.q1.params, bx, B, W(w.c1), W(w.c2), st);
+    } else {
+        net_fwd(n.q1, n.q1.params, bx, B, W(w.c1), false, nullptr, nullptr, nullptr, st);
+        net_fwd(n.q2, n.q2.params, bx, B, W(w.c2), false, nullptr, nullptr, nullptr, st);
+    }
     sac_critic_loss_kernel<<<1, 1024, 0, st>>>(layer_out(n.q1, W(w.c1), B, Lq1 - 1),
                                                layer_out(n.q2, W(w.c2), B, Lq2 - 1), W(w.y), B,
                                                W(w.g1), W(w.g2), losses);
-    net_bwd(n.q1, n.q1.params, n.critic_grad, bx, B, W(w.c1), W(w.g1), W(w.d0), W(w.d1), W(w.part),
-            splits, 0, 0, nullptr, nullptr, nullptr, st);
-    net_bwd(n.q2, n.q2.params, n.critic_grad, bx, B, W(w.c2), W(w.g2), W(w.d0), W(w.d1), W(w.part),
-            splits, 0, 0, nullptr, nullptr, nullptr, st);
+    if (twin) {
+        twin_bwd(n.q1, n.q2, n.q1.params, n.critic_grad, bx, B, W(w.c1), W(w.c2), W(w.g1), W(w.g2), dd,
+                 W(w.part), W(w.part2), splits, 0, 0, nullptr, nullptr, st);
+    } else {
+        net_bwd(n.q1, n.q1.params, n.critic_grad, bx, B, W(w.c1), W(w.g1), W(w.d0), W(w.d1),
+                W(w.part), splits, 0, 0, nullptr, nullptr, nullptr, st);
+        net_bwd(n.q2, n.q2.params, n.critic_grad, bx, B, W(w.c2), W(w.g2), W(w.d0), W(w.d1),
+                W(w.part), splits, 0, 0, nullptr, nullptr, nullptr, st);
+    }
     // optimizer steps (actor, critic, temperature), then the soft target update
     adam_dev(n.actor.params, n.actor_grad, n.actor_m, n.actor_v, n.actor.n_params, cfg->actor_adam,
              n.steps, st);
