@@ -166,16 +166,25 @@ __device__ __forceinline__ void stage_panel(const Opnd &o, bool is_a, int u0, in
 // [m][r] and B as [n][r] (row stride 260 floats: the 16 x 4 fragment reads hit 64 distinct banks);
 // the reduction order is permuted so that each lane's operands for four consecutive MFMA steps
 // are contiguous (one 16-byte LDS read): step s, lane group g reads r = g * Q + s.
-// Two problems of the same shape in one launch (the twin critic's chains): row tiles
-// [0, mt0) of the grid run (A0, B0, e0), the rest (A1, B1, e1); one problem: mt0 = gridDim.y.
-__global__ void __launch_bounds__(256) dense_gemm_kernel(Opnd A0, Opnd B0, Epi e0, Opnd A1, Opnd B1,
-                                                         Epi e1, int mt0, int R, int rchunk) {
+struct Prob {
+    Opnd A, B;
+    Epi e;
+    int R, rchunk;  // reduction length, rows per gridDim.z slice
+};
+
+// Up to two independent problems in one launch (the twin critic's chains, a layer's weight
+// gradient beside its backward data pass): row tiles [0, mt0) of the grid run p0, the rest p1;
+// blocks past a problem's column tiles or reduction slices exit at once (one problem: mt0 =
+// gridDim.y).
+__global__ void __launch_bounds__(256) dense_gemm_kernel(Prob p0, Prob p1, int mt0) {
     extern __shared__ float lds[];
     float *As = lds, *Bs = lds + kDT * kDLd;
     const bool second = (int)blockIdx.y >= mt0;  // block-uniform
-    const Opnd A = second ? A1 : A0, B = second ? B1 : B0;
-    const Epi e = second ? e1 : e0;
+    const Opnd A = second ? p1.A : p0.A, B = second ? p1.B : p0.B;
+    const Epi e = second ? p1.e : p0.e;
+    const int R = second ? p1.R : p0.R, rchunk = second ? p1.rchunk : p0.rchunk;
     const int m0 = ((int)blockIdx.y - (second ? mt0 : 0)) * kDT, n0 = blockIdx.x * kDT;
+    if (n0 >= e.N || (int)blockIdx.z * rchunk >= R) return;  // (before any barrier)
     const int r_lo = blockIdx.z * rchunk, rc = min(R, r_lo + rchunk) - r_lo;
     const int Q = (rc + 15) / 16 * 4;  // MFMA steps (multiple of 4); rows g * Q + s, s < Q
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
@@ -549,24 +558,35 @@ inline Opnd transposed(const float *p, int rows, int cols, int ld) {  // (i, j) 
 constexpr size_t kDenseLds = 2 * kDT * kDLd * sizeof(float);  // 133 120 B
 
 // splits >= ceil(R / 256) slices of the reduction (each <= 256 rows); returns the slice count
-// one problem, or two of the same shape (A1 != nullptr) in one launch
-int gemm_impl(const Opnd &A, const Opnd &B, const Epi &e, const Opnd *A1, const Opnd *B1,
-              const Epi *e1, int M, int N, int R, int splits, hipStream_t s) {
+// a problem's reduction slicing: splits >= ceil(R / 256) slices, each <= 256 rows
+inline Prob make_prob(const Opnd &A, const Opnd &B, const Epi &e, int R, int splits) {
+    const int need = (R + kDRc - 1) / kDRc;
+    const int sp = splits > need ? splits : need;
+    return Prob{A, B, e, R, ((R + sp - 1) / sp + 15) / 16 * 16};
+}
+inline int prob_slices(const Prob &p) { return p.R > 0 ? (p.R + p.rchunk - 1) / p.rchunk : 1; }
+
+// one problem, or two (q1 != nullptr) in one launch; returns p0's slice count
+int gemm_launch(const Prob &q0, int M0, const Prob *q1, int M1, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)dense_gemm_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDenseLds);
         attr = true;
     }
-    const int need = (R + kDRc - 1) / kDRc;
-    const int sp = splits > need ? splits : need;
-    const int rchunk = ((R + sp - 1) / sp + 15) / 16 * 16;
-    const int z = (R + rchunk - 1) / rchunk;
-    const int mt = (M + kDT - 1) / kDT;
-    dim3 grid((N + kDT - 1) / kDT, A1 ? 2 * mt : mt, z > 0 ? z : 1);
-    dense_gemm_kernel<<<grid, 256, kDenseLds, s>>>(A, B, e, A1 ? *A1 : A, B1 ? *B1 : B, e1 ? *e1 : e, mt,
-                                                   R, rchunk);
-    return z > 0 ? z : 1;
+    const int mt0 = (M0 + kDT - 1) / kDT, mt1 = q1 ? (M1 + kDT - 1) / kDT : 0;
+    const int nt0 = (q0.e.N + kDT - 1) / kDT, nt1 = q1 ? (q1->e.N + kDT - 1) / kDT : 0;
+    const int z0 = prob_slices(q0), z1 = q1 ? prob_slices(*q1) : 0;
+    dim3 grid(nt0 > nt1 ? nt0 : nt1, mt0 + mt1, z0 > z1 ? z0 : z1);
+    dense_gemm_kernel<<<grid, 256, kDenseLds, s>>>(q0, q1 ? *q1 : q0, mt0);
+    return z0;
+}
+int gemm_impl(const Opnd &A, const Opnd &B, const Epi &e, const Opnd *A1, const Opnd *B1,
+              const Epi *e1, int M, int N, int R, int splits, hipStream_t s) {
+    const Prob q0 = make_prob(A, B, e, R, splits);
+    if (!A1) return gemm_launch(q0, M, nullptr, 0, s);
+    const Prob q1 = make_prob(*A1, *B1, *e1, R, splits);
+    return gemm_launch(q0, M, &q1, M, s);
 }
 int gemm(const Opnd &A, const Opnd &B, int M, int N, int R, int splits, const Epi &e, hipStream_t s) {
     return gemm_impl(A, B, e, nullptr, nullptr, nullptr, M, N, R, splits, s);
@@ -592,25 +612,47 @@ void dense_fwd(const Opnd &x, const Layer &L, int B, int act, float *y, const fl
 }
 
 // dX[:, c0:c0+nc] = (dY W[:, c0:c0+nc]) with the epilogue (relu' mask or tanh-affine backward)
-void dense_bwd_data(const float *dy, const Layer &L, int B, int c0, int nc, int kind,
-                    const float *mask, int64_t ldm, const float *gain, float *dx, hipStream_t s) {
+Prob bwd_data_prob(const float *dy, const Layer &L, int B, int c0, int nc, int kind, const float *mask,
+                   int64_t ldm, const float *gain, float *dx) {
     Epi e{};
     e.y = dx; e.ldy = nc; e.kind = kind; e.M = B; e.N = nc; e.mask = mask; e.ldm = ldm; e.gain = gain;
-    gemm(mat(dy, B, L.out, L.out), mat(L.W + c0, L.out, nc, L.in), B, nc, L.out, 1, e, s);
+    return make_prob(mat(dy, B, L.out, L.out), mat(L.W + c0, L.out, nc, L.in), e, L.out, 1);
+}
+
+void dense_bwd_data(const float *dy, const Layer &L, int B, int c0, int nc, int kind,
+                    const float *mask, int64_t ldm, const float *gain, float *dx, hipStream_t s) {
+    const Prob q = bwd_data_prob(dy, L, B, c0, nc, kind, mask, ldm, gain, dx);
+    gemm_launch(q, B, nullptr, 0, s);
 }
 
 // gW = dY^T X, gb = column sums of dY: split over the batch, partials reduced in fixed order
-void dense_wgrad(const float *dy, const Opnd &x, const Layer &L, int B, float *part, int splits,
-                 float *gW, float *gb, hipStream_t s, int64_t ldy = -1) {
+Prob wgrad_prob(const float *dy, const Opnd &x, const Layer &L, int B, float *part, int splits,
+                int64_t ldy) {
     Epi e{};
     e.y = part; e.kind = kEpiPartial; e.M = L.out; e.N = L.in + 1;
     Opnd xo = x;
     xo.cols = L.in + 1;
     xo.ones = L.in;
-    const int z = gemm(transposed(dy, L.out, B, (int)(ldy < 0 ? L.out : ldy)), xo, L.out, L.in + 1, B, splits,
-                       e, s);
+    return make_prob(transposed(dy, L.out, B, (int)(ldy < 0 ? L.out : ldy)), xo, e, B, splits);
+}
+void wgrad_reduce(const Layer &L, const float *part, int z, float *gW, float *gb, hipStream_t s) {
     const int tot = L.out * (L.in + 1);
     wgrad_reduce_kernel<<<(tot + 255) / 256, 256, 0, s>>>(part, z, L.out, L.in + 1, gW, gb, part, gW, gb);
+}
+
+void dense_wgrad(const float *dy, const Opnd &x, const Layer &L, int B, float *part, int splits,
+                 float *gW, float *gb, hipStream_t s, int64_t ldy = -1) {
+    const Prob q = wgrad_prob(dy, x, L, B, part, splits, ldy);
+    wgrad_reduce(L, part, gemm_launch(q, L.out, nullptr, 0, s), gW, gb, s);
+}
+
+// a layer's weight gradient and its backward data pass (both read only dY) in one launch
+void dense_wgrad_bwd(const float *dy, const Opnd &x, const Layer &L, int B, float *part, int splits,
+                     float *gW, float *gb, int c0, int nc, int kind, const float *mask, int64_t ldm,
+                     const float *gain, float *dx, hipStream_t s) {
+    const Prob qw = wgrad_prob(dy, x, L, B, part, splits, -1);
+    const Prob qb = bwd_data_prob(dy, L, B, c0, nc, kind, mask, ldm, gain, dx);
+    wgrad_reduce(L, part, gemm_launch(qw, L.out, &qb, B, s), gW, gb, s);
 }
 
 void adam_dev(float *p, const float *g, float *m, float *v, int64_t n, const rlp_adam_cfg &c,
@@ -714,17 +756,25 @@ void net_bwd(const rlp_dense_net &n, const float *params, float *grad, const Opn
     for (int l = n.n_layers - 1; l >= 0; --l) {
         const Layer L = layer_of(n, params, l);
         const Opnd xin = l == 0 ? x : mat(layer_out(n, act, B, l - 1), B, L.in, L.in);
-        if (grad)
-            dense_wgrad(dy, xin, L, B, part, splits, grad + n.offset[l],
-                        grad + n.offset[l] + (int64_t)L.in * L.out, s);
+        float *gW = grad ? grad + n.offset[l] : nullptr, *gb = grad ? gW + (int64_t)L.in * L.out : nullptr;
         if (l > 0) {
             const float *h = layer_out(n, act, B, l - 1);
-            dense_bwd_data(dy, L, B, 0, L.in, kEpiReluBack, h, L.in, nullptr, dn, s);
+            if (grad)
+                dense_wgrad_bwd(dy, xin, L, B, part, splits, gW, gb, 0, L.in, kEpiReluBack, h, L.in,
+                                nullptr, dn, s);
+            else
+                dense_bwd_data(dy, L, B, 0, L.in, kEpiReluBack, h, L.in, nullptr, dn, s);
             float *nxt = dn == g0 ? g1 : g0;
             dy = dn;
             dn = nxt;
         } else if (dx) {
-            dense_bwd_data(dy, L, B, c0, nc, t_in ? kEpiTanhAffBack : kEpiNone, t_in, nc, gain, dx, s);
+            const int kind = t_in ? kEpiTanhAffBack : kEpiNone;
+            if (grad)
+                dense_wgrad_bwd(dy, xin, L, B, part, splits, gW, gb, c0, nc, kind, t_in, nc, gain, dx, s);
+            else
+                dense_bwd_data(dy, L, B, c0, nc, kind, t_in, nc, gain, dx, s);
+        } else if (grad) {
+            dense_wgrad(dy, xin, L, B, part, splits, gW, gb, s);
         }
     }
 }
@@ -876,13 +926,14 @@ int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const fl
         for (int l = La - 1; l >= 0; --l) {
             const Layer L = layer_of(n.actor, n.actor.params, l);
             const Opnd xin = l == 0 ? s_in : mat(layer_out(n.actor, pa, B, l - 1), B, L.in, L.in);
-            dense_wgrad(dy, xin, L, B, part, splits, n.actor_grad + n.actor.offset[l],
-                        n.actor_grad + n.actor.offset[l] + (int64_t)L.in * L.out, st);
+            float *gW = n.actor_grad + n.actor.offset[l], *gb = gW + (int64_t)L.in * L.out;
             if (l > 0) {
-                dense_bwd_data(dy, L, B, 0, L.in, kEpiReluBack, layer_out(n.actor, pa, B, l - 1), L.in,
-                               nullptr, d0, st);
+                dense_wgrad_bwd(dy, xin, L, B, part, splits, gW, gb, 0, L.in, kEpiReluBack,
+                                layer_out(n.actor, pa, B, l - 1), L.in, nullptr, d0, st);
                 dy = d0;
                 float *tmp = d0; d0 = d1; d1 = tmp;
+            } else {
+                dense_wgrad(dy, xin, L, B, part, splits, gW, gb, st);
             }
         }
     }
@@ -1070,10 +1121,15 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
         const Opnd hx = mat(h_last, B, H, H);
         const Layer Lm{P + n.mean_offset, P + n.mean_offset + (int64_t)A * H, H, A};
         const Layer Ll{P + n.log_std_offset, P + n.log_std_offset + (int64_t)A * H, H, A};
-        dense_wgrad(W(w.gz), hx, Lm, B, W(w.part), splits, G + n.mean_offset,
-                    G + n.mean_offset + (int64_t)A * H, st, 2 * A);
-        dense_wgrad(W(w.gz) + A, hx, Ll, B, W(w.part), splits, G + n.log_std_offset,
-                    G + n.log_std_offset + (int64_t)A * H, st, 2 * A);
+        {  // both heads' weight gradients in one launch and one two-problem reduce
+            const Prob qm = wgrad_prob(W(w.gz), hx, Lm, B, W(w.part), splits, 2 * A);
+            const Prob ql = wgrad_prob(W(w.gz) + A, hx, Ll, B, W(w.part2), splits, 2 * A);
+            const int z = gemm_launch(qm, A, &ql, A, st);
+            const int tot = A * (H + 1);
+            wgrad_reduce_kernel<<<dim3((tot + 255) / 256, 2), 256, 0, st>>>(
+                W(w.part), z, A, H + 1, G + n.mean_offset, G + n.mean_offset + (int64_t)A * H,
+                W(w.part2), G + n.log_std_offset, G + n.log_std_offset + (int64_t)A * H);
+        }
         // dh = (gz [Wm; Wl]) * relu'(h)
         Epi e{};
         e.y = W(w.d0); e.ldy = H; e.kind = kEpiReluBack; e.M = B; e.N = H; e.mask = h_last; e.ldm = H;
@@ -1083,12 +1139,13 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
         for (int l = Lt - 1; l >= 0; --l) {
             const Layer L = layer_of(n.actor, P, l);
             const Opnd xin = l == 0 ? mat(s, B, S, S) : mat(layer_out(n.actor, W(w.ta), B, l - 1), B, L.in, L.in);
-            dense_wgrad(dy, xin, L, B, W(w.part), splits, G + n.actor.offset[l],
-                        G + n.actor.offset[l] + (int64_t)L.in * L.out, st);
+            float *gW = G + n.actor.offset[l], *gb = gW + (int64_t)L.in * L.out;
             if (l > 0) {
-                dense_bwd_data(dy, L, B, 0, L.in, kEpiReluBack, layer_out(n.actor, W(w.ta), B, l - 1),
-                               L.in, nullptr, dn, st);
+                dense_wgrad_bwd(dy, xin, L, B, W(w.part), splits, gW, gb, 0, L.in, kEpiReluBack,
+                                layer_out(n.actor, W(w.ta), B, l - 1), L.in, nullptr, dn, st);
                 float *tmp = dy; dy = dn; dn = tmp;
+            } else {
+                dense_wgrad(dy, xin, L, B, W(w.part), splits, gW, gb, st);
             }
         }
     }
