@@ -169,23 +169,26 @@ __device__ __forceinline__ void stage_panel(const Opnd &o, bool is_a, int u0, in
 struct Prob {
     Opnd A, B;
     Epi e;
-    int R, rchunk;  // reduction length, rows per gridDim.z slice
+    int R, rchunk;   // reduction length, rows per slice
+    int nx, ny, nz;  // column tiles, row tiles, reduction slices
 };
 
 // Up to two independent problems in one launch (the twin critic's chains, a layer's weight
-// gradient beside its backward data pass): row tiles [0, mt0) of the grid run p0, the rest p1;
-// blocks past a problem's column tiles or reduction slices exit at once (one problem: mt0 =
-// gridDim.y).
-__global__ void __launch_bounds__(256) dense_gemm_kernel(Prob p0, Prob p1, int mt0) {
+// gradient beside its backward data pass): the 1-D grid's first nx*ny*nz blocks run p0, the rest
+// p1 (one problem: gridDim.x = p0's block count).
+__global__ void __launch_bounds__(256) dense_gemm_kernel(Prob p0, Prob p1) {
     extern __shared__ float lds[];
     float *As = lds, *Bs = lds + kDT * kDLd;
-    const bool second = (int)blockIdx.y >= mt0;  // block-uniform
+    const int nb0 = p0.nx * p0.ny * p0.nz;
+    const bool second = (int)blockIdx.x >= nb0;  // block-uniform
     const Opnd A = second ? p1.A : p0.A, B = second ? p1.B : p0.B;
     const Epi e = second ? p1.e : p0.e;
     const int R = second ? p1.R : p0.R, rchunk = second ? p1.rchunk : p0.rchunk;
-    const int m0 = ((int)blockIdx.y - (second ? mt0 : 0)) * kDT, n0 = blockIdx.x * kDT;
-    if (n0 >= e.N || (int)blockIdx.z * rchunk >= R) return;  // (before any barrier)
-    const int r_lo = blockIdx.z * rchunk, rc = min(R, r_lo + rchunk) - r_lo;
+    const int nx = second ? p1.nx : p0.nx, ny = second ? p1.ny : p0.ny;
+    const int bid = (int)blockIdx.x - (second ? nb0 : 0);
+    const int bx = bid % nx, by = (bid / nx) % ny, bz = bid / (nx * ny);
+    const int m0 = by * kDT, n0 = bx * kDT;
+    const int r_lo = bz * rchunk, rc = min(R, r_lo + rchunk) - r_lo;
     const int Q = (rc + 15) / 16 * 4;  // MFMA steps (multiple of 4); rows g * Q + s, s < Q
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
     const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
@@ -223,7 +226,7 @@ __global__ void __launch_bounds__(256) dense_gemm_kernel(Prob p0, Prob p1, int m
                 float v = acc[i][j][q];
                 switch (e.kind) {
                 case kEpiPartial:
-                    e.y[(size_t)blockIdx.z * e.M * e.N + (size_t)m * e.N + n] = v;
+                    e.y[(size_t)bz * e.M * e.N + (size_t)m * e.N + n] = v;
                     continue;
                 case kEpiReluBack:
                     v = e.mask[m * e.ldm + n] > 0.f ? v : 0.f;
@@ -558,35 +561,33 @@ inline Opnd transposed(const float *p, int rows, int cols, int ld) {  // (i, j) 
 constexpr size_t kDenseLds = 2 * kDT * kDLd * sizeof(float);  // 133 120 B
 
 // splits >= ceil(R / 256) slices of the reduction (each <= 256 rows); returns the slice count
-// a problem's reduction slicing: splits >= ceil(R / 256) slices, each <= 256 rows
+// a problem's reduction slicing (splits >= ceil(R / 256) slices, each <= 256 rows) and tiling
 inline Prob make_prob(const Opnd &A, const Opnd &B, const Epi &e, int R, int splits) {
     const int need = (R + kDRc - 1) / kDRc;
     const int sp = splits > need ? splits : need;
-    return Prob{A, B, e, R, ((R + sp - 1) / sp + 15) / 16 * 16};
+    const int rchunk = ((R + sp - 1) / sp + 15) / 16 * 16;
+    const int nz = R > 0 ? (R + rchunk - 1) / rchunk : 1;
+    return Prob{A, B, e, R, rchunk, (e.N + kDT - 1) / kDT, (e.M + kDT - 1) / kDT, nz};
 }
-inline int prob_slices(const Prob &p) { return p.R > 0 ? (p.R + p.rchunk - 1) / p.rchunk : 1; }
 
 // one problem, or two (q1 != nullptr) in one launch; returns p0's slice count
-int gemm_launch(const Prob &q0, int M0, const Prob *q1, int M1, hipStream_t s) {
+int gemm_launch(const Prob &q0, const Prob *q1, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)dense_gemm_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDenseLds);
         attr = true;
     }
-    const int mt0 = (M0 + kDT - 1) / kDT, mt1 = q1 ? (M1 + kDT - 1) / kDT : 0;
-    const int nt0 = (q0.e.N + kDT - 1) / kDT, nt1 = q1 ? (q1->e.N + kDT - 1) / kDT : 0;
-    const int z0 = prob_slices(q0), z1 = q1 ? prob_slices(*q1) : 0;
-    dim3 grid(nt0 > nt1 ? nt0 : nt1, mt0 + mt1, z0 > z1 ? z0 : z1);
-    dense_gemm_kernel<<<grid, 256, kDenseLds, s>>>(q0, q1 ? *q1 : q0, mt0);
-    return z0;
+    const int nb = q0.nx * q0.ny * q0.nz + (q1 ? q1->nx * q1->ny * q1->nz : 0);
+    dense_gemm_kernel<<<nb, 256, kDenseLds, s>>>(q0, q1 ? *q1 : q0);
+    return q0.nz;
 }
 int gemm_impl(const Opnd &A, const Opnd &B, const Epi &e, const Opnd *A1, const Opnd *B1,
               const Epi *e1, int M, int N, int R, int splits, hipStream_t s) {
     const Prob q0 = make_prob(A, B, e, R, splits);
-    if (!A1) return gemm_launch(q0, M, nullptr, 0, s);
+    if (!A1) return gemm_launch(q0, nullptr, s);
     const Prob q1 = make_prob(*A1, *B1, *e1, R, splits);
-    return gemm_launch(q0, M, &q1, M, s);
+    return gemm_launch(q0, &q1, s);
 }
 int gemm(const Opnd &A, const Opnd &B, int M, int N, int R, int splits, const Epi &e, hipStream_t s) {
     return gemm_impl(A, B, e, nullptr, nullptr, nullptr, M, N, R, splits, s);
@@ -622,7 +623,7 @@ Prob bwd_data_prob(const float *dy, const Layer &L, int B, int c0, int nc, int k
 void dense_bwd_data(const float *dy, const Layer &L, int B, int c0, int nc, int kind,
                     const float *mask, int64_t ldm, const float *gain, float *dx, hipStream_t s) {
     const Prob q = bwd_data_prob(dy, L, B, c0, nc, kind, mask, ldm, gain, dx);
-    gemm_launch(q, B, nullptr, 0, s);
+    gemm_launch(q, nullptr, s);
 }
 
 // gW = dY^T X, gb = column sums of dY: split over the batch, partials reduced in fixed order
@@ -643,7 +644,7 @@ void wgrad_reduce(const Layer &L, const float *part, int z, float *gW, float *gb
 void dense_wgrad(const float *dy, const Opnd &x, const Layer &L, int B, float *part, int splits,
                  float *gW, float *gb, hipStream_t s, int64_t ldy = -1) {
     const Prob q = wgrad_prob(dy, x, L, B, part, splits, ldy);
-    wgrad_reduce(L, part, gemm_launch(q, L.out, nullptr, 0, s), gW, gb, s);
+    wgrad_reduce(L, part, gemm_launch(q, nullptr, s), gW, gb, s);
 }
 
 // a layer's weight gradient and its backward data pass (both read only dY) in one launch
@@ -652,7 +653,7 @@ void dense_wgrad_bwd(const float *dy, const Opnd &x, const Layer &L, int B, floa
                      const float *gain, float *dx, hipStream_t s) {
     const Prob qw = wgrad_prob(dy, x, L, B, part, splits, -1);
     const Prob qb = bwd_data_prob(dy, L, B, c0, nc, kind, mask, ldm, gain, dx);
-    wgrad_reduce(L, part, gemm_launch(qw, L.out, &qb, B, s), gW, gb, s);
+    wgrad_reduce(L, part, gemm_launch(qw, &qb, s), gW, gb, s);
 }
 
 void adam_dev(float *p, const float *g, float *m, float *v, int64_t n, const rlp_adam_cfg &c,
@@ -1124,7 +1125,7 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
         {  // both heads' weight gradients in one launch and one two-problem reduce
             const Prob qm = wgrad_prob(W(w.gz), hx, Lm, B, W(w.part), splits, 2 * A);
             const Prob ql = wgrad_prob(W(w.gz) + A, hx, Ll, B, W(w.part2), splits, 2 * A);
-            const int z = gemm_launch(qm, A, &ql, A, st);
+            const int z = gemm_launch(qm, &ql, st);
             const int tot = A * (H + 1);
             wgrad_reduce_kernel<<<dim3((tot + 255) / 256, 2), 256, 0, st>>>(
                 W(w.part), z, A, H + 1, G + n.mean_offset, G + n.mean_offset + (int64_t)A * H,
