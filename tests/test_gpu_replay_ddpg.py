@@ -278,3 +278,59 @@ def test_native_ddpg_rejects_other_nets():
     assert mk("auto")._native is None
     with pytest.raises(ValueError):
         mk(True)
+
+
+def test_native_ddpg_odd_shapes_track_torch():
+    """Shapes that take the dense GEMM's generic staging paths: 3 states, 1 action, hidden widths
+    48 / 20 (not multiples of 4 or of the 64-wide tiles), batch 777 (not a multiple of the
+    256-row weight-gradient slices): native vs torch update from the same weights, 3 steps."""
+    class C(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc1, self.fc2, self.q = nn.Linear(4, 48), nn.Linear(48, 20), nn.Linear(20, 1)
+            self.optimizer = torch.optim.Adam(self.parameters(), lr=3e-4)
+
+        def forward(self, s, a):
+            return self.q(func.relu(self.fc2(func.relu(self.fc1(torch.cat([s, a], 1))))))
+
+    class Ac(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a_min, self.a_max = torch.tensor([-2.]), torch.tensor([2.])
+            self.off = (self.a_min + self.a_max) / 2.0
+            self.gain = self.a_max - self.off
+            self.fc1, self.fc2, self.mu = nn.Linear(3, 48), nn.Linear(48, 20), nn.Linear(20, 1)
+            self.optimizer = torch.optim.Adam(self.parameters(), lr=1e-4)
+
+        def forward(self, s):
+            return self.gain * torch.tanh(self.mu(func.relu(self.fc2(func.relu(self.fc1(s)))))) + self.off
+
+    msg = {'state_dim': 3, 'action_dim': 1, 'action_range': np.array([[-2., 2.]]), 'name': 'x'}
+    torch.manual_seed(9)
+    nets = [Ac(), Ac(), C(), C()]
+    agents = []
+    for native in (False, True):
+        ns = [type(m)() for m in nets]
+        for m, src in zip(ns, nets):
+            m.load_state_dict(src.state_dict())
+        agents.append(DDPG(msg, 0.99, 0.005, 0.005, 10000, 777, *ns, device="cuda", native=native))
+    assert agents[0]._native is None and agents[1]._native is not None
+    rng = np.random.default_rng(4)
+    B = 777
+    d = lambda x: torch.as_tensor(x, dtype=torch.float32, device="cuda")
+    for it in range(3):
+        batch = (d(rng.uniform(-2, 2, (B, 3))), d(rng.uniform(-2, 2, (B, 1))), d(rng.normal(size=B)),
+                 d(rng.uniform(-2, 2, (B, 3))), d((rng.uniform(size=B) > 0.1).astype(np.float32)))
+        lt = agents[0].update(*batch)
+        ln = agents[1].update(*batch)
+        for x, y in zip(lt, ln):
+            torch.testing.assert_close(y, x, rtol=2e-4, atol=1e-6)
+        if it == 0:
+            for k in ("actor", "critic"):
+                gt = torch.cat([p.grad.reshape(-1) for p in getattr(agents[0], k).parameters()])
+                gn = agents[1]._native.grad[k]
+                assert float((gn - gt).abs().max()) <= 1e-4 * float(gt.abs().max()) + 1e-8, k
+    for k in ("actor", "target_actor", "critic", "target_critic"):
+        a = _flat(getattr(agents[1], k))
+        b = _flat(getattr(agents[0], k))
+        assert float((a - b).abs().max()) <= 3e-5, (k, float((a - b).abs().max()))
