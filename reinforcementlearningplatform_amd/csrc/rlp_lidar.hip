@@ -62,18 +62,29 @@ __device__ __forceinline__ void oa_scan(const OA::P &p, const OaLds<EB> &L, int 
 }
 
 // STEP: step_update (+ obs_cur if requested); !STEP: get_state only
+// !STEP with `keep` (the rollout's next observation): a block none of whose envs was reset
+// (keep[i] == 0 for all) copies its rows of `prev` (the step's obs_next — the driver's
+// current_state = next_state) instead of scanning again
 template <int EB, bool STEP>
 __global__ void __launch_bounds__(kOaThreads) oa_kernel(OA::P p, double *state, int n,
                                                         const float *__restrict__ action,
                                                         float *obs_cur, float *obs_next,
                                                         double *reward, int32_t *flag,
-                                                        uint8_t *done) {
+                                                        uint8_t *done, const uint8_t *keep,
+                                                        const float *prev) {
     __shared__ OaLds<EB> L;
     const int t = threadIdx.x;
     const int e0 = blockIdx.x * EB;
     const int ne = n - e0 < EB ? n - e0 : EB;
     const bool own = t < ne;
     const size_t i = (size_t)e0 + t;
+    if (!STEP && keep) {
+        if (!__syncthreads_or(own && keep[i])) {
+            for (int k = t; k < ne * OA::S; k += kOaThreads)
+                obs_next[(size_t)e0 * OA::S + k] = prev[(size_t)e0 * OA::S + k];
+            return;
+        }
+    }
     double s[OA::DW];
     if (own) {
 #pragma unroll
@@ -129,7 +140,8 @@ static int g_oa_cus = 0;
 
 template <bool STEP>
 static int launch_oa(const OA::P &p, double *state, int n, const float *action, float *obs_cur,
-                     float *obs_next, double *reward, int32_t *flag, uint8_t *done, hipStream_t st) {
+                     float *obs_next, double *reward, int32_t *flag, uint8_t *done, hipStream_t st,
+                     const uint8_t *keep = nullptr, const float *prev = nullptr) {
     if (p.n_obs < 0 || p.n_obs > OA::NOBS)
         return fail(RLP_EINVAL, "UGVForwardObstacleAvoidance: n_obs=%d (0..%d)", p.n_obs, OA::NOBS);
     if (!g_oa_cus) {
@@ -141,10 +153,12 @@ static int launch_oa(const OA::P &p, double *state, int n, const float *action, 
     // fewer envs per block when the batch is small, so every CU gets several blocks
     if ((n + 63) / 64 >= 4 * g_oa_cus)
         oa_kernel<64, STEP><<<(n + 63) / 64, kOaThreads, 0, st>>>(p, state, n, action, obs_cur,
-                                                                 obs_next, reward, flag, done);
+                                                                 obs_next, reward, flag, done, keep,
+                                                                 prev);
     else
         oa_kernel<16, STEP><<<(n + 15) / 16, kOaThreads, 0, st>>>(p, state, n, action, obs_cur,
-                                                                 obs_next, reward, flag, done);
+                                                                 obs_next, reward, flag, done, keep,
+                                                                 prev);
     RLP_CHECK_LAUNCH("UGVForwardObstacleAvoidance lidar");
     return RLP_OK;
 }
@@ -159,6 +173,14 @@ int launch_ugvoa_observe(const rlp_ugv_oa_params &p, const double *state, int n,
                          hipStream_t st) {
     return launch_oa<false>(p, const_cast<double *>(state), n, nullptr, nullptr, obs, nullptr,
                             nullptr, nullptr, st);
+}
+
+// the rollout's next observation: envs reset this step (reset[i]) scanned, blocks without one
+// copy the step's obs_next
+int launch_ugvoa_observe_after(const rlp_ugv_oa_params &p, const double *state, int n, float *obs,
+                               const uint8_t *reset, const float *obs_next, hipStream_t st) {
+    return launch_oa<false>(p, const_cast<double *>(state), n, nullptr, nullptr, obs, nullptr,
+                            nullptr, nullptr, st, reset, obs_next);
 }
 
 // reset(random=True) with one wave per env: each round, lane l tests try (round * 64 + l) of the

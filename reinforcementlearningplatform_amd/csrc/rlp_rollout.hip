@@ -21,6 +21,8 @@ int launch_ugvoa_step(const rlp_ugv_oa_params &p, double *state, int n, const fl
                       uint8_t *done, hipStream_t st);
 int launch_ugvoa_observe(const rlp_ugv_oa_params &p, const double *state, int n, float *obs,
                          hipStream_t st);
+int launch_ugvoa_observe_after(const rlp_ugv_oa_params &p, const double *state, int n, float *obs,
+                               const uint8_t *reset, const float *obs_next, hipStream_t st);
 int launch_ugvoa_reset(const rlp_ugv_oa_params &p, double *state, int n, const uint8_t *mask,
                        const double *init, uint64_t seed, uint64_t counter, uint64_t env_id0,
                        hipStream_t st);
@@ -797,7 +799,9 @@ static int rollout_oa(const void *params, double *state, uint8_t *need_reset, co
         if (t + 1 < T) {  // the ended envs' reset with the next step's counter, then obs_{t+1}
             rc = launch_ugvoa_reset(p, state, n, b.done + k0, nullptr, ra.seed, ra.step0 + t + 1,
                                     ra.env_id0, s);
-            if (rc == RLP_OK) rc = launch_ugvoa_observe(p, state, n, b.obs + (k0 + n) * OA::S, s);
+            if (rc == RLP_OK)
+                rc = launch_ugvoa_observe_after(p, state, n, b.obs + (k0 + n) * OA::S, b.done + k0,
+                                                b.obs_next + k0 * OA::S, s);
         }
     }
     if (rc == RLP_OK) {  // V(s'_{T-1}) of the envs still running
