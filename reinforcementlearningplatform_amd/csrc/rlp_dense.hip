@@ -43,7 +43,7 @@ __device__ __forceinline__ float opnd_ld(const Opnd &o, int i, int j) {
     return __builtin_fmaf(v, ld ? 1.f : 0.f, (in && j == o.ones) ? 1.f : 0.f);
 }
 
-enum : int { kEpiNone = 0, kEpiRelu, kEpiTanhAff, kEpiReluBack, kEpiTanhAffBack, kEpiPartial };
+enum : int { kEpiNone = 0, kEpiRelu, kEpiTanhAff, kEpiReluBack, kEpiTanhAffBack, kEpiPartial, kEpiTanh };
 
 struct Epi {
     float *y;
@@ -240,6 +240,8 @@ __global__ void __launch_bounds__(256) dense_gemm_kernel(Prob p0, Prob p1) {
                     if (e.bias) v = v + e.bias[n];
                     if (e.kind == kEpiRelu) {
                         v = fmaxf(v, 0.f);
+                    } else if (e.kind == kEpiTanh) {
+                        v = tanhf(v);
                     } else if (e.kind == kEpiTanhAff) {
                         const float tt = tanhf(v);
                         e.aux[m * e.ldaux + n] = tt;
@@ -859,6 +861,33 @@ void twin_bwd(const rlp_dense_net &n1, const rlp_dense_net &n2, const float *par
             }
         }
     }
+}
+
+// rlp_mlp_forward on the tiled GEMM (one launch per layer) for large batches: y = MLP(x) for
+// the plain Linear-stack layout (W_l [out][in] then b_l), activations RLP_ACT_*; the hidden
+// activations in stream-ordered scratch
+int dense_mlp_forward(const rlp_mlp_desc &d, const float *params, const float *x, float *y, int n,
+                      hipStream_t s) {
+    int maxw = 0;
+    for (int l = 1; l < d.n_layers; ++l) maxw = d.dims[l] > maxw ? d.dims[l] : maxw;
+    float *buf = nullptr;
+    if (d.n_layers > 1 &&
+        hipMallocAsync((void **)&buf, sizeof(float) * 2 * (size_t)n * maxw, s) != hipSuccess)
+        return fail(RLP_EINVAL, "rlp_mlp_forward: scratch");
+    const float *in = x;
+    int64_t off = 0;
+    for (int l = 0; l < d.n_layers; ++l) {
+        const int K = d.dims[l], N = d.dims[l + 1];
+        const Layer L{params + off, params + off + (int64_t)K * N, K, N};
+        off += (int64_t)K * N + N;
+        const int kind = d.act[l] == RLP_ACT_RELU ? kEpiRelu : d.act[l] == RLP_ACT_TANH ? kEpiTanh : kEpiNone;
+        float *out = l == d.n_layers - 1 ? y : buf + (size_t)(l & 1) * n * maxw;
+        dense_fwd(mat(in, n, K, K), L, n, kind, out, nullptr, nullptr, nullptr, s);
+        in = out;
+    }
+    if (buf) (void)hipFreeAsync(buf, s);
+    RLP_CHECK_LAUNCH("rlp_mlp_forward (dense)");
+    return RLP_OK;
 }
 
 }  // namespace rlp

@@ -274,6 +274,12 @@ __global__ void __launch_bounds__(256) sac_sample_kernel(const float *__restrict
 
 using namespace rlp;
 
+namespace rlp {
+int dense_mlp_forward(const rlp_mlp_desc &d, const float *params, const float *x, float *y, int n,
+                      hipStream_t s);  // rlp_dense.hip
+constexpr int kMlpDenseRows = 2048;
+}  // namespace rlp
+
 extern "C" {
 
 int64_t rlp_mlp_param_count(const rlp_mlp_desc *desc) {
@@ -296,6 +302,14 @@ int rlp_mlp_forward(const rlp_mlp_desc *desc, const float *params, const float *
         maxw = desc->dims[l] > maxw ? desc->dims[l] : maxw;
     }
     if (n <= 0) return n == 0 ? RLP_OK : RLP_EINVAL;
+    // large unmasked batches (the off-policy drivers' acting forward over every env) on the tiled
+    // GEMM of rlp_dense.hip: one launch per layer, weights staged once per 64-row tile
+    bool acts_ok = true;
+    for (int l = 0; l < desc->n_layers; ++l)
+        acts_ok &= desc->act[l] == RLP_ACT_RELU || desc->act[l] == RLP_ACT_TANH ||
+                   desc->act[l] == RLP_ACT_NONE;
+    if (!mask && n >= kMlpDenseRows && acts_ok)
+        return dense_mlp_forward(*desc, params, x, y, n, as_stream(stream));
     // row stride: multiple of 32 (+2) so the B-operand reads (16 rows x 2 k per half-wave) hit
     // 32 distinct banks
     const int ldw = ((maxw + 31) / 32) * 32 + 2;
