@@ -308,7 +308,8 @@ int rlp_mlp_forward(const rlp_mlp_desc *desc, const float *params, const float *
     for (int l = 0; l < desc->n_layers; ++l)
         acts_ok &= desc->act[l] == RLP_ACT_RELU || desc->act[l] == RLP_ACT_TANH ||
                    desc->act[l] == RLP_ACT_NONE;
-    if (!mask && n >= kMlpDenseRows && acts_ok)
+    // (the GEMM's element offsets are 32-bit: rows x width < 2^31)
+    if (!mask && n >= kMlpDenseRows && acts_ok && (int64_t)n * maxw < (int64_t(1) << 31))
         return dense_mlp_forward(*desc, params, x, y, n, as_stream(stream));
     // row stride: multiple of 32 (+2) so the B-operand reads (16 rows x 2 k per half-wave) hit
     // 32 distinct banks

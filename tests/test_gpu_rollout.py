@@ -242,3 +242,28 @@ def test_per_call_selection_overrides_library_default():
     assert torch.equal(run(mlp_precision=_native.MLP_F16X3, physics=4), vx3)
     assert torch.equal(run(mlp_precision=_native.MLP_F16X3, physics=5), vx3)
     assert torch.equal(run(mlp_precision=_native.MLP_F16X3, physics=6), vx3)
+
+
+@pytest.mark.parametrize("acts", ["relu", "tanh"])
+def test_mlp_forward_large_batch_dense_path(acts):
+    """rlp_mlp_forward on >= 2048 unmasked rows runs the tiled dense GEMM (one launch per layer):
+    against torch float32 Linear stacks for the DDPG driver's relu actor [4,256,256,2] and a
+    tanh net, and against the one-wave-per-16-rows kernel (masked call) on the same rows."""
+    torch.manual_seed(1)
+    act = A.RLP_ACT_RELU if acts == "relu" else A.RLP_ACT_TANH
+    d = A.MLPDesc.make([4, 256, 256, 2], [act, act, A.RLP_ACT_NONE])
+    layers = [torch.nn.Linear(4, 256), torch.nn.Linear(256, 256), torch.nn.Linear(256, 2)]
+    flat = torch.cat([t.detach().reshape(-1) for l in layers for t in (l.weight, l.bias)]).cuda()
+    n = 5003
+    x = torch.rand(n, 4, device="cuda") * 4 - 2
+    f = torch.relu if acts == "relu" else torch.tanh
+    with torch.no_grad():
+        h = x
+        for i, l in enumerate(layers):
+            h = torch.nn.functional.linear(h, l.weight.cuda(), l.bias.cuda())
+            if i < 2:
+                h = f(h)
+    y = K.mlp_forward(d, flat, x)
+    torch.testing.assert_close(y, h, rtol=1e-5, atol=2e-6)
+    y_small = K.mlp_forward(d, flat, x, mask=torch.ones(n, dtype=torch.uint8, device="cuda"))
+    torch.testing.assert_close(y, y_small, rtol=1e-5, atol=2e-6)
