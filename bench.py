@@ -648,7 +648,7 @@ def main():
                     help="rlp_set_rollout_prio (-1: library default)")
     ap.add_argument("--update-prio", type=int, default=-1, choices=[-1, 0, 1],
                     help="rlp_set_update_prio for the PPO2 update kernels (-1: library default)")
-    ap.add_argument("--wgrad-waves", type=int, default=0, choices=[0, 4, 8],
+    ap.add_argument("--wgrad-waves", type=int, default=0, choices=[0, 4, 8, 32],
                     help="PPO2 update's weight-gradient kernel block shape (0: library default)")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="rollout hidden-layer arithmetic (include/rlp.h rlp_set_mlp_precision)")

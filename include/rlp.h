@@ -440,6 +440,9 @@ int rlp_get_fd_mode(void);
  * results. */
 int rlp_set_update_prio(int mode);
 int rlp_get_update_prio(void);
+/* Weight-gradient kernel variant of rlp_ppo2_grad: 8 (default) / 4 = 8- / 4-wave blocks on
+ * v_mfma_f32_16x16x32_f16 (identical results), 32 = the v_mfma_f32_32x32x16_f16 form (half the
+ * MFMA issue slots; its K order differs, so results agree to f32 rounding). */
 int rlp_set_wgrad_waves(int waves);
 int rlp_get_wgrad_waves(void);
 

@@ -27,6 +27,7 @@ int fail(int code, const char *fmt, ...);
 inline hipStream_t as_stream(rlp_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // Global-address-space views: loads through them are global_load_* (counted, in-order vmcnt
 // waits) rather than flat_load_*, which the compiler emits when it cannot prove the address space

@@ -740,6 +740,176 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
         }
 }
 
+// The same weight gradient on v_mfma_f32_32x32x16_f16 (twice the FLOPs per instruction: half the
+// MFMA issue slots of the 16x16x32 form for the same VALU work). 8 waves, wave wv owns the 32
+// dW2 rows [32 wv, 32 wv + 32) x all 256 columns (8 column tiles of 32, 128 accumulator
+// registers). K = 16 rows per MFMA, 4 K-steps per 64-row tile. The h1 B fragments come from
+// layer 1 on v_mfma_f32_32x32x2_f32 (32 rows x 32 neurons per tile, neuron on the lane): its C
+// registers 0-7 / 8-15 hold rows {0-3, 8-11} / {16-19, 24-27} + 4 (lane / 32) of the 32-row half,
+// which fixes the K order of each step; the g2 A operands are loaded in that order (two float4
+// per lane from the [tile][neuron][64 rows] G2 layout).
+template <int KS1>
+__global__ void __launch_bounds__(512, 1) ppo2_wgrad32_kernel(WArgs w) {
+    constexpr int W = 8, H = kUpdH, SP = 4 * KS1, NT = 64 * W;
+    constexpr int SV = (kUpdRows * SP + NT - 1) / NT;
+    constexpr int FRAG = 4 * 8 * 2 * 64 * 8;  // [ks 4][nt 8][hi, lo][64 lanes][8 halfs] (64 KiB)
+    __shared__ float srow[2][kUpdRows][SP];
+    __shared__ float w1s[H][SP + 1];
+    __shared__ float b1s[H];
+    __shared__ __attribute__((aligned(16))) _Float16 hfrag[2][FRAG];
+    const MfmaNet &net = w.net;
+    const int S = net.S;
+    const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (w.prio && wv >= W / 2) __builtin_amdgcn_s_setprio(1);
+    {
+        const float *W1c = w.packed + net.off_small_r;
+        const float *B1c = w.packed + net.off_small_r + (net.off_b1 - net.off_w1);
+        for (int i = threadIdx.x; i < H * SP; i += blockDim.x) w1s[i / SP][i % SP] = W1c[i];
+        for (int i = threadIdx.x; i < H; i += blockDim.x) b1s[i] = B1c[i];
+    }
+    const float gm = __uint_as_float(*w.g2max);
+    const int gex = gm > 0.f ? __builtin_amdgcn_frexp_expf(gm) : 0;
+    const float sg = __builtin_amdgcn_ldexpf(1.f, 14 - gex);
+    const float un2 = __builtin_amdgcn_ldexpf(1.f, gex - 14) / kX3HScale;
+    const float unb = __builtin_amdgcn_ldexpf(1.f, gex - 14);
+    half8 ones;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ones[i] = (_Float16)1.0f;
+    floatx16 acc[8], accb;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) accb[i] = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[nt][i] = 0.f;
+    const int64_t ntiles = (w.rows + kUpdRows - 1) / kUpdRows;
+    auto load_s = [&](int64_t tile, float (&sv)[SV]) {
+#pragma unroll
+        for (int u = 0; u < SV; ++u) {
+            const int i = threadIdx.x + NT * u, rr = i / SP, k = i % SP;
+            const int64_t row = tile * kUpdRows + rr;
+            sv[u] = (tile < ntiles && i < kUpdRows * SP && row < w.rows && k < S)
+                        ? w.s[(w.index ? w.index[row] : row) * S + k] : 0.f;
+        }
+    };
+    auto store_s = [&](int buf, const float (&sv)[SV]) {
+#pragma unroll
+        for (int u = 0; u < SV; ++u) {
+            const int i = threadIdx.x + NT * u;
+            if (i < kUpdRows * SP) srow[buf][i / SP][i % SP] = sv[u];
+        }
+    };
+    // fragment pair P = (rh, nt): layer 1 of rows 32 rh .. 32 rh + 31 x neurons 32 nt .. on
+    // 32x32x2 f32 MFMAs (the FD's small_r W1 / b1: the exp2 argument), tanh, the f16 split; its
+    // C registers 0-7 are K-step 2 rh, 8-15 K-step 2 rh + 1
+    auto build_pair = [&](int buf, int P) {
+        const int rh = P >> 3, nt = P & 7;
+        const float b1 = b1s[32 * nt + r];
+        floatx16 c;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c[i] = b1;
+#pragma unroll
+        for (int kk = 0; kk < 2 * KS1; ++kk)
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(srow[buf][32 * rh + r][2 * kk + hh],
+                                                      w1s[32 * nt + r][2 * kk + hh], c, 0, 0, 0);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            float x[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                x[q] = __builtin_fmaf(-2.0f * kX3HScale,
+                                      __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c[8 * half + q])),
+                                      kX3HScale);
+            half8 h8, l8;
+            split8(x, h8, l8);
+            const int F = (2 * rh + half) * 8 + nt;
+            *reinterpret_cast<half8 *>(&hfrag[buf][((F * 2 + 0) * 64 + lane) * 8]) = h8;
+            *reinterpret_cast<half8 *>(&hfrag[buf][((F * 2 + 1) * 64 + lane) * 8]) = l8;
+        }
+    };
+    const float *g2base = w.g2t;
+    asm volatile("" : "+s"(g2base));
+    // A operands of K-step ks: g2(j = 32 wv + r, rows 16 ks + 4 hh + {0..3} and + 8)
+    auto load_g2 = [&](int64_t tile, int ks, floatx4 (&gv)[2]) {
+        const int64_t t = tile < ntiles ? tile : ntiles - 1;
+        const gptr<float> src = as_global(g2base + t * kUpdTileFloats + (32 * wv + r) * kUpdRows +
+                                          16 * ks + 4 * hh);
+        gv[0] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src);
+        gv[1] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 8);
+    };
+    auto frag = [&](int buf, int F, int hl) {
+        return *reinterpret_cast<const half8 *>(&hfrag[buf][((F * 2 + hl) * 64 + lane) * 8]);
+    };
+    int64_t tile = blockIdx.x;
+    {
+        float sv[SV];
+        load_s(tile, sv);
+        store_s(0, sv);
+    }
+    lds_barrier();
+#pragma unroll 1
+    for (int u = 0; u < 2; ++u) build_pair(0, 2 * wv + u);
+    float svn[SV];
+    load_s(tile + gridDim.x, svn);
+    floatx4 gv[2];
+    load_g2(tile, 0, gv);
+    lds_barrier();
+    for (int i = 0; tile < ntiles; tile += gridDim.x, ++i) {
+        const int cur = i & 1, nxt = cur ^ 1;
+        store_s(nxt, svn);
+        lds_barrier();
+        load_s(tile + 2 * (int64_t)gridDim.x, svn);
+        half8 bh = frag(cur, 0, 0), bl = frag(cur, 0, 1);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            half8 ah, al;
+            {
+                float x[8];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    x[u] = gv[0][u] * sg;
+                    x[u + 4] = gv[1][u] * sg;
+                }
+                split8(x, ah, al);
+            }
+            if (ks < 3) load_g2(tile, ks + 1, gv);
+            else load_g2(tile + gridDim.x, 0, gv);
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt) {
+                const int F = ks * 8 + nt;
+                half8 nbh, nbl;
+                if (F + 1 < 32) {
+                    nbh = frag(cur, F + 1, 0);
+                    nbl = frag(cur, F + 1, 1);
+                }
+                floatx16 v = acc[nt];
+                v = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, v, 0, 0, 0);
+                v = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, v, 0, 0, 0);
+                v = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, v, 0, 0, 0);
+                acc[nt] = v;
+                if (F == 15 || F == 31) build_pair(nxt, 2 * wv + (F == 31));  // next tile's pairs
+                if (F + 1 < 32) {
+                    bh = nbh;
+                    bl = nbl;
+                }
+            }
+            accb = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ones, accb, 0, 0, 0);
+            accb = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ones, accb, 0, 0, 0);
+        }
+        lds_barrier();
+    }
+    // C layout: lane (r, hh), register q: row (q & 3) + 8 (q >> 2) + 4 hh, column r
+    float *out = w.part + (size_t)blockIdx.x * (H * H + H);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int j = 32 * wv + (q & 3) + 8 * (q >> 2) + 4 * hh;
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) out[j * H + 32 * nt + r] = acc[nt][q] * un2;
+        if (r == 0) out[H * H + j] = accb[q] * unb;
+    }
+}
+
 // grad (torch order W1 b1 W2 b2 W3 b3) = sum over blocks / waves of the partials, in order
 // 64 consecutive outputs per block x kRedSplit partial-slices: each thread sums every
 // kRedSplit-th partial of its output (loads coalesced across the 64 outputs), then a fixed-order
@@ -932,7 +1102,10 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     WArgs w{};
     w.packed = packed; w.net = net; w.s = s; w.index = index; w.rows = rows;
     w.g2t = g.g2t; w.g2max = g.g2max; w.part = partw; w.prio = g_update_prio;
-    if (g_wgrad_waves == 4) {
+    if (g_wgrad_waves == 32) {  // the 32x32x16 variant (rlp_set_wgrad_waves(32))
+        if (net.ks1 == 1) ppo2_wgrad32_kernel<1><<<grid, 512, 0, st>>>(w);
+        else ppo2_wgrad32_kernel<2><<<grid, 512, 0, st>>>(w);
+    } else if (g_wgrad_waves == 4) {
         if (net.ks1 == 1) ppo2_wgrad_kernel<1, 4><<<grid, 256, 0, st>>>(w);
         else ppo2_wgrad_kernel<2, 4><<<grid, 256, 0, st>>>(w);
     } else {
@@ -965,7 +1138,7 @@ int rlp_set_update_prio(int mode) {
 int rlp_get_update_prio(void) { return g_update_prio; }
 
 int rlp_set_wgrad_waves(int waves) {
-    if (waves != 4 && waves != 8) return fail(RLP_EINVAL, "rlp_set_wgrad_waves: %d", waves);
+    if (waves != 4 && waves != 8 && waves != 32) return fail(RLP_EINVAL, "rlp_set_wgrad_waves: %d", waves);
     g_wgrad_waves = waves;
     return RLP_OK;
 }

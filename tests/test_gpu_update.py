@@ -65,9 +65,10 @@ def split(flat, module):
     return out
 
 
-@pytest.fixture(params=[8, 4], ids=["wgrad8", "wgrad4"])
+@pytest.fixture(params=[8, 4, 32], ids=["wgrad8", "wgrad4", "wgrad32x32"])
 def wgrad_waves(request):
-    """Both block shapes of the weight-gradient kernel (include/rlp.h rlp_set_wgrad_waves)."""
+    """The weight-gradient kernel's variants (include/rlp.h rlp_set_wgrad_waves: 8- / 4-wave
+    blocks on 16x16x32 MFMAs, 32 = the 32x32x16 form)."""
     from reinforcementlearningplatform_amd import _native
     old = _native.lib().rlp_get_wgrad_waves()
     assert _native.lib().rlp_set_wgrad_waves(request.param) == 0
