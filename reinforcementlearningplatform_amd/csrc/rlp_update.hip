@@ -860,7 +860,10 @@ __global__ void __launch_bounds__(512, 1) ppo2_wgrad32_kernel(WArgs w) {
         store_s(nxt, svn);
         lds_barrier();
         load_s(tile + 2 * (int64_t)gridDim.x, svn);
-        half8 bh = frag(cur, 0, 0), bl = frag(cur, 0, 1);
+        // two column tiles at a time, their MFMAs interleaved (a 32x32x16 result is not ready
+        // for the next MFMA on the same accumulator for many cycles); the next pair's fragments
+        // are read one step ahead
+        half8 bh0 = frag(cur, 0, 0), bl0 = frag(cur, 0, 1), bh1 = frag(cur, 1, 0), bl1 = frag(cur, 1, 1);
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
             half8 ah, al;
@@ -876,22 +879,27 @@ __global__ void __launch_bounds__(512, 1) ppo2_wgrad32_kernel(WArgs w) {
             if (ks < 3) load_g2(tile, ks + 1, gv);
             else load_g2(tile + gridDim.x, 0, gv);
 #pragma unroll
-            for (int nt = 0; nt < 8; ++nt) {
-                const int F = ks * 8 + nt;
-                half8 nbh, nbl;
-                if (F + 1 < 32) {
-                    nbh = frag(cur, F + 1, 0);
-                    nbl = frag(cur, F + 1, 1);
+            for (int np = 0; np < 4; ++np) {
+                const int F = ks * 8 + 2 * np;  // this pair: F, F + 1
+                half8 nh0, nl0, nh1, nl1;
+                if (F + 2 < 32) {
+                    nh0 = frag(cur, F + 2, 0);
+                    nl0 = frag(cur, F + 2, 1);
+                    nh1 = frag(cur, F + 3, 0);
+                    nl1 = frag(cur, F + 3, 1);
                 }
-                floatx16 v = acc[nt];
-                v = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, v, 0, 0, 0);
-                v = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, v, 0, 0, 0);
-                v = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, v, 0, 0, 0);
-                acc[nt] = v;
-                if (F == 15 || F == 31) build_pair(nxt, 2 * wv + (F == 31));  // next tile's pairs
-                if (F + 1 < 32) {
-                    bh = nbh;
-                    bl = nbl;
+                floatx16 v0 = acc[2 * np], v1 = acc[2 * np + 1];
+                v0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh0, v0, 0, 0, 0);
+                v1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh1, v1, 0, 0, 0);
+                v0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl0, v0, 0, 0, 0);
+                v1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl1, v1, 0, 0, 0);
+                v0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh0, v0, 0, 0, 0);
+                v1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh1, v1, 0, 0, 0);
+                acc[2 * np] = v0;
+                acc[2 * np + 1] = v1;
+                if (F == 14 || F == 30) build_pair(nxt, 2 * wv + (F == 30));  // next tile's pairs
+                if (F + 2 < 32) {
+                    bh0 = nh0; bl0 = nl0; bh1 = nh1; bl1 = nl1;
                 }
             }
             accb = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ones, accb, 0, 0, 0);
