@@ -113,7 +113,7 @@ int launch_ugvoa_observe(const rlp_ugv_oa_params &p, const double *state, int n,
                          hipStream_t st);
 int launch_ugvoa_reset(const rlp_ugv_oa_params &p, double *state, int n, const uint8_t *mask,
                        const double *init, uint64_t seed, uint64_t counter, uint64_t env_id0,
-                       hipStream_t st);
+                       hipStream_t st, float *obs = nullptr);
 
 // kind -> template dispatch
 template <typename F>

@@ -188,10 +188,13 @@ int launch_ugvoa_observe_after(const rlp_ugv_oa_params &p, const double *state, 
 // (Env<7>::reset) at ~1 round per draw instead of the wave waiting on its unluckiest lane.
 constexpr int kOaResetWaves = 4;
 
+// obs (nullable): also the reset env's observation (get_state: the head and the 37-beam scan of
+// the new pose, one beam per lane) — the rollout's next observation of the envs it resets
 __global__ void __launch_bounds__(64 * kOaResetWaves) oa_reset_kernel(
     OA::P p, double *state, int n, const uint8_t *mask, const double *init, uint64_t seed,
-    uint64_t counter, uint64_t env_id0) {
+    uint64_t counter, uint64_t env_id0, float *obs) {
     __shared__ double obl[kOaResetWaves][OA::NOBS * 3];
+    __shared__ OaLds<kOaResetWaves> L;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int e = blockIdx.x * kOaResetWaves + w;
     if (e >= n || (mask && !mask[e])) return;  // uniform per wave
@@ -265,16 +268,44 @@ __global__ void __launch_bounds__(64 * kOaResetWaves) oa_reset_kernel(
         state[(size_t)lane * n + i] = v;
     }
     if (lane < OA::NOBS * 3) state[(size_t)(OA::OB + lane) * n + i] = obl[w][lane];
+    if (!obs) return;
+    if (lane == 0) {  // the per-pose setup of oa_kernel's observe, for this wave's env
+        for (int k = 0; k < p.n_obs; ++k) {
+            L.ob[w][k].x0 = obl[w][3 * k];
+            L.ob[w][k].y0 = obl[w][3 * k + 1];
+            L.ob[w][k].r0 = obl[w][3 * k + 2];
+        }
+        oa_setup(p, L, w, head);
+        float h[4];
+        OA::obs_head(p, head, OA::get_e(head), OA::e_phi(head), h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) obs[i * OA::S + j] = h[j];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < OA::NL) {  // oa_scan's beam, one per lane
+        float v = OA::beam_obs(p, p.laser_blind);
+        if (!L.coll[w]) {
+            const OA::Pose q = L.q[w];
+            v = OA::beam_obs(p, OA::beam(p, q, lane, [&](int k, double &x0, double &y0, double &r0,
+                                                         double &rf) {
+                const OaObstacle o = L.ob[w][k];
+                x0 = o.x0; y0 = o.y0; r0 = o.r0; rf = o.ref;
+            }));
+        }
+        obs[i * OA::S + 4 + lane] = v;
+    }
 }
 
 int launch_ugvoa_reset(const rlp_ugv_oa_params &p, double *state, int n, const uint8_t *mask,
                        const double *init, uint64_t seed, uint64_t counter, uint64_t env_id0,
-                       hipStream_t st) {
+                       hipStream_t st, float *obs) {
     if (p.n_obs < 0 || p.n_obs > OA::NOBS || p.max_tries < 0 || p.max_tries > 65535)
         return fail(RLP_EINVAL, "rlp_env_reset: n_obs=%d (0..%d) max_tries=%d (0..65535)", p.n_obs,
                     OA::NOBS, p.max_tries);
     oa_reset_kernel<<<(n + kOaResetWaves - 1) / kOaResetWaves, 64 * kOaResetWaves, 0, st>>>(
-        p, state, n, mask, init, seed, counter, env_id0);
+        p, state, n, mask, init, seed, counter, env_id0, init ? nullptr : obs);
     RLP_CHECK_LAUNCH("rlp_env_reset (UGVForwardObstacleAvoidance)");
     return RLP_OK;
 }

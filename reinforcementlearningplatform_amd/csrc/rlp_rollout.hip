@@ -25,7 +25,7 @@ int launch_ugvoa_observe_after(const rlp_ugv_oa_params &p, const double *state, 
                                const uint8_t *reset, const float *obs_next, hipStream_t st);
 int launch_ugvoa_reset(const rlp_ugv_oa_params &p, double *state, int n, const uint8_t *mask,
                        const double *init, uint64_t seed, uint64_t counter, uint64_t env_id0,
-                       hipStream_t st);
+                       hipStream_t st, float *obs = nullptr);
 
 // Each wave stages only its own envs' observations in LDS, so a wave-level fence suffices; no
 // block barrier keeps the two waves of a SIMD in lockstep (one's f64 physics overlaps the other's
@@ -755,6 +755,12 @@ __global__ void __launch_bounds__(256) oa_post_kernel(RolloutArgs ra, int t, con
     b.flag[k] = (int8_t)f32[i];
     b.success[k] = success_of(ra.success_rule, ra.success_flag, dn, f32[i]);
     if (t == ra.T - 1) need_reset[i] = dn;  // ended envs of the last step reset next segment
+    if (t + 1 < ra.T && !dn) {  // current_state = next_state (the reset kernel writes the others)
+        const float *src = b.obs_next + (size_t)k * OA::S;
+        float *dst = b.obs + (size_t)(k + n) * OA::S;
+#pragma unroll
+        for (int j = 0; j < OA::S; ++j) dst[j] = src[j];
+    }
 }
 
 __global__ void __launch_bounds__(256) oa_boot_kernel(int T, int n, const float *v, rlp_rollout_bufs b) {
@@ -796,13 +802,10 @@ static int rollout_oa(const void *params, double *state, uint8_t *need_reset, co
                                r64, f32, b.done + k0, s);
         if (rc != RLP_OK) break;
         oa_post_kernel<<<nb, 256, 0, s>>>(ra, t, r64, f32, b, need_reset);
-        if (t + 1 < T) {  // the ended envs' reset with the next step's counter, then obs_{t+1}
+        if (t + 1 < T)  // the ended envs' reset with the next step's counter and their obs_{t+1}
+                        // (the others' obs_{t+1} = obs_next_t, copied by oa_post_kernel)
             rc = launch_ugvoa_reset(p, state, n, b.done + k0, nullptr, ra.seed, ra.step0 + t + 1,
-                                    ra.env_id0, s);
-            if (rc == RLP_OK)
-                rc = launch_ugvoa_observe_after(p, state, n, b.obs + (k0 + n) * OA::S, b.done + k0,
-                                                b.obs_next + k0 * OA::S, s);
-        }
+                                    ra.env_id0, s, b.obs + (k0 + n) * OA::S);
     }
     if (rc == RLP_OK) {  // V(s'_{T-1}) of the envs still running
         rc = launch_packed_forward<0>(cn, critic, b.obs_next + (size_t)(T - 1) * n * OA::S, vb, n,
