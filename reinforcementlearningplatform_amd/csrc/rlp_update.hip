@@ -19,6 +19,17 @@
 // A deterministic reduce assembles the flat gradient (torch parameter order).
 #include "rlp_mfma_x3.hpp"
 
+// RLP_FD_PIPE: the GEMM chunks' fragment reads one tile pair ahead of the MFMAs (1: source order
+// only, 2: pinned with sched_group_barrier); 0: two groups of four tiles, each read then multiplied
+#ifndef RLP_FD_PIPE
+#define RLP_FD_PIPE 0
+#endif
+// RLP_FD_ILP: the FD tails' tanh chains issued in lock step (independent exp / rcp / fma streams)
+// and the g1 pass's layer-1 MFMA one neuron tile ahead
+#ifndef RLP_FD_ILP
+#define RLP_FD_ILP 0
+#endif
+
 namespace rlp {
 
 constexpr int kUpdRows = 64;          // rows per block tile (4 waves x 16)
@@ -104,6 +115,49 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
             const float *slot = ring + (((c / CPB) % kX3Ring) * CPB + c % CPB) * kX3ChunkFloats + lane * 4;
             if (hf == 0 && P + 1 < 8) pre(P + 1);
             if (hf == 1 && P + 1 < 8) bop(P + 1, nbh, nbl);
+#if RLP_FD_PIPE
+            // the chunk's 8 output tiles in four pairs, each pair's 4 fragments read while the
+            // previous pair's 6 MFMAs run (two register buffers: the same 32 fragment registers)
+            {
+                half8 fh[2][2], fl[2][2];
+                auto rd = [&](int grp, int buf) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        fh[buf][u] = *reinterpret_cast<const half8 *>(slot + (2 * (2 * grp + u)) * 256);
+                        fl[buf][u] = *reinterpret_cast<const half8 *>(slot + (2 * (2 * grp + u) + 1) * 256);
+                    }
+                };
+                rd(0, 0);
+#pragma unroll
+                for (int grp = 0; grp < 4; ++grp) {
+                    if (grp + 1 < 4) {
+                        rd(grp + 1, (grp + 1) & 1);
+#if RLP_FD_PIPE > 1
+                        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#endif
+                    }
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const half8 ah = fh[grp & 1][u], al = fl[grp & 1][u];
+                        floatx4 v = acc[8 * hf + 2 * grp + u];
+                        if constexpr (SWAP) {
+                            v = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, ah, v, 0, 0, 0);
+                            v = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, ah, v, 0, 0, 0);
+                            v = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, al, v, 0, 0, 0);
+                        } else {
+                            v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, v, 0, 0, 0);
+                            v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, v, 0, 0, 0);
+                            v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, v, 0, 0, 0);
+                        }
+                        acc[8 * hf + 2 * grp + u] = v;
+                    }
+#if RLP_FD_PIPE > 1
+                    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+#endif
+                }
+            }
+            if (false)
+#endif
             // the chunk's 8 output tiles in two groups of 4 (8 fragment reads, then 12 MFMAs):
             // 32 fragment registers instead of 64 keep two waves per SIMD within 256 registers
 #pragma unroll
@@ -302,12 +356,27 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
         floatx4 p0, p1;  // layer-1 tiles of the next phase (pre), consumed by its B operands (bop)
         x3_gemm16<false, kFdWaves, kFdCpb>(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
+#if RLP_FD_ILP
+            // eight independent chains in lock step (exp, then add, rcp, fma across all eight):
+            // the scheduler otherwise runs them one after another through one temporary
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = __builtin_amdgcn_exp2f(i < 4 ? p0[i] : p1[i - 4]);
+            asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
+                         "+v"(x[6]), "+v"(x[7]));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = __builtin_amdgcn_rcpf(1.0f + x[i]);
+            asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
+                         "+v"(x[6]), "+v"(x[7]));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = __builtin_fmaf(-2.0f * kX3HScale, x[i], kX3HScale);
+#else
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const float pre = i < 4 ? p0[i] : p1[i - 4];
                 const float ex = __builtin_amdgcn_exp2f(pre);  // pre = 2 h1 / ln 2 (small_r)
                 x[i] = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + ex), kX3HScale);
             }
+#endif
             split8(x, bh, bl);
         }, [&](int P) { p0 = layer1(2 * P); p1 = layer1(2 * P + 1); });
         // ---- h2 = tanh(z2), z3 = W3 h2 + b3 (every lane group ends with its row's z3)
@@ -458,6 +527,24 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
             split8(x, bh, bl);
         }, [](int) {});
         // ---- g1 = dh1 * (1 - h1^2), h1 = 1 - 2 r recomputed (r as in the forward's), neuron on lane
+#if RLP_FD_ILP
+        // layer 1 of the next neuron tile issued before this tile's VALU (its f32 MFMA result
+        // latency off the chain), the four elements' chains in lock step
+        floatx4 pn = layer1_t(0);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            floatx4 r = pn;
+            if (t + 1 < 16) pn = layer1_t(t + 1);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) r[q] = __builtin_amdgcn_exp2f(r[q]);
+            asm volatile("" : "+v"(r));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) r[q] = __builtin_amdgcn_rcpf(1.0f + r[q]);
+            asm volatile("" : "+v"(r));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dh1[t][q] = dh1[t][q] * unscale4 * __builtin_fmaf(-r[q], r[q], r[q]);
+        }
+#else
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const floatx4 pre = layer1_t(t);
@@ -467,6 +554,7 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
                 dh1[t][q] = dh1[t][q] * unscale4 * __builtin_fmaf(-r, r, r);
             }
         }
+#endif
         // ---- dW1 | db1 = sum_rows g1 [s | 1]^T: the lane's 4 rows in registers (s rows from srw),
         // then the 4 lane groups by a 2-stage permlane butterfly, per half of the neuron tiles
         // (8 NC -> 2 NC values)
@@ -554,6 +642,11 @@ struct WArgs {
 // VGPR + AGPR budget (JT = 4): every fragment read from LDS feeds 12 MFMAs instead of 6, so the
 // CU reads half the LDS bytes per tile, and the next fragment pair is read one step ahead.
 constexpr int kWgWaves = 8;
+// RLP_WG_SGB: pin each fragment pair's LDS reads one step ahead of the MFMAs that precede their
+// use (sched_group_barrier); without it the scheduler sinks them to just before their MFMAs
+#ifndef RLP_WG_SGB
+#define RLP_WG_SGB 0
+#endif
 template <int KS1, int W = kWgWaves>
 __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
     constexpr int H = kUpdH, SP = 4 * KS1, NT = 64 * W, JT = 16 / W;
@@ -641,7 +734,11 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
     // A operands of one K step: g2(rows 32 ks + 4 gq + i and 32 ks + 16 + 4 gq + i,
     // j = 16 JT wv + 16 jt + e) (the fragments' K order); loaded one K step ahead
     auto load_g2 = [&](int64_t tile, int ks, floatx4 (&gv)[JT][2]) {
+#if defined(RLP_WG_EXP) && (RLP_WG_EXP & 1)
+        const int64_t t = 0;  // timing experiment only: every block reads tile 0 (L2-resident)
+#else
         const int64_t t = tile < ntiles ? tile : ntiles - 1;
+#endif
 #pragma unroll
         for (int jt = 0; jt < JT; ++jt) {
             const gptr<float> src = as_global(g2base + t * kUpdTileFloats +
@@ -702,6 +799,9 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
                 if (F + 1 < 32) {
                     nbh = frag(cur, F + 1, 0);
                     nbl = frag(cur, F + 1, 1);
+#if RLP_WG_SGB
+                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // (pinned ahead of the MFMAs)
+#endif
                 }
 #pragma unroll
                 for (int jt = 0; jt < JT; ++jt) {
@@ -711,9 +811,14 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
                     v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jt], bh, v, 0, 0, 0);
                     acc2[jt][nt] = v;
                 }
+#if RLP_WG_SGB
+                __builtin_amdgcn_sched_group_barrier(0x008, 3 * JT, 0);
+#endif
                 // the next tile's fragments, spread over this tile's MFMAs (FPW per wave)
+#if !(defined(RLP_WG_EXP) && (RLP_WG_EXP & 2))  // (2: timing experiment without the h1 rebuild)
                 if (F % (32 / FPW) == (32 / FPW) - 1)
                     build_frag(nxt, FPW * wv + F / (32 / FPW));
+#endif
                 if (F + 1 < 32) {
                     bh = nbh;
                     bl = nbl;
