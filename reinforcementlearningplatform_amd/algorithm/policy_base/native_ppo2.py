@@ -124,15 +124,19 @@ class NativePPO2Learner:
             self.ws = torch.empty(int(need), dtype=torch.float32, device=self.device)
         return self.ws
 
-    def grads(self, s, a, a_lp, adv, vt, index=None):
-        """Gradients of one step's actor and critic losses into net.grad (no optimiser step)."""
+    def grads(self, s, a, a_lp, adv, vt, index=None, actor_cfg=None):
+        """Gradients of one step's actor and critic losses into net.grad (no optimiser step).
+        actor_cfg: the loss constants (_actor_cfg()) when the caller already holds them — reading
+        the actor's std / bounds from device tensors is a host synchronisation, which update()
+        pays once per call instead of once per optimiser step."""
         rows = int(index.shape[0]) if index is not None else int(s.shape[0])
         ws = self._workspace(rows)
         self.loss.zero_()
         adv, vt = adv.reshape(-1), vt.reshape(-1)
         na, nc = self.net_a, self.net_c
         K.mfma_pack(na.desc, na.flat, out=na.packed)
-        K.ppo2_grad(na.desc, na.packed, self._actor_cfg(), s, a=a, a_logprob=a_lp, adv=adv,
+        K.ppo2_grad(na.desc, na.packed, actor_cfg if actor_cfg is not None else self._actor_cfg(),
+                    s, a=a, a_logprob=a_lp, adv=adv,
                     index=index, grad=na.grad, loss_sum=self.loss[0:1], workspace=ws)
         K.mfma_pack(nc.desc, nc.flat, out=nc.packed)
         K.ppo2_grad(nc.desc, nc.packed, K.ppo2_loss_cfg(_abi.RLP_LOSS_CRITIC), s, v_target=vt,
@@ -153,8 +157,8 @@ class NativePPO2Learner:
                     beta2=self.betas[1], eps=self.eps, clip_sqnorm=clip_sqnorm,
                     max_norm=self.max_norm)
 
-    def step(self, s, a, a_lp, adv, vt, index=None):
-        rows = self.grads(s, a, a_lp, adv, vt, index)
+    def step(self, s, a, a_lp, adv, vt, index=None, actor_cfg=None):
+        rows = self.grads(s, a, a_lp, adv, vt, index, actor_cfg)
         if self.distributed:
             self._allreduce_grads()
         clip = self.msg['use_grad_clip']
@@ -196,15 +200,17 @@ class NativePPO2Learner:
         adv, vt = adv.reshape(-1).contiguous(), vt.reshape(-1).contiguous()
         if self.rule == 'dppo2':
             return self._update_dppo2(s, a, a_lp, adv, vt)
+        acfg = self._actor_cfg()  # one host read of std / bounds for all K epochs
         for k in range(m['K_epochs']):
             if m['using_mini_batch']:
                 perm = (perms[k].to(s.device) if perms is not None else
                         torch.randperm(N, device=s.device, generator=generator))
                 mb = m['mini_batch_size']
                 for i in range(0, N, mb):  # BatchSampler(..., drop_last=False)
-                    losses = self.step(s, a, a_lp, adv, vt, index=perm[i:i + mb].contiguous())
+                    losses = self.step(s, a, a_lp, adv, vt, index=perm[i:i + mb].contiguous(),
+                                       actor_cfg=acfg)
             else:
-                losses = self.step(s, a, a_lp, adv, vt)
+                losses = self.step(s, a, a_lp, adv, vt, actor_cfg=acfg)
         return losses
 
     def lr_decay(self, total_steps):

@@ -21,8 +21,12 @@
 
 // RLP_FD_PIPE: the GEMM chunks' fragment reads one tile pair ahead of the MFMAs (1: source order
 // only, 2: pinned with sched_group_barrier); 0: two groups of four tiles, each read then multiplied
+// (the next group's reads wait for the current MFMAs to release their registers: s_nop hazards and
+// exposed LDS latency). Same-box rocprof A/B (profiles/r3/r3s_fd_ab.txt): actor / critic FD
+// 8.25 / 8.17 -> 8.02 / 7.99 ms with 2; RLP_FD_ILP (lock-step tanh chains) gave nothing on top
+// and slowed the critic alone.
 #ifndef RLP_FD_PIPE
-#define RLP_FD_PIPE 0
+#define RLP_FD_PIPE 2
 #endif
 // RLP_FD_ILP: the FD tails' tanh chains issued in lock step (independent exp / rcp / fma streams)
 // and the g1 pass's layer-1 MFMA one neuron tile ahead
@@ -816,8 +820,15 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
 #endif
                 // the next tile's fragments, spread over this tile's MFMAs (FPW per wave)
 #if !(defined(RLP_WG_EXP) && (RLP_WG_EXP & 2))  // (2: timing experiment without the h1 rebuild)
-                if (F % (32 / FPW) == (32 / FPW) - 1)
+                if (F % (32 / FPW) == (32 / FPW) - 1) {
+#if RLP_WG_SGB > 1
+                    __builtin_amdgcn_sched_barrier(0);  // (the build stays a region of its own)
+#endif
                     build_frag(nxt, FPW * wv + F / (32 / FPW));
+#if RLP_WG_SGB > 1
+                    __builtin_amdgcn_sched_barrier(0);
+#endif
+                }
 #endif
                 if (F + 1 < 32) {
                     bh = nbh;

@@ -12,7 +12,7 @@ mkdir -p "$OUT"
 cp "$SRC"/build/rlp_*.o "$OUT"/
 for f in $FILES; do
   extra=""
-  [ "$f" = rlp_update ] && extra=-fno-slp-vectorize
+  [ "$f" = rlp_update ] && [ -z "${SLP:-}" ] && extra=-fno-slp-vectorize
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off \
       -munsafe-fp-atomics -w $extra "$@" -c "$SRC/$f.hip" -o "$OUT/$f.o" &
 done
