@@ -646,10 +646,14 @@ struct WArgs {
 // VGPR + AGPR budget (JT = 4): every fragment read from LDS feeds 12 MFMAs instead of 6, so the
 // CU reads half the LDS bytes per tile, and the next fragment pair is read one step ahead.
 constexpr int kWgWaves = 8;
-// RLP_WG_SGB: pin each fragment pair's LDS reads one step ahead of the MFMAs that precede their
-// use (sched_group_barrier); without it the scheduler sinks them to just before their MFMAs
+// RLP_WG_SGB: pin each fragment pair's LDS reads ahead of the MFMAs that precede their use
+// (sched_group_barrier); without it the scheduler sinks them to just before their MFMAs (exposed
+// LDS latency per column step). 2 (default) also fences each fragment build into a region of its
+// own so the pinned groups only see the GEMM: wgrad 3.16-3.19 -> 3.04-3.07 ms (same box, three
+// boxes -2.5 to -4 %, profiles/r3/r3v_wgrad_ab.txt); 1 (no fences) was 8 % slower, and the build
+// spread over four steps in stages measured neutral
 #ifndef RLP_WG_SGB
-#define RLP_WG_SGB 0
+#define RLP_WG_SGB 2
 #endif
 template <int KS1, int W = kWgWaves>
 __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
