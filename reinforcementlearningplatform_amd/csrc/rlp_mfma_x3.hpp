@@ -89,7 +89,11 @@ __device__ __forceinline__ void block_barrier_raw() {
 // W: waves of the block sharing the ring (4 or 8); each DMAs 16 / W of the 16 KiB of every chunk.
 // CPB: 16-KiB chunks per ring slot and block barrier (2: one barrier per k-phase instead of per
 // half-phase; the ring then holds RG x CPB chunks).
-template <int H, int SUB, int KS1, int NOUT, int RG = kX3Ring, int W = kX3Waves, int CPB = 1>
+// PB (pipelined B operands; one wave per SIMD): phase P + 1's tanh / split runs pair by pair
+// between phase P's MFMAs instead of as a VALU-only stretch at the head of phase P + 1, which a
+// lone wave cannot hide behind another wave's MFMAs.
+template <int H, int SUB, int KS1, int NOUT, int RG = kX3Ring, int W = kX3Waves, int CPB = 1,
+          bool PB = false>
 __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, const float *small,
                                                float *ring, const MfmaNet &net, const int nout,
                                                const float (&bobs)[SUB][KS1],
@@ -157,36 +161,51 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
     floatx4 hp0[SUB], hp1[SUB];
     layer1(0, hp0);
     layer1(1, hp1);
-
-#pragma unroll 1
-    for (int P = 0; P < NPH; ++P) {
-        half8 bh[SUB], bl[SUB];
+    // B operands of one neuron pair (values i, i + 1 of sub-block sb) from the layer-1 tiles
+    auto bop_pair = [&](int sb, int i, half8 (&dh)[SUB], half8 (&dl)[SUB]) {
+        const float2v pre = i < 4 ? (float2v){hp0[sb][i], hp0[sb][i + 1]}
+                                  : (float2v){hp1[sb][i - 4], hp1[sb][i - 3]};
+        // 2^SH tanh(h1) = 2^SH - 2^(SH+1) / (1 + exp2(pre)), pre = 2 h1 / ln 2 (small_r)
+        const float2v ex = {__builtin_amdgcn_exp2f(pre.x), __builtin_amdgcn_exp2f(pre.y)};
+        const float2v dn = ex + 1.0f;
+        const float2v rc = {__builtin_amdgcn_rcpf(dn.x), __builtin_amdgcn_rcpf(dn.y)};
+        const float2v x = __builtin_elementwise_fma(
+            rc, (float2v){-2.0f * kX3HScale, -2.0f * kX3HScale}, (float2v){kX3HScale, kX3HScale});
+        half2v hi, lo;
+#if RLP_X3_SPLIT_MIX
+        split2_mix(x, hi, lo);
+#else
+        split2(x, hi, lo);
+#endif
+        dh[sb][i] = hi.x;
+        dh[sb][i + 1] = hi.y;
+        dl[sb][i] = lo.x;
+        dl[sb][i + 1] = lo.y;
+    };
+    half8 bh[SUB], bl[SUB];
+    if constexpr (PB) {  // phase 0's operands up front, phase 1's layer-1 tiles
 #pragma unroll
         for (int sb = 0; sb < SUB; ++sb)
 #pragma unroll
-            for (int i = 0; i < 8; i += 2) {
-                const float2v pre = i < 4 ? (float2v){hp0[sb][i], hp0[sb][i + 1]}
-                                          : (float2v){hp1[sb][i - 4], hp1[sb][i - 3]};
-                // 2^SH tanh(h1) = 2^SH - 2^(SH+1) / (1 + exp2(pre)), pre = 2 h1 / ln 2 (small_r)
-                const float2v ex = {__builtin_amdgcn_exp2f(pre.x), __builtin_amdgcn_exp2f(pre.y)};
-                const float2v dn = ex + 1.0f;
-                const float2v rc = {__builtin_amdgcn_rcpf(dn.x), __builtin_amdgcn_rcpf(dn.y)};
-                const float2v x = __builtin_elementwise_fma(
-                    rc, (float2v){-2.0f * kX3HScale, -2.0f * kX3HScale}, (float2v){kX3HScale, kX3HScale});
-                half2v hi, lo;
-#if RLP_X3_SPLIT_MIX
-                split2_mix(x, hi, lo);
-#else
-                split2(x, hi, lo);
-#endif
-                bh[sb][i] = hi.x;
-                bh[sb][i + 1] = hi.y;
-                bl[sb][i] = lo.x;
-                bl[sb][i + 1] = lo.y;
+            for (int i = 0; i < 8; i += 2) bop_pair(sb, i, bh, bl);
+        layer1(2, hp0);
+        layer1(3, hp1);
+    }
+    // pairs per phase SUB * 4, spread over the phase's 16 tile steps
+    constexpr int PSTEP = 16 / (SUB * 4) > 0 ? 16 / (SUB * 4) : 1;
+
+#pragma unroll 1
+    for (int P = 0; P < NPH; ++P) {
+        half8 nbh[SUB], nbl[SUB];
+        if constexpr (!PB) {
+#pragma unroll
+            for (int sb = 0; sb < SUB; ++sb)
+#pragma unroll
+                for (int i = 0; i < 8; i += 2) bop_pair(sb, i, bh, bl);
+            if (P + 1 < NPH) {  // next phase's layer-1 tiles, under this phase's MFMAs
+                layer1(2 * P + 2, hp0);
+                layer1(2 * P + 3, hp1);
             }
-        if (P + 1 < NPH) {  // next phase's layer-1 tiles, under this phase's MFMAs
-            layer1(2 * P + 2, hp0);
-            layer1(2 * P + 3, hp1);
         }
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
@@ -226,6 +245,22 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
                     acc[sb][8 * hf + jj] = a;
                 }
                 __builtin_amdgcn_sched_group_barrier(0x008, 3 * SUB, 0);
+                if constexpr (PB) {  // next phase's operands (the last phase computes unused ones)
+                    const int st = 8 * hf + jj;
+                    if (st % PSTEP == PSTEP - 1 && st / PSTEP < SUB * 4)
+                        bop_pair((st / PSTEP) / 4, 2 * ((st / PSTEP) % 4), nbh, nbl);
+                }
+            }
+        }
+        if constexpr (PB) {
+#pragma unroll
+            for (int sb = 0; sb < SUB; ++sb) {
+                bh[sb] = nbh[sb];
+                bl[sb] = nbl[sb];
+            }
+            if (P + 2 < NPH) {  // the phase after next's layer-1 tiles
+                layer1(2 * P + 4, hp0);
+                layer1(2 * P + 5, hp1);
             }
         }
     }

@@ -240,6 +240,10 @@ constexpr int rollout_sp_lds_bytes() {
 #endif
 // UAV physics lanes per physics wave: 64 (half waves, 32, measured 6 % slower: the UAV step is
 // issue-bound, not latency-bound, so spreading it over more waves only adds issue)
+// pipelined B operands (mlp_x3_forward PB) in the one-wave-per-SIMD variants (modes 5 / 6)
+#ifndef RLP_SP_PB
+#define RLP_SP_PB 0
+#endif
 #ifndef RLP_SP_UAV_PHL
 #define RLP_SP_UAV_PHL 64
 #endif
@@ -371,7 +375,7 @@ rollout_sp_kernel(SpArgs<KIND> args) {
 #pragma unroll 1
         for (int which = both ? 0 : 1; which < 2; ++which) {
             float out[SUB][A];
-            mlp_x3_forward<H, SUB, KS1, A, RG, W, CPB>(which ? critic : actor, which ? small_c : small_a,
+            mlp_x3_forward<H, SUB, KS1, A, RG, W, CPB, RLP_SP_PB && WPS == 1>(which ? critic : actor, which ? small_c : small_a,
                                                   ring, which ? cn : an, which ? 1 : A, bobs, out);
             // lane (sub-block g, env e) owns out[g]
             float sel[A];

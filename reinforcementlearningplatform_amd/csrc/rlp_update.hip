@@ -73,15 +73,21 @@ __device__ __forceinline__ void lds_barrier() {
 // between the second chunk's MFMAs with sched_group_barrier measured within noise).
 // W: waves of the block sharing the ring (each DMAs 16 / W KiB of every chunk). CPB: 16-KiB
 // chunks per ring slot and block barrier (the ring holds kX3Ring x CPB chunks).
-template <bool SWAP = false, int W = 4, int CPB = 1, class BOp, class Pre>
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N <= 63, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <bool SWAP = false, int W = 4, int CPB = 1, int RG = kX3Ring, class BOp, class Pre>
 __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, float *my_part,
                                           floatx4 (&acc)[16], BOp &&bop, Pre &&pre) {
     constexpr int NC = 16, NPW = 16 / W, NS = NC / CPB;
+    static_assert(RG >= 3 && RG <= 6, "ring slots");
     const int lane = threadIdx.x & 63;
     auto issue = [&](int sc) {  // chunks CPB sc .. CPB sc + CPB - 1
 #pragma unroll
         for (int cc = 0; cc < CPB; ++cc) {
-            float *slot = my_part + ((sc % kX3Ring) * CPB + cc) * kX3ChunkFloats;
+            float *slot = my_part + ((sc % RG) * CPB + cc) * kX3ChunkFloats;
             // scalar chunk base (opaque: the unrolled loop would otherwise materialise all 64 piece
             // addresses up front) + the lane's 16 B: saddr DMA, no per-piece VALU address math
 #pragma unroll
@@ -93,8 +99,8 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
         }
     };
     lds_barrier();  // every wave is done with the ring
-    issue(0);
-    issue(1);
+#pragma unroll
+    for (int q = 0; q < RG - 1; ++q) issue(q);
     half8 bh, bl;
     pre(0);
     bop(0, bh, bl);
@@ -106,17 +112,18 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
             const int c = 2 * P + hf;
             if (c % CPB == 0) {
                 const int sc = c / CPB;
-                if (sc + 1 < NS) {  // own part of group sc landed (sc + 1's pieces may not)
-                    if constexpr (NPW * CPB == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-                    else if constexpr (NPW * CPB == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
+                // own part of group sc landed; the groups issued after it (up to RG - 2 of them)
+                // may still be in flight
+                const int newer = (sc + RG - 2 < NS ? sc + RG - 2 : NS - 1) - sc;
+                if (newer >= 4) wait_vmcnt<4 * NPW * CPB>();
+                else if (newer == 3) wait_vmcnt<3 * NPW * CPB>();
+                else if (newer == 2) wait_vmcnt<2 * NPW * CPB>();
+                else if (newer == 1) wait_vmcnt<NPW * CPB>();
+                else wait_vmcnt<0>();
                 block_barrier_raw();
-                if (sc + 2 < NS) issue(sc + 2);
+                if (sc + RG - 1 < NS) issue(sc + RG - 1);
             }
-            const float *slot = ring + (((c / CPB) % kX3Ring) * CPB + c % CPB) * kX3ChunkFloats + lane * 4;
+            const float *slot = ring + (((c / CPB) % RG) * CPB + c % CPB) * kX3ChunkFloats + lane * 4;
             if (hf == 0 && P + 1 < 8) pre(P + 1);
             if (hf == 1 && P + 1 < 8) bop(P + 1, nbh, nbl);
 #if RLP_FD_PIPE
@@ -256,7 +263,11 @@ constexpr int kFdRows = 16 * kFdWaves;
 #define RLP_FD_CPB 1
 #endif
 constexpr int kFdCpb = RLP_FD_CPB;
-constexpr int kFdRegion = kX3RingFloats * kFdCpb;
+// W2 chunk-ring slots of the FD GEMMs (RG - 2 groups in flight while one is read)
+#ifndef RLP_FD_RING
+#define RLP_FD_RING 3
+#endif
+constexpr int kFdRing = RLP_FD_RING;
 
 
 // W: waves per block (kFdWaves by default; 4 with one block per CU when the actor's and the
@@ -266,6 +277,8 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
     constexpr int kFdWaves = W, kFdRows = 16 * W;
     constexpr int H = kUpdH, SMALL = mlp_small_floats<H, KS1, A>();
     constexpr int NC = 4 * KS1 + 1;  // dW1 columns per neuron: s features | bias
+    // (the deeper ring only for the one-block-per-CU shape: two 4-wave blocks share a CU's LDS)
+    constexpr int kRing = W == 8 ? kFdRing : kX3Ring, kFdRegion = kRing * kX3ChunkFloats * kFdCpb;
     __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + kFdWaves * 16 * 8];
     float *ring = lds, *small = lds + kFdRegion;
     // the wave index as a scalar (readfirstlane): every wave-derived offset, the G2 tile and its
@@ -358,7 +371,7 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[j] = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * gq);
         floatx4 p0, p1;  // layer-1 tiles of the next phase (pre), consumed by its B operands (bop)
-        x3_gemm16<false, kFdWaves, kFdCpb>(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
+        x3_gemm16<false, kFdWaves, kFdCpb, kRing>(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
 #if RLP_FD_ILP
             // eight independent chains in lock step (exp, then add, rcp, fma across all eight):
@@ -521,7 +534,7 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) dh1[j] = floatx4{0.f, 0.f, 0.f, 0.f};
         // (operands swapped: dh1 comes out "neuron on lane", dh1[t][q] = row 4 gq + q, neuron 16 t + e)
-        x3_gemm16<true, kFdWaves, kFdCpb>(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
+        x3_gemm16<true, kFdWaves, kFdCpb, kRing>(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
