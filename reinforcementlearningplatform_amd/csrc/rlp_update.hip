@@ -755,11 +755,7 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
     // A operands of one K step: g2(rows 32 ks + 4 gq + i and 32 ks + 16 + 4 gq + i,
     // j = 16 JT wv + 16 jt + e) (the fragments' K order); loaded one K step ahead
     auto load_g2 = [&](int64_t tile, int ks, floatx4 (&gv)[JT][2]) {
-#if defined(RLP_WG_EXP) && (RLP_WG_EXP & 1)
-        const int64_t t = 0;  // timing experiment only: every block reads tile 0 (L2-resident)
-#else
         const int64_t t = tile < ntiles ? tile : ntiles - 1;
-#endif
 #pragma unroll
         for (int jt = 0; jt < JT; ++jt) {
             const gptr<float> src = as_global(g2base + t * kUpdTileFloats +
@@ -836,7 +832,6 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 3 * JT, 0);
 #endif
                 // the next tile's fragments, spread over this tile's MFMAs (FPW per wave)
-#if !(defined(RLP_WG_EXP) && (RLP_WG_EXP & 2))  // (2: timing experiment without the h1 rebuild)
                 if (F % (32 / FPW) == (32 / FPW) - 1) {
 #if RLP_WG_SGB > 1
                     __builtin_amdgcn_sched_barrier(0);  // (the build stays a region of its own)
@@ -846,7 +841,6 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
                     __builtin_amdgcn_sched_barrier(0);
 #endif
                 }
-#endif
                 if (F + 1 < 32) {
                     bh = nbh;
                     bl = nbl;
