@@ -8,16 +8,65 @@ normalisation, GAE(lambda) and advantage normalisation — everything learn() co
 With --e2e the K-epoch PPO2 update (librlp's native HIP update kernels on the same GPU) is also
 timed and reported separately under "e2e".
 
-Launch: python bench.py [--gpus 1]   |   torchrun --nproc-per-node N bench.py --gpus N
+Launch: python bench.py [--gpus N]   |   torchrun --nproc-per-node N bench.py --gpus N
+With --gpus N > 1 and no torchrun environment (WORLD_SIZE unset) bench.py starts the N rank
+processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, one GPU
+each); the launching process makes no GPU call. Every rank checks WORLD_SIZE == --gpus.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(argv):
+    """`python bench.py --gpus N` (N > 1) outside torchrun: run N rank processes of this script,
+    pass rank 0's JSON line through, return the first failing exit code (0 when all succeed).
+    Runs before torch is imported, so this process never touches the GPU (no exec after a HIP
+    call: the ranks are children)."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=None)
+    n = pre.parse_known_args(argv)[0].gpus
+    if n is None or n <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:   # one rank failed: the others would wait in a collective forever
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+if __name__ == "__main__":
+    _rc = _self_launch(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc if _rc >= 0 else 128 - _rc)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -126,6 +175,7 @@ class Segment:
 
     def __init__(self, env, n, T, seed, env_id0, H=256):
         kind, pf, timeout_flag = ENVS[env]
+        self.env = env
         self.kind, self.params = kind, pf()
         D, S, Ad = A.ENV_DIMS[kind]
         self.S, self.Ad, self.n, self.T = S, Ad, n, T
@@ -172,14 +222,28 @@ class Segment:
         self.learn_side()
 
 
+E2E_ENVS = {"cartpole": ("CartPole", "CartPole"), "uav": ("UavRobust", "uav_hover_outer_loop")}
+
+
 def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
-    """Whole PPO2 iterations: rollout + advantages + K full-batch epochs of the clipped-surrogate /
-    MSE update (torch autograd + Adam on this GPU; the DPPO2 CartPole drivers' k_epo = 6,
-    demonstration/DPPO2/DPPO2-4-CartPole/train.py:161). Returns env-steps/s of this rank."""
-    from reinforcementlearningplatform_amd.algorithm.policy_base.native_ppo2 import NativePPO2Learner
+    """Whole PPO2 iterations through the product driver class VecPPO2 (the Distributed_PPO2
+    Worker): rollout + value fix-up + reward normalisation + GAE + advantage normalisation + K
+    full-batch epochs of the clipped-surrogate / MSE update (librlp's native update, or torch
+    autograd + Adam, on this GPU). Under torch.distributed this is the data-parallel Worker with
+    norm_scope='global' (the Distributed_PPO2 default): every optimiser step all-reduces the
+    actor+critic gradients and every iteration gathers the reward / advantage statistics.
+    k_epochs: the DPPO2 CartPole drivers' k_epo = 6 (demonstration/DPPO2/DPPO2-4-CartPole/
+    train.py:161) or the PPO2 demo's K = 30 (PPO2-4-CartPole/train.py:146).
+    Returns env-steps/s of this rank, s per iteration, and the rollout launch time inside the
+    training loop (HIP events on the launch stream)."""
+    import importlib
     from reinforcementlearningplatform_amd.algorithm.policy_base.vec_ppo2 import (DEFAULT_PPO_MSG,
-                                                                                   PPO2Learner)
+                                                                                   VecPPO2)
     from reinforcementlearningplatform_amd.utils.classes import PPOActor_Gaussian, PPOCritic
+    pkg, cls_name = E2E_ENVS[seg.env]
+    env_cls = getattr(importlib.import_module(
+        f"reinforcementlearningplatform_amd.environment.{pkg}.{cls_name}"), cls_name)
+    env = env_cls(n_envs=seg.n, seed=seg.seed, env_id0=seg.env_id0)
     actor = PPOActor_Gaussian(seg.S, seg.Ad, np.array(seg.lo), np.array(seg.hi), init_std=seg.std[0])
     critic = PPOCritic(seg.S)
     with torch.no_grad():   # start from the bench nets
@@ -188,19 +252,19 @@ def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
             for p in m.parameters():
                 p.copy_(flat[off:off + p.numel()].view_as(p).cpu())
                 off += p.numel()
-    cls = NativePPO2Learner if learner == "native" else PPO2Learner
-    learner = cls(actor, critic, dict(DEFAULT_PPO_MSG, K_epochs=k_epochs), device="cuda")
-    b = seg.bufs
+    msg = dict(DEFAULT_PPO_MSG, K_epochs=k_epochs, norm_scope="global")
+    vec = VecPPO2(env, actor, critic, msg, T=seg.T, seed=seg.seed, learner=learner,
+                  success_rule=(seg.rule, seg.flag))
+    evs = []
 
-    def one():
-        seg.iteration()
-        learner.update(b["obs"].view(-1, seg.S), b["action"].view(-1, seg.Ad),
-                       b["logp"].view(-1, seg.Ad), seg.adv.view(-1, 1), seg.vt.view(-1, 1))
-        with torch.no_grad():   # the rollout's packed nets follow the learner
-            seg.actor.copy_(torch.cat([p.reshape(-1) for p in actor.parameters()]))
-            seg.critic.copy_(torch.cat([p.reshape(-1) for p in critic.parameters()]))
-            K.mfma_pack(seg.ad, seg.actor, out=seg.apk)
-            K.mfma_pack(seg.cd, seg.critic, out=seg.cpk)
+    def one(ev=None):
+        if ev is not None:
+            ev[0].record()
+        vec.rollout()
+        if ev is not None:
+            ev[1].record()
+        vec.advantages()
+        vec.update()
     one()
     dist_on = torch.distributed.is_available() and torch.distributed.is_initialized()
     if dist_on:
@@ -208,7 +272,8 @@ def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(iters):
-        one()
+        evs.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+        one(evs[-1])
     if dist_on:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -217,7 +282,36 @@ def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
         t = torch.tensor([dt], device="cuda")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
-    return seg.n * seg.T * iters / dt, dt / iters
+    rollout_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    info = {"rollout_ms": rollout_ms, "learner": type(vec.learner).__name__,
+            "norm_scope": "global" if vec.global_norm else "rank"}
+    if dist_on:
+        info["allreduce"] = allreduce_probe(vec)
+    del vec, env
+    return seg.n * seg.T * iters / dt, dt / iters, info
+
+
+def allreduce_probe(vec, reps=30):
+    """The per-optimiser-step RCCL all-reduce of the learner (one flat buffer of the actor+critic
+    gradients, native_ppo2.NativePPO2Learner._allreduce_grads), timed alone on this rank with HIP
+    events, and the collectives one PPO2 iteration issues."""
+    lrn = vec.learner
+    numel = sum(p.numel() for p in lrn.params())
+    buf = torch.zeros(numel, dtype=torch.float32, device="cuda")
+    for _ in range(3):
+        torch.distributed.all_reduce(buf, group=lrn.pg)
+    torch.distributed.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        torch.distributed.all_reduce(buf, group=lrn.pg)
+    e1.record()
+    torch.cuda.synchronize()
+    per_iter = vec.msg['K_epochs'] + (2 if vec.global_norm else 0)
+    return {"bytes": numel * 4, "ms_per_allreduce": e0.elapsed_time(e1) / reps,
+            "allreduces_per_iteration": per_iter,
+            "note": "K gradient all-reduces (one per optimiser step) + the reward-chunk and "
+                    "advantage-partial gathers of norm_scope='global'"}
 
 
 def soi_ddpg_leg(rank, n=65536, steps=20, warmup=3, batch=4096, capacity=1 << 20, seed=11):
@@ -614,7 +708,8 @@ def cpu_baseline(env, seconds=10.0):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one GPU each); default WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--env", default="cartpole", choices=sorted(ENVS))
@@ -657,15 +752,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch with torchrun "
+                 f"--nproc-per-node {args.gpus}, or without WORLD_SIZE set so bench.py starts the "
+                 f"ranks itself)")
     # one process per GPU; RLP_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks folded
     # onto the visible devices) — the driver's runs use RCCL ("nccl") with one GPU per rank
-    ndev = torch.cuda.device_count()
+    backend = os.environ.get("RLP_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()   # counting devices does not initialise HIP
+    if world > 1 and backend == "nccl" and ndev < world:
+        sys.exit(f"bench.py: --gpus {world} needs {world} visible GPUs, this node has {ndev} "
+                 f"(RLP_BENCH_BACKEND=gloo folds the ranks onto the visible GPUs for a rehearsal)")
     local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        backend = os.environ.get("RLP_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -827,18 +929,25 @@ def main():
             dist.all_reduce(t)   # independent env shards / replicas: sum of the ranks' rates
             d["value"], d["env_only"] = float(t[0]), float(t[1])
         out["ugvoa_sac"] = d
-    if args.e2e:
+    if args.e2e and args.env in E2E_ENVS:
         upd = ("librlp rlp_ppo2_grad + rlp_adam_step" if args.learner == "native"
                else "torch autograd + Adam (fp32)")
-        v, it_s = e2e_iterations(seg, args.e2e, learner=args.learner)
-        out["e2e"] = {"value": v * world, "unit": "env-steps/s", "s_per_iteration": it_s,
-                      "update": f"K=6 full-batch epochs per iteration (DPPO2 drivers' k_epo), {upd}",
-                      "note": "rollout + GAE + PPO update; `value` above is the rollout hot path"}
+        v, it_s, info = e2e_iterations(seg, args.e2e, learner=args.learner)
+        out["e2e"] = dict({"value": v * world, "unit": "env-steps/s", "s_per_iteration": it_s,
+                           "update": f"K=6 full-batch epochs per iteration (DPPO2 drivers' k_epo), {upd}",
+                           "note": "VecPPO2 iterations (rollout + value fix-up + reward / advantage "
+                                   "normalisation + GAE + PPO update); `value` above is the rollout "
+                                   "hot path"}, **info)
+        out["e2e"]["rollout_frac"] = flop_launch / (info["rollout_ms"] * 1e-3) / 1e12 / peak
         if args.e2e_k30:
-            v30, it30 = e2e_iterations(seg, max(1, args.e2e // 2), k_epochs=30, learner=args.learner)
-            out["e2e"]["k30"] = {
+            v30, it30, info30 = e2e_iterations(seg, max(1, args.e2e // 2), k_epochs=30,
+                                               learner=args.learner)
+            out["e2e"]["k30"] = dict({
                 "value": v30 * world, "unit": "env-steps/s", "s_per_iteration": it30,
-                "update": f"K=30 full-batch epochs per iteration (PPO2-4-CartPole/train.py:146), {upd}"}
+                "update": f"K=30 full-batch epochs per iteration (PPO2-4-CartPole/train.py:146), {upd}"},
+                **info30)
+            out["e2e"]["k30"]["rollout_frac"] = (flop_launch / (info30["rollout_ms"] * 1e-3) / 1e12
+                                                 / peak)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.env, args.cpu_seconds)
     if rank == 0:

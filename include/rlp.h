@@ -548,8 +548,9 @@ int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const fl
  *   alpha (adaptive): -mean(exp(log_alpha) * (log_pi + target_entropy)) -> grad -> Adam
  *   soft update target = tau * critic + (1 - tau) * target.
  * Noise: `noise` [2][B][A] (eps for s', then for s: the reference's two rsample calls in order) or
- * NULL for Philox draws keyed by (seed, *counter, row), *counter advanced per update on the device
- * (graph-capturable). */
+ * NULL for Philox draws keyed by (seed, *counter, row + (d + 1) * 2^40) for draw d (0: s', 1: s) —
+ * a stream disjoint from rlp_sac_sample's exploration draws, which key env ids < 2^40 — with
+ * *counter advanced per update on the device (graph-capturable). */
 typedef struct rlp_sac_nets {
     rlp_dense_net actor;       /* the trunk layers (relu after each); params = the actor's buffer */
     int64_t mean_offset;       /* mean head W [A][H] (b follows) in actor.params */

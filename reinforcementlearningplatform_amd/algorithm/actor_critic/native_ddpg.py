@@ -110,10 +110,14 @@ class _FlatNet:
 
 
 def _adam_hyper(opt):
-    if opt is None or len(opt.param_groups) != 1:
+    """The single param group of a plain torch.optim.Adam (or AdamW with weight_decay 0: the same
+    update), else None — any other optimizer (SGD, RMSprop, NAdam, RAdam, Adamax, ...) keeps the
+    torch update path."""
+    if type(opt) not in (torch.optim.Adam, torch.optim.AdamW) or len(opt.param_groups) != 1:
         return None
     g = opt.param_groups[0]
-    if g.get("weight_decay", 0) or g.get("amsgrad", False) or g.get("maximize", False):
+    if (g.get("weight_decay", 0) or g.get("amsgrad", False) or g.get("maximize", False)
+            or g.get("differentiable", False) or torch.is_tensor(g.get("lr"))):
         return None
     return g
 
@@ -216,4 +220,5 @@ class DDPGNativeUpdate:
         f = lambda t: t.to(torch.float32).contiguous()
         s, a, r, s_, end = f(s), f(a), f(r).reshape(-1), f(s_), f(end).reshape(-1)
         K.ddpg_update(self.c_nets, self._cfg(B), s, a, r, s_, end, self.work, self.losses)
-        return self.losses[0], self.losses[1]
+        out = self.losses.clone()   # fresh tensors: self.losses is rewritten by the next call
+        return out[0], out[1]

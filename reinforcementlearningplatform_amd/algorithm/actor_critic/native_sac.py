@@ -257,7 +257,8 @@ class SACNativeUpdate:
         nz = None if noise is None else f(noise)
         with torch.no_grad():
             K.sac_update(self.c_nets, self._cfg(B), s, a, r, s_, dw, nz, self.work, self.losses)
-        return self.losses[0], self.losses[1]
+        out = self.losses.clone()   # fresh tensors: self.losses is rewritten by the next call
+        return out[0], out[1]
 
 
 def _offsets(params):

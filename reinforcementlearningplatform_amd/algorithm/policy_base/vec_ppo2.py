@@ -219,6 +219,16 @@ class VecPPO2:
         if self.norm_scope not in ('global', 'rank'):
             raise ValueError(f"VecPPO2: norm_scope {self.norm_scope!r} (global | rank)")
         self.global_norm = self.norm_scope == 'global' and self.world > 1
+        if self.global_norm:
+            # the gathers size every rank's slot as this rank's, and the merges count n envs per
+            # rank chunk: every rank must hold the same number of envs
+            nn_ = torch.tensor([self.n, -self.n], dtype=torch.int64,
+                               device=self.device if self.device.type == "cuda" else "cpu")
+            torch.distributed.all_reduce(nn_, op=torch.distributed.ReduceOp.MAX,
+                                         group=self.learner.pg)
+            if int(nn_[0]) != -int(nn_[1]):
+                raise ValueError(f"VecPPO2: norm_scope='global' needs the same n_envs on every rank "
+                                 f"(min {-int(nn_[1])}, max {int(nn_[0])}); use norm_scope='rank'")
         self.adv_parts = K.adv_stats_parts(self.n)
         self.stats = K.adv_stats_buffer(self.n, self.world if self.global_norm else 1, self.device)
         self.gen = torch.Generator(device=self.device)

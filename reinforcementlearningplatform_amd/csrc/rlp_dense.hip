@@ -376,7 +376,9 @@ __global__ void __launch_bounds__(256) sac_head_kernel(const float *__restrict__
 #pragma unroll
         for (int j = 0; j < A; ++j) eps[j] = noise[(size_t)i * A + j];
     } else {
-        philox_normal_f32<A>(seed, *counter, (uint64_t)i + (draw << 40), eps);
+        // draw + 1 in the high bits: the update's stream never meets rlp_sac_sample's exploration
+        // draws, which key (seed, counter, env id) with env ids below 2^40
+        philox_normal_f32<A>(seed, *counter, (uint64_t)i + ((draw + 1) << 40), eps);
     }
     const float kHalfLog2Pi = 0.918938533204672742f, kLog2 = 0.693147180559945309f;
     float l = 0.f, corr = 0.f;

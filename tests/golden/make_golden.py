@@ -791,6 +791,103 @@ def gen_sac():
            for k in ("actor", "critic", "target_critic")})
 
 
+def _grad_tap(grads, name, opt, params):
+    """Record the .grad every parameter of `params` holds when `opt.step()` is first called (a
+    parameter without .grad is recorded as zeros: the optimizer skips it)."""
+    step = opt.step
+
+    def wrapped(*a, **k):
+        if name not in grads:
+            grads[name] = np.concatenate([
+                (p.grad.detach().reshape(-1).numpy().copy() if p.grad is not None
+                 else np.zeros(p.numel(), np.float32)) for p in params])
+        return step(*a, **k)
+    opt.step = wrapped
+
+
+def gen_ddpg_grad():
+    """DDPG.learn (algorithm/actor_critic/DDPG.py:72-109) once on a 1000-row batch with the
+    DDPG-SOI driver's nets (demonstration/DDPG/DDPG-4-SecondOrderIntegration/train.py:26-100): the
+    critic's and the actor's p.grad at their optimizer.step() (the actor's is taken through the
+    critic after its Adam step, as learn() does), plus before / after weights. Own RNG streams."""
+    g = np.random.default_rng(20264)
+    with quiet():
+        drv_d = load("demonstration/DDPG/DDPG-4-SecondOrderIntegration/train.py", "ref_ddpg_soi_train")
+        ddpg_mod = load("algorithm/actor_critic/DDPG.py", "ref_ddpg")
+    torch.manual_seed(23)
+    lo, hi = np.array([-3., -3.]), np.array([3., 3.])
+    nets = [drv_d.Actor(1e-4, 4, 2, lo, hi), drv_d.Actor(1e-4, 4, 2, lo, hi),
+            drv_d.Critic(3e-4, 4, 2), drv_d.Critic(3e-4, 4, 2)]
+    env_msg = {'state_dim': 4, 'action_dim': 2, 'action_range': np.stack([lo, hi], 1), 'name': 'SOI'}
+    B = 1000
+    agent = ddpg_mod.DDPG(env_msg=env_msg, gamma=0.99, actor_soft_update=0.005,
+                          critic_soft_update=0.005, memory_capacity=10000, batch_size=B,
+                          actor=nets[0], target_actor=nets[1], critic=nets[2], target_critic=nets[3])
+    names = ("actor", "target_actor", "critic", "target_critic")
+    mods_ = (agent.actor, agent.target_actor, agent.critic, agent.target_critic)
+    before = {k: _flat(m) for k, m in zip(names, mods_)}
+    batch = (g.uniform(-2, 2, (B, 4)), g.uniform(-3, 3, (B, 2)), g.normal(size=B),
+             g.uniform(-2, 2, (B, 4)), (g.uniform(size=B) > 0.1).astype(np.float32))
+    agent.memory.mem_counter = 10000
+    agent.memory.sample_buffer = lambda is_reward_ascent=True, has_log_prob=False: batch
+    grads = {}
+    _grad_tap(grads, "critic", agent.critic.optimizer, list(agent.critic.parameters()))
+    _grad_tap(grads, "actor", agent.actor.optimizer, list(agent.actor.parameters()))
+    agent.learn(is_reward_ascent=False, iter=1)
+    after = {k: _flat(m) for k, m in zip(names, mods_)}
+    np.savez_compressed(os.path.join(OUT, "ddpg_soi_grad.npz"), s=batch[0], a=batch[1], r=batch[2],
+                        s2=batch[3], end=batch[4], **{f"before_{k}": v for k, v in before.items()},
+                        **{f"after_{k}": v for k, v in after.items()},
+                        **{f"grad_{k}": v for k, v in grads.items()})
+    print("ddpg_grad", {k: float(np.abs(v).max()) for k, v in grads.items()})
+
+
+def gen_sac_grad():
+    """SAC.learn (algorithm/actor_critic/Soft_Actor_Critic.py:70-124) once on a 1000-row batch
+    with the SAC-UGVForward demo's nets (demonstration/SAC/SAC-4-UGVForward/train.py:32-120, 41
+    inputs), the log_std layer scaled so rows reach both clamp bounds: the actor's, critic's and
+    log_alpha's p.grad at their optimizer.step(), Normal.rsample's noise (both draws), before /
+    after weights. Own RNG streams."""
+    g = np.random.default_rng(20265)
+    with quiet():
+        drv_s = load("demonstration/SAC/SAC-4-UGVForward/train.py", "ref_sac_ugvf_train")
+        sac_mod = load("algorithm/actor_critic/Soft_Actor_Critic.py", "ref_sac")
+    torch.manual_seed(29)
+    S, A, B = 41, 2, 1000
+    lo, hi = np.array([-3., -2 * np.pi]), np.array([3., 2 * np.pi])
+    actor = drv_s.SACActor(S, A, lo, hi, std_scale=1.)
+    with torch.no_grad():
+        actor.log_std_layer.weight.mul_(150.0)
+        actor.mean_layer.weight.mul_(30.0)
+    critic, target = drv_s.SACCritic(S, A), drv_s.SACCritic(S, A)
+    env_msg = {'state_dim': S, 'action_dim': A, 'action_range': np.stack([lo, hi], 1), 'name': 'OA'}
+    agent = sac_mod.SAC(env_msg=env_msg, gamma=0.99, critic_tau=0.005, memory_capacity=10000,
+                        batch_size=B, actor=actor, critic=critic, target_critic=target, a_lr=1e-4,
+                        c_lr=1e-4, alpha_lr=1e-4, adaptive_alpha=True)
+    out = {f"before_{k}": _flat(m) for k, m in (("actor", agent.actor), ("critic", agent.critic),
+                                                ("target_critic", agent.target_critic))}
+    out["before_log_alpha"] = agent.log_alpha.detach().numpy().copy()
+    batch = (g.uniform(-1, 1, (B, S)), g.uniform(lo, hi, (B, A)), g.normal(size=B),
+             g.uniform(-1, 1, (B, S)), (g.uniform(size=B) < 0.1).astype(np.float32))
+    agent.memory.mem_counter = 10000
+    agent.memory.sample_buffer = lambda is_reward_ascent=True, has_log_prob=False: batch
+    grads = {}
+    _grad_tap(grads, "actor", agent.actor_optimizer, list(agent.actor.parameters()))
+    _grad_tap(grads, "critic", agent.critic_optimizer, list(agent.critic.parameters()))
+    _grad_tap(grads, "log_alpha", agent.alpha_optimizer, [agent.log_alpha])
+    with _EpsTape() as tp:
+        agent.learn(is_reward_ascent=False, iter=1)
+    for k, m in (("actor", agent.actor), ("critic", agent.critic), ("target_critic", agent.target_critic)):
+        out[f"after_{k}"] = _flat(m)
+    out["after_log_alpha"] = agent.log_alpha.detach().numpy().copy()
+    out["eps"] = np.stack([e.numpy() for e in tp.tape])
+    for name, v in zip(("s", "a", "r", "s2", "dw"), batch):
+        out[name] = v
+    out.update({f"grad_{k}": v for k, v in grads.items()})
+    np.savez_compressed(os.path.join(OUT, "sac_grad.npz"), **out)
+    print("sac_grad", len(tp.tape), {k: float(np.abs(v).max()) for k, v in grads.items()})
+
+
 # ---------------------------------------------------------------------------------------------
 # PPO2 learn() (Proximal_Policy_Optimization2.py:78-174) on a fixed buffer, the DPPO2 Worker's
 # learn() (demonstration/DPPO2/DPPO2-4-CartPole/Distributed_PPO2.py:54-103), and N=1 driver
@@ -1082,6 +1179,8 @@ if __name__ == "__main__":
     gen_replay()
     gen_ddpg()
     gen_sac()
+    gen_ddpg_grad()
+    gen_sac_grad()
     gen_ppo2_learn()
     gen_dppo2_learn()
     gen_ppo2_transcript("cartpole")
