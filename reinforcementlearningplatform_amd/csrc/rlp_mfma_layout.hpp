@@ -20,7 +20,11 @@
 //   small_r                   the resident part in the f16x3 forward's form (same internal
 //                             offsets; rlp_mfma_x3.hpp): W1, b1 times 2 / ln 2 (layer 1 yields
 //                             tanh's exp2 argument), B2c times 2^(sw+SH), info {2^sw, 1,
-//                             2^-(sw+SH), 0}
+//                             2^-(sw+SH), 0}; its W1 as [j / 16][k][j % 16] (w1r_index): a layer-1
+//                             A operand (lane (g, e) reads W1[16 t + e][4 kk + g]) is then 64
+//                             consecutive floats, conflict-free for ds_read_b32 (the [H][4 KS1]
+//                             form put lanes e and e + 8 on one bank: 2-way at KS1 = 1, 4-way at
+//                             KS1 = 2, the UAV's 6 inputs)
 //   X3  (256-B aligned)       W2 * 2^sw split into f16 hi + lo, the f16x3 path's chunks
 //                             (rlp_mfma_x3.hpp)
 //   X3T                       the same for W2^T (the PPO2 update's backward GEMM, rlp_update.hip)
@@ -31,6 +35,11 @@ namespace rlp {
 
 // f16x3 path: hidden activations h in [-1, 1] are scaled by 2^SH before the f16 split
 constexpr float kX3HScale = 4096.f;
+
+// offset of W1[j][k] in small_r's W1 block ([j / 16][k][j % 16], k < 4 KS1)
+__host__ __device__ constexpr int w1r_index(int j, int k, int KS1) {
+    return (j >> 4) * (64 * KS1) + k * 16 + (j & 15);
+}
 
 struct MfmaNet {
     int S, H, A, ks1;

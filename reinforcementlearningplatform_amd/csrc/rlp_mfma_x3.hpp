@@ -148,7 +148,7 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
     auto layer1 = [&](int t, floatx4(&c)[SUB]) {
         float w1[KS1];
 #pragma unroll
-        for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[(16 * t + e) * (4 * KS1) + 4 * kk + g];
+        for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[w1r_index(16 * t + e, 4 * kk + g, KS1)];
         const floatx4 b1 = *reinterpret_cast<const floatx4 *>(B1c + 16 * t + 4 * g);
 #pragma unroll
         for (int sb = 0; sb < SUB; ++sb) {

@@ -152,8 +152,9 @@ __global__ void mfma_pack_kernel(MfmaNet net, const float *__restrict__ P, float
         } else if (idx < net.off_x3) {  // small_r + alignment pad
             const int q = idx - net.off_small_r + net.off_w1;
             constexpr float k2 = 2.8853900817779268f;  // 2 / ln 2: tanh's exp(2x) as exp2
-            if (q < net.off_b1) {
-                const int j = (q - net.off_w1) / (4 * KS1), k = (q - net.off_w1) % (4 * KS1);
+            if (q < net.off_b1) {  // W1 as [j / 16][k][j % 16] (w1r_index)
+                const int o = q - net.off_w1;
+                const int j = 16 * (o / (64 * KS1)) + (o & 15), k = (o % (64 * KS1)) >> 4;
                 v = k < S ? W1[j * S + k] * k2 : 0.f;
             } else if (q < net.off_b2) {
                 v = b1[q - net.off_b1] * k2;

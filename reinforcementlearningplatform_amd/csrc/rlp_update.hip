@@ -23,15 +23,10 @@
 // only, 2: pinned with sched_group_barrier); 0: two groups of four tiles, each read then multiplied
 // (the next group's reads wait for the current MFMAs to release their registers: s_nop hazards and
 // exposed LDS latency). Same-box rocprof A/B (profiles/r3/r3s_fd_ab.txt): actor / critic FD
-// 8.25 / 8.17 -> 8.02 / 7.99 ms with 2; RLP_FD_ILP (lock-step tanh chains) gave nothing on top
-// and slowed the critic alone.
+// 8.25 / 8.17 -> 8.02 / 7.99 ms with 2; lock-step tanh chains in the tails gave nothing on top
+// and slowed the critic alone (removed).
 #ifndef RLP_FD_PIPE
 #define RLP_FD_PIPE 2
-#endif
-// RLP_FD_ILP: the FD tails' tanh chains issued in lock step (independent exp / rcp / fma streams)
-// and the g1 pass's layer-1 MFMA one neuron tile ahead
-#ifndef RLP_FD_ILP
-#define RLP_FD_ILP 0
 #endif
 
 namespace rlp {
@@ -313,6 +308,72 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
         for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] = 0.f;
     float g2max = 0.f;
+    floatx4 dh1[16];  // dh1 -> g1 of the wave's tile
+
+    // the small weights are re-read from LDS per use, not hoisted into registers (an opaque offset
+    // keeps the LDS address space; a pointer would go FLAT)
+    auto small_at = [&](int off) {
+        int smo = 0;
+        asm volatile("" : "+s"(smo));
+        return small + smo + off;
+    };
+    // layer 1 of neuron tile t "neuron on lane": C[row 4 gq + q][neuron 16 t + e] (operands swapped)
+    auto layer1_t = [&](int t, const float (&bo)[KS1]) {
+        const float *W1c = small_at(0);
+        const float *B1c = small_at(net.off_b1 - net.off_w1);
+        float w1[KS1];
+#pragma unroll
+        for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[w1r_index(16 * t + e, 4 * kk + gq, KS1)];
+        const float b1 = B1c[16 * t + e];
+        floatx4 c = {b1, b1, b1, b1};
+#pragma unroll
+        for (int kk = 0; kk < KS1; ++kk)
+            c = __builtin_amdgcn_mfma_f32_16x16x4f32(bo[kk], w1[kk], c, 0, 0, 0);
+        return c;
+    };
+    // g1 = dh1 * (1 - h1^2) of neuron tile t, h1 = 1 - 2 r recomputed (r as in the forward's)
+    auto g1_tile = [&](int t, const float (&bo)[KS1], float us) {
+        const floatx4 pre = layer1_t(t, bo);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(pre[q]));
+            dh1[t][q] = dh1[t][q] * us * __builtin_fmaf(-r, r, r);
+        }
+    };
+    // dW1 | db1 += sum_rows g1 [s | 1]^T: the lane's 4 rows in registers (s rows from srw), then
+    // the 4 lane groups by a 2-stage permlane butterfly, per half of the neuron tiles
+    // (8 NC -> 2 NC values)
+    auto dw1_acc = [&](const float *srw) {
+        float sv[4][4 * KS1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int kk = 0; kk < KS1; ++kk) {
+                const floatx4 v = *reinterpret_cast<const floatx4 *>(srw + (4 * gq + q) * 8 + 4 * kk);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) sv[q][4 * kk + u] = v[u];
+            }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float v[8 * NC];
+#pragma unroll
+            for (int tt = 0; tt < 8; ++tt) {
+                const floatx4 gt = dh1[8 * h + tt];
+#pragma unroll
+                for (int f = 0; f < 4 * KS1; ++f) {
+                    float x = gt[0] * sv[0][f];
+#pragma unroll
+                    for (int q = 1; q < 4; ++q) x = __builtin_fmaf(gt[q], sv[q][f], x);
+                    v[tt * NC + f] = x;
+                }
+                v[tt * NC + 4 * KS1] = (gt[0] + gt[1]) + (gt[2] + gt[3]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4 * NC; ++i) v[i] = pair_sum_x32(v[i], v[i + 4 * NC]);
+#pragma unroll
+            for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] += pair_sum_x16(v[i], v[i + 2 * NC]);
+        }
+    };
 
     const int64_t nbt = (g.rows + kFdRows - 1) / kFdRows;  // block tiles of kFdRows rows
     for (int64_t bt = blockIdx.x; bt < nbt; bt += gridDim.x) {
@@ -346,23 +407,11 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
         auto layer1 = [&](int t) {
             float w1[KS1];
 #pragma unroll
-            for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[(16 * t + e) * (4 * KS1) + 4 * kk + gq];
+            for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[w1r_index(16 * t + e, 4 * kk + gq, KS1)];
             floatx4 c = *reinterpret_cast<const floatx4 *>(B1c + 16 * t + 4 * gq);
 #pragma unroll
             for (int kk = 0; kk < KS1; ++kk)
                 c = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[kk], bobs[kk], c, 0, 0, 0);
-            return c;
-        };
-        // the same tile "neuron on lane": C[row 4 gq + q][neuron 16 t + e] (operands swapped)
-        auto layer1_t = [&](int t) {
-            float w1[KS1];
-#pragma unroll
-            for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[(16 * t + e) * (4 * KS1) + 4 * kk + gq];
-            const float b1 = B1c[16 * t + e];
-            floatx4 c = {b1, b1, b1, b1};
-#pragma unroll
-            for (int kk = 0; kk < KS1; ++kk)
-                c = __builtin_amdgcn_mfma_f32_16x16x4f32(bobs[kk], w1[kk], c, 0, 0, 0);
             return c;
         };
 
@@ -373,27 +422,12 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
         floatx4 p0, p1;  // layer-1 tiles of the next phase (pre), consumed by its B operands (bop)
         x3_gemm16<false, kFdWaves, kFdCpb, kRing>(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
-#if RLP_FD_ILP
-            // eight independent chains in lock step (exp, then add, rcp, fma across all eight):
-            // the scheduler otherwise runs them one after another through one temporary
-#pragma unroll
-            for (int i = 0; i < 8; ++i) x[i] = __builtin_amdgcn_exp2f(i < 4 ? p0[i] : p1[i - 4]);
-            asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
-                         "+v"(x[6]), "+v"(x[7]));
-#pragma unroll
-            for (int i = 0; i < 8; ++i) x[i] = __builtin_amdgcn_rcpf(1.0f + x[i]);
-            asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
-                         "+v"(x[6]), "+v"(x[7]));
-#pragma unroll
-            for (int i = 0; i < 8; ++i) x[i] = __builtin_fmaf(-2.0f * kX3HScale, x[i], kX3HScale);
-#else
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const float pre = i < 4 ? p0[i] : p1[i - 4];
                 const float ex = __builtin_amdgcn_exp2f(pre);  // pre = 2 h1 / ln 2 (small_r)
                 x[i] = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + ex), kX3HScale);
             }
-#endif
             split8(x, bh, bl);
         }, [&](int P) { p0 = layer1(2 * P); p1 = layer1(2 * P + 1); });
         // ---- h2 = tanh(z2), z3 = W3 h2 + b3 (every lane group ends with its row's z3)
@@ -530,7 +564,6 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
         const float sc = __builtin_amdgcn_ldexpf(1.f, 14 - ex);
         // exact powers of two; x 4: 1 - h1^2 = 4 r (1 - r) for h1 = 1 - 2 r
         const float unscale4 = 4.f * __builtin_amdgcn_ldexpf(1.f, ex - 14) / sw;
-        floatx4 dh1[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) dh1[j] = floatx4{0.f, 0.f, 0.f, 0.f};
         // (operands swapped: dh1 comes out "neuron on lane", dh1[t][q] = row 4 gq + q, neuron 16 t + e)
@@ -543,69 +576,10 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
             }
             split8(x, bh, bl);
         }, [](int) {});
-        // ---- g1 = dh1 * (1 - h1^2), h1 = 1 - 2 r recomputed (r as in the forward's), neuron on lane
-#if RLP_FD_ILP
-        // layer 1 of the next neuron tile issued before this tile's VALU (its f32 MFMA result
-        // latency off the chain), the four elements' chains in lock step
-        floatx4 pn = layer1_t(0);
+        // ---- g1 = dh1 * (1 - h1^2) and dW1 | db1 of this tile
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            floatx4 r = pn;
-            if (t + 1 < 16) pn = layer1_t(t + 1);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) r[q] = __builtin_amdgcn_exp2f(r[q]);
-            asm volatile("" : "+v"(r));
-#pragma unroll
-            for (int q = 0; q < 4; ++q) r[q] = __builtin_amdgcn_rcpf(1.0f + r[q]);
-            asm volatile("" : "+v"(r));
-#pragma unroll
-            for (int q = 0; q < 4; ++q) dh1[t][q] = dh1[t][q] * unscale4 * __builtin_fmaf(-r[q], r[q], r[q]);
-        }
-#else
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const floatx4 pre = layer1_t(t);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(pre[q]));
-                dh1[t][q] = dh1[t][q] * unscale4 * __builtin_fmaf(-r, r, r);
-            }
-        }
-#endif
-        // ---- dW1 | db1 = sum_rows g1 [s | 1]^T: the lane's 4 rows in registers (s rows from srw),
-        // then the 4 lane groups by a 2-stage permlane butterfly, per half of the neuron tiles
-        // (8 NC -> 2 NC values)
-        {
-            float sv[4][4 * KS1];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int kk = 0; kk < KS1; ++kk) {
-                    const floatx4 v = *reinterpret_cast<const floatx4 *>(srw + (4 * gq + q) * 8 + 4 * kk);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) sv[q][4 * kk + u] = v[u];
-                }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                float v[8 * NC];
-#pragma unroll
-                for (int tt = 0; tt < 8; ++tt) {
-                    const floatx4 gt = dh1[8 * h + tt];
-#pragma unroll
-                    for (int f = 0; f < 4 * KS1; ++f) {
-                        float x = gt[0] * sv[0][f];
-#pragma unroll
-                        for (int q = 1; q < 4; ++q) x = __builtin_fmaf(gt[q], sv[q][f], x);
-                        v[tt * NC + f] = x;
-                    }
-                    v[tt * NC + 4 * KS1] = (gt[0] + gt[1]) + (gt[2] + gt[3]);
-                }
-#pragma unroll
-                for (int i = 0; i < 4 * NC; ++i) v[i] = pair_sum_x32(v[i], v[i + 4 * NC]);
-#pragma unroll
-                for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] += pair_sum_x16(v[i], v[i + 2 * NC]);
-            }
-        }
+        for (int t = 0; t < 16; ++t) g1_tile(t, bobs, unscale4);
+        dw1_acc(srw);
     }
 
     // ---- per-wave partials: dW3 (lane's neurons) | db3 summed over the 16 row lanes | dW1 | db1
@@ -689,7 +663,8 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
         // small_r: W1, b1 x 2/ln 2 (h1 as in the FD forward)
         const float *W1c = w.packed + net.off_small_r;
         const float *B1c = w.packed + net.off_small_r + (net.off_b1 - net.off_w1);
-        for (int i = threadIdx.x; i < H * SP; i += blockDim.x) w1s[i / SP][i % SP] = W1c[i];
+        for (int i = threadIdx.x; i < H * SP; i += blockDim.x)
+            w1s[i / SP][i % SP] = W1c[w1r_index(i / SP, i % SP, KS1)];
         for (int i = threadIdx.x; i < H; i += blockDim.x) b1s[i] = B1c[i];
     }
     // g2 scale: max|g2| * 2^sg in [2^13, 2^14)
@@ -892,7 +867,8 @@ __global__ void __launch_bounds__(512, 1) ppo2_wgrad32_kernel(WArgs w) {
     {
         const float *W1c = w.packed + net.off_small_r;
         const float *B1c = w.packed + net.off_small_r + (net.off_b1 - net.off_w1);
-        for (int i = threadIdx.x; i < H * SP; i += blockDim.x) w1s[i / SP][i % SP] = W1c[i];
+        for (int i = threadIdx.x; i < H * SP; i += blockDim.x)
+            w1s[i / SP][i % SP] = W1c[w1r_index(i / SP, i % SP, KS1)];
         for (int i = threadIdx.x; i < H; i += blockDim.x) b1s[i] = B1c[i];
     }
     const float gm = __uint_as_float(*w.g2max);

@@ -857,7 +857,7 @@ def gen_sac_grad():
     lo, hi = np.array([-3., -2 * np.pi]), np.array([3., 2 * np.pi])
     actor = drv_s.SACActor(S, A, lo, hi, std_scale=1.)
     with torch.no_grad():
-        actor.log_std_layer.weight.mul_(150.0)
+        actor.log_std_layer.weight.mul_(1500.0)
         actor.mean_layer.weight.mul_(30.0)
     critic, target = drv_s.SACCritic(S, A), drv_s.SACCritic(S, A)
     env_msg = {'state_dim': S, 'action_dim': A, 'action_range': np.stack([lo, hi], 1), 'name': 'OA'}

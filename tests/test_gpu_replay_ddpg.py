@@ -219,6 +219,39 @@ def _batch(B, seed):
             dev(rng.uniform(-2, 2, (B, 4))), dev((rng.uniform(size=B) > 0.1).astype(np.float32)))
 
 
+def ddpg_f64_grads(before, critic_after, batch, gamma=0.99):
+    """DDPG.learn's gradients (DDPG.py:83-104) in float64 on the CPU: `before` = deep copies of
+    (actor, target_actor, critic, target_critic) at the step's start; the critic's gradient at the
+    before-weights, the actor's through `critic_after` (the critic after its own Adam step)."""
+    import copy
+    dbl = lambda m: copy.deepcopy(m).cpu().double()
+    actor, t_actor, critic, t_critic = (dbl(m) for m in before)
+    for m in (actor, t_actor):   # (non-parameter tensors: .cpu() / .double() do not move them)
+        m.gain, m.off = m.gain.detach().cpu().double(), m.off.detach().cpu().double()
+    s, a, r, s_, end = (x.detach().cpu().double() for x in batch)
+    with torch.no_grad():
+        target = r.unsqueeze(1) + gamma * end.unsqueeze(1) * t_critic(s_, t_actor(s_))
+    func.mse_loss(target, critic(s, a)).backward()
+    gc = torch.cat([p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), dtype=torch.float64)
+                    for p in critic.parameters()])
+    ca = dbl(critic_after)
+    for p in ca.parameters():
+        p.requires_grad_(False)
+    (-ca(s, actor(s)).mean()).backward()
+    ga = torch.cat([p.grad.reshape(-1) for p in actor.parameters()])
+    return {"critic": gc.numpy(), "actor": ga.numpy()}
+
+
+def assert_f32_class(name, native, torch32, truth_n, truth_t, floor_rel=2e-7):
+    """|native - f64| <= 4 |torch f32 - f64| + 2e-7 max|g| (each against the float64 gradient of
+    the inputs it used): the f32-class bound tests/test_learn_golden.py puts on the PPO2 update."""
+    native, torch32 = (np.asarray(x, np.float64) for x in (native, torch32))
+    e32 = np.abs(torch32 - truth_t).max()
+    en = np.abs(native - truth_n).max()
+    floor = floor_rel * np.abs(truth_n).max()
+    assert en <= 4 * e32 + floor, (name, en, e32, floor)
+
+
 @pytest.mark.parametrize("B", [4096, 1000])
 def test_native_ddpg_tracks_torch_update(B):
     """rlp_ddpg_update against the torch autograd + Adam path from the same weights over 5
@@ -231,12 +264,22 @@ def test_native_ddpg_tracks_torch_update(B):
         getattr(n_agent, k).load_state_dict(getattr(t_agent, k).state_dict())
     av0 = n_agent.critic.action_value.weight.detach().clone()
     tav0 = n_agent.target_critic.action_value.weight.detach().clone()
+    import copy
     for it in range(5):
         batch = _batch(B, it)
+        before = [copy.deepcopy(getattr(t_agent, k)) for k in
+                  ("actor", "target_actor", "critic", "target_critic")]
         lt = t_agent.update(*batch)
         ln = n_agent.update(*batch)
         for x, y in zip(lt, ln):
             torch.testing.assert_close(y, x, rtol=2e-4, atol=1e-6)
+        if it == 0:   # the same start: both gradients against float64, f32-class bound
+            tn = ddpg_f64_grads(before, n_agent.critic, batch)
+            tt = ddpg_f64_grads(before, t_agent.critic, batch)
+            for k in ("critic", "actor"):
+                gt = torch.cat([p.grad.reshape(-1) if p.grad is not None else torch.zeros_like(p).reshape(-1)
+                                for p in getattr(t_agent, k).parameters()])
+                assert_f32_class(k, n_agent._native.grad[k].cpu(), gt.cpu(), tn[k], tt[k])
     for k in ("actor", "target_actor", "critic", "target_critic"):
         torch.testing.assert_close(_flat(getattr(n_agent, k)), _flat(getattr(t_agent, k)),
                                    rtol=1e-4, atol=2e-6, msg=k)
@@ -318,19 +361,51 @@ def test_native_ddpg_odd_shapes_track_torch():
     rng = np.random.default_rng(4)
     B = 777
     d = lambda x: torch.as_tensor(x, dtype=torch.float32, device="cuda")
+    import copy
     for it in range(3):
         batch = (d(rng.uniform(-2, 2, (B, 3))), d(rng.uniform(-2, 2, (B, 1))), d(rng.normal(size=B)),
                  d(rng.uniform(-2, 2, (B, 3))), d((rng.uniform(size=B) > 0.1).astype(np.float32)))
+        before = [copy.deepcopy(getattr(agents[0], k)) for k in
+                  ("actor", "target_actor", "critic", "target_critic")]
         lt = agents[0].update(*batch)
         ln = agents[1].update(*batch)
         for x, y in zip(lt, ln):
             torch.testing.assert_close(y, x, rtol=2e-4, atol=1e-6)
-        if it == 0:
+        if it == 0:   # the same start: both gradients against float64, f32-class bound
+            tn = ddpg_f64_grads(before, agents[1].critic, batch)
+            tt = ddpg_f64_grads(before, agents[0].critic, batch)
             for k in ("actor", "critic"):
                 gt = torch.cat([p.grad.reshape(-1) for p in getattr(agents[0], k).parameters()])
-                gn = agents[1]._native.grad[k]
-                assert float((gn - gt).abs().max()) <= 1e-4 * float(gt.abs().max()) + 1e-8, k
+                assert_f32_class(k, agents[1]._native.grad[k].cpu(), gt.cpu(), tn[k], tt[k])
     for k in ("actor", "target_actor", "critic", "target_critic"):
         a = _flat(getattr(agents[1], k))
         b = _flat(getattr(agents[0], k))
         assert float((a - b).abs().max()) <= 3e-5, (k, float((a - b).abs().max()))
+
+
+@pytest.mark.parametrize("opt", ["sgd", "nadam", "adamw_wd"])
+def test_native_ddpg_needs_plain_adam(opt):
+    """The native update implements torch.optim.Adam only: an SGD, NAdam or weight-decayed AdamW
+    optimizer keeps the torch update path under native='auto' (and trains with that optimizer),
+    and native=True refuses it."""
+    lo, hi = np.array([-3., -3.]), np.array([3., 3.])
+    env_msg = {'state_dim': 4, 'action_dim': 2, 'action_range': np.stack([lo, hi], 1), 'name': 'x'}
+
+    def mk(native):
+        torch.manual_seed(2)
+        nets = [Actor(1e-4, 4, 2, lo, hi), Actor(1e-4, 4, 2, lo, hi), Critic(3e-4, 4, 2),
+                Critic(3e-4, 4, 2)]
+        for m in (nets[0], nets[2]):
+            m.optimizer = {"sgd": lambda p: torch.optim.SGD(p, lr=1e-3),
+                           "nadam": lambda p: torch.optim.NAdam(p, lr=1e-3),
+                           "adamw_wd": lambda p: torch.optim.AdamW(p, lr=1e-3, weight_decay=0.01),
+                           }[opt](m.parameters())
+        return DDPG(env_msg, actor=nets[0], target_actor=nets[1], critic=nets[2],
+                    target_critic=nets[3], device="cuda", native=native)
+    ag = mk("auto")
+    assert ag._native is None
+    p0 = _flat(ag.actor).clone()
+    ag.update(*_batch(256, 0))
+    assert not torch.equal(p0, _flat(ag.actor))
+    with pytest.raises(ValueError):
+        mk(True)
