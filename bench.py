@@ -83,14 +83,11 @@ PEAK_F16X3_TFLOPS = PEAK_F16_MFMA_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0
 # the rollout kernel each --physics mode launches (rlp_rollout.hip; the name rocprof reports)
 ROLLOUT_KERNEL = {"shared": "rlp::rollout_sp_kernel<KIND,256,SUB,4>",
-                  "shared8": "rlp::rollout_sp_kernel<KIND,256,1,8>",
                   "cu": "rlp::rollout_sp_kernel<KIND,256,2,8>",
-                  "cu16": "rlp::rollout_sp_kernel<KIND,256,1,8,2>",
                   "cu4": "rlp::rollout_sp_kernel<KIND,256,2,4,1>",
-                  "cu64": "rlp::rollout_sp_kernel<KIND,256,4,4,1>",
                   "lanes": "rlp::rollout_kernel<KIND,256,SUB,true>"}
 
-PHYSICS_MODES = {"auto": -1, "lanes": 0, "shared": 1, "shared8": 2, "cu": 3, "cu16": 4, "cu4": 5, "cu64": 6}
+PHYSICS_MODES = {"auto": -1, "lanes": 0, "shared": 1, "cu": 3, "cu4": 5}
 
 
 def rollout_kernel_name(physics, n, env="cartpole", sub=0):
@@ -312,6 +309,119 @@ def allreduce_probe(vec, reps=30):
             "allreduces_per_iteration": per_iter,
             "note": "K gradient all-reduces (one per optimiser step) + the reward-chunk and "
                     "advantage-partial gathers of norm_scope='global'"}
+
+
+def _demo_nets(S, A, lo, hi, actor_widths, critic_widths, seed):
+    """The demo drivers' PPOActor_Gaussian / PPOCritic with their own hidden widths (tanh hidden
+    layers, tanh(mean) * gain + off; orthogonal init, demonstration/PPO2/*/train.py)."""
+    import torch.nn as nn
+
+    class DemoActor(nn.Module):
+        def __init__(self):
+            super().__init__()
+            d = (S,) + tuple(actor_widths)
+            self.hidden = nn.ModuleList([nn.Linear(d[i], d[i + 1]) for i in range(len(actor_widths))])
+            self.mean_layer = nn.Linear(d[-1], A)
+            self.a_min, self.a_max = torch.tensor(lo, dtype=torch.float), torch.tensor(hi, dtype=torch.float)
+            self.off = (self.a_min + self.a_max) / 2.0
+            self.gain = self.a_max - self.off
+            self.std = torch.tensor(float((hi[0] - lo[0]) / 6), dtype=torch.float)
+            for l in self.hidden:
+                nn.init.orthogonal_(l.weight)
+                nn.init.constant_(l.bias, 0)
+            nn.init.orthogonal_(self.mean_layer.weight, gain=0.01)
+            nn.init.constant_(self.mean_layer.bias, 0)
+
+        def forward(self, s):
+            for l in self.hidden:
+                s = torch.tanh(l(s))
+            return torch.tanh(self.mean_layer(s)) * self.gain + self.off
+
+    class DemoCritic(nn.Module):
+        def __init__(self):
+            super().__init__()
+            d = (S,) + tuple(critic_widths) + (1,)
+            self.layers = nn.ModuleList([nn.Linear(d[i], d[i + 1]) for i in range(len(d) - 1)])
+            for l in self.layers:
+                nn.init.orthogonal_(l.weight)
+                nn.init.constant_(l.bias, 0)
+
+        def forward(self, s):
+            for l in self.layers[:-1]:
+                s = torch.tanh(l(s))
+            return self.layers[-1](s)
+
+    torch.manual_seed(seed)
+    return DemoActor(), DemoCritic()
+
+
+DEMO_E2E = {
+    # demonstration/PPO2/PPO2-4-SecondOrderIntegration/train.py:37-125,146 (K = 30)
+    "soi": dict(actor=(128, 64, 32), critic=(64, 64), K=30, n=65536, T=64),
+    # demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97,146 (K = 25)
+    "ugvoa": dict(actor=(256, 256), critic=(256, 256), K=25, n=16384, T=64),
+}
+
+
+def demo_nets_e2e_leg(rank, which, iters=2, seed=19):
+    """Whole PPO2 iterations (VecPPO2) for the PPO2 drivers whose nets the fused f16x3 kernels do
+    not take: the rollout through rlp_rollout's plain-layout path (SOI) or its per-step lidar path
+    (UGV-OA), the K-epoch update through rlp_ppo2_dense_grad (exact f32 MFMA GEMMs) + Adam."""
+    from reinforcementlearningplatform_amd.algorithm.policy_base.vec_ppo2 import VecPPO2
+    c = DEMO_E2E[which]
+    n, T = c["n"], c["T"]
+    if which == "soi":
+        from reinforcementlearningplatform_amd.environment.SecondOrderIntegration.SecondOrderIntegration \
+            import SecondOrderIntegration
+        env = SecondOrderIntegration(n_envs=n, seed=seed, env_id0=rank * n)
+    else:
+        from reinforcementlearningplatform_amd.environment.UGVForwardObstacleAvoidance import \
+            UGVForwardObstacleAvoidance
+        env = UGVForwardObstacleAvoidance(n_envs=n, variant="ppo2", seed=seed, env_id0=rank * n)
+    env.reset(random=True)
+    ar = np.array(env.action_range, dtype=np.float64)
+    actor, critic = _demo_nets(env.state_dim, env.action_dim, ar[:, 0], ar[:, 1], c["actor"],
+                               c["critic"], seed)
+    vec = VecPPO2(env, actor, critic, {'K_epochs': c["K"], 'gamma': 0.99}, T=T)
+    evs = []
+
+    def one(ev=None):
+        if ev is not None:
+            ev[0].record()
+        vec.rollout()
+        if ev is not None:
+            ev[1].record()
+        vec.advantages()
+        vec.update()
+    one()
+    dist_on = torch.distributed.is_available() and torch.distributed.is_initialized()
+    if dist_on:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        evs.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+        one(evs[-1])
+    if dist_on:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([dt], device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    lr = vec.learner
+    out = {"value": n * T * iters / dt, "unit": "env-steps/s", "s_per_iteration": dt / iters,
+           "rollout_ms": float(np.mean([a.elapsed_time(b) for a, b in evs])), "envs_per_gpu": n,
+           "T": T, "K_epochs": c["K"], "learner": type(lr).__name__,
+           "update": ("rlp_ppo2_dense_grad (exact f32 MFMA GEMMs) + rlp_adam_step"
+                      if getattr(lr, "net_a", None) is not None and lr.net_a.dense else "other"),
+           "rollout": "plain-layout nets (per-step rlp_mlp_forward + sample/step kernel)"
+                      if vec.plain else "fused / lidar per-step path",
+           "config": f"{env.name} PPO2, actor {[env.state_dim, *c['actor'], env.action_dim]} / "
+                     f"critic {[env.state_dim, *c['critic'], 1]} tanh (the demo driver's nets)"}
+    del vec, env
+    return out
 
 
 def soi_ddpg_leg(rank, n=65536, steps=20, warmup=3, batch=4096, capacity=1 << 20, seed=11):
@@ -550,9 +660,12 @@ def hbm_legs(seg, n_env=1 << 22, iters=10, warmup=2):
 
     def put(name, kernel, nbytes, ms, extra=None):
         gbs = nbytes / (ms * 1e-3) / 1e9
+        # "effective": algorithmic bytes / time. Part of a small kernel's reads can come from the
+        # L2 / Infinity Cache (PMC HBM bytes below the algorithmic ones), so this is not HBM
+        # utilisation; hbm_frac_pmc beside it prices the PMC-measured HBM bytes instead
         out[name] = dict({"kernel": kernel, "bytes_per_launch": int(nbytes), "avg_launch_ms": ms,
-                          "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                          "frac": gbs / PEAK_HBM_GBS}, **(extra or {}))
+                          "bandwidth": "effective", "achieved": gbs, "peak": PEAK_HBM_GBS,
+                          "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS}, **(extra or {}))
 
     b, smp = seg.bufs, seg.n * seg.T
     ms = timed(lambda: K.gae(seg.rnorm, b["value"], b["value_next"], b["done"], b["success"], 0.999,
@@ -721,15 +834,17 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e", type=int, default=2, help="PPO2 iterations incl. the K-epoch update to time (0: skip)")
     ap.add_argument("--e2e-k30", type=int, default=1, help="also time e2e at the PPO2 demo's K=30")
+    ap.add_argument("--demo-e2e", type=int, default=1, help="also time whole PPO2 iterations of the "
+                    "SOI (4-128-64-32) and UGV-OA (41-256-256) demo nets (dense native update)")
     ap.add_argument("--uav", type=int, default=1, help="also time the UavRobust rollout (32768 envs/GPU)")
     ap.add_argument("--fp32-leg", type=int, default=1, help="also time the exact-f32 MLP path")
     ap.add_argument("--ddpg", type=int, default=1, help="also time SOI DDPG with the HBM replay (config 3)")
     ap.add_argument("--oa", type=int, default=1, help="also time UGVForwardObstacleAvoidance env steps (lidar)")
     ap.add_argument("--sac", type=int, default=1, help="also time UGVForwardObstacleAvoidance SAC (config 5 shard)")
     ap.add_argument("--physics", default="auto", choices=list(PHYSICS_MODES),
-                    help="rollout kernel: env state in LDS + full-lane physics waves (4-wave blocks, "
-                         "8-wave blocks of 16-env waves, or one 8-wave block of 32- / 16-env waves "
-                         "per CU; auto: those when the envs fill every CU), or per-wave registers")
+                    help="rollout kernel: env state in LDS + full-lane physics waves (two 4-wave "
+                         "blocks per CU, one 8-wave block per CU, or one 4-wave block per CU; auto: "
+                         "cu when the envs fill every CU, else cu4), or per-wave registers")
     ap.add_argument("--uav-envs", type=int, default=32768, help="UavRobust leg's envs per GPU (config 4: 262144 / 8)")
     ap.add_argument("--uav-physics", default=None, choices=list(PHYSICS_MODES),
                     help="rollout kernel of the UavRobust leg (default: --physics)")
@@ -737,14 +852,6 @@ def main():
                     "advantage normalisation, SOI / UGV / UAV env steps) against the HBM roof")
     ap.add_argument("--learner", default="native", choices=["native", "torch"],
                     help="e2e leg's K-epoch update: librlp kernels or torch autograd + Adam")
-    ap.add_argument("--fd-mode", type=int, default=-1, choices=[-1, 0, 1, 2],
-                    help="rlp_set_fd_mode for the PPO2 update's FD kernel (-1: library default)")
-    ap.add_argument("--rollout-prio", type=int, default=-1, choices=[-1, 0, 1],
-                    help="rlp_set_rollout_prio (-1: library default)")
-    ap.add_argument("--update-prio", type=int, default=-1, choices=[-1, 0, 1],
-                    help="rlp_set_update_prio for the PPO2 update kernels (-1: library default)")
-    ap.add_argument("--wgrad-waves", type=int, default=0, choices=[0, 4, 8, 32],
-                    help="PPO2 update's weight-gradient kernel block shape (0: library default)")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="rollout hidden-layer arithmetic (include/rlp.h rlp_set_mlp_precision)")
     args = ap.parse_args()
@@ -774,14 +881,6 @@ def main():
             dist.init_process_group(backend)
     if args.sub:
         _native.set_rollout_sub(args.sub)
-    if args.wgrad_waves:
-        _native.lib().rlp_set_wgrad_waves(args.wgrad_waves)
-    if args.update_prio >= 0:
-        _native.lib().rlp_set_update_prio(args.update_prio)
-    if args.rollout_prio >= 0:
-        _native.lib().rlp_set_rollout_prio(args.rollout_prio)
-    if args.fd_mode >= 0:
-        _native.lib().rlp_set_fd_mode(args.fd_mode)
     _native.set_rollout_physics(PHYSICS_MODES[args.physics])
     prec = _native.MLP_F16X3 if args.precision == "f16x3" else _native.MLP_FP32
     _native.set_mlp_precision(prec)
@@ -901,6 +1000,8 @@ def main():
         out["hbm_kernels"] = hbm_legs(seg)
         for k, v in out["hbm_kernels"].items():
             v["traffic"] = pmc_kernel_traffic(k)
+            v["hbm_frac_pmc"] = (None if v["traffic"] is None else
+                                 v["traffic"] / (v["avg_launch_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS)
     if args.ddpg and args.env == "cartpole":
         d = soi_ddpg_leg(rank)
         if dist is not None:
@@ -929,6 +1030,11 @@ def main():
             dist.all_reduce(t)   # independent env shards / replicas: sum of the ranks' rates
             d["value"], d["env_only"] = float(t[0]), float(t[1])
         out["ugvoa_sac"] = d
+    if args.demo_e2e and args.env == "cartpole":
+        for which in ("soi", "ugvoa"):
+            d = demo_nets_e2e_leg(rank, which)
+            d["value"] *= world
+            out[f"{which}_ppo2_e2e"] = d
     if args.e2e and args.env in E2E_ENVS:
         upd = ("librlp rlp_ppo2_grad + rlp_adam_step" if args.learner == "native"
                else "torch autograd + Adam (fp32)")

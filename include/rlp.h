@@ -35,6 +35,7 @@ typedef void *rlp_stream_t; /* hipStream_t */
 #define RLP_OK 0
 #define RLP_EINVAL (-1000)
 #define RLP_EUNSUPPORTED (-1001)
+#define RLP_ENOMEM (-1002)  /* a stream-ordered scratch allocation failed */
 
 #define RLP_ABI_VERSION 1
 
@@ -316,11 +317,14 @@ typedef struct rlp_rollout_cfg {
     float a_min[4], a_max[4];
     /* per-call kernel selection; 0 = the library-wide default set by rlp_set_mlp_precision /
      * rlp_set_rollout_physics / rlp_set_rollout_sub, else value + 1 (mlp_precision: 1 RLP_MLP_FP32,
-     * 2 RLP_MLP_F16X3; physics: 1 register-resident, 2 shared, 3 shared 8-wave, 4 shared
-     * one-block-per-CU, 5 shared one-block-per-CU of 16-env waves, 6 / 7 one 4-wave block of 32- /
-     * 64-env waves per CU, 8 auto — the knob's -1); sub: 0 default,
-     * 1, 2, 4 */
-    int32_t mlp_precision, physics, sub, reserved;
+     * 2 RLP_MLP_F16X3; physics: 1 register-resident, 2 shared, 4 one 8-wave block per CU, 6 one
+     * 4-wave block per CU, 8 auto — the knob's -1; 3, 5, 7 RLP_EINVAL); sub: 0 default, 1, 2, 4 */
+    int32_t mlp_precision, physics, sub;
+    /* 0: actor / critic are rlp_mfma_pack buffers of [S -> 256 -> 256 -> A] tanh nets (the fused
+     * kernels); 1: plain parameters (rlp_mlp_param_count floats, torch order) of any Linear stack
+     * whose actor ends in tanh (the PPO2-SOI demo's 4-128-64-32-2 / 4-64-64-1): per step
+     * rlp_mlp_forward's kernels + one sample / env-step / append kernel, same draws and buffers */
+    int32_t net_layout;
 } rlp_rollout_cfg;
 
 /* state: [D][n] f64 in/out, carried across segments. need_reset: [n] u8 in/out (1 = env is
@@ -424,27 +428,21 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
                   const float *v_target, const int64_t *index, int64_t rows, float *grad,
                   double *loss_sum, float *workspace, rlp_stream_t stream);
 
-/* Block shape of rlp_ppo2_grad's forward/backward (FD) kernel, library-wide: 0 one 8-wave block
- * per CU (default), 1 two 4-wave blocks per CU, 2 one 4-wave block per CU (so that the actor's and
- * the critic's rlp_ppo2_grad, launched on two streams with their own workspaces, can share every
- * CU; measured no faster than mode 0 on one stream: e2e K=30 0.749 vs 0.733 s). */
-int rlp_set_fd_mode(int mode);
-int rlp_get_fd_mode(void);
-
-/* Block shape of rlp_ppo2_grad's weight-gradient (dW2 = sum_rows g2 h1^T) kernel, library-wide:
- * 8 (default) one 8-wave block per CU, each wave 32 output rows (2 waves per SIMD); 4 one 4-wave
- * block per CU, each wave 64 output rows with the VGPR + AGPR budget (1 wave per SIMD: half the
- * LDS fragment reads per tile, fragments read one step ahead). Same partial-sum order. */
-/* Tuning knob of rlp_ppo2_grad: 1 = the second half of each FD / wgrad block's waves (the younger
- * wave of every SIMD pair) runs at s_setprio 1, 0 = all waves at priority 0 (default). Same
- * results. */
-int rlp_set_update_prio(int mode);
-int rlp_get_update_prio(void);
-/* Weight-gradient kernel variant of rlp_ppo2_grad: 8 (default) / 4 = 8- / 4-wave blocks on
- * v_mfma_f32_16x16x32_f16 (identical results), 32 = the v_mfma_f32_32x32x16_f16 form (half the
- * MFMA issue slots; its K order differs, so results agree to f32 rounding). */
-int rlp_set_wgrad_waves(int waves);
-int rlp_get_wgrad_waves(void);
+/* The same gradient for any tanh Linear stack that rlp_ppo2_grad does not take (other widths, more
+ * or fewer hidden layers, more inputs): the PPO2-SecondOrderIntegration demo's actor
+ * 4 -> 128 -> 64 -> 32 -> A / critic 4 -> 64 -> 64 -> 1 (demonstration/PPO2/PPO2-4-
+ * SecondOrderIntegration/train.py:37-125), the obstacle-avoidance demos' 41 -> 256 -> 256 -> A
+ * (demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97). Hidden layers
+ * tanh; the actor's last layer tanh (A <= 4), the critic's linear with one output; widths <= 1024.
+ * `params` is the plain layout (rlp_mlp_param_count floats, torch order); rows are contiguous (a
+ * mini-batch is gathered by the caller). Exact f32 MFMA products (v_mfma_f32_16x16x4_f32),
+ * activations and the weight gradients' partials in `workspace`
+ * (rlp_ppo2_dense_workspace_floats), fixed summation order (run-to-run identical). */
+int64_t rlp_ppo2_dense_workspace_floats(const rlp_mlp_desc *desc, int64_t rows);
+int rlp_ppo2_dense_grad(const rlp_mlp_desc *desc, const float *params, const rlp_ppo2_loss_cfg *cfg,
+                        const float *s, const float *a, const float *a_logprob, const float *adv,
+                        const float *v_target, int64_t rows, float *grad, double *loss_sum,
+                        float *workspace, rlp_stream_t stream);
 
 /* out[0] += sum(grad^2) (torch.nn.utils.clip_grad_norm_'s total norm, squared), accumulated in
  * double in a fixed order: bit-identical on every run and every data-parallel rank. */
@@ -590,19 +588,14 @@ int64_t rlp_struct_size(int which);
  * 2 or 4. */
 int rlp_set_rollout_sub(int sub);
 /* Tuning knob of rlp_rollout (f16x3 path): -1 = auto (default: 3 when the envs fill every CU with
- * a 256-env block, else — and always for RLP_ENV_UAV_HOVER_OUTER_LOOP — 5), 5 = one 4-wave block
- * of 32-env waves per CU (1 wave per SIMD, VGPR + AGPR budget), 6 = the same with 64-env waves,
- * 1 = shared-physics
- * kernel (the block's env state in LDS, each step's f64 physics on full 64-lane waves; two 4-wave
- * blocks per CU), 4 = one 8-wave block of 16-env waves per CU (2 waves per SIMD), 2 = 8-wave
- * blocks of 16-env waves, two per CU (4 waves per SIMD), 3 = one 8-wave block of 32-env waves per CU
- * (2 waves per SIMD), 0 = the register-resident kernel (physics on the 16*sub lanes of each env's
- * own wave). Same results. */
+ * a 256-env block, else — and always for RLP_ENV_UAV_HOVER_OUTER_LOOP — 5), 3 = one 8-wave block
+ * of 32-env waves per CU (2 waves per SIMD), 5 = one 4-wave block of 32-env waves per CU (1 wave
+ * per SIMD, VGPR + AGPR budget), 1 = two 4-wave blocks per CU (the block's env state in LDS, each
+ * step's f64 physics on full 64-lane waves; the kernel for rlp_set_rollout_sub 1), 0 = the
+ * register-resident kernel (physics on the 16*sub lanes of each env's own wave; the RLP_MLP_FP32
+ * path's kernel). 2, 4 and 6 (measured-slower variants of earlier releases) return RLP_EINVAL.
+ * Same results. */
 int rlp_set_rollout_physics(int shared);
-/* Tuning knob of the fused rollout (rollout_sp_kernel): 1 = the younger half of each block's waves
- * (the second wave of every SIMD pair in the 8-wave variants) runs at s_setprio 1; 0 (default) =
- * all at priority 0. Same results. */
-int rlp_set_rollout_prio(int mode);
 /* Arithmetic of rlp_rollout's hidden layer (the [256 x 256] GEMM, 99 % of its FLOPs):
  *   RLP_MLP_F16X3 (default): error-compensated split, w*x = wh*xh + wh*xl + wl*xh on f16 MFMA with
  *     f32 accumulation — fp32-class accuracy (see tests/test_gpu_rollout.py) at 16/3 x the f32

@@ -57,14 +57,9 @@ def _declare(lib):
         "rlp_reward_norm_finish": (i32, [vp, i32, i32, i32, vp, vp, vp, vp, vp]),
         "rlp_ppo2_workspace_floats": (i64, [vp, i64]),
         "rlp_ppo2_grad": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp]),
+        "rlp_ppo2_dense_workspace_floats": (i64, [vp, i64]),
+        "rlp_ppo2_dense_grad": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp]),
         "rlp_grad_sqnorm": (i32, [vp, i64, vp, vp]),
-        "rlp_set_fd_mode": (i32, [i32]),
-        "rlp_get_fd_mode": (i32, []),
-        "rlp_set_wgrad_waves": (i32, [i32]),
-        "rlp_set_update_prio": (i32, [i32]),
-        "rlp_set_rollout_prio": (i32, [i32]),
-        "rlp_get_update_prio": (i32, []),
-        "rlp_get_wgrad_waves": (i32, []),
         "rlp_grad_clip": (i32, [vp, i64, vp, C.c_float, vp]),
         "rlp_adam_step": (i32, [vp, vp, vp, vp, i64, vp, vp, vp]),
         "rlp_replay_store": (i32, [vp, i64, vp, vp, vp, vp, vp, i64, vp]),
@@ -141,8 +136,7 @@ def set_rollout_sub(sub):
 
 def set_rollout_physics(shared):
     """-1: auto (default: 3 when the envs fill every CU with a 256-env block, else — and always
-    for the UAV — 5), 1: shared-physics rollout kernel (two 4-wave blocks per CU), 2: 8-wave
-    blocks of 16-env waves (4 waves per SIMD), 3: one 8-wave block of 32-env waves per CU, 4: one
-    8-wave block of 16-env waves per CU, 5 / 6: one 4-wave block of 32- / 64-env waves per CU
-    (1 wave per SIMD), 0: register-resident kernel (include/rlp.h rlp_set_rollout_physics)."""
+    for the UAV — 5), 1: shared-physics rollout kernel (two 4-wave blocks per CU), 3: one 8-wave
+    block of 32-env waves per CU, 5: one 4-wave block of 32-env waves per CU (1 wave per SIMD),
+    0: register-resident kernel (include/rlp.h rlp_set_rollout_physics)."""
     check(lib().rlp_set_rollout_physics(int(shared)), "rlp_set_rollout_physics")

@@ -6,8 +6,9 @@ PPO2_info). What runs where:
   choose_action / evaluate   actor forward on fp32 MFMA + Philox Gaussian sample (librlp)
   learn(): V(s), V(s')       critic forward on fp32 MFMA (librlp)
            GAE(lambda)       rlp_gae (bit-identical to the reference's NumPy-2 loop)
-           K epochs          learner="native" (default for the drivers' [S,256,256,A] tanh nets):
-                             librlp's update kernels (NativePPO2Learner); learner="torch": torch
+           K epochs          learner="native" (default for the drivers' Linear/Tanh nets):
+                             librlp's update kernels (NativePPO2Learner: f16x3 for [S,256,256,A],
+                             exact f32 GEMMs for other widths); learner="torch": torch
                              autograd + Adam on the same GPU. Both pinned to the reference's
                              learn() (tests/test_learn_golden.py, tests/test_gpu_transcript.py).
 The reference pins PPO2 to the CPU (:11-13); here everything lives on `device` (default cuda).
@@ -60,15 +61,15 @@ class Proximal_Policy_Optimization2:
         self.seed = int(seed) if seed is not None else int(np.random.randint(0, 2 ** 31 - 1))
         self.sample_counter = 0
         self.cnt = 0
-        fits = all(n.mfma_ok and n.desc.n_layers == 3 and n.desc.dims[1] == 256 and
-                   n.desc.dims[2] == 256 and n.desc.act[0] == _abi.RLP_ACT_TANH
-                   for n in (self.gpu_actor, self.gpu_critic))
+        from .native_ppo2 import NativePPO2Learner, dense_fits, native_fits
+        fits = all(native_fits(m) or dense_fits(m, a)
+                   for m, a in ((self.actor, True), (self.critic, False)))
         self.learner = learner or ("native" if fits else "torch")
         self.native = None
         if self.learner == "native":
             if not fits:
-                raise ValueError("learner='native' needs [S<=8 -> 256 -> 256 -> A<=4] tanh nets")
-            from .native_ppo2 import NativePPO2Learner
+                raise ValueError("learner='native' needs Linear/Tanh nets (tanh hidden layers, "
+                                 "tanh * gain + off actor head, linear critic head)")
             self.native = NativePPO2Learner(self.actor, self.critic, ppo_msg, device=self.device)
         elif self.learner != "torch":
             raise ValueError(f"learner {learner!r} (native | torch)")

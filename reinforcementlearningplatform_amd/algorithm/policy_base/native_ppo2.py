@@ -2,7 +2,9 @@
 algorithm/policy_base/Proximal_Policy_Optimization2.py:102-174) on librlp's HIP kernels.
 
 Per optimiser step and net: rlp_mfma_pack (packed weights), rlp_ppo2_grad (forward + loss
-gradient + backward + weight gradients on MFMA, include/rlp.h), optional RCCL all-reduce of the
+gradient + backward + weight gradients on MFMA, include/rlp.h) — or, for nets those f16x3 kernels
+do not take (the PPO2-SOI demo's 4-128-64-32 actor / 4-64-64 critic, the 41-input lidar nets),
+rlp_ppo2_dense_grad on exact f32 MFMA GEMMs — optional RCCL all-reduce of the
 actor+critic gradients (one flat buffer, as PPO2Learner), rlp_grad_sqnorm + rlp_adam_step
 (clip_grad_norm_ and torch.optim.Adam, evaluated on the device). Same interface and semantics as
 PPO2Learner (vec_ppo2.py), which stays as the torch-autograd reference the parity tests compare
@@ -31,22 +33,64 @@ from ... import _abi
 from ... import kernels as K
 
 
-def native_fits(module):
-    """True when librlp's update kernels take the net: a [S<=8 -> 256 -> 256 -> A<=4] Linear stack."""
+def _linears(module):
     lin = [m for m in module.modules() if isinstance(m, nn.Linear)]
     dims = [lin[0].in_features] + [l.out_features for l in lin] if lin else []
+    return lin, dims
+
+
+def native_fits(module):
+    """True when librlp's f16x3 update kernels (rlp_ppo2_grad) take the net: a
+    [S<=8 -> 256 -> 256 -> A<=4] Linear stack."""
+    lin, dims = _linears(module)
     return len(lin) == 3 and dims[1] == 256 and dims[2] == 256 and dims[0] <= 8 and dims[3] <= 4
+
+
+def dense_fits(module, is_actor):
+    """True when rlp_ppo2_dense_grad takes the net: Linear layers that chain, tanh after every
+    hidden layer, the actor's output tanh(z) * gain + off (A <= 4), the critic's linear (one
+    output), widths <= 1024 — checked against the module's own forward on a probe batch (the
+    PPO2-SOI demo's 4-128-64-32-A actor / 4-64-64-1 critic, the 41-input lidar nets)."""
+    lin, dims = _linears(module)
+    if not lin or len(lin) > _abi.RLP_MLP_MAX_LAYERS or max(dims) > 1024:
+        return False
+    if any(a.out_features != b.in_features for a, b in zip(lin[:-1], lin[1:])):
+        return False
+    if (is_actor and dims[-1] > 4) or (not is_actor and dims[-1] != 1):
+        return False
+    dev = lin[0].weight.device
+    x = torch.rand(64, dims[0], generator=torch.Generator().manual_seed(0)).to(dev) * 4 - 2
+    with torch.no_grad():
+        h = x
+        for i, l in enumerate(lin):
+            h = l(h)
+            if i < len(lin) - 1:
+                h = torch.tanh(h)
+        if is_actor:
+            gain, off = getattr(module, "gain", None), getattr(module, "off", None)
+            if not (torch.is_tensor(gain) and torch.is_tensor(off)):
+                return False
+            h = torch.tanh(h) * gain.to(dev) + off.to(dev)
+        try:
+            ref = module(x)
+        except Exception:
+            return False
+    return ref.shape == h.shape and bool(torch.allclose(ref, h, rtol=1e-5, atol=1e-6))
 
 
 class _Net:
     def __init__(self, module, is_actor, device):
-        lin = [m for m in module.modules() if isinstance(m, nn.Linear)]
-        dims = [lin[0].in_features] + [l.out_features for l in lin] if lin else []
-        if not native_fits(module):
-            raise ValueError(f"NativePPO2Learner: needs a [S<=8 -> 256 -> 256 -> A<=4] Linear/Tanh "
-                             f"stack (got {dims})")
-        acts = [_abi.RLP_ACT_TANH, _abi.RLP_ACT_TANH,
-                _abi.RLP_ACT_TANH if is_actor else _abi.RLP_ACT_NONE]
+        lin, dims = _linears(module)
+        if native_fits(module):
+            self.dense = False  # rlp_ppo2_grad (f16x3 FD + wgrad kernels)
+        elif dense_fits(module, is_actor):
+            self.dense = True   # rlp_ppo2_dense_grad (tiled f32 MFMA GEMMs)
+        else:
+            raise ValueError(f"NativePPO2Learner: needs a Linear/Tanh stack (got {dims} or a "
+                             f"forward that is not tanh hidden layers + "
+                             f"{'tanh * gain + off' if is_actor else 'linear'} output)")
+        acts = [_abi.RLP_ACT_TANH] * (len(lin) - 1) + [
+            _abi.RLP_ACT_TANH if is_actor else _abi.RLP_ACT_NONE]
         self.desc = _abi.MLPDesc.make(dims, acts)
         params = [p for l in lin for p in (l.weight, l.bias)]
         self.flat = torch.cat([p.detach().reshape(-1).to(device, torch.float32)
@@ -59,7 +103,7 @@ class _Net:
         self.acc = None        # the DPPO2 Worker's persistent local gradient buffer
         self.exp_avg = torch.zeros_like(self.flat)
         self.exp_avg_sq = torch.zeros_like(self.flat)
-        self.packed = K.mfma_pack(self.desc, self.flat)
+        self.packed = None if self.dense else K.mfma_pack(self.desc, self.flat)
         self.sqnorm = torch.zeros(1, dtype=torch.float64, device=device)
         self.step = 0
 
@@ -118,11 +162,25 @@ class NativePPO2Learner:
                                std, lo, hi)
 
     def _workspace(self, rows):
-        need = max(K.lib().rlp_ppo2_workspace_floats(__import__("ctypes").byref(n.desc), rows)
+        import ctypes
+        need = max((K.lib().rlp_ppo2_dense_workspace_floats if n.dense else
+                    K.lib().rlp_ppo2_workspace_floats)(ctypes.byref(n.desc), rows)
                    for n in (self.net_a, self.net_c))
         if self.ws is None or self.ws.numel() < need:
             self.ws = torch.empty(int(need), dtype=torch.float32, device=self.device)
         return self.ws
+
+    def _net_grad(self, net, cfg, s, index, ws, loss, **kw):
+        if net.dense:   # plain layout, contiguous rows: gather the mini-batch first
+            if index is not None:
+                s = s.index_select(0, index)
+                kw = {k: v.index_select(0, index) for k, v in kw.items()}
+            K.ppo2_dense_grad(net.desc, net.flat, cfg, s, grad=net.grad, loss_sum=loss,
+                              workspace=ws, **kw)
+        else:
+            K.mfma_pack(net.desc, net.flat, out=net.packed)
+            K.ppo2_grad(net.desc, net.packed, cfg, s, index=index, grad=net.grad, loss_sum=loss,
+                        workspace=ws, **kw)
 
     def grads(self, s, a, a_lp, adv, vt, index=None, actor_cfg=None):
         """Gradients of one step's actor and critic losses into net.grad (no optimiser step).
@@ -133,14 +191,10 @@ class NativePPO2Learner:
         ws = self._workspace(rows)
         self.loss.zero_()
         adv, vt = adv.reshape(-1), vt.reshape(-1)
-        na, nc = self.net_a, self.net_c
-        K.mfma_pack(na.desc, na.flat, out=na.packed)
-        K.ppo2_grad(na.desc, na.packed, actor_cfg if actor_cfg is not None else self._actor_cfg(),
-                    s, a=a, a_logprob=a_lp, adv=adv,
-                    index=index, grad=na.grad, loss_sum=self.loss[0:1], workspace=ws)
-        K.mfma_pack(nc.desc, nc.flat, out=nc.packed)
-        K.ppo2_grad(nc.desc, nc.packed, K.ppo2_loss_cfg(_abi.RLP_LOSS_CRITIC), s, v_target=vt,
-                    index=index, grad=nc.grad, loss_sum=self.loss[1:2], workspace=ws)
+        self._net_grad(self.net_a, actor_cfg if actor_cfg is not None else self._actor_cfg(), s,
+                       index, ws, self.loss[0:1], a=a, a_logprob=a_lp, adv=adv)
+        self._net_grad(self.net_c, K.ppo2_loss_cfg(_abi.RLP_LOSS_CRITIC), s, index, ws,
+                       self.loss[1:2], v_target=vt)
         return rows
 
     def _allreduce_grads(self):

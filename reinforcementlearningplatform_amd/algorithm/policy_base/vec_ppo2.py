@@ -187,19 +187,26 @@ class VecPPO2:
             self.msg['K_epochs'] = self.msg['k_epo']
         if learner not in ("auto", "native", "torch"):
             raise ValueError(f"VecPPO2: learner {learner!r} (auto | native | torch)")
-        from .native_ppo2 import NativePPO2Learner, native_fits
-        if learner == "auto":  # librlp's update covers [S<=8 -> 256 -> 256 -> A<=4]; the lidar
-            # env's 41-input nets take the torch-autograd learner (on the same device)
-            learner = "native" if native_fits(actor) and native_fits(critic) else "torch"
+        from .native_ppo2 import NativePPO2Learner, dense_fits, native_fits
+        if learner == "auto":  # librlp's update: f16x3 kernels for [S<=8 -> 256 -> 256 -> A<=4],
+            # exact-f32 dense GEMMs for other Linear/Tanh stacks (the lidar env's 41-input nets,
+            # the PPO2-SOI demo's 4-128-64-32 / 4-64-64 nets); anything else: torch autograd
+            fits = all(native_fits(m) or dense_fits(m, a) for m, a in ((actor, True), (critic, False)))
+            learner = "native" if fits else "torch"
         cls = NativePPO2Learner if learner == "native" else PPO2Learner
         self.learner = cls(actor, critic, self.msg, process_group, self.device)
         self.actor, self.critic = self.learner.actor, self.learner.critic
         self.world = self.learner.world
         self.gpu_actor = GPUNet(self.actor, True, self.device)
         self.gpu_critic = GPUNet(self.critic, False, self.device)
-        if not (self.gpu_actor.mfma_ok and self.gpu_critic.mfma_ok):
-            raise ValueError("VecPPO2 needs [S->256->256->A] actor / [S->256->256->1] critic nets "
-                             "(S <= 8, or 41-44) for rlp_rollout")
+        # the fused rollout kernels take [S->256->256->A] / [S->256->256->1] tanh nets (packed);
+        # any other Linear/Tanh stack (the PPO2-SOI demo's 4-128-64-32-2 / 4-64-64-1) runs
+        # rlp_rollout's plain-layout path (per-step MLP kernels, same draws and buffers)
+        fused = all(n.mfma_ok and n.desc.n_layers == 3 and n.desc.dims[1] == 256
+                    for n in (self.gpu_actor, self.gpu_critic))
+        self.plain = not fused
+        if self.plain and self.gpu_actor.desc.act[self.gpu_actor.desc.n_layers - 1] != _abi.RLP_ACT_TANH:
+            raise ValueError("VecPPO2: the actor's output layer must be tanh (mean = tanh * gain + off)")
         rule, flag = success_rule or (_abi.RLP_SUCCESS_DONE_AND_FLAG_NE, _abi.timeout_flag(self.kind))
         self.rule, self.flag = rule, flag
         lo, hi = _abi.action_bounds(self.kind, self.params)
@@ -240,11 +247,16 @@ class VecPPO2:
         std = torch.as_tensor(self.actor.std, dtype=torch.float32).reshape(-1).cpu().numpy()
         return list(np.broadcast_to(std, (len(self.lo),)))
 
+    def _net_buf(self, net):
+        return net.flat if self.plain else net.packed
+
     def rollout(self):
         cfg = K.make_rollout_cfg(self.T, self.n, self.seed, self.step0, self.env_id0,
-                                 self.std_list(), self.lo, self.hi, self.rule, self.flag)
+                                 self.std_list(), self.lo, self.hi, self.rule, self.flag,
+                                 plain=self.plain)
         K.rollout(self.kind, self.params, self.env.state, self.need, self.gpu_actor.desc,
-                  self.gpu_actor.packed, self.gpu_critic.desc, self.gpu_critic.packed, cfg, self.bufs)
+                  self._net_buf(self.gpu_actor), self.gpu_critic.desc,
+                  self._net_buf(self.gpu_critic), cfg, self.bufs)
         self.step0 += self.T
         self.total_steps += self.T * self.n * self.world
 
@@ -259,8 +271,14 @@ class VecPPO2:
 
     def advantages(self):
         b = self.bufs
-        K.value_fixup(self.gpu_critic.desc, self.gpu_critic.packed, b["obs_next"], b["done"],
-                      b["success"], b["value_next"])
+        if self.plain:   # V(s') of the done && !success rows through the generic forward
+            mask = (b["done"] & (1 - b["success"])).view(-1).contiguous()
+            K.mlp_forward(self.gpu_critic.desc, self.gpu_critic.flat,
+                          b["obs_next"].view(-1, self.env.state_dim), mask=mask,
+                          out=b["value_next"].view(-1, 1))
+        else:
+            K.value_fixup(self.gpu_critic.desc, self.gpu_critic.packed, b["obs_next"], b["done"],
+                          b["success"], b["value_next"])
         if self.global_norm:
             parts = self._gather(K.reward_norm_stats(b["reward"], self.work))
             K.reward_norm_finish(b["reward"], self.rms, self.work, parts, self.world, out=self.rnorm)

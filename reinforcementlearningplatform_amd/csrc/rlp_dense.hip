@@ -188,32 +188,39 @@ __global__ void __launch_bounds__(256) dense_gemm_kernel(Prob p0, Prob p1) {
     const int bid = (int)blockIdx.x - (second ? nb0 : 0);
     const int bx = bid % nx, by = (bid / nx) % ny, bz = bid / (nx * ny);
     const int m0 = by * kDT, n0 = bx * kDT;
-    const int r_lo = bz * rchunk, rc = min(R, r_lo + rchunk) - r_lo;
-    const int Q = (rc + 15) / 16 * 4;  // MFMA steps (multiple of 4); rows g * Q + s, s < Q
+    // the block's reduction slice [r_lo, r_end), staged kDRc rows at a time (one stage unless the
+    // problem was built with make_prob_long: the PPO2 update's weight gradients over 2^18 rows)
+    const int r_lo = bz * rchunk, r_end = min(R, r_lo + rchunk);
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
     const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
-    stage_panel(A, true, m0, e_rows(A, true), r_lo, rc, 4 * Q, As);
-    stage_panel(B, false, n0, e_rows(B, false), r_lo, rc, 4 * Q, Bs);
-    __syncthreads();
     floatx4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int g = l >> 4, c = l & 15;
-    for (int s = 0; s < Q; s += 4) {
-        floatx4 af[2], bf[2];
+    for (int rs = r_lo; rs < r_end || rs == r_lo; rs += kDRc) {
+        const int rc = min(r_end, rs + kDRc) - rs;
+        const int Q = (rc + 15) / 16 * 4;  // MFMA steps (multiple of 4); rows g * Q + s, s < Q
+        if (rs != r_lo) __syncthreads();   // the previous stage's fragments are read
+        stage_panel(A, true, m0, e_rows(A, true), rs, rc, 4 * Q, As);
+        stage_panel(B, false, n0, e_rows(B, false), rs, rc, 4 * Q, Bs);
+        __syncthreads();
+        for (int s = 0; s < Q; s += 4) {
+            floatx4 af[2], bf[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = *(const floatx4 *)&As[(wm + 16 * i + c) * kDLd + g * Q + s];
+            for (int i = 0; i < 2; ++i) af[i] = *(const floatx4 *)&As[(wm + 16 * i + c) * kDLd + g * Q + s];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bf[j] = *(const floatx4 *)&Bs[(wn + 16 * j + c) * kDLd + g * Q + s];
+            for (int j = 0; j < 2; ++j) bf[j] = *(const floatx4 *)&Bs[(wn + 16 * j + c) * kDLd + g * Q + s];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][u], bf[j][u], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][u], bf[j][u], acc[i][j], 0, 0, 0);
+        }
+        if (rc <= 0) break;
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -875,7 +882,7 @@ int dense_mlp_forward(const rlp_mlp_desc &d, const float *params, const float *x
     float *buf = nullptr;
     if (d.n_layers > 1 &&
         hipMallocAsync((void **)&buf, sizeof(float) * 2 * (size_t)n * maxw, s) != hipSuccess)
-        return fail(RLP_EINVAL, "rlp_mlp_forward: scratch");
+        return fail(RLP_ENOMEM, "rlp_mlp_forward: scratch");
     const float *in = x;
     int64_t off = 0;
     for (int l = 0; l < d.n_layers; ++l) {
@@ -1213,6 +1220,258 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
             n.target_critic, n.q1.params, nn, cfg->tau, (float)(1.0 - (double)cfg->tau));
     }
     RLP_CHECK_LAUNCH("rlp_sac_update");
+    return RLP_OK;
+}
+
+}  // extern "C"
+
+namespace rlp {
+
+// ---- PPO2 update for any tanh Linear stack (Proximal_Policy_Optimization2.learn, algorithm/
+// policy_base/Proximal_Policy_Optimization2.py:133-163) on the dense GEMM -------------------------
+// The nets rlp_ppo2_grad's f16x3 kernels do not take: the PPO2-SecondOrderIntegration demo's
+// actor 4 -> 128 -> 64 -> 32 -> A and critic 4 -> 64 -> 64 -> 1 (demonstration/PPO2/PPO2-4-
+// SecondOrderIntegration/train.py:37-125), the obstacle-avoidance demos' 41-input nets
+// (demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97). Exact f32
+// products (v_mfma_f32_16x16x4_f32) throughout, rows in chunks of kPpoChunk:
+//   forward   layer by layer, tanh epilogues (the actor's head keeps t = tanh(z) beside
+//             mean = gain t + off), activations of the chunk in the workspace
+//   head      per row dL/dz_L: the clipped-surrogate actor loss (torch.min / clamp backward
+//             semantics, as ppo2_fd_kernel) or the critic's MSE, and the loss sum
+//   backward  per layer: dW | db = dY^T [X | 1] over the chunk (long reduction slices, one
+//             partial per slice), dX = dY W with the tanh backward (1 - h^2) epilogue
+// Every chunk's gradient lands in its own slot; the slots are summed in chunk order (fixed order
+// throughout: the same bits on every run and rank).
+constexpr int kPpoChunk = 1 << 18;
+
+inline Prob make_prob_long(const Opnd &A, const Opnd &B, const Epi &e, int R, int nz) {
+    if (nz < 1) nz = 1;
+    const int rchunk = ((R + nz - 1) / nz + 15) / 16 * 16;
+    const int z = R > 0 ? (R + rchunk - 1) / rchunk : 1;
+    return Prob{A, B, e, R, rchunk, (e.N + kDT - 1) / kDT, (e.M + kDT - 1) / kDT, z};
+}
+
+struct PpoDenseArgs {
+    const float *t, *mean, *v;   // actor: tanh(z_L), gain t + off ([B][A]); critic: V ([B])
+    const float *a, *lp, *adv, *vt;
+    int B, A;
+    float inv_rows, eps_clip, ent_row;
+    float gain[4], log_std[4], inv_var[4];
+    float *dy;                   // [B][A]: dL/dz_L
+    double *loss_sum;
+};
+
+template <bool ACTOR>
+__global__ void __launch_bounds__(256) ppo2_dense_head_kernel(PpoDenseArgs h) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    double l = 0.0;
+    if (i < h.B) {
+        if constexpr (ACTOR) {
+            float lp_now = 0.f, lp_old = 0.f, d[4], t[4];
+            for (int a = 0; a < h.A; ++a) {
+                t[a] = h.t[(size_t)i * h.A + a];
+                d[a] = h.a[(size_t)i * h.A + a] - h.mean[(size_t)i * h.A + a];
+                lp_now += -(d[a] * d[a]) * (0.5f * h.inv_var[a]) - h.log_std[a] - 0.91893853320467274178f;
+                lp_old += h.lp[(size_t)i * h.A + a];
+            }
+            const float adv = h.adv[i];
+            const float ratio = expf(lp_now - lp_old);
+            const float lo = 1.f - h.eps_clip, hi = 1.f + h.eps_clip;
+            const float s1 = ratio * adv, rc = fminf(fmaxf(ratio, lo), hi), s2 = rc * adv;
+            const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);  // torch.min: a tie splits
+            const float w2 = s2 < s1 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+            const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;  // clamp backward
+            const float dl_dlp = -adv * (w1 + w2 * inr) * ratio * h.inv_rows;
+            for (int a = 0; a < h.A; ++a)
+                h.dy[(size_t)i * h.A + a] = dl_dlp * (d[a] * h.inv_var[a]) * h.gain[a] * (1.f - t[a] * t[a]);
+            l = (double)(-fminf(s1, s2) - h.ent_row);
+        } else {
+            const float diff = h.v[i] - h.vt[i];
+            h.dy[i] = 2.f * diff * h.inv_rows;
+            l = (double)(diff * diff);
+        }
+    }
+    for (int o = 1; o < 64; o <<= 1) l += __shfl_xor(l, o);
+    __shared__ double red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
+    __syncthreads();
+    if (threadIdx.x == 0 && h.loss_sum) atomicAdd(h.loss_sum, (red[0] + red[1]) + (red[2] + red[3]));
+}
+
+// the workspace's constant vectors: 1024 ones (the hidden layers' tanh backward through the
+// kEpiTanhAffBack epilogue with gain 1) and the actor head's gain / off
+struct PpoConsts {
+    float gain[4], off[4];
+};
+__global__ void __launch_bounds__(256) ppo2_consts_kernel(float *ones, float *head, PpoConsts c) {
+    for (int i = threadIdx.x; i < 1024; i += 256) ones[i] = 1.f;
+    if (threadIdx.x < 4) {
+        head[threadIdx.x] = c.gain[threadIdx.x];
+        head[4 + threadIdx.x] = c.off[threadIdx.x];
+    }
+}
+
+// grad[i] = sum over the chunk slots, in chunk order
+__global__ void __launch_bounds__(256) chunk_sum_kernel(const float *__restrict__ slots, int nchunks,
+                                                        int64_t n, float *__restrict__ grad) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int c = 0; c < nchunks; ++c) s += slots[(size_t)c * n + i];
+    grad[i] = s;
+}
+
+struct PpoDenseWs {  // float offsets into the workspace
+    int64_t act, t, g0, g1, part, ones, head, slots, total;
+};
+inline bool ppo2_dense_ok(const rlp_mlp_desc &d, bool actor) {
+    if (d.n_layers < 1 || d.n_layers > RLP_MLP_MAX_LAYERS) return false;
+    for (int l = 0; l <= d.n_layers; ++l)
+        if (d.dims[l] < 1 || d.dims[l] > 1024) return false;
+    for (int l = 0; l + 1 < d.n_layers; ++l)
+        if (d.act[l] != RLP_ACT_TANH) return false;
+    const int A = d.dims[d.n_layers];
+    return actor ? (A <= 4 && d.act[d.n_layers - 1] == RLP_ACT_TANH)
+                 : (A == 1 && d.act[d.n_layers - 1] == RLP_ACT_NONE);
+}
+inline PpoDenseWs ppo2_dense_ws(const rlp_mlp_desc &d, int64_t rows) {
+    const int64_t B = rows < kPpoChunk ? rows : kPpoChunk;
+    int64_t hid = 0, maxw = 0, np = 0, maxpart = 0;
+    for (int l = 0; l < d.n_layers; ++l) {
+        hid += d.dims[l + 1];
+        maxw = d.dims[l + 1] > maxw ? d.dims[l + 1] : maxw;
+        np += (int64_t)d.dims[l] * d.dims[l + 1] + d.dims[l + 1];
+        const int64_t tiles = ((d.dims[l] + 1 + kDT - 1) / kDT) * ((d.dims[l + 1] + kDT - 1) / kDT);
+        const int64_t nz = 512 / tiles > 1 ? 512 / tiles : 1;
+        const int64_t p = nz * d.dims[l + 1] * (d.dims[l] + 1);
+        maxpart = p > maxpart ? p : maxpart;
+    }
+    const int64_t chunks = (rows + kPpoChunk - 1) / kPpoChunk;
+    PpoDenseWs w{};
+    int64_t o = 0;
+    auto take = [&](int64_t k) { int64_t r = o; o += (k + 63) / 64 * 64; return r; };
+    w.act = take(B * hid);
+    w.t = take(B * 4);
+    w.g0 = take(B * maxw);
+    w.g1 = take(B * maxw);
+    w.part = take(maxpart);
+    w.ones = take(1024);
+    w.head = take(8);
+    w.slots = take(chunks * np);
+    w.total = o;
+    return w;
+}
+
+}  // namespace rlp
+
+extern "C" {
+
+int64_t rlp_ppo2_dense_workspace_floats(const rlp_mlp_desc *desc, int64_t rows) {
+    if (!desc || rows < 0 || desc->n_layers < 1 || desc->n_layers > RLP_MLP_MAX_LAYERS) return RLP_EINVAL;
+    return ppo2_dense_ws(*desc, rows > 0 ? rows : 1).total;
+}
+
+int rlp_ppo2_dense_grad(const rlp_mlp_desc *desc, const float *params, const rlp_ppo2_loss_cfg *cfg,
+                        const float *s, const float *a, const float *a_logprob, const float *adv,
+                        const float *v_target, int64_t rows, float *grad, double *loss_sum,
+                        float *workspace, rlp_stream_t stream) {
+    RLP_REQUIRE(desc && params && cfg && s && grad && workspace, "rlp_ppo2_dense_grad: null argument");
+    const bool actor = cfg->kind == RLP_LOSS_ACTOR;
+    RLP_REQUIRE(actor || cfg->kind == RLP_LOSS_CRITIC, "rlp_ppo2_dense_grad: loss kind %d", cfg->kind);
+    if (!ppo2_dense_ok(*desc, actor))
+        return fail(RLP_EUNSUPPORTED, "rlp_ppo2_dense_grad: need a tanh Linear stack (widths <= 1024, "
+                                      "%s)", actor ? "tanh output, A <= 4" : "linear 1-output head");
+    if (actor) RLP_REQUIRE(a && a_logprob && adv, "rlp_ppo2_dense_grad: actor loss needs a, a_logprob, adv");
+    else RLP_REQUIRE(v_target, "rlp_ppo2_dense_grad: critic loss needs v_target");
+    RLP_REQUIRE(rows > 0, "rlp_ppo2_dense_grad: rows=%lld", (long long)rows);
+    const rlp_mlp_desc &d = *desc;
+    const int L = d.n_layers, S = d.dims[0], A = d.dims[L];
+    hipStream_t st = as_stream(stream);
+    const PpoDenseWs w = ppo2_dense_ws(d, rows);
+    float *ws = workspace;
+    int64_t np = 0, off[RLP_MLP_MAX_LAYERS];
+    for (int l = 0; l < L; ++l) {
+        off[l] = np;
+        np += (int64_t)d.dims[l] * d.dims[l + 1] + d.dims[l + 1];
+    }
+    PpoDenseArgs h{};
+    h.A = A; h.inv_rows = 1.f / (float)rows; h.eps_clip = cfg->eps_clip; h.loss_sum = loss_sum;
+    PpoConsts pc{};
+    float ent = 0.f;
+    for (int k = 0; k < A && actor; ++k) {
+        pc.off[k] = (cfg->a_min[k] + cfg->a_max[k]) / 2.0f;
+        h.gain[k] = pc.gain[k] = cfg->a_max[k] - pc.off[k];
+        h.log_std[k] = logf(cfg->std[k]);
+        h.inv_var[k] = 1.0f / (cfg->std[k] * cfg->std[k]);
+        ent += 0.5f + 0.91893853320467274178f + logf(cfg->std[k]);  // Normal.entropy()
+    }
+    h.ent_row = cfg->entropy_coef * ent;
+    ppo2_consts_kernel<<<1, 256, 0, st>>>(ws + w.ones, ws + w.head, pc);
+    const float *gain_d = ws + w.head, *off_d = ws + w.head + 4;
+    const int64_t nchunks = (rows + kPpoChunk - 1) / kPpoChunk;
+    for (int64_t c = 0; c < nchunks; ++c) {
+        const int64_t r0 = c * kPpoChunk;
+        const int B = (int)((rows - r0) < kPpoChunk ? rows - r0 : kPpoChunk);
+        // forward
+        float *act = ws + w.act;
+        int64_t ao[RLP_MLP_MAX_LAYERS];
+        Opnd in = mat(s + r0 * S, B, S, S);
+        int64_t o = 0;
+        for (int l = 0; l < L; ++l) {
+            const Layer Ly{params + off[l], params + off[l] + (int64_t)d.dims[l] * d.dims[l + 1],
+                           d.dims[l], d.dims[l + 1]};
+            const bool last = l == L - 1;
+            const int kind = !last ? kEpiTanh : actor ? kEpiTanhAff : kEpiNone;
+            ao[l] = o;
+            dense_fwd(in, Ly, B, kind, act + o, gain_d, off_d, ws + w.t, st);
+            in = mat(act + o, B, Ly.out, Ly.out);
+            o += (int64_t)B * Ly.out;
+        }
+        // head: dL/dz_L into g0
+        h.B = B;
+        h.dy = ws + w.g0;
+        if (actor) {
+            h.t = ws + w.t; h.mean = act + ao[L - 1];
+            h.a = a + r0 * A; h.lp = a_logprob + r0 * A; h.adv = adv + r0;
+            ppo2_dense_head_kernel<true><<<(B + 255) / 256, 256, 0, st>>>(h);
+        } else {
+            h.v = act + ao[L - 1]; h.vt = v_target + r0;
+            ppo2_dense_head_kernel<false><<<(B + 255) / 256, 256, 0, st>>>(h);
+        }
+        // backward: layer by layer from the top; chunk c's gradient into its slot
+        float *slot = ws + w.slots + c * np;
+        const float *dy = ws + w.g0;
+        float *dn = ws + w.g1;
+        for (int l = L - 1; l >= 0; --l) {
+            const Layer Ly{params + off[l], params + off[l] + (int64_t)d.dims[l] * d.dims[l + 1],
+                           d.dims[l], d.dims[l + 1]};
+            const Opnd xin = l == 0 ? mat(s + r0 * S, B, S, S) : mat(act + ao[l - 1], B, Ly.in, Ly.in);
+            Epi ew{};
+            ew.y = ws + w.part; ew.kind = kEpiPartial; ew.M = Ly.out; ew.N = Ly.in + 1;
+            Opnd xo = xin;
+            xo.cols = Ly.in + 1;
+            xo.ones = Ly.in;
+            const int tiles = ((Ly.in + 1 + kDT - 1) / kDT) * ((Ly.out + kDT - 1) / kDT);
+            const Prob qw = make_prob_long(transposed(dy, Ly.out, B, Ly.out), xo, ew, B,
+                                           512 / tiles > 1 ? 512 / tiles : 1);
+            int z;
+            if (l > 0) {  // dX = dY W, then (1 - h^2) with h = tanh output of layer l - 1
+                const Prob qb = bwd_data_prob(dy, Ly, B, 0, Ly.in, kEpiTanhAffBack, act + ao[l - 1],
+                                              Ly.in, ws + w.ones, dn);
+                z = gemm_launch(qw, &qb, st);
+            } else {
+                z = gemm_launch(qw, nullptr, st);
+            }
+            wgrad_reduce(Ly, ws + w.part, z, slot + off[l], slot + off[l] + (int64_t)Ly.in * Ly.out, st);
+            if (l > 0) {
+                float *nx = dn == ws + w.g0 ? ws + w.g1 : ws + w.g0;
+                dy = dn;
+                dn = nx;
+            }
+        }
+    }
+    chunk_sum_kernel<<<(int)((np + 255) / 256), 256, 0, st>>>(ws + w.slots, (int)nchunks, np, grad);
+    RLP_CHECK_LAUNCH("rlp_ppo2_dense_grad");
     return RLP_OK;
 }
 

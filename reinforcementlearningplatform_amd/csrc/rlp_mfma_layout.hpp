@@ -98,16 +98,6 @@ __device__ __forceinline__ void lds_dma_1k(gptr<float> src_lane, float *dst_wave
                                      0, 0);
 }
 
-// The same DMA as inline asm: the compiler does not track it, so it inserts no vmcnt(0) of its own
-// before later LDS reads (it cannot tell the ring slot being read from the one being filled and
-// otherwise waits for every DMA in flight, the prefetched slots included). The caller's counted
-// vmcnt waits + block barriers are then the only ordering, as in the ring protocol.
-__device__ __forceinline__ void lds_dma_1k_untracked(gptr<float> src_lane, float *dst_wave_base) {
-    const unsigned m0 = __builtin_amdgcn_readfirstlane(
-        (unsigned)(uintptr_t)(__attribute__((address_space(3))) void *)dst_wave_base);
-    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src_lane), "{m0}"(m0) : "memory");
-}
-
 // Fused forward of one [S -> H -> H -> NOUT] net for the wave's SUB x 16 envs.
 //   P      : packed net (global); W2 fragments are read from it by LDS-DMA
 //   small  : the net's resident part in LDS (mlp_small_to_lds)

@@ -54,7 +54,7 @@ __device__ __forceinline__ void split2(float2v x, half2v &hi, half2v &lo) {
 // the same with lo = f16(x - hi) by v_fma_mix (the f16 hi read as a source operand, x - hi exact in
 // f32, one rounding to f16 into the low / high half): bit-identical, 3 VALU ops instead of 5
 // (tools/mix_split_probe.hip checks the identity on the GPU). The PPO2 update's B operands use it
-// (-1.6 % FD cycles); in the rollout the opaque asm costs more in scheduling than it saves (+3 %).
+// (-1.6 % FD cycles); in the rollout the opaque asm cost more in scheduling than it saved (+3 %).
 __device__ __forceinline__ void split2_mix(float2v x, half2v &hi, half2v &lo) {
     hi = __builtin_convertvector(x, half2v);
     const unsigned h = __builtin_bit_cast(unsigned, hi);
@@ -65,12 +65,6 @@ __device__ __forceinline__ void split2_mix(float2v x, half2v &hi, half2v &lo) {
     lo = __builtin_bit_cast(half2v, l);
 }
 
-#ifndef RLP_X3_ASM_DMA
-#define RLP_X3_ASM_DMA 0  // the W2 ring's LDS-DMA as inline asm (lds_dma_1k_untracked)
-#endif
-#ifndef RLP_X3_SPLIT_MIX
-#define RLP_X3_SPLIT_MIX 0  // rollout B operands' lo halves by v_fma_mix (split2_mix)
-#endif
 
 constexpr int kX3Waves = 4;             // waves per block sharing the W2 ring
 constexpr int kX3Ring = 3;              // chunks resident in the ring
@@ -89,11 +83,9 @@ __device__ __forceinline__ void block_barrier_raw() {
 // W: waves of the block sharing the ring (4 or 8); each DMAs 16 / W of the 16 KiB of every chunk.
 // CPB: 16-KiB chunks per ring slot and block barrier (2: one barrier per k-phase instead of per
 // half-phase; the ring then holds RG x CPB chunks).
-// PB (pipelined B operands; one wave per SIMD): phase P + 1's tanh / split runs pair by pair
-// between phase P's MFMAs instead of as a VALU-only stretch at the head of phase P + 1, which a
-// lone wave cannot hide behind another wave's MFMAs.
-template <int H, int SUB, int KS1, int NOUT, int RG = kX3Ring, int W = kX3Waves, int CPB = 1,
-          bool PB = false>
+// (Pipelining the next phase's B operands between the current phase's MFMAs, for the lone wave of
+// the one-wave-per-SIMD variants, measured 7 % slower on the UAV: DESIGN.md §4, removed.)
+template <int H, int SUB, int KS1, int NOUT, int RG = kX3Ring, int W = kX3Waves, int CPB = 1>
 __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, const float *small,
                                                float *ring, const MfmaNet &net, const int nout,
                                                const float (&bobs)[SUB][KS1],
@@ -126,11 +118,7 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
             const gptr<float> src = X + (sc * CPB + cc) * kX3ChunkFloats;
 #pragma unroll
             for (int q = 0; q < NPW; ++q) {
-#if RLP_X3_ASM_DMA
-                lds_dma_1k_untracked(src + q * 256, slot + q * 256);
-#else
                 lds_dma_1k(src + q * 256, slot + q * 256);
-#endif
             }
         }
     };
@@ -172,40 +160,23 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
         const float2v x = __builtin_elementwise_fma(
             rc, (float2v){-2.0f * kX3HScale, -2.0f * kX3HScale}, (float2v){kX3HScale, kX3HScale});
         half2v hi, lo;
-#if RLP_X3_SPLIT_MIX
-        split2_mix(x, hi, lo);
-#else
         split2(x, hi, lo);
-#endif
         dh[sb][i] = hi.x;
         dh[sb][i + 1] = hi.y;
         dl[sb][i] = lo.x;
         dl[sb][i + 1] = lo.y;
     };
     half8 bh[SUB], bl[SUB];
-    if constexpr (PB) {  // phase 0's operands up front, phase 1's layer-1 tiles
+
+#pragma unroll 1
+    for (int P = 0; P < NPH; ++P) {
 #pragma unroll
         for (int sb = 0; sb < SUB; ++sb)
 #pragma unroll
             for (int i = 0; i < 8; i += 2) bop_pair(sb, i, bh, bl);
-        layer1(2, hp0);
-        layer1(3, hp1);
-    }
-    // pairs per phase SUB * 4, spread over the phase's 16 tile steps
-    constexpr int PSTEP = 16 / (SUB * 4) > 0 ? 16 / (SUB * 4) : 1;
-
-#pragma unroll 1
-    for (int P = 0; P < NPH; ++P) {
-        half8 nbh[SUB], nbl[SUB];
-        if constexpr (!PB) {
-#pragma unroll
-            for (int sb = 0; sb < SUB; ++sb)
-#pragma unroll
-                for (int i = 0; i < 8; i += 2) bop_pair(sb, i, bh, bl);
-            if (P + 1 < NPH) {  // next phase's layer-1 tiles, under this phase's MFMAs
-                layer1(2 * P + 2, hp0);
-                layer1(2 * P + 3, hp1);
-            }
+        if (P + 1 < NPH) {  // next phase's layer-1 tiles, under this phase's MFMAs
+            layer1(2 * P + 2, hp0);
+            layer1(2 * P + 3, hp1);
         }
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
@@ -245,22 +216,6 @@ __device__ __forceinline__ void mlp_x3_forward(const float *__restrict__ P0, con
                     acc[sb][8 * hf + jj] = a;
                 }
                 __builtin_amdgcn_sched_group_barrier(0x008, 3 * SUB, 0);
-                if constexpr (PB) {  // next phase's operands (the last phase computes unused ones)
-                    const int st = 8 * hf + jj;
-                    if (st % PSTEP == PSTEP - 1 && st / PSTEP < SUB * 4)
-                        bop_pair((st / PSTEP) / 4, 2 * ((st / PSTEP) % 4), nbh, nbl);
-                }
-            }
-        }
-        if constexpr (PB) {
-#pragma unroll
-            for (int sb = 0; sb < SUB; ++sb) {
-                bh[sb] = nbh[sb];
-                bl[sb] = nbl[sb];
-            }
-            if (P + 2 < NPH) {  // the phase after next's layer-1 tiles
-                layer1(2 * P + 4, hp0);
-                layer1(2 * P + 5, hp1);
             }
         }
     }

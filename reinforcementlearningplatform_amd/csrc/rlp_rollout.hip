@@ -232,48 +232,30 @@ constexpr int rollout_sp_lds_bytes() {
     return 4 * (2 * mlp_small_floats<256, KS1, E::A>() + EB * 8 + EB * (E::A + 1) + RG * kX3ChunkFloats) +
            8 * E::D * EB + 2 * EB;
 }
-#ifndef RLP_SP_RING1
-#define RLP_SP_RING1 3  // W2 ring slots of the one-block-per-CU variants (4 measured 1 % slower)
-#endif
-#ifndef RLP_SP_CPB1
-#define RLP_SP_CPB1 2   // 16-KiB chunks per ring slot / block barrier there (one barrier per k-phase)
-#endif
+constexpr int kSpRing1 = 3;  // W2 ring slots of the one-block-per-CU variants (4 measured 1 % slower)
+constexpr int kSpCpb1 = 2;   // 16-KiB chunks per ring slot / block barrier there (one barrier per k-phase)
 // UAV physics lanes per physics wave: 64 (half waves, 32, measured 6 % slower: the UAV step is
 // issue-bound, not latency-bound, so spreading it over more waves only adds issue)
-// pipelined B operands (mlp_x3_forward PB) in the one-wave-per-SIMD variants (modes 5 / 6)
-#ifndef RLP_SP_PB
-#define RLP_SP_PB 0
-#endif
-#ifndef RLP_SP_UAV_PHL
-#define RLP_SP_UAV_PHL 64
-#endif
-template <int KIND, int SUB, int W>
-constexpr int rollout_sp_physics_lanes() {
-    return (KIND == RLP_ENV_UAV_HOVER_OUTER_LOOP && W * 16 * SUB / RLP_SP_UAV_PHL <= W) ? RLP_SP_UAV_PHL : 64;
-}
-// waves per SIMD of a variant: 4-wave blocks 2; 8-wave blocks of 32-env waves 2 (one block per
-// CU); 8-wave blocks of 16-env waves 4 (two blocks per CU, <= 128 registers) or, with WPS = 2, 2
-// (one block per CU, 256 registers)
-template <int SUB, int W>
-constexpr int rollout_sp_default_wps() { return SUB == 1 ? W / 2 : 2; }
+// waves per SIMD of a variant: 4-wave blocks 2 (two blocks per CU, or one per CU with WPS = 1 and
+// 512 registers); 8-wave blocks of 32-env waves 2 (one block per CU)
 template <int SUB, int W, int WPS>
 constexpr int rollout_sp_blocks_per_cu() { return 4 * WPS / W; }
 // the CU's 160 KiB split over its blocks: a 3-chunk W2 ring where it fits, else 2 (UAV)
-template <int KIND, int SUB, int W = 4, int WPS = rollout_sp_default_wps<SUB, W>()>
+template <int KIND, int SUB, int W = 4, int WPS = 2>
 constexpr int rollout_sp_ring() {
     constexpr int bpc = rollout_sp_blocks_per_cu<SUB, W, WPS>(), budget = 160 * 1024 / bpc;
-    return bpc == 1 && rollout_sp_lds_bytes<KIND, SUB, RLP_SP_RING1 * RLP_SP_CPB1, W>() <= budget
-               ? RLP_SP_RING1
+    return bpc == 1 && rollout_sp_lds_bytes<KIND, SUB, kSpRing1 * kSpCpb1, W>() <= budget
+               ? kSpRing1
          : rollout_sp_lds_bytes<KIND, SUB, 3, W>() <= budget ? 3
          : rollout_sp_lds_bytes<KIND, SUB, 2, W>() <= budget ? 2 : 0;
 }
 template <int KIND, int SUB>
 constexpr bool rollout_sp_fits() { return SUB <= 2 && rollout_sp_ring<KIND, SUB>() != 0; }
 
-// W = 4: 4-wave blocks, two per CU (2 waves per SIMD, <= 256 registers); W = 8 (SUB = 1): 8-wave
-// blocks, two per CU (4 waves per SIMD, <= 128 registers): twice the waves to hide latency with,
-// each wave 16 envs, the ring shared by 8 waves; W = 8, SUB = 2: ONE 8-wave block per CU (2 waves
-// per SIMD, 256 registers). Two co-resident 4-wave blocks do not share a CU fairly: the SQ's
+// W = 4: 4-wave blocks, two per CU (2 waves per SIMD, <= 256 registers) or, WPS = 1, one per CU
+// (1 wave per SIMD, 512 registers); W = 8, SUB = 2: ONE 8-wave block per CU (2 waves per SIMD,
+// 256 registers). (8-wave blocks of 16-env waves, 2 or 4 waves per SIMD, and 4-wave blocks of
+// 64-env waves measured slower and were removed: DESIGN.md §4.) Two co-resident 4-wave blocks do not share a CU fairly: the SQ's
 // oldest-first issue arbitration lets one run ahead (measured: half the blocks finish their
 // segment in 12.0M cycles, the other half in 16.9M, and the launch waits for the slow half); in
 // one block the barriers keep all eight waves in step.
@@ -293,10 +275,9 @@ struct SpArgs {
     MfmaNet cn;
     RolloutArgs ra;
     rlp_rollout_bufs b;
-    int prio;  // rlp_set_rollout_prio: the block's younger half of waves at s_setprio 1
 };
 
-template <int KIND, int H, int SUB, int W = 4, int WPS = rollout_sp_default_wps<SUB, W>()>
+template <int KIND, int H, int SUB, int W = 4, int WPS = 2>
 __global__ void __launch_bounds__(64 * W, WPS)  // (HIP's second argument: waves per SIMD)
 rollout_sp_kernel(SpArgs<KIND> args) {
     const typename Env<KIND>::P &p = args.p;
@@ -309,15 +290,14 @@ rollout_sp_kernel(SpArgs<KIND> args) {
     const rlp_rollout_bufs &b = args.b;
     using E = Env<KIND>;
     constexpr int S = E::S, A = E::A, D = E::D, KS1 = (S + 3) / 4, WENV = 16 * SUB;
-    // physics lanes per physics wave: 64 (full waves; RLP_SP_UAV_PHL can give the UAV half waves)
-    constexpr int PHL = rollout_sp_physics_lanes<KIND, SUB, W>();
+    constexpr int PHL = 64;  // physics lanes per physics wave
     constexpr int WAVES = W, EB = WAVES * WENV, PW = EB / PHL, ROT = WAVES / PW;
     static_assert(EB % PHL == 0 && WAVES % PW == 0, "physics waves cover the block's envs");
     constexpr int SMALL = mlp_small_floats<H, KS1, A>(), RG = rollout_sp_ring<KIND, SUB, W, WPS>();
-    // one block per CU: ring slots of RLP_SP_CPB1 chunks (fewer block barriers per k-phase)
+    // one block per CU: ring slots of kSpCpb1 chunks (fewer block barriers per k-phase)
     constexpr int CPB = rollout_sp_blocks_per_cu<SUB, W, WPS>() == 1 &&
-                                rollout_sp_lds_bytes<KIND, SUB, RG * RLP_SP_CPB1, W>() <= 160 * 1024
-                            ? RLP_SP_CPB1 : 1;
+                                rollout_sp_lds_bytes<KIND, SUB, RG * kSpCpb1, W>() <= 160 * 1024
+                            ? kSpCpb1 : 1;
     __shared__ __attribute__((aligned(16))) float lds[2 * SMALL + EB * 8 + EB * (A + 1) + RG * CPB * kX3ChunkFloats];
     __shared__ double st[D][EB];
     __shared__ uint8_t s_need[EB], s_pdone[EB];
@@ -357,8 +337,6 @@ rollout_sp_kernel(SpArgs<KIND> args) {
         s_pdone[le] = 1;  // no value_next write before step 0
     }
     __syncthreads();
-    if (args.prio && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= W / 2)
-        __builtin_amdgcn_s_setprio(1);
 
     auto mlp_pass = [&](bool both) {
         // the nets' pointers and layouts re-read from the kernarg segment (scalar loads) per pass
@@ -375,7 +353,7 @@ rollout_sp_kernel(SpArgs<KIND> args) {
 #pragma unroll 1
         for (int which = both ? 0 : 1; which < 2; ++which) {
             float out[SUB][A];
-            mlp_x3_forward<H, SUB, KS1, A, RG, W, CPB, RLP_SP_PB && WPS == 1>(which ? critic : actor, which ? small_c : small_a,
+            mlp_x3_forward<H, SUB, KS1, A, RG, W, CPB>(which ? critic : actor, which ? small_c : small_a,
                                                   ring, which ? cn : an, which ? 1 : A, bobs, out);
             // lane (sub-block g, env e) owns out[g]
             float sel[A];
@@ -588,7 +566,6 @@ static int launch_packed_forward(const MfmaNet &net, const float *P, const float
 }
 
 static int g_rollout_shared_physics = -1;  // rlp_set_rollout_physics (-1: auto)
-static int g_rollout_prio = 0;             // rlp_set_rollout_prio
 
 template <int KIND, int H, int SUB, bool X3>
 static int launch_rollout(const void *params, double *state, uint8_t *need_reset,
@@ -599,26 +576,10 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     constexpr int threads = rollout_block<SUB, X3>();
     constexpr int envs_per_block = threads / 64 * 16 * SUB;
     const int blocks = (ra.n + envs_per_block - 1) / envs_per_block;
-    if constexpr (X3 && SUB == 1 && rollout_sp_ring<KIND, 1, 8>() != 0) {
-        if (physics == 2) {  // 8-wave blocks, 16 envs per wave
-            const int blocks8 = (ra.n + 127) / 128;
-            rollout_sp_kernel<KIND, H, 1, 8><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
-            RLP_CHECK_LAUNCH("rlp_rollout");
-            return RLP_OK;
-        }
-    }
-    if constexpr (X3 && SUB == 1 && rollout_sp_ring<KIND, 1, 8, 2>() != 0) {
-        if (physics == 4) {  // one 8-wave block of 16-env waves per CU (2 waves per SIMD)
-            const int blocks8 = (ra.n + 127) / 128;
-            rollout_sp_kernel<KIND, H, 1, 8, 2><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
-            RLP_CHECK_LAUNCH("rlp_rollout");
-            return RLP_OK;
-        }
-    }
     if constexpr (X3 && SUB == 2 && rollout_sp_ring<KIND, 2, 8>() != 0) {
         if (physics == 3) {  // one 8-wave block per CU, 32 envs per wave
             const int blocks8 = (ra.n + 255) / 256;
-            rollout_sp_kernel<KIND, H, 2, 8><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
+            rollout_sp_kernel<KIND, H, 2, 8><<<blocks8, 512, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
@@ -626,22 +587,14 @@ static int launch_rollout(const void *params, double *state, uint8_t *need_reset
     if constexpr (X3 && SUB == 2 && rollout_sp_ring<KIND, 2, 4, 1>() != 0) {
         if (physics == 5) {  // one 4-wave block of 32-env waves per CU (1 wave per SIMD, 512 registers)
             const int blocks4 = (ra.n + 127) / 128;
-            rollout_sp_kernel<KIND, H, 2, 4, 1><<<blocks4, 256, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
-            RLP_CHECK_LAUNCH("rlp_rollout");
-            return RLP_OK;
-        }
-    }
-    if constexpr (X3 && SUB == 4 && rollout_sp_ring<KIND, 4, 4, 1>() != 0) {
-        if (physics == 6) {  // one 4-wave block of 64-env waves per CU (1 wave per SIMD, 512 registers)
-            const int blocks4 = (ra.n + 255) / 256;
-            rollout_sp_kernel<KIND, H, 4, 4, 1><<<blocks4, 256, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
+            rollout_sp_kernel<KIND, H, 2, 4, 1><<<blocks4, 256, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
             RLP_CHECK_LAUNCH("rlp_rollout");
             return RLP_OK;
         }
     }
     if constexpr (X3 && rollout_sp_fits<KIND, SUB>()) {
         if (physics)
-            rollout_sp_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b, g_rollout_prio});
+            rollout_sp_kernel<KIND, H, SUB><<<blocks, threads, 0, stream>>>(SpArgs<KIND>{p, state, need_reset, actor, an, critic, cn, ra, b});
         else
             rollout_kernel<KIND, H, SUB, X3><<<blocks, threads, 0, stream>>>(p, state, need_reset, actor,
                                                                          an, critic, cn, ra, b);
@@ -689,9 +642,7 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
             else
                 physics = 1;
         }
-        if (physics == 2 || physics == 4) sub = 1;  // the 8-wave variants of 16-env waves
         if (physics == 3 || physics == 5) sub = 2;  // the one-block-per-CU variants of 32-env waves
-        if (physics == 6) sub = 4;                  // ... of 64-env waves
         if (sub == 0)  // auto: 32-env waves unless that leaves fewer than 2 blocks per CU
             sub = (ra.n + 127) / 128 < 2 * cus ? 1 : 2;
         if (sub == 1)
@@ -787,7 +738,7 @@ static int rollout_oa(const void *params, double *state, uint8_t *need_reset, co
     // per-call scratch (stream-ordered): the step's f64 reward, i32 flag, the bootstrap V
     void *ws = nullptr;
     const size_t wsz = (size_t)n * (sizeof(double) + sizeof(int32_t) + sizeof(float));
-    if (hipMallocAsync(&ws, wsz, s) != hipSuccess) return fail(RLP_EINVAL, "rlp_rollout: scratch");
+    if (hipMallocAsync(&ws, wsz, s) != hipSuccess) return fail(RLP_ENOMEM, "rlp_rollout: scratch");
     double *r64 = static_cast<double *>(ws);
     int32_t *f32 = reinterpret_cast<int32_t *>(r64 + n);
     float *vb = reinterpret_cast<float *>(f32 + n);
@@ -822,6 +773,131 @@ static int rollout_oa(const void *params, double *state, uint8_t *need_reset, co
     return RLP_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// Nets in the plain layout (cfg->net_layout = 1): any Linear stack the fused kernels do not take
+// — the PPO2-SecondOrderIntegration demo's 4 -> 128 -> 64 -> 32 -> 2 actor and 4 -> 64 -> 64 -> 1
+// critic (demonstration/PPO2/PPO2-4-SecondOrderIntegration/train.py:37-125). The same driver
+// loop, random draws and buffers as the fused kernel, as a sequence of launches per step on the
+// caller's stream (no host round trip):
+//   critic V(s_t), actor tanh(z_t)       rlp_mlp_forward's kernels (exact f32 MFMA)
+//   plain_step_kernel                     mean = tanh(z) gain + off, Philox eps (the fused
+//                                         kernel's stream), clamp, log-prob, V(s'_{t-1}) = V(s_t)
+//                                         where the env did not end at t-1, env step, buffer
+//                                         append, and s_{t+1}: obs_next, or the reset (counter
+//                                         step0 + t + 1) and observation of an env that ended
+// and after the segment the bootstrap V(s'_{T-1}) of the envs still running.
+template <int KIND>
+__global__ void __launch_bounds__(256) plain_begin_kernel(typename Env<KIND>::P p, double *state,
+                                                          uint8_t *need_reset, RolloutArgs ra,
+                                                          float *obs) {
+    using E = Env<KIND>;
+    const int i = blockIdx.x * 256 + threadIdx.x, n = ra.n;
+    if (i >= n) return;
+    const auto &pk = *(const typename E::P *)(const __attribute__((address_space(4))) typename E::P *)
+        __builtin_amdgcn_kernarg_segment_ptr();
+    double s[E::D];
+#pragma unroll
+    for (int d = 0; d < E::D; ++d) s[d] = state[(size_t)d * n + i];
+    if (need_reset[i]) {
+        E::reset(pk, s, ra.seed, ra.step0, ra.env_id0 + (uint64_t)i);
+#pragma unroll
+        for (int d = 0; d < E::D; ++d) state[(size_t)d * n + i] = s[d];
+    }
+    need_reset[i] = 0;
+    float o[E::S];
+    E::observe(pk, s, o);
+#pragma unroll
+    for (int j = 0; j < E::S; ++j) obs[(size_t)i * E::S + j] = o[j];
+}
+
+template <int KIND>
+__global__ void __launch_bounds__(256) plain_step_kernel(typename Env<KIND>::P p, double *state,
+                                                         uint8_t *need_reset, RolloutArgs ra, int t,
+                                                         rlp_rollout_bufs b) {
+    using E = Env<KIND>;
+    constexpr int A = E::A, S = E::S;
+    const int i = blockIdx.x * 256 + threadIdx.x, n = ra.n;
+    if (i >= n) return;
+    const auto &pk = *(const typename E::P *)(const __attribute__((address_space(4))) typename E::P *)
+        __builtin_amdgcn_kernarg_segment_ptr();
+    const int k = t * n + i;
+    const uint64_t eid = ra.env_id0 + (uint64_t)i, gstep = ra.step0 + (uint64_t)t;
+    float eps[A], act[A];
+    philox_normal_f32<A>(ra.seed, gstep, eid, eps);
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        const float m = b.action[k * A + a] * ra.gain[a] + ra.off[a];  // actor output tanh(z)
+        float x = m + ra.std_[a] * eps[a];
+        x = fmaxf(fminf(x, ra.a_max[a]), ra.a_min[a]);
+        act[a] = x;
+        b.action[k * A + a] = x;
+        b.logp[k * A + a] = normal_logp_c(x, m, ra.half_inv_var[a], ra.log_std[a]);
+    }
+    if (t > 0 && !b.done[k - n]) b.value_next[k - n] = b.value[k];  // V(s'_{t-1}) == V(s_t)
+    double s[E::D];
+#pragma unroll
+    for (int d = 0; d < E::D; ++d) s[d] = state[(size_t)d * n + i];
+    float on[S];
+    double r;
+    int f;
+    bool dn;
+    E::step(pk, s, act, on, r, f, dn);
+#pragma unroll
+    for (int j = 0; j < S; ++j) b.obs_next[(size_t)k * S + j] = on[j];
+    b.reward[k] = (float)r;
+    b.done[k] = dn;
+    b.success[k] = success_of(ra.success_rule, ra.success_flag, dn, f);
+    b.flag[k] = (int8_t)f;
+    if (t + 1 < ra.T) {
+        if (dn) {  // the next step's reset (as the fused kernel: right after the terminal step)
+            E::reset(pk, s, ra.seed, gstep + 1, eid);
+            E::observe(pk, s, on);
+        }
+#pragma unroll
+        for (int j = 0; j < S; ++j) b.obs[(size_t)(k + n) * S + j] = on[j];
+    } else {
+        need_reset[i] = dn;
+    }
+#pragma unroll
+    for (int d = 0; d < E::D; ++d) state[(size_t)d * n + i] = s[d];
+}
+
+template <int KIND>
+static int rollout_plain(const void *params, double *state, uint8_t *need_reset,
+                         const rlp_mlp_desc &ad, const float *actor, const rlp_mlp_desc &cd,
+                         const float *critic, const RolloutArgs &ra, const rlp_rollout_bufs &b,
+                         hipStream_t s) {
+    using E = Env<KIND>;
+    const auto &p = *static_cast<const typename E::P *>(params);
+    if (ad.dims[0] != E::S || cd.dims[0] != E::S || ad.dims[ad.n_layers] != E::A ||
+        cd.dims[cd.n_layers] != 1)
+        return fail(RLP_EINVAL, "rlp_rollout: net dims (S=%d,A=%d / S=%d,A=%d) != env (S=%d,A=%d)",
+                    ad.dims[0], ad.dims[ad.n_layers], cd.dims[0], cd.dims[cd.n_layers], E::S, E::A);
+    if (ad.act[ad.n_layers - 1] != RLP_ACT_TANH)
+        return fail(RLP_EUNSUPPORTED, "rlp_rollout: the actor's last layer must be tanh");
+    const int n = ra.n, T = ra.T, nb = (n + 255) / 256;
+    float *vb = nullptr;  // the bootstrap V (stream-ordered scratch)
+    if (hipMallocAsync((void **)&vb, sizeof(float) * (size_t)n, s) != hipSuccess)
+        return fail(RLP_ENOMEM, "rlp_rollout: scratch of %d floats", n);
+    plain_begin_kernel<KIND><<<nb, 256, 0, s>>>(p, state, need_reset, ra, b.obs);
+    int rc = RLP_OK;
+    for (int t = 0; t < T && rc == RLP_OK; ++t) {
+        const size_t k0 = (size_t)t * n;
+        const float *obs_t = b.obs + k0 * E::S;
+        rc = rlp_mlp_forward(&cd, critic, obs_t, b.value + k0, n, nullptr, s);
+        if (rc == RLP_OK) rc = rlp_mlp_forward(&ad, actor, obs_t, b.action + k0 * E::A, n, nullptr, s);
+        if (rc == RLP_OK) plain_step_kernel<KIND><<<nb, 256, 0, s>>>(p, state, need_reset, ra, t, b);
+    }
+    if (rc == RLP_OK) {  // V(s'_{T-1}) of the envs still running
+        rc = rlp_mlp_forward(&cd, critic, b.obs_next + (size_t)(T - 1) * n * E::S, vb, n, nullptr, s);
+        if (rc == RLP_OK) oa_boot_kernel<<<nb, 256, 0, s>>>(T, n, vb, b);
+    }
+    (void)hipFreeAsync(vb, s);
+    if (rc != RLP_OK) return rc;
+    RLP_CHECK_LAUNCH("rlp_rollout (plain-layout nets)");
+    return RLP_OK;
+}
+
 static int g_rollout_sub = 0;  // 0: auto
 static int g_mlp_precision = RLP_MLP_F16X3;
 
@@ -844,16 +920,11 @@ int rlp_get_mlp_precision(void) { return g_mlp_precision; }
 // than 2 blocks per CU, else 2; f32: 2), 1 (f16x3 only), 2, 4
 
 // tuning knob (include/rlp.h): -1 (default) = auto (3 when the envs fill every CU with a 256-env
-// block, else — and always for the UAV — 5), 0-6 the kernel variants listed there
+// block, else — and always for the UAV — 5), 0 / 1 / 3 / 5 the kernel variants listed there
 int rlp_set_rollout_physics(int shared) {
-    if (shared < -1 || shared > 6) return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
+    if (shared < -1 || shared > 5 || shared == 2 || shared == 4)
+        return fail(RLP_EINVAL, "rlp_set_rollout_physics: %d", shared);
     g_rollout_shared_physics = shared;
-    return RLP_OK;
-}
-
-int rlp_set_rollout_prio(int mode) {
-    if (mode < 0 || mode > 1) return fail(RLP_EINVAL, "rlp_set_rollout_prio: %d", mode);
-    g_rollout_prio = mode;
     return RLP_OK;
 }
 
@@ -902,9 +973,13 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
                 "rlp_rollout: T*n = %lld too large for one segment (32-bit buffer indices)",
                 (long long)cfg->T * cfg->n);
     if (cfg->n == 0) return RLP_OK;
+    RLP_REQUIRE(cfg->net_layout == 0 || cfg->net_layout == 1, "rlp_rollout: net_layout %d",
+                cfg->net_layout);
     MfmaNet an, cn;
-    if (!mfma_net_from_desc(*actor_desc, &an) || !mfma_net_from_desc(*critic_desc, &cn))
-        return fail(RLP_EUNSUPPORTED, "rlp_rollout: nets must be [S->H->H->A] tanh MLPs");
+    if (cfg->net_layout == 0 &&
+        (!mfma_net_from_desc(*actor_desc, &an) || !mfma_net_from_desc(*critic_desc, &cn)))
+        return fail(RLP_EUNSUPPORTED, "rlp_rollout: packed nets must be [S->H->H->A] tanh MLPs "
+                                      "(net_layout = 1 takes any Linear stack)");
     RolloutArgs ra;
     ra.T = cfg->T; ra.n = cfg->n;
     ra.seed = cfg->seed; ra.step0 = cfg->step0; ra.env_id0 = cfg->env_id0;
@@ -921,13 +996,30 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
     hipStream_t s = as_stream(stream);
     // per-call selections (cfg, 0 = the library-wide default of the rlp_set_* knobs)
     RLP_REQUIRE(cfg->mlp_precision >= 0 && cfg->mlp_precision <= 2 && cfg->physics >= 0 &&
-                    cfg->physics <= 8 && (cfg->sub == 0 || cfg->sub == 1 || cfg->sub == 2 ||
+                    cfg->physics <= 8 && cfg->physics != 3 && cfg->physics != 5 &&
+                    cfg->physics != 7 && (cfg->sub == 0 || cfg->sub == 1 || cfg->sub == 2 ||
                                           cfg->sub == 4),
                 "rlp_rollout: cfg mlp_precision=%d physics=%d sub=%d", cfg->mlp_precision,
                 cfg->physics, cfg->sub);
     const int sub = cfg->sub ? cfg->sub : g_rollout_sub;
     const int prec = cfg->mlp_precision ? cfg->mlp_precision - 1 : g_mlp_precision;
     const int physics = cfg->physics == 8 ? -1 : cfg->physics ? cfg->physics - 1 : g_rollout_shared_physics;
+    if (cfg->net_layout == 1) {
+        switch (kind) {
+#define RLP_PLAIN(K)                                                                              \
+    case K:                                                                                       \
+        return rollout_plain<K>(env_params, state, need_reset, *actor_desc, actor_packed,        \
+                                *critic_desc, critic_packed, ra, b, s);
+            RLP_PLAIN(RLP_ENV_CARTPOLE)
+            RLP_PLAIN(RLP_ENV_CARTPOLE_ANGLEONLY)
+            RLP_PLAIN(RLP_ENV_SOI)
+            RLP_PLAIN(RLP_ENV_UGV_FORWARD)
+            RLP_PLAIN(RLP_ENV_UGV_BIDIRECTIONAL)
+            RLP_PLAIN(RLP_ENV_UAV_HOVER_OUTER_LOOP)
+#undef RLP_PLAIN
+        }
+        return fail(RLP_EUNSUPPORTED, "rlp_rollout: plain-layout nets for env kind %d", kind);
+    }
     switch (kind) {
     case RLP_ENV_CARTPOLE:
         return rollout_kind<RLP_ENV_CARTPOLE>(env_params, state, need_reset, actor_packed, an,

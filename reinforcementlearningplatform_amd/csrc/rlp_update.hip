@@ -19,16 +19,6 @@
 // A deterministic reduce assembles the flat gradient (torch parameter order).
 #include "rlp_mfma_x3.hpp"
 
-// RLP_FD_PIPE: the GEMM chunks' fragment reads one tile pair ahead of the MFMAs (1: source order
-// only, 2: pinned with sched_group_barrier); 0: two groups of four tiles, each read then multiplied
-// (the next group's reads wait for the current MFMAs to release their registers: s_nop hazards and
-// exposed LDS latency). Same-box rocprof A/B (profiles/r3/r3s_fd_ab.txt): actor / critic FD
-// 8.25 / 8.17 -> 8.02 / 7.99 ms with 2; lock-step tanh chains in the tails gave nothing on top
-// and slowed the critic alone (removed).
-#ifndef RLP_FD_PIPE
-#define RLP_FD_PIPE 2
-#endif
-
 namespace rlp {
 
 constexpr int kUpdRows = 64;          // rows per block tile (4 waves x 16)
@@ -48,7 +38,6 @@ struct Ppo2Args {
     unsigned *g2max;    // bits of max|g2| (atomicMax)
     float *part3;       // [grid * 4][A*256 + A + 256*S + 256]: per-wave dW3 | db3 | dW1 | db1
     double *loss_sum;
-    int prio;           // rlp_set_update_prio: the second half of the block's waves at priority 1
 };
 
 // block barrier for LDS hand-offs only: drains this wave's LDS ops, not its global loads (HIP's
@@ -121,9 +110,11 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
             const float *slot = ring + (((c / CPB) % RG) * CPB + c % CPB) * kX3ChunkFloats + lane * 4;
             if (hf == 0 && P + 1 < 8) pre(P + 1);
             if (hf == 1 && P + 1 < 8) bop(P + 1, nbh, nbl);
-#if RLP_FD_PIPE
             // the chunk's 8 output tiles in four pairs, each pair's 4 fragments read while the
-            // previous pair's 6 MFMAs run (two register buffers: the same 32 fragment registers)
+            // previous pair's 6 MFMAs run (two register buffers: the same 32 fragment registers;
+            // pinned with sched_group_barrier). Same-box rocprof A/B (profiles/r3/r3s_fd_ab.txt):
+            // actor / critic FD 8.25 / 8.17 -> 8.02 / 7.99 ms against two groups of four tiles,
+            // each read then multiplied (s_nop hazards and exposed LDS latency; removed)
             {
                 half8 fh[2][2], fl[2][2];
                 auto rd = [&](int grp, int buf) {
@@ -138,9 +129,7 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
                 for (int grp = 0; grp < 4; ++grp) {
                     if (grp + 1 < 4) {
                         rd(grp + 1, (grp + 1) & 1);
-#if RLP_FD_PIPE > 1
                         __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#endif
                     }
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
@@ -157,36 +146,7 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
                         }
                         acc[8 * hf + 2 * grp + u] = v;
                     }
-#if RLP_FD_PIPE > 1
                     __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-#endif
-                }
-            }
-            if (false)
-#endif
-            // the chunk's 8 output tiles in two groups of 4 (8 fragment reads, then 12 MFMAs):
-            // 32 fragment registers instead of 64 keep two waves per SIMD within 256 registers
-#pragma unroll
-            for (int g4 = 0; g4 < 2; ++g4) {
-                half8 ah[4], al[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    ah[u] = *reinterpret_cast<const half8 *>(slot + (2 * (4 * g4 + u)) * 256);
-                    al[u] = *reinterpret_cast<const half8 *>(slot + (2 * (4 * g4 + u) + 1) * 256);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    floatx4 v = acc[8 * hf + 4 * g4 + u];
-                    if constexpr (SWAP) {
-                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, ah[u], v, 0, 0, 0);
-                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, ah[u], v, 0, 0, 0);
-                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, al[u], v, 0, 0, 0);
-                    } else {
-                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[u], bh, v, 0, 0, 0);
-                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[u], bl, v, 0, 0, 0);
-                        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[u], bh, v, 0, 0, 0);
-                    }
-                    acc[8 * hf + 4 * g4 + u] = v;
                 }
             }
         }
@@ -239,52 +199,39 @@ __device__ __forceinline__ float pair_sum_x16(float a, float b) {
 }
 constexpr int kDppRowMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1;
 
-// LDS of one FD block (floats): [ ring (3 x CPB x 16 KiB) | small weights | srw ].
-// waves per FD block: 8 (default: one block per CU, half the W2 DMA per CU) or 4 (two blocks per
-// CU); 2 waves per SIMD either way. A block iteration covers kFdWaves / 4 G2 tiles of 64 rows.
-// The 8-wave block is ~2 % slower per wave tile (diag_fd.py: its barriers span 8 waves) but 4-5 %
-// faster per launch: two co-resident 4-wave blocks do not get equal shares of the CU (oldest-first
-// issue arbitration) and the launch waits for the slower half; a tile queue (atomic counter)
-// instead of the static grid stride recovered only half of that (rocprof A/B,
-// scripts/ab_fdwaves.sh).
-#ifndef RLP_FD_WAVES
-#define RLP_FD_WAVES 8
-#endif
-constexpr int kFdWaves = RLP_FD_WAVES;
+// LDS of one FD block (floats): [ W2 ring (3 x 16 KiB) | small weights | srw | dW1 partials ].
+// One 8-wave block per CU (2 waves per SIMD; a block iteration covers 2 G2 tiles of 64 rows): half
+// the W2 DMA per CU of two 4-wave blocks. The 8-wave block is ~2 % slower per wave tile
+// (diag_fd.py: its barriers span 8 waves) but 4-5 % faster per launch: two co-resident 4-wave blocks
+// do not get equal shares of the CU (oldest-first issue arbitration) and the launch waits for the
+// slower half; a tile queue (atomic counter) instead of the static grid stride recovered only half
+// of that. Measured and removed: 4-wave blocks (two per CU, or one per CU for the
+// actor's and critic's FD on two streams), 2 chunks per ring slot (the actor's FD spilled 56 B),
+// the second half of each block's waves at s_setprio 1.
+constexpr int kFdWaves = 8;
 constexpr int kFdRows = 16 * kFdWaves;
-// chunks per ring slot / block barrier: 2 (one barrier per k-phase) measured no faster here (the
-// actor's FD spills 56 B with it) — unlike the rollout
-#ifndef RLP_FD_CPB
-#define RLP_FD_CPB 1
-#endif
-constexpr int kFdCpb = RLP_FD_CPB;
-// W2 chunk-ring slots of the FD GEMMs (RG - 2 groups in flight while one is read)
-#ifndef RLP_FD_RING
-#define RLP_FD_RING 3
-#endif
-constexpr int kFdRing = RLP_FD_RING;
+constexpr int kFdRing = 3;  // W2 chunk-ring slots (one group in flight while one is read)
 
-
-// W: waves per block (kFdWaves by default; 4 with one block per CU when the actor's and the
-// critic's FD kernels run concurrently on two streams, rlp_set_fd_mode)
-template <int KS1, int A, int LOSS, int W = kFdWaves>
-__global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
-    constexpr int kFdWaves = W, kFdRows = 16 * W;
+template <int KS1, int A, int LOSS>
+__global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
     constexpr int H = kUpdH, SMALL = mlp_small_floats<H, KS1, A>();
     constexpr int NC = 4 * KS1 + 1;  // dW1 columns per neuron: s features | bias
-    // (the deeper ring only for the one-block-per-CU shape: two 4-wave blocks share a CU's LDS)
-    constexpr int kRing = W == 8 ? kFdRing : kX3Ring, kFdRegion = kRing * kX3ChunkFloats * kFdCpb;
-    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + kFdWaves * 16 * 8];
+    constexpr int kFdRegion = kFdRing * kX3ChunkFloats;
+    // the wave's dW1 | db1 partial [256 neurons][NCS] in LDS (NCS: the row stride that puts the
+    // two 16-lane groups of a ds_add_f32 on disjoint banks)
+    constexpr int NCS = NC == 5 ? 5 : 11;
+    static_assert(NC <= 9, "dW1 columns");
+    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + kFdWaves * 16 * 8 +
+                                                      kFdWaves * kUpdH * NCS];
     float *ring = lds, *small = lds + kFdRegion;
     // the wave index as a scalar (readfirstlane): every wave-derived offset, the G2 tile and its
     // store guard become SGPR values (no per-lane 64-bit address arithmetic, no exec-masked stores)
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // (the younger half of the SIMD pairs loses VALU arbitration at every segment start otherwise;
-    // wv is wave-uniform, so this is a scalar branch around one s_setprio)
-    if (g.prio && wv >= kFdWaves / 2) __builtin_amdgcn_s_setprio(1);
     float *const srw = lds + kFdRegion + SMALL + wv * 128;  // [16 rows][8]
+    float *const dw1s = lds + kFdRegion + SMALL + kFdWaves * 128 + wv * kUpdH * NCS;
     const MfmaNet &net = g.net;
     mlp_small_to_lds(g.packed, net, small, true);  // small_r: W1, b1 x 2/ln 2, b2 x 2^(sw+SH)
+    for (int i = threadIdx.x & 63; i < kUpdH * NCS; i += 64) dw1s[i] = 0.f;
     __syncthreads();
 
     const int lane = threadIdx.x & 63, gq = lane >> 4, e = lane & 15;
@@ -302,11 +249,6 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
         for (int c = 0; c < 4; ++c) dW3p[a][c] = 0.f;
     }
     double lsum = 0.0;
-    float dW1p[2][2 * NC];  // [h][i]: neuron 16 (8 h + 2 gq + i / NC) + e, column i % NC
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] = 0.f;
     float g2max = 0.f;
     floatx4 dh1[16];  // dh1 -> g1 of the wave's tile
 
@@ -331,47 +273,40 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
             c = __builtin_amdgcn_mfma_f32_16x16x4f32(bo[kk], w1[kk], c, 0, 0, 0);
         return c;
     };
-    // g1 = dh1 * (1 - h1^2) of neuron tile t, h1 = 1 - 2 r recomputed (r as in the forward's)
-    auto g1_tile = [&](int t, const float (&bo)[KS1], float us) {
+    // g1 / (4 x the tile's unscale) = dh1 * r (1 - r) of neuron tile t (1 - h1^2 = 4 r (1 - r),
+    // h1 = 1 - 2 r recomputed, r as in the forward's); neuron on lane: dh1[t][q] = row 4 gq + q
+    auto g1_tile = [&](int t, const float (&bo)[KS1]) {
         const floatx4 pre = layer1_t(t, bo);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(pre[q]));
-            dh1[t][q] = dh1[t][q] * us * __builtin_fmaf(-r, r, r);
+            dh1[t][q] = dh1[t][q] * __builtin_fmaf(-r, r, r);
         }
     };
-    // dW1 | db1 += sum_rows g1 [s | 1]^T: the lane's 4 rows in registers (s rows from srw), then
-    // the 4 lane groups by a 2-stage permlane butterfly, per half of the neuron tiles
-    // (8 NC -> 2 NC values)
-    auto dw1_acc = [&](const float *srw) {
-        float sv[4][4 * KS1];
+    // dW1 | db1 += sum_rows g1 [s | 1]^T on the f32 MFMA instead of VALU products and lane
+    // butterflies: A[neuron][row] = the g1 registers above (K = the 4 rows of lane group gq),
+    // B[row][column] = [s | 1] x us (the tile's 4 x unscale folded into the 4 B registers instead
+    // of the 64 g1 values); four 16x16x4 steps give C[neuron 16 t + 4 gq + q][column e], columns
+    // 0 .. 4 KS1 - 1 the s features, 4 KS1 the bias, added into the wave's LDS partial (ds_add_f32:
+    // every address belongs to one lane of this wave, so the sums keep program order)
+    auto dw1_acc = [&](const float *srw, float us) {
+        float bq[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < 4; ++q) {
+            const float sv = srw[(4 * gq + q) * 8 + (e & 7)];
+            bq[q] = (e < 4 * KS1 ? sv : (e == 4 * KS1 ? 1.f : 0.f)) * us;
+        }
 #pragma unroll
-            for (int kk = 0; kk < KS1; ++kk) {
-                const floatx4 v = *reinterpret_cast<const floatx4 *>(srw + (4 * gq + q) * 8 + 4 * kk);
+        for (int t = 0; t < 16; ++t) {
+            floatx4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int u = 0; u < 4; ++u) sv[q][4 * kk + u] = v[u];
+            for (int q = 0; q < 4; ++q) c = __builtin_amdgcn_mfma_f32_16x16x4f32(dh1[t][q], bq[q], c, 0, 0, 0);
+            if (e < NC) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    __hip_atomic_fetch_add(dw1s + (16 * t + 4 * gq + q) * NCS + e, c[q], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WAVEFRONT);
             }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            float v[8 * NC];
-#pragma unroll
-            for (int tt = 0; tt < 8; ++tt) {
-                const floatx4 gt = dh1[8 * h + tt];
-#pragma unroll
-                for (int f = 0; f < 4 * KS1; ++f) {
-                    float x = gt[0] * sv[0][f];
-#pragma unroll
-                    for (int q = 1; q < 4; ++q) x = __builtin_fmaf(gt[q], sv[q][f], x);
-                    v[tt * NC + f] = x;
-                }
-                v[tt * NC + 4 * KS1] = (gt[0] + gt[1]) + (gt[2] + gt[3]);
-            }
-#pragma unroll
-            for (int i = 0; i < 4 * NC; ++i) v[i] = pair_sum_x32(v[i], v[i + 4 * NC]);
-#pragma unroll
-            for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] += pair_sum_x16(v[i], v[i + 2 * NC]);
         }
     };
 
@@ -420,7 +355,7 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[j] = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * gq);
         floatx4 p0, p1;  // layer-1 tiles of the next phase (pre), consumed by its B operands (bop)
-        x3_gemm16<false, kFdWaves, kFdCpb, kRing>(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
+        x3_gemm16<false, kFdWaves, 1, kFdRing>(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -567,7 +502,7 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) dh1[j] = floatx4{0.f, 0.f, 0.f, 0.f};
         // (operands swapped: dh1 comes out "neuron on lane", dh1[t][q] = row 4 gq + q, neuron 16 t + e)
-        x3_gemm16<true, kFdWaves, kFdCpb, kRing>(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
+        x3_gemm16<true, kFdWaves, 1, kFdRing>(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -578,20 +513,19 @@ __global__ void __launch_bounds__(64 * W, 8 / W) ppo2_fd_kernel(Ppo2Args g) {
         }, [](int) {});
         // ---- g1 = dh1 * (1 - h1^2) and dW1 | db1 of this tile
 #pragma unroll
-        for (int t = 0; t < 16; ++t) g1_tile(t, bobs, unscale4);
-        dw1_acc(srw);
+        for (int t = 0; t < 16; ++t) g1_tile(t, bobs);
+        dw1_acc(srw, unscale4);
     }
 
     // ---- per-wave partials: dW3 (lane's neurons) | db3 summed over the 16 row lanes | dW1 | db1
     float *out = g.part3 + (size_t)(blockIdx.x * kFdWaves + wv) * (A * H + A + H * S + H);
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 2 * NC; ++i) {
-            const int n = 16 * (8 * h + 2 * gq + i / NC) + e, f = i % NC;
-            if (f < S) out[A * H + A + n * S + f] = dW1p[h][i];
-            else if (f == 4 * KS1) out[A * H + A + H * S + n] = dW1p[h][i];
-        }
+    wave_sync_lds();  // the wave's LDS adds have landed
+    for (int i = lane; i < kUpdH * NC; i += 64) {
+        const int n = i / NC, f = i % NC;
+        const float v = dw1s[n * NCS + f];
+        if (f < S) out[A * H + A + n * S + f] = v;
+        else if (f == 4 * KS1) out[A * H + A + H * S + n] = v;
+    }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) g2max = fmaxf(g2max, __shfl_xor(g2max, o));
     if (lane == 0) atomicMax(g.g2max, __float_as_uint(g2max));  // non-negative: uint order
@@ -620,31 +554,26 @@ struct WArgs {
     const float *g2t;
     const unsigned *g2max;
     float *part;  // [grid][H*H + H]: dW2 | db2
-    int prio;
 };
 
 // B fragments of h1 for one 64-row tile: [ks 2][nt 16][hi, lo][64 lanes][8 halfs] (64 KiB):
 // lane (g, e) of MFMA step ks holds h1(row, neuron 16 nt + e) * 2^SH for rows 32 ks + 4 g + i and
 // 32 ks + 16 + 4 g + i (i < 4): the C layout of two layer-1 MFMA tiles (rows on the lane groups),
 // with the A operands (g2 rows) loaded in the same K order.
-// W waves per block, one block per CU; wave wv owns the JT = 16 / W output-row tiles j in
-// [16 JT wv, 16 JT wv + 16 JT) of dW2 (64 JT accumulator registers); all waves share the tile's
-// h1 fragments. W = 8: 2 waves per SIMD (256 registers, JT = 2). W = 4: 1 wave per SIMD with the
-// VGPR + AGPR budget (JT = 4): every fragment read from LDS feeds 12 MFMAs instead of 6, so the
-// CU reads half the LDS bytes per tile, and the next fragment pair is read one step ahead.
-constexpr int kWgWaves = 8;
-// RLP_WG_SGB: pin each fragment pair's LDS reads ahead of the MFMAs that precede their use
-// (sched_group_barrier); without it the scheduler sinks them to just before their MFMAs (exposed
-// LDS latency per column step). 2 (default) also fences each fragment build into a region of its
+// 8 waves per block (2 per SIMD, 256 registers), one block per CU; wave wv owns the JT = 2
+// output-row tiles j in [32 wv, 32 wv + 32) of dW2 (128 accumulator registers); all waves share the
+// tile's h1 fragments. Each fragment pair's LDS reads are pinned ahead of the MFMAs that precede
+// their use (sched_group_barrier; without it the scheduler sinks them to just before their MFMAs,
+// exposing LDS latency per column step), and each fragment build is fenced into a region of its
 // own so the pinned groups only see the GEMM: wgrad 3.16-3.19 -> 3.04-3.07 ms (same box, three
-// boxes -2.5 to -4 %, profiles/r3/r3v_wgrad_ab.txt); 1 (no fences) was 8 % slower, and the build
-// spread over four steps in stages measured neutral
-#ifndef RLP_WG_SGB
-#define RLP_WG_SGB 2
-#endif
-template <int KS1, int W = kWgWaves>
-__global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
-    constexpr int H = kUpdH, SP = 4 * KS1, NT = 64 * W, JT = 16 / W;
+// boxes -2.5 to -4 %, profiles/r3/r3v_wgrad_ab.txt). Measured and removed: 4-wave
+// blocks with the VGPR + AGPR budget (half the LDS fragment reads per tile), the
+// v_mfma_f32_32x32x16_f16 form (half the MFMA issue slots), the pinning without the fences (8 %
+// slower), the build spread over four steps, the younger waves at s_setprio 1.
+constexpr int kWgWaves = 8;
+template <int KS1>
+__global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
+    constexpr int W = kWgWaves, H = kUpdH, SP = 4 * KS1, NT = 64 * W, JT = 16 / W;
     constexpr int SV = (kUpdRows * SP + NT - 1) / NT;
     constexpr int FRAG = 2 * 16 * 2 * 64 * 8;  // halfs of one tile's h1 fragments (64 KiB)
     constexpr int FPW = 32 / W;                // fragments (ks, nt) built per wave and tile
@@ -658,7 +587,6 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
     const int S = net.S;
     const int lane = threadIdx.x & 63, gq = lane >> 4, e = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (w.prio && wv >= W / 2) __builtin_amdgcn_s_setprio(1);
     {
         // small_r: W1, b1 x 2/ln 2 (h1 as in the FD forward)
         const float *W1c = w.packed + net.off_small_r;
@@ -791,9 +719,7 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
                 if (F + 1 < 32) {
                     nbh = frag(cur, F + 1, 0);
                     nbl = frag(cur, F + 1, 1);
-#if RLP_WG_SGB
                     __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // (pinned ahead of the MFMAs)
-#endif
                 }
 #pragma unroll
                 for (int jt = 0; jt < JT; ++jt) {
@@ -803,18 +729,12 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
                     v = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jt], bh, v, 0, 0, 0);
                     acc2[jt][nt] = v;
                 }
-#if RLP_WG_SGB
                 __builtin_amdgcn_sched_group_barrier(0x008, 3 * JT, 0);
-#endif
                 // the next tile's fragments, spread over this tile's MFMAs (FPW per wave)
                 if (F % (32 / FPW) == (32 / FPW) - 1) {
-#if RLP_WG_SGB > 1
                     __builtin_amdgcn_sched_barrier(0);  // (the build stays a region of its own)
-#endif
                     build_frag(nxt, FPW * wv + F / (32 / FPW));
-#if RLP_WG_SGB > 1
                     __builtin_amdgcn_sched_barrier(0);
-#endif
                 }
                 if (F + 1 < 32) {
                     bh = nbh;
@@ -840,185 +760,6 @@ __global__ void __launch_bounds__(64 * W, 1) ppo2_wgrad_kernel(WArgs w) {
             for (int nt = 0; nt < 16; ++nt) out[j * H + 16 * nt + e] = acc2[jt][nt][q] * un2;
             if (e == 0) out[H * H + j] = accb[jt][q] * unb;
         }
-}
-
-// The same weight gradient on v_mfma_f32_32x32x16_f16 (twice the FLOPs per instruction: half the
-// MFMA issue slots of the 16x16x32 form for the same VALU work). 8 waves, wave wv owns the 32
-// dW2 rows [32 wv, 32 wv + 32) x all 256 columns (8 column tiles of 32, 128 accumulator
-// registers). K = 16 rows per MFMA, 4 K-steps per 64-row tile. The h1 B fragments come from
-// layer 1 on v_mfma_f32_32x32x2_f32 (32 rows x 32 neurons per tile, neuron on the lane): its C
-// registers 0-7 / 8-15 hold rows {0-3, 8-11} / {16-19, 24-27} + 4 (lane / 32) of the 32-row half,
-// which fixes the K order of each step; the g2 A operands are loaded in that order (two float4
-// per lane from the [tile][neuron][64 rows] G2 layout).
-template <int KS1>
-__global__ void __launch_bounds__(512, 1) ppo2_wgrad32_kernel(WArgs w) {
-    constexpr int W = 8, H = kUpdH, SP = 4 * KS1, NT = 64 * W;
-    constexpr int SV = (kUpdRows * SP + NT - 1) / NT;
-    constexpr int FRAG = 4 * 8 * 2 * 64 * 8;  // [ks 4][nt 8][hi, lo][64 lanes][8 halfs] (64 KiB)
-    __shared__ float srow[2][kUpdRows][SP];
-    __shared__ float w1s[H][SP + 1];
-    __shared__ float b1s[H];
-    __shared__ __attribute__((aligned(16))) _Float16 hfrag[2][FRAG];
-    const MfmaNet &net = w.net;
-    const int S = net.S;
-    const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (w.prio && wv >= W / 2) __builtin_amdgcn_s_setprio(1);
-    {
-        const float *W1c = w.packed + net.off_small_r;
-        const float *B1c = w.packed + net.off_small_r + (net.off_b1 - net.off_w1);
-        for (int i = threadIdx.x; i < H * SP; i += blockDim.x)
-            w1s[i / SP][i % SP] = W1c[w1r_index(i / SP, i % SP, KS1)];
-        for (int i = threadIdx.x; i < H; i += blockDim.x) b1s[i] = B1c[i];
-    }
-    const float gm = __uint_as_float(*w.g2max);
-    const int gex = gm > 0.f ? __builtin_amdgcn_frexp_expf(gm) : 0;
-    const float sg = __builtin_amdgcn_ldexpf(1.f, 14 - gex);
-    const float un2 = __builtin_amdgcn_ldexpf(1.f, gex - 14) / kX3HScale;
-    const float unb = __builtin_amdgcn_ldexpf(1.f, gex - 14);
-    half8 ones;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ones[i] = (_Float16)1.0f;
-    floatx16 acc[8], accb;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) accb[i] = 0.f;
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[nt][i] = 0.f;
-    const int64_t ntiles = (w.rows + kUpdRows - 1) / kUpdRows;
-    auto load_s = [&](int64_t tile, float (&sv)[SV]) {
-#pragma unroll
-        for (int u = 0; u < SV; ++u) {
-            const int i = threadIdx.x + NT * u, rr = i / SP, k = i % SP;
-            const int64_t row = tile * kUpdRows + rr;
-            sv[u] = (tile < ntiles && i < kUpdRows * SP && row < w.rows && k < S)
-                        ? w.s[(w.index ? w.index[row] : row) * S + k] : 0.f;
-        }
-    };
-    auto store_s = [&](int buf, const float (&sv)[SV]) {
-#pragma unroll
-        for (int u = 0; u < SV; ++u) {
-            const int i = threadIdx.x + NT * u;
-            if (i < kUpdRows * SP) srow[buf][i / SP][i % SP] = sv[u];
-        }
-    };
-    // fragment pair P = (rh, nt): layer 1 of rows 32 rh .. 32 rh + 31 x neurons 32 nt .. on
-    // 32x32x2 f32 MFMAs (the FD's small_r W1 / b1: the exp2 argument), tanh, the f16 split; its
-    // C registers 0-7 are K-step 2 rh, 8-15 K-step 2 rh + 1
-    auto build_pair = [&](int buf, int P) {
-        const int rh = P >> 3, nt = P & 7;
-        const float b1 = b1s[32 * nt + r];
-        floatx16 c;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) c[i] = b1;
-#pragma unroll
-        for (int kk = 0; kk < 2 * KS1; ++kk)
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(srow[buf][32 * rh + r][2 * kk + hh],
-                                                      w1s[32 * nt + r][2 * kk + hh], c, 0, 0, 0);
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            float x[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-                x[q] = __builtin_fmaf(-2.0f * kX3HScale,
-                                      __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c[8 * half + q])),
-                                      kX3HScale);
-            half8 h8, l8;
-            split8(x, h8, l8);
-            const int F = (2 * rh + half) * 8 + nt;
-            *reinterpret_cast<half8 *>(&hfrag[buf][((F * 2 + 0) * 64 + lane) * 8]) = h8;
-            *reinterpret_cast<half8 *>(&hfrag[buf][((F * 2 + 1) * 64 + lane) * 8]) = l8;
-        }
-    };
-    const float *g2base = w.g2t;
-    asm volatile("" : "+s"(g2base));
-    // A operands of K-step ks: g2(j = 32 wv + r, rows 16 ks + 4 hh + {0..3} and + 8)
-    auto load_g2 = [&](int64_t tile, int ks, floatx4 (&gv)[2]) {
-        const int64_t t = tile < ntiles ? tile : ntiles - 1;
-        const gptr<float> src = as_global(g2base + t * kUpdTileFloats + (32 * wv + r) * kUpdRows +
-                                          16 * ks + 4 * hh);
-        gv[0] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src);
-        gv[1] = *reinterpret_cast<const __attribute__((address_space(1))) floatx4 *>(src + 8);
-    };
-    auto frag = [&](int buf, int F, int hl) {
-        return *reinterpret_cast<const half8 *>(&hfrag[buf][((F * 2 + hl) * 64 + lane) * 8]);
-    };
-    int64_t tile = blockIdx.x;
-    {
-        float sv[SV];
-        load_s(tile, sv);
-        store_s(0, sv);
-    }
-    lds_barrier();
-#pragma unroll 1
-    for (int u = 0; u < 2; ++u) build_pair(0, 2 * wv + u);
-    float svn[SV];
-    load_s(tile + gridDim.x, svn);
-    floatx4 gv[2];
-    load_g2(tile, 0, gv);
-    lds_barrier();
-    for (int i = 0; tile < ntiles; tile += gridDim.x, ++i) {
-        const int cur = i & 1, nxt = cur ^ 1;
-        store_s(nxt, svn);
-        lds_barrier();
-        load_s(tile + 2 * (int64_t)gridDim.x, svn);
-        // two column tiles at a time, their MFMAs interleaved (a 32x32x16 result is not ready
-        // for the next MFMA on the same accumulator for many cycles); the next pair's fragments
-        // are read one step ahead
-        half8 bh0 = frag(cur, 0, 0), bl0 = frag(cur, 0, 1), bh1 = frag(cur, 1, 0), bl1 = frag(cur, 1, 1);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            half8 ah, al;
-            {
-                float x[8];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    x[u] = gv[0][u] * sg;
-                    x[u + 4] = gv[1][u] * sg;
-                }
-                split8(x, ah, al);
-            }
-            if (ks < 3) load_g2(tile, ks + 1, gv);
-            else load_g2(tile + gridDim.x, 0, gv);
-#pragma unroll
-            for (int np = 0; np < 4; ++np) {
-                const int F = ks * 8 + 2 * np;  // this pair: F, F + 1
-                half8 nh0, nl0, nh1, nl1;
-                if (F + 2 < 32) {
-                    nh0 = frag(cur, F + 2, 0);
-                    nl0 = frag(cur, F + 2, 1);
-                    nh1 = frag(cur, F + 3, 0);
-                    nl1 = frag(cur, F + 3, 1);
-                }
-                floatx16 v0 = acc[2 * np], v1 = acc[2 * np + 1];
-                v0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh0, v0, 0, 0, 0);
-                v1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh1, v1, 0, 0, 0);
-                v0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl0, v0, 0, 0, 0);
-                v1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl1, v1, 0, 0, 0);
-                v0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh0, v0, 0, 0, 0);
-                v1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh1, v1, 0, 0, 0);
-                acc[2 * np] = v0;
-                acc[2 * np + 1] = v1;
-                if (F == 14 || F == 30) build_pair(nxt, 2 * wv + (F == 30));  // next tile's pairs
-                if (F + 2 < 32) {
-                    bh0 = nh0; bl0 = nl0; bh1 = nh1; bl1 = nl1;
-                }
-            }
-            accb = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ones, accb, 0, 0, 0);
-            accb = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ones, accb, 0, 0, 0);
-        }
-        lds_barrier();
-    }
-    // C layout: lane (r, hh), register q: row (q & 3) + 8 (q >> 2) + 4 hh, column r
-    float *out = w.part + (size_t)blockIdx.x * (H * H + H);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int j = 32 * wv + (q & 3) + 8 * (q >> 2) + 4 * hh;
-#pragma unroll
-        for (int nt = 0; nt < 8; ++nt) out[j * H + 32 * nt + r] = acc[nt][q] * un2;
-        if (r == 0) out[H * H + j] = accb[q] * unb;
-    }
 }
 
 // grad (torch order W1 b1 W2 b2 W3 b3) = sum over blocks / waves of the partials, in order
@@ -1110,10 +851,6 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
     }
 }
 
-static int g_fd_mode = 0;      // rlp_set_fd_mode
-static int g_wgrad_waves = 8;  // rlp_set_wgrad_waves
-static int g_update_prio = 0;  // rlp_set_update_prio
-
 static int ppo2_grid() {  // CUs of the device (cached: device properties are slow)
     static int cus = 0;
     if (cus == 0) {
@@ -1164,12 +901,8 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     hipStream_t st = as_stream(stream);
     const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
     const int grid = (int)(tiles < ppo2_grid() ? tiles : ppo2_grid());         // wgrad: 1 per CU
-    // FD block shape (rlp_set_fd_mode): 0 one 8-wave block per CU (default), 1 two 4-wave blocks
-    // per CU, 2 one 4-wave block per CU (the other net's FD kernel co-resident from another stream)
-    const int fdw = g_fd_mode == 0 ? kFdWaves : 4;
-    const int64_t fd_tiles = (rows + 16 * fdw - 1) / (16 * fdw);
-    const int fd_per_cu = g_fd_mode == 2 ? 1 : 8 / fdw;
-    const int gfd = (int)(fd_tiles < fd_per_cu * ppo2_grid() ? fd_tiles : fd_per_cu * ppo2_grid());
+    const int64_t fd_tiles = (rows + kFdRows - 1) / kFdRows;  // FD: one 8-wave block per CU
+    const int gfd = (int)(fd_tiles < ppo2_grid() ? fd_tiles : ppo2_grid());
     const int gfull = ppo2_grid();
     Ppo2Args g{};
     g.packed = packed; g.net = net;
@@ -1193,12 +926,7 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     if (hipMemsetAsync(g.g2max, 0, sizeof(unsigned), st) != hipSuccess)
         return fail(RLP_EINVAL, "rlp_ppo2_grad: memset");
     g.loss_sum = loss_sum;
-    g.prio = g_update_prio;
-#define RLP_FD(KS1, A_, L)                                                                      \
-    do {                                                                                        \
-        if (fdw == 8) ppo2_fd_kernel<KS1, A_, L, 8><<<gfd, 512, 0, st>>>(g);                    \
-        else ppo2_fd_kernel<KS1, A_, L, 4><<<gfd, 256, 0, st>>>(g);                             \
-    } while (0)
+#define RLP_FD(KS1, A_, L) ppo2_fd_kernel<KS1, A_, L><<<gfd, 64 * kFdWaves, 0, st>>>(g)
     if (actor) {
         if (net.ks1 == 1) {
             if (net.A == 1) RLP_FD(1, 1, 0); else if (net.A == 2) RLP_FD(1, 2, 0); else if (net.A == 3) RLP_FD(1, 3, 0); else RLP_FD(1, 4, 0);
@@ -1212,49 +940,17 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (fd)");
     WArgs w{};
     w.packed = packed; w.net = net; w.s = s; w.index = index; w.rows = rows;
-    w.g2t = g.g2t; w.g2max = g.g2max; w.part = partw; w.prio = g_update_prio;
-    if (g_wgrad_waves == 32) {  // the 32x32x16 variant (rlp_set_wgrad_waves(32))
-        if (net.ks1 == 1) ppo2_wgrad32_kernel<1><<<grid, 512, 0, st>>>(w);
-        else ppo2_wgrad32_kernel<2><<<grid, 512, 0, st>>>(w);
-    } else if (g_wgrad_waves == 4) {
-        if (net.ks1 == 1) ppo2_wgrad_kernel<1, 4><<<grid, 256, 0, st>>>(w);
-        else ppo2_wgrad_kernel<2, 4><<<grid, 256, 0, st>>>(w);
-    } else {
-        if (net.ks1 == 1) ppo2_wgrad_kernel<1, 8><<<grid, 512, 0, st>>>(w);
-        else ppo2_wgrad_kernel<2, 8><<<grid, 512, 0, st>>>(w);
-    }
+    w.g2t = g.g2t; w.g2max = g.g2max; w.part = partw;
+    if (net.ks1 == 1) ppo2_wgrad_kernel<1><<<grid, 64 * kWgWaves, 0, st>>>(w);
+    else ppo2_wgrad_kernel<2><<<grid, 64 * kWgWaves, 0, st>>>(w);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (wgrad)");
     const int64_t total = (int64_t)net.H * net.S + net.H + (int64_t)net.H * net.H + net.H +
                           (int64_t)net.A * net.H + net.A;
     ppo2_reduce_kernel<<<(int)((total + 63) / 64), 64 * kRedSplit, 0, st>>>(net, partw, grid,
-                                                                          g.part3, gfd * fdw, grad);
+                                                                          g.part3, gfd * kFdWaves, grad);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (reduce)");
     return RLP_OK;
 }
-
-int rlp_set_fd_mode(int mode) {
-    if (mode < 0 || mode > 2) return fail(RLP_EINVAL, "rlp_set_fd_mode: %d", mode);
-    g_fd_mode = mode;
-    return RLP_OK;
-}
-
-int rlp_get_fd_mode(void) { return g_fd_mode; }
-
-int rlp_set_update_prio(int mode) {
-    if (mode < 0 || mode > 1) return fail(RLP_EINVAL, "rlp_set_update_prio: %d", mode);
-    g_update_prio = mode;
-    return RLP_OK;
-}
-
-int rlp_get_update_prio(void) { return g_update_prio; }
-
-int rlp_set_wgrad_waves(int waves) {
-    if (waves != 4 && waves != 8 && waves != 32) return fail(RLP_EINVAL, "rlp_set_wgrad_waves: %d", waves);
-    g_wgrad_waves = waves;
-    return RLP_OK;
-}
-
-int rlp_get_wgrad_waves(void) { return g_wgrad_waves; }
 
 int rlp_grad_sqnorm(const float *grad, int64_t n, double *out, rlp_stream_t stream) {
     RLP_REQUIRE(grad && out && n >= 0, "rlp_grad_sqnorm: bad argument");

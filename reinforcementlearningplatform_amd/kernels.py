@@ -152,15 +152,17 @@ def rollout(kind, params, state, need_reset, actor_desc, actor_packed, critic_de
 
 
 def make_rollout_cfg(T, n, seed, step0, env_id0, std, a_min, a_max, success_rule, success_flag,
-                     mlp_precision=None, physics=None, sub=None):
+                     mlp_precision=None, physics=None, sub=None, plain=False):
     """rlp_rollout_cfg. mlp_precision (RLP_MLP_FP32 | RLP_MLP_F16X3), physics (-1 auto, 0
-    register-resident, 1 shared, 2 shared 8-wave, 3 / 4 shared one-block-per-CU of 32- / 16-env
-    waves, 5 / 6 one 4-wave block of 32- / 64-env waves per CU; include/rlp.h) and sub (1 | 2 | 4)
-    select the kernel for this call only; None keeps the library-wide defaults (rlp_set_*)."""
+    register-resident, 1 shared (two 4-wave blocks per CU), 3 one 8-wave block per CU, 5 one
+    4-wave block per CU; include/rlp.h) and sub (1 | 2 | 4)
+    select the kernel for this call only; None keeps the library-wide defaults (rlp_set_*).
+    plain: the nets are passed in the plain parameter layout (any Linear stack; net_layout 1)."""
     cfg = _abi.RolloutCfg()
+    cfg.net_layout = 1 if plain else 0
     cfg.mlp_precision = 0 if mlp_precision is None else int(mlp_precision) + 1
-    if physics is not None and not -1 <= int(physics) <= 6:
-        raise ValueError(f"make_rollout_cfg: physics={physics} (-1 auto, 0..6)")
+    if physics is not None and int(physics) not in (-1, 0, 1, 3, 5):
+        raise ValueError(f"make_rollout_cfg: physics={physics} (-1 auto, 0, 1, 3, 5)")
     cfg.physics = 0 if physics is None else 8 if int(physics) == -1 else int(physics) + 1
     cfg.sub = 0 if sub is None else int(sub)
     cfg.T, cfg.n, cfg.seed, cfg.step0, cfg.env_id0 = T, n, seed, step0, env_id0
@@ -270,6 +272,30 @@ def ppo2_grad(desc, packed, cfg, s, a=None, a_logprob=None, adv=None, v_target=N
     check(lib().rlp_ppo2_grad(C.byref(desc), ptr(packed), C.byref(cfg), ptr(s_), ptr(a_),
                               ptr(lp_), ptr(adv_), ptr(vt_), ptr(idx_), rows, ptr(grad),
                               ptr(loss_sum), ptr(workspace), stream_ptr()), "rlp_ppo2_grad")
+    return grad
+
+
+def ppo2_dense_workspace(desc, rows, device=None):
+    n = lib().rlp_ppo2_dense_workspace_floats(C.byref(desc), int(rows))
+    check(n if n < 0 else 0, "rlp_ppo2_dense_workspace_floats")
+    return torch.empty(int(n), dtype=torch.float32, device=_dev(device))
+
+
+def ppo2_dense_grad(desc, params, cfg, s, a=None, a_logprob=None, adv=None, v_target=None,
+                    grad=None, loss_sum=None, workspace=None):
+    """rlp_ppo2_dense_grad: ppo2_grad for any tanh Linear stack, on the plain parameter layout;
+    rows are the rows of s (contiguous; gather a mini-batch first)."""
+    rows = int(s.shape[0])
+    dev = s.device
+    grad = grad if grad is not None else torch.empty(desc.param_count(), dtype=torch.float32,
+                                                     device=dev)
+    if workspace is None:
+        workspace = ppo2_dense_workspace(desc, rows, dev)
+    s_, a_, lp_, adv_, vt_ = (None if t is None else t.contiguous()
+                              for t in (s, a, a_logprob, adv, v_target))
+    check(lib().rlp_ppo2_dense_grad(C.byref(desc), ptr(params), C.byref(cfg), ptr(s_), ptr(a_),
+                                    ptr(lp_), ptr(adv_), ptr(vt_), rows, ptr(grad), ptr(loss_sum),
+                                    ptr(workspace), stream_ptr()), "rlp_ppo2_dense_grad")
     return grad
 
 

@@ -7,7 +7,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); TAG=${TAG:-lab}; OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 export TMPDIR=/tmp
-BASE="--no-cpu-baseline --ddpg 0 --sac 0 --oa 0 --fp32-leg 0 --hbm 0 --uav 0 --e2e 0 --e2e-k30 0"
+BASE="--no-cpu-baseline --ddpg 0 --sac 0 --oa 0 --fp32-leg 0 --hbm 0 --uav 0 --e2e 0 --e2e-k30 0 --demo-e2e 0"
 i=0
 for rep in $(seq 1 ${REPS:-1}); do
 for lib in ${LIBS:--}; do

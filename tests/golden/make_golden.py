@@ -1004,6 +1004,58 @@ def gen_ppo2_learn():
     np.savez_compressed(os.path.join(OUT, "ppo2_learn.npz"), std=np.float32(8 / 3), **out)
 
 
+def gen_ppo2_soi_learn():
+    """learn() (K = 3, full batch) with the PPO2-SecondOrderIntegration demo's nets (actor
+    4 -> 128 -> 64 -> 32 -> 2, critic 4 -> 64 -> 64 -> 1; demonstration/PPO2/
+    PPO2-4-SecondOrderIntegration/train.py:37-125, ppo_msg :146-160 with K_epochs 3) on a 500-row
+    buffer (the demo's buffer_size = time_max / dt * 2): the reference's first-step p.grad,
+    the GAE / v_target / normalised advantages learn() computed, and the after-weights."""
+    g = np.random.default_rng(20266)
+    with quiet():
+        drv_soi = load("demonstration/PPO2/PPO2-4-SecondOrderIntegration/train.py", "ref_ppo2_soi_train")
+    torch.manual_seed(31)
+    lo, hi = np.array([-3., -3.]), np.array([3., 3.])
+    actor = drv_soi.PPOActor_Gaussian(state_dim=4, action_dim=2, a_min=lo, a_max=hi, init_std=1.0,
+                                      use_orthogonal_init=True)
+    critic = drv_soi.PPOCritic(state_dim=4, use_orthogonal_init=True)
+    with torch.no_grad():   # a last layer large enough for a non-trivial tanh'(z)
+        torch.nn.init.orthogonal_(actor.mean_layer.weight, gain=1.0)
+    B = 500
+    ppo_msg = {'gamma': 0.99, 'K_epochs': 3, 'eps_clip': 0.2, 'buffer_size': B, 'state_dim': 4,
+               'action_dim': 2, 'a_lr': 3e-4, 'c_lr': 1e-3, 'set_adam_eps': True, 'lmd': 0.95,
+               'use_adv_norm': True, 'mini_batch_size': 64, 'entropy_coef': 0.01,
+               'use_grad_clip': False, 'use_lr_decay': False, 'max_train_steps': int(5e6),
+               'using_mini_batch': False}
+    env_msg = {'state_dim': 4, 'action_dim': 2, 'name': 'SecondOrderIntegration',
+               'action_range': [[-3., 3.], [-3., 3.]]}
+    agent = ppo2_mod.Proximal_Policy_Optimization2(env_msg, ppo_msg, actor=actor, critic=critic)
+    s, a, lp, r, s2, done, success = _learn_buffer(g, B, 4, actor, 0.3)
+    for i in range(B):
+        agent.buffer.append(s=s[i], a=a[i], log_prob=lp[i], r=r[i], s_=s2[i], done=done[i],
+                            success=success[i], index=i)
+    before_a, before_c = _flat(actor), _flat(critic)
+    with torch.no_grad():
+        vs = critic(torch.tensor(s, dtype=torch.float))
+    rec, grads = {}, {}
+    _grad_tap(grads, "actor", agent.optimizer_actor, list(actor.parameters()))
+    _grad_tap(grads, "critic", agent.optimizer_critic, list(critic.parameters()))
+    real = ppo2_mod.torch
+    ppo2_mod.torch = _TorchProbe(rec)
+    try:
+        agent.learn(0, buf_num=1)
+    finally:
+        ppo2_mod.torch = real
+    adv = torch.tensor(rec["gae_list"]).view(-1, 1)
+    v_target = adv + vs
+    adv_n = (adv - adv.mean()) / (adv.std() + 1e-5)
+    np.savez_compressed(os.path.join(OUT, "ppo2_soi_learn.npz"), s=s, a=a, a_lp=lp, r=r, s_=s2,
+                        done=done, success=success, before_actor=before_a, before_critic=before_c,
+                        after_actor=_flat(actor), after_critic=_flat(critic),
+                        adv_norm=adv_n.numpy()[:, 0], v_target=v_target.numpy()[:, 0],
+                        grad_actor=grads["actor"], grad_critic=grads["critic"], std=np.float32(1.0))
+    print("ppo2_soi_learn", {k: float(np.abs(v).max()) for k, v in grads.items()})
+
+
 def gen_dppo2_learn():
     """Two consecutive Worker.learn() iterations of the DPPO2-CartPole copy (SharedAdam with the
     driver's lr / eps, k_epo = 6, use_grad_clip=True, clip 0.2), the local nets reloaded from the
@@ -1182,6 +1234,7 @@ if __name__ == "__main__":
     gen_ddpg_grad()
     gen_sac_grad()
     gen_ppo2_learn()
+    gen_ppo2_soi_learn()
     gen_dppo2_learn()
     gen_ppo2_transcript("cartpole")
     gen_ppo2_transcript("angleonly")

@@ -172,7 +172,8 @@ def _oa_env(n_envs, seed, **kw):
 def test_vec_ppo2_iterations(cls, kwargs):
     """VecPPO2 iterations (rlp_rollout + advantages + K epochs); the lidar env's 41-input nets
     (the PPO2-UGVForwardObstacleAvoidance demo shape) roll out through rlp_rollout's per-step
-    kernel sequence and update on the torch learner (learner='auto')."""
+    kernel sequence and update on librlp's dense-GEMM gradient (learner='auto' picks the native
+    learner for every Linear/Tanh stack)."""
     env = cls(n_envs=4096, seed=5, **kwargs)
     ar = np.array(env.action_range)
     actor = PPOActor_Gaussian(env.state_dim, env.action_dim, ar[:, 0], ar[:, 1],
@@ -180,8 +181,8 @@ def test_vec_ppo2_iterations(cls, kwargs):
     critic = PPOCritic(env.state_dim)
     agent = VecPPO2(env, actor, critic, {'K_epochs': 2, 'using_mini_batch': True,
                                          'mini_batch_size': 32768}, T=32)
-    expect = "torch" if env.state_dim > 8 else "native"
-    assert type(agent.learner).__name__ == ("PPO2Learner" if expect == "torch" else "NativePPO2Learner")
+    assert type(agent.learner).__name__ == "NativePPO2Learner"
+    assert agent.learner.net_a.dense == (env.state_dim > 8)
     for _ in range(3):
         out = agent.iteration()
     assert torch.isfinite(out["actor_loss"]) and torch.isfinite(out["critic_loss"])

@@ -57,8 +57,8 @@ def f32_ulps(a, b):
 
 def policy_bounds(ad, ap, obs, a_ref, lo, hi, std):
     """Per-row absolute bounds for action and log-prob in teacher-forced comparisons, derived the
-    way the V(s) bound is: the mean is tanh(z3) * gain + off with z3 = sum_j w3_j h2_j + b3, a
-    256-term sum whose f32 evaluations (the reference's, ours, the f16x3 split's 3 * 2^-22 per
+    way the V(s) bound is: the mean is tanh(z3) * gain + off with z3 = sum_j w3_j h2_j + b3 (the
+    last layer of any tanh stack), a 256-term sum whose f32 evaluations (the reference's, ours, the f16x3 split's 3 * 2^-22 per
     product) differ by ~1e-6 of the TERMS' magnitude S = sum_j |w3_j h2_j| + |b3| (float64 h2 on
     the row's observation), so |d mean| <= gain * sech^2(z3) * 1e-6 * S, plus f32 rounding of the
     output (1e-7 * gain). d logp / d mean = (a - mean) / std^2."""
@@ -66,12 +66,12 @@ def policy_bounds(ad, ap, obs, a_ref, lo, hi, std):
     x = np.asarray(obs, np.float64).reshape(-1, ds[0])
     prm = np.asarray(ap, np.float64)
     off, h = 0, x
-    for i in range(3):
+    for i in range(ad.n_layers):
         W = prm[off:off + ds[i + 1] * ds[i]].reshape(ds[i + 1], ds[i])
         off += W.size
         b = prm[off:off + ds[i + 1]]
         off += b.size
-        if i < 2:
+        if i < ad.n_layers - 1:
             h = np.tanh(h @ W.T + b)
         else:
             z3 = h @ W.T + b

@@ -65,19 +65,8 @@ def split(flat, module):
     return out
 
 
-@pytest.fixture(params=[8, 4, 32], ids=["wgrad8", "wgrad4", "wgrad32x32"])
-def wgrad_waves(request):
-    """The weight-gradient kernel's variants (include/rlp.h rlp_set_wgrad_waves: 8- / 4-wave
-    blocks on 16x16x32 MFMAs, 32 = the 32x32x16 form)."""
-    from reinforcementlearningplatform_amd import _native
-    old = _native.lib().rlp_get_wgrad_waves()
-    assert _native.lib().rlp_set_wgrad_waves(request.param) == 0
-    yield request.param
-    _native.lib().rlp_set_wgrad_waves(old)
-
-
 @pytest.mark.parametrize("S,A,N", [(4, 1, 3037), (6, 3, 2113), (2, 2, 64), (4, 1, 1)])
-def test_ppo2_grads_vs_torch(S, A, N, wgrad_waves):
+def test_ppo2_grads_vs_torch(S, A, N):
     msg = dict(DEFAULT_PPO_MSG)
     actor, critic, s, a, lp, adv, vt = make_case(S, A, N, seed=S * 10 + A)
     ga64, gc64, al64, cl64 = torch_grads(actor, critic, s, a, lp, adv, vt, msg, torch.float64)
@@ -98,7 +87,7 @@ def test_ppo2_grads_vs_torch(S, A, N, wgrad_waves):
     assert abs(la - al64) <= 1e-5 * (abs(al64) + 1) and abs(lc - cl64) <= 1e-5 * (abs(cl64) + 1)
 
 
-def test_ppo2_grads_minibatch_index(wgrad_waves):
+def test_ppo2_grads_minibatch_index():
     msg = dict(DEFAULT_PPO_MSG)
     actor, critic, s, a, lp, adv, vt = make_case(4, 1, 2000, seed=5)
     idx = torch.randperm(2000, generator=torch.Generator().manual_seed(1))[:517]
@@ -225,23 +214,3 @@ def test_native_update_data_parallel_duplicated_batch_bit_exact():
         ref = torch.cat([nl.net_a.flat, nl.net_c.flat]).cpu().numpy()
         for r in (0, 1):
             np.testing.assert_array_equal(out[r][i], ref, err_msg=f"rank {r} {rule} clip={clip}")
-
-
-def test_wgrad_block_shapes_agree():
-    """The two wgrad block shapes sum every block's rows in the same order (per-wave output rows
-    differ, each output element's K sequence does not): identical gradients."""
-    from reinforcementlearningplatform_amd import _native
-    actor, critic, s, a, lp, adv, vt = make_case(4, 1, 20000, seed=77)
-    dev = lambda t: t.cuda().contiguous()
-    out = []
-    old = _native.lib().rlp_get_wgrad_waves()
-    try:
-        for wv in (8, 4):
-            _native.lib().rlp_set_wgrad_waves(wv)
-            nl = NativePPO2Learner(copy.deepcopy(actor), copy.deepcopy(critic), dict(DEFAULT_PPO_MSG),
-                                   device="cuda")
-            nl.grads(dev(s), dev(a), dev(lp), dev(adv), dev(vt))
-            out.append(torch.cat([nl.net_a.grad, nl.net_c.grad]).cpu())
-    finally:
-        _native.lib().rlp_set_wgrad_waves(old)
-    assert torch.equal(out[0], out[1])
