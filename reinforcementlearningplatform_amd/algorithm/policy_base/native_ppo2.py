@@ -152,7 +152,7 @@ class NativePPO2Learner:
         self.net_c.flat.copy_(flat[na:])
 
     def _actor_cfg(self):
-        A = self.net_a.desc.dims[3]
+        A = self.net_a.desc.dims[self.net_a.desc.n_layers]
         std = np.broadcast_to(torch.as_tensor(self.actor.std, dtype=torch.float32).reshape(-1)
                               .cpu().numpy(), (A,))
         lo = torch.as_tensor(self.actor.a_min, dtype=torch.float32).reshape(-1).cpu().numpy()

@@ -10,11 +10,12 @@
 // each wave a 32 x 32 quarter (2 x 2 MFMA tiles), the reduction staged through LDS 16 deep. The
 // operands are strided views (row / column strides, an optional column split for torch.cat and
 // an all-ones column), so transposes and concatenations are never materialised. Weight
-// gradients split the batch over gridDim.z into partials summed in fixed order by a second
-// kernel (deterministic, no atomics). Fused epilogues: + bias, relu, gain * tanh + off (keeping
-// tanh for the backward), relu' mask, (. * gain) * (1 - t^2). Adam (torch.optim.Adam's
-// non-capturable arithmetic, step count read from device memory so a captured HIP graph can be
-// replayed) and the soft target update are elementwise kernels.
+// gradients split the batch over gridDim.z into partials summed in fixed order (deterministic,
+// no atomics) by the optimizer kernel itself: per net one launch sums every layer's partials,
+// takes the Adam step (torch.optim.Adam's non-capturable arithmetic, step count read from device
+// memory so a captured HIP graph can be replayed) and the soft target update. Fused epilogues:
+// + bias, relu, gain * tanh + off (keeping tanh for the backward), relu' mask,
+// (. * gain) * (1 - t^2).
 #include "rlp_common.hpp"
 
 namespace rlp {
@@ -351,11 +352,53 @@ __global__ void __launch_bounds__(256) adam_dev_kernel(float *__restrict__ p, co
     }
 }
 
-// target = target * keep + param * take (DDPG.py:116-118: tp * (1 - tau) + p * tau, fp32)
-__global__ void __launch_bounds__(256) soft_update_kernel(float *__restrict__ tp, const float *__restrict__ p,
-                                                          int64_t n, float keep, float take) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-        tp[i] = tp[i] * keep + p[i] * take;
+// The weight-gradient partials of the layers of one parameter buffer ([z][out][in + 1] each, the
+// bias as the last column), left unreduced by the backward pass for adam_reduce_kernel
+constexpr int kMaxParts = 8;  // a net's layers (SAC: both critic chains, the actor's two heads)
+struct NetParts {
+    const float *part[kMaxParts];
+    int64_t off[kMaxParts];  // the layer's W in the flat parameters (b follows)
+    int z[kMaxParts], in[kMaxParts], out[kMaxParts];
+    int n;
+};
+
+// One launch for what wgrad_reduce (per layer), Adam and the soft target update did in five: the
+// gradient element summed over its layer's partials in split order (wgrad_reduce's order, so the
+// same bits), stored to g, the Adam step on it, and — when tp is set — the soft target update
+// with the new parameter, tp (1 - tau) + p tau (DDPG.py:113-118, Soft_Actor_Critic.py:126-127;
+// the target is not read again in the update).
+// Elements outside every layer (a module's unused parameters) keep the gradient in g.
+__global__ void __launch_bounds__(256) adam_reduce_kernel(float *__restrict__ p, float *__restrict__ g,
+                                                          float *__restrict__ m, float *__restrict__ v,
+                                                          int64_t n, NetParts np, float lr, float beta1,
+                                                          float beta2, float eps, const int32_t *step,
+                                                          float *__restrict__ tp, float keep, float take) {
+    const float st = (float)*step;
+    const float bc1 = 1.f - powf(beta1, st);
+    const float bc2 = 1.f - powf(beta2, st);
+    const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        float gi = g[i];
+        for (int l = 0; l < np.n; ++l) {
+            const int64_t r = i - np.off[l], in = np.in[l], out = np.out[l];
+            if (r < 0 || r >= out * (in + 1)) continue;
+            const int64_t idx = r < in * out ? (r / in) * (in + 1) + r % in : (r - in * out) * (in + 1) + in;
+            const int64_t stride = out * (in + 1);
+            float s = 0.f;
+            for (int zz = 0; zz < np.z[l]; ++zz) s += np.part[l][zz * stride + idx];
+            gi = s;
+            g[i] = s;
+        }
+        float mi = m[i];
+        mi = mi + (1.f - beta1) * (gi - mi);
+        const float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        const float pi = p[i] + (-step_size) * (mi / denom);
+        p[i] = pi;
+        if (tp) tp[i] = tp[i] * keep + pi * take;
+    }
 }
 
 // ---- SAC (algorithm/actor_critic/Soft_Actor_Critic.py:70-129) --------------------------------
@@ -549,14 +592,6 @@ __global__ void __launch_bounds__(1024) sac_critic_loss_kernel(const float *__re
     }
 }
 
-// target = tau * p + (1 - tau) * target (:126-127)
-__global__ void __launch_bounds__(256) soft_update_sac_kernel(float *__restrict__ tp,
-                                                              const float *__restrict__ p, int64_t n,
-                                                              float tau, float keep) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-        tp[i] = tau * p[i] + keep * tp[i];
-}
-
 // ---- host side ------------------------------------------------------------------------------
 
 inline Opnd mat(const float *p, int rows, int cols, int ld) {  // row-major rows x cols
@@ -652,19 +687,40 @@ void wgrad_reduce(const Layer &L, const float *part, int z, float *gW, float *gb
     wgrad_reduce_kernel<<<(tot + 255) / 256, 256, 0, s>>>(part, z, L.out, L.in + 1, gW, gb, part, gW, gb);
 }
 
+// record a layer's partials (its own region) in np for adam_reduce_kernel
+bool parts_add(NetParts *np, const float *part, int z, int in, int out, int64_t woff) {
+    if (np->n >= kMaxParts) return false;
+    np->part[np->n] = part;
+    np->z[np->n] = z;
+    np->in[np->n] = in;
+    np->out[np->n] = out;
+    np->off[np->n] = woff;
+    ++np->n;
+    return true;
+}
+
+// the layer's partials reduced into gW / gb now, or (np) left for adam_reduce_kernel (part must
+// then be the layer's own region)
+void wgrad_finish(const Layer &L, const float *part, int z, float *gW, float *gb, NetParts *np,
+                  int64_t woff, hipStream_t s) {
+    if (!np || !parts_add(np, part, z, L.in, L.out, woff)) wgrad_reduce(L, part, z, gW, gb, s);
+}
+
 void dense_wgrad(const float *dy, const Opnd &x, const Layer &L, int B, float *part, int splits,
-                 float *gW, float *gb, hipStream_t s, int64_t ldy = -1) {
+                 float *gW, float *gb, hipStream_t s, int64_t ldy = -1, NetParts *np = nullptr,
+                 int64_t woff = 0) {
     const Prob q = wgrad_prob(dy, x, L, B, part, splits, ldy);
-    wgrad_reduce(L, part, gemm_launch(q, nullptr, s), gW, gb, s);
+    wgrad_finish(L, part, gemm_launch(q, nullptr, s), gW, gb, np, woff, s);
 }
 
 // a layer's weight gradient and its backward data pass (both read only dY) in one launch
 void dense_wgrad_bwd(const float *dy, const Opnd &x, const Layer &L, int B, float *part, int splits,
                      float *gW, float *gb, int c0, int nc, int kind, const float *mask, int64_t ldm,
-                     const float *gain, float *dx, hipStream_t s) {
+                     const float *gain, float *dx, hipStream_t s, NetParts *np = nullptr,
+                     int64_t woff = 0) {
     const Prob qw = wgrad_prob(dy, x, L, B, part, splits, -1);
     const Prob qb = bwd_data_prob(dy, L, B, c0, nc, kind, mask, ldm, gain, dx);
-    wgrad_reduce(L, part, gemm_launch(qw, &qb, s), gW, gb, s);
+    wgrad_finish(L, part, gemm_launch(qw, &qb, s), gW, gb, np, woff, s);
 }
 
 void adam_dev(float *p, const float *g, float *m, float *v, int64_t n, const rlp_adam_cfg &c,
@@ -674,10 +730,11 @@ void adam_dev(float *p, const float *g, float *m, float *v, int64_t n, const rlp
                                                               c.eps, step);
 }
 
-void soft_update(float *tp, const float *p, int64_t n, float tau, hipStream_t s) {
+void adam_reduce(float *p, float *g, float *m, float *v, int64_t n, const NetParts &np,
+                 const rlp_adam_cfg &c, const int32_t *step, float *tp, float tau, hipStream_t s) {
     const int64_t b = (n + 255) / 256;
-    soft_update_kernel<<<(int)(b < 2048 ? b : 2048), 256, 0, s>>>(tp, p, n, (float)(1.0 - (double)tau),
-                                                                 tau);
+    adam_reduce_kernel<<<(int)(b < 2048 ? b : 2048), 256, 0, s>>>(
+        p, g, m, v, n, np, c.lr, c.beta1, c.beta2, c.eps, step, tp, (float)(1.0 - (double)tau), tau);
 }
 
 bool net_ok(const rlp_dense_net &n) {
@@ -730,7 +787,14 @@ DdpgWs ddpg_ws(const rlp_ddpg_nets &n, int B) {
     w.g1 = take((int64_t)B * mw);
     w.dq = take((int64_t)B * n.actor.dims[n.actor.n_layers]);
     const int splits = (B + kWgradRows - 1) / kWgradRows;
-    w.part = take((int64_t)splits * mw * (mw + 1));
+    // every layer's weight-gradient partials at once (left for adam_reduce_kernel)
+    auto parts = [](const rlp_dense_net &d) {
+        int64_t t = 0;
+        for (int l = 0; l < d.n_layers; ++l) t += (int64_t)d.dims[l + 1] * (d.dims[l] + 1);
+        return t;
+    };
+    const int64_t pa = parts(n.actor), pc = parts(n.critic);
+    w.part = take((int64_t)splits * (pa > pc ? pa : pc));
     w.total = o;
     return w;
 }
@@ -760,20 +824,26 @@ const float *layer_out(const rlp_dense_net &n, const float *act, int B, int l) {
 // layout as params) when grad != NULL; optionally the input gradient of columns [c0, c0 + nc)
 // with the tanh-affine backward of the layer that produced them (the actor's head) into dx
 // (dy_top: dY of the last layer; g0 / g1 ping-pong for the layers below, either may be dy_top)
+// (np: every layer's partials in a region of its own, splits x out x (in + 1) floats from part
+// upwards, left for adam_reduce_kernel)
 void net_bwd(const rlp_dense_net &n, const float *params, float *grad, const Opnd &x, int B,
              const float *act, const float *dy_top, float *g0, float *g1, float *part, int splits,
-             int c0, int nc, const float *t_in, const float *gain, float *dx, hipStream_t s) {
+             int c0, int nc, const float *t_in, const float *gain, float *dx, hipStream_t s,
+             NetParts *np = nullptr) {
     const float *dy = dy_top;
     float *dn = dy_top == g0 ? g1 : g0;
+    int64_t po = 0;
     for (int l = n.n_layers - 1; l >= 0; --l) {
         const Layer L = layer_of(n, params, l);
         const Opnd xin = l == 0 ? x : mat(layer_out(n, act, B, l - 1), B, L.in, L.in);
         float *gW = grad ? grad + n.offset[l] : nullptr, *gb = grad ? gW + (int64_t)L.in * L.out : nullptr;
+        float *pl = part + po;
+        if (np) po += (int64_t)splits * L.out * (L.in + 1);
         if (l > 0) {
             const float *h = layer_out(n, act, B, l - 1);
             if (grad)
-                dense_wgrad_bwd(dy, xin, L, B, part, splits, gW, gb, 0, L.in, kEpiReluBack, h, L.in,
-                                nullptr, dn, s);
+                dense_wgrad_bwd(dy, xin, L, B, pl, splits, gW, gb, 0, L.in, kEpiReluBack, h, L.in,
+                                nullptr, dn, s, np, n.offset[l]);
             else
                 dense_bwd_data(dy, L, B, 0, L.in, kEpiReluBack, h, L.in, nullptr, dn, s);
             float *nxt = dn == g0 ? g1 : g0;
@@ -782,11 +852,12 @@ void net_bwd(const rlp_dense_net &n, const float *params, float *grad, const Opn
         } else if (dx) {
             const int kind = t_in ? kEpiTanhAffBack : kEpiNone;
             if (grad)
-                dense_wgrad_bwd(dy, xin, L, B, part, splits, gW, gb, c0, nc, kind, t_in, nc, gain, dx, s);
+                dense_wgrad_bwd(dy, xin, L, B, pl, splits, gW, gb, c0, nc, kind, t_in, nc, gain, dx, s,
+                                np, n.offset[l]);
             else
                 dense_bwd_data(dy, L, B, c0, nc, kind, t_in, nc, gain, dx, s);
         } else if (grad) {
-            dense_wgrad(dy, xin, L, B, part, splits, gW, gb, s);
+            dense_wgrad(dy, xin, L, B, pl, splits, gW, gb, s, -1, np, n.offset[l]);
         }
     }
 }
@@ -824,30 +895,42 @@ void twin_fwd(const rlp_dense_net &n1, const rlp_dense_net &n2, const float *par
 // backward of both chains from their last layers' dY (dy1 / dy2): weight gradients into grad
 // (when non-null; part1 / part2 the two problems' partials), input gradients of columns
 // [c0, c0 + nc) into dx1 / dx2 (when non-null). d[0..3]: ping-pong buffers (two per chain).
+// (np: each layer's two partial sets in regions of their own from part1 upwards — part2 unused —
+// left for adam_reduce_kernel)
 void twin_bwd(const rlp_dense_net &n1, const rlp_dense_net &n2, const float *params, float *grad,
               const Opnd &x, int B, const float *act1, const float *act2, const float *dy1,
               const float *dy2, float *const d[4], float *part1, float *part2, int splits, int c0,
-              int nc, float *dx1, float *dx2, hipStream_t s) {
+              int nc, float *dx1, float *dx2, hipStream_t s, NetParts *np = nullptr) {
     const float *y1 = dy1, *y2 = dy2;
     int pp = 0;
+    int64_t po = 0;
     for (int l = n1.n_layers - 1; l >= 0; --l) {
         const Layer L1 = layer_of(n1, params, l), L2 = layer_of(n2, params, l);
         const Opnd x1 = l == 0 ? x : mat(layer_out(n1, act1, B, l - 1), B, L1.in, L1.in);
         const Opnd x2 = l == 0 ? x : mat(layer_out(n2, act2, B, l - 1), B, L2.in, L2.in);
         if (grad) {
+            const bool keep = np && np->n + 2 <= kMaxParts;
+            const int64_t region = (int64_t)splits * L1.out * (L1.in + 1);
+            float *p1 = keep ? part1 + po : part1, *p2 = keep ? part1 + po + region : part2;
+            if (keep) po += 2 * region;
             Epi e1{}, e2{};
-            e1.y = part1; e1.kind = kEpiPartial; e1.M = L1.out; e1.N = L1.in + 1;
+            e1.y = p1; e1.kind = kEpiPartial; e1.M = L1.out; e1.N = L1.in + 1;
             e2 = e1;
-            e2.y = part2;
+            e2.y = p2;
             Opnd xo1 = x1, xo2 = x2;
             xo1.cols = xo2.cols = L1.in + 1;
             xo1.ones = xo2.ones = L1.in;
             const Opnd t1 = transposed(y1, L1.out, B, L1.out), t2 = transposed(y2, L2.out, B, L2.out);
             const int z = gemm_impl(t1, xo1, e1, &t2, &xo2, &e2, L1.out, L1.in + 1, B, splits, s);
-            const int tot = L1.out * (L1.in + 1);
-            wgrad_reduce_kernel<<<dim3((tot + 255) / 256, 2), 256, 0, s>>>(
-                part1, z, L1.out, L1.in + 1, grad + n1.offset[l], grad + n1.offset[l] + (int64_t)L1.in * L1.out,
-                part2, grad + n2.offset[l], grad + n2.offset[l] + (int64_t)L2.in * L2.out);
+            if (keep) {
+                parts_add(np, p1, z, L1.in, L1.out, n1.offset[l]);
+                parts_add(np, p2, z, L2.in, L2.out, n2.offset[l]);
+            } else {
+                const int tot = L1.out * (L1.in + 1);
+                wgrad_reduce_kernel<<<dim3((tot + 255) / 256, 2), 256, 0, s>>>(
+                    p1, z, L1.out, L1.in + 1, grad + n1.offset[l], grad + n1.offset[l] + (int64_t)L1.in * L1.out,
+                    p2, grad + n2.offset[l], grad + n2.offset[l] + (int64_t)L2.in * L2.out);
+            }
         }
         if (l > 0 || dx1) {
             const int cc = l > 0 ? 0 : c0, nn = l > 0 ? L1.in : nc;
@@ -946,10 +1029,12 @@ int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const fl
     ddpg_td_kernel<<<1, 1024, 0, st>>>(r, end, layer_out(n.target_critic, tc, B, Lc - 1),
                                        layer_out(n.critic, c, B, Lc - 1), B, cfg->gamma, g0, losses,
                                        n.steps);
+    NetParts cp{};
     net_bwd(n.critic, n.critic.params, n.critic_grad, sa, B, c, g0, g0, g1, part, splits, 0, 0, nullptr,
-            nullptr, nullptr, st);
-    adam_dev(n.critic.params, n.critic_grad, n.critic_m, n.critic_v, n.critic.n_params, cfg->critic_adam,
-             n.steps + 1, st);
+            nullptr, nullptr, st, &cp);
+    // critic Adam + its soft target update (DDPG.py:113-115; the target critic is not read again)
+    adam_reduce(n.critic.params, n.critic_grad, n.critic_m, n.critic_v, n.critic.n_params, cp,
+                cfg->critic_adam, n.steps + 1, n.target_critic.params, cfg->critic_tau, st);
     // actor: a = mu(s), Q(s, a) with the updated critic (no critic gradients), -mean(Q) backward
     net_fwd(n.actor, n.actor.params, mat(s, B, S, S), B, pa, true, n.gain, n.off, pa_t, st);
     const float *a_pi = layer_out(n.actor, pa, B, La - 1);
@@ -960,27 +1045,30 @@ int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const fl
             dq, st);
     // dq now holds dL/dz of the actor's head ([B][A]); back through the actor
     const Opnd s_in = mat(s, B, S, S);
+    NetParts ap{};
     {
         float *dy = dq, *d0 = g0, *d1 = g1;
+        int64_t po = 0;
         for (int l = La - 1; l >= 0; --l) {
             const Layer L = layer_of(n.actor, n.actor.params, l);
             const Opnd xin = l == 0 ? s_in : mat(layer_out(n.actor, pa, B, l - 1), B, L.in, L.in);
             float *gW = n.actor_grad + n.actor.offset[l], *gb = gW + (int64_t)L.in * L.out;
+            float *pl = part + po;
+            po += (int64_t)splits * L.out * (L.in + 1);
             if (l > 0) {
-                dense_wgrad_bwd(dy, xin, L, B, part, splits, gW, gb, 0, L.in, kEpiReluBack,
-                                layer_out(n.actor, pa, B, l - 1), L.in, nullptr, d0, st);
+                dense_wgrad_bwd(dy, xin, L, B, pl, splits, gW, gb, 0, L.in, kEpiReluBack,
+                                layer_out(n.actor, pa, B, l - 1), L.in, nullptr, d0, st, &ap,
+                                n.actor.offset[l]);
                 dy = d0;
                 float *tmp = d0; d0 = d1; d1 = tmp;
             } else {
-                dense_wgrad(dy, xin, L, B, part, splits, gW, gb, st);
+                dense_wgrad(dy, xin, L, B, pl, splits, gW, gb, st, -1, &ap, n.actor.offset[l]);
             }
         }
     }
-    adam_dev(n.actor.params, n.actor_grad, n.actor_m, n.actor_v, n.actor.n_params, cfg->actor_adam,
-             n.steps, st);
-    // soft target updates (critic first, DDPG.py:113-118)
-    soft_update(n.target_critic.params, n.critic.params, n.critic.n_params, cfg->critic_tau, st);
-    soft_update(n.target_actor.params, n.actor.params, n.actor.n_params, cfg->actor_tau, st);
+    // actor Adam + its soft target update (DDPG.py:116-118)
+    adam_reduce(n.actor.params, n.actor_grad, n.actor_m, n.actor_v, n.actor.n_params, ap,
+                cfg->actor_adam, n.steps, n.target_actor.params, cfg->actor_tau, st);
     RLP_CHECK_LAUNCH("rlp_ddpg_update");
     return RLP_OK;
 }
@@ -992,8 +1080,13 @@ namespace rlp {
 
 struct SacWs {
     int64_t tn_act, tn_z, tn_a, tn_lp, tq1, tq2, ta, tz, ta_a, ta_lp, save, p1, p2, c1, c2, y, g1,
-        g2, da1, da2, gz, d0, d1, d2, d3, part, part2, total;
+        g2, da1, da2, gz, d0, d1, d2, d3, part, part2, apart, total;
 };
+int64_t layer_parts(const rlp_dense_net &d) {  // sum over layers of out x (in + 1)
+    int64_t t = 0;
+    for (int l = 0; l < d.n_layers; ++l) t += (int64_t)d.dims[l + 1] * (d.dims[l] + 1);
+    return t;
+}
 SacWs sac_ws(const rlp_sac_nets &n, int B) {
     SacWs w{};
     int64_t o = 0;
@@ -1014,8 +1107,13 @@ SacWs sac_ws(const rlp_sac_nets &n, int B) {
     w.d0 = take((int64_t)B * mw); w.d1 = take((int64_t)B * mw);
     w.d2 = take((int64_t)B * mw); w.d3 = take((int64_t)B * mw);
     const int splits = (B + kWgradRows - 1) / kWgradRows;
-    w.part = take((int64_t)splits * mw * (mw + 1));
-    w.part2 = take((int64_t)splits * mw * (mw + 1));
+    // part: the critic chains' per-layer partial regions (left for adam_reduce_kernel); apart: the
+    // actor's (both heads, then the trunk)
+    const int64_t pq = layer_parts(n.q1) + layer_parts(n.q2), one = (int64_t)mw * (mw + 1);
+    const int H = n.actor.dims[n.actor.n_layers];
+    w.part = take((int64_t)splits * (pq > one ? pq : one));
+    w.part2 = take((int64_t)splits * one);
+    w.apart = take((int64_t)splits * (layer_parts(n.actor) + 2 * (int64_t)A * (H + 1)));
     w.total = o;
     return w;
 }
@@ -1152,7 +1250,8 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
     case 3: sac_head_back_kernel<3><<<g, 256, 0, st>>>(W(w.save), W(w.da1), W(w.da2), B, n.gain, n.log_alpha, ad, cfg->alpha, W(w.gz)); break;
     default: sac_head_back_kernel<4><<<g, 256, 0, st>>>(W(w.save), W(w.da1), W(w.da2), B, n.gain, n.log_alpha, ad, cfg->alpha, W(w.gz)); break;
     }
-    // actor backward: heads' weight gradients, then the trunk
+    // actor backward: heads' weight gradients, then the trunk (partials left for the actor's Adam)
+    NetParts ap{};
     {
         const int Lt = n.actor.n_layers;
         float *P = n.actor.params, *G = n.actor_grad;
@@ -1160,15 +1259,16 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
         const Opnd hx = mat(h_last, B, H, H);
         const Layer Lm{P + n.mean_offset, P + n.mean_offset + (int64_t)A * H, H, A};
         const Layer Ll{P + n.log_std_offset, P + n.log_std_offset + (int64_t)A * H, H, A};
-        {  // both heads' weight gradients in one launch and one two-problem reduce
-            const Prob qm = wgrad_prob(W(w.gz), hx, Lm, B, W(w.part), splits, 2 * A);
-            const Prob ql = wgrad_prob(W(w.gz) + A, hx, Ll, B, W(w.part2), splits, 2 * A);
+        float *apart = W(w.apart);
+        const int64_t hreg = (int64_t)splits * A * (H + 1);
+        {  // both heads' weight gradients in one launch, partials left for the actor's Adam
+            const Prob qm = wgrad_prob(W(w.gz), hx, Lm, B, apart, splits, 2 * A);
+            const Prob ql = wgrad_prob(W(w.gz) + A, hx, Ll, B, apart + hreg, splits, 2 * A);
             const int z = gemm_launch(qm, &ql, st);
-            const int tot = A * (H + 1);
-            wgrad_reduce_kernel<<<dim3((tot + 255) / 256, 2), 256, 0, st>>>(
-                W(w.part), z, A, H + 1, G + n.mean_offset, G + n.mean_offset + (int64_t)A * H,
-                W(w.part2), G + n.log_std_offset, G + n.log_std_offset + (int64_t)A * H);
+            parts_add(&ap, apart, z, H, A, n.mean_offset);
+            parts_add(&ap, apart + hreg, z, H, A, n.log_std_offset);
         }
+        int64_t po = 2 * hreg;
         // dh = (gz [Wm; Wl]) * relu'(h)
         Epi e{};
         e.y = W(w.d0); e.ldy = H; e.kind = kEpiReluBack; e.M = B; e.N = H; e.mask = h_last; e.ldm = H;
@@ -1179,12 +1279,15 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
             const Layer L = layer_of(n.actor, P, l);
             const Opnd xin = l == 0 ? mat(s, B, S, S) : mat(layer_out(n.actor, W(w.ta), B, l - 1), B, L.in, L.in);
             float *gW = G + n.actor.offset[l], *gb = gW + (int64_t)L.in * L.out;
+            float *pl = apart + po;
+            po += (int64_t)splits * L.out * (L.in + 1);
             if (l > 0) {
-                dense_wgrad_bwd(dy, xin, L, B, W(w.part), splits, gW, gb, 0, L.in, kEpiReluBack,
-                                layer_out(n.actor, W(w.ta), B, l - 1), L.in, nullptr, dn, st);
+                dense_wgrad_bwd(dy, xin, L, B, pl, splits, gW, gb, 0, L.in, kEpiReluBack,
+                                layer_out(n.actor, W(w.ta), B, l - 1), L.in, nullptr, dn, st, &ap,
+                                n.actor.offset[l]);
                 float *tmp = dy; dy = dn; dn = tmp;
             } else {
-                dense_wgrad(dy, xin, L, B, W(w.part), splits, gW, gb, st);
+                dense_wgrad(dy, xin, L, B, pl, splits, gW, gb, st, -1, &ap, n.actor.offset[l]);
             }
         }
     }
@@ -1199,26 +1302,24 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
     sac_critic_loss_kernel<<<1, 1024, 0, st>>>(layer_out(n.q1, W(w.c1), B, Lq1 - 1),
                                                layer_out(n.q2, W(w.c2), B, Lq2 - 1), W(w.y), B,
                                                W(w.g1), W(w.g2), losses);
+    NetParts cp{};
     if (twin) {
         twin_bwd(n.q1, n.q2, n.q1.params, n.critic_grad, bx, B, W(w.c1), W(w.c2), W(w.g1), W(w.g2), dd,
-                 W(w.part), W(w.part2), splits, 0, 0, nullptr, nullptr, st);
+                 W(w.part), W(w.part2), splits, 0, 0, nullptr, nullptr, st, &cp);
     } else {
         net_bwd(n.q1, n.q1.params, n.critic_grad, bx, B, W(w.c1), W(w.g1), W(w.d0), W(w.d1),
-                W(w.part), splits, 0, 0, nullptr, nullptr, nullptr, st);
+                W(w.part), splits, 0, 0, nullptr, nullptr, nullptr, st, &cp);
         net_bwd(n.q2, n.q2.params, n.critic_grad, bx, B, W(w.c2), W(w.g2), W(w.d0), W(w.d1),
-                W(w.part), splits, 0, 0, nullptr, nullptr, nullptr, st);
+                W(w.part) + (int64_t)splits * layer_parts(n.q1), splits, 0, 0, nullptr, nullptr,
+                nullptr, st, &cp);
     }
-    // optimizer steps (actor, critic, temperature), then the soft target update
-    adam_dev(n.actor.params, n.actor_grad, n.actor_m, n.actor_v, n.actor.n_params, cfg->actor_adam,
-             n.steps, st);
-    adam_dev(n.q1.params, n.critic_grad, n.critic_m, n.critic_v, n.q1.n_params, cfg->critic_adam,
-             n.steps + 1, st);
+    // optimizer steps (actor; critic with the soft target update, :126-127 — tau p + (1 - tau) tp
+    // is the same sum as tp (1 - tau) + p tau; temperature), each reducing its weight gradients
+    adam_reduce(n.actor.params, n.actor_grad, n.actor_m, n.actor_v, n.actor.n_params, ap,
+                cfg->actor_adam, n.steps, nullptr, 0.f, st);
+    adam_reduce(n.q1.params, n.critic_grad, n.critic_m, n.critic_v, n.q1.n_params, cp,
+                cfg->critic_adam, n.steps + 1, n.target_critic, cfg->tau, st);
     if (ad) adam_dev(n.log_alpha, n.alpha_grad, n.alpha_m, n.alpha_v, 1, cfg->alpha_adam, n.steps + 2, st);
-    {
-        const int64_t nn = n.q1.n_params, b = (nn + 255) / 256;
-        soft_update_sac_kernel<<<(int)(b < 2048 ? b : 2048), 256, 0, st>>>(
-            n.target_critic, n.q1.params, nn, cfg->tau, (float)(1.0 - (double)cfg->tau));
-    }
     RLP_CHECK_LAUNCH("rlp_sac_update");
     return RLP_OK;
 }

@@ -217,21 +217,14 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
     constexpr int H = kUpdH, SMALL = mlp_small_floats<H, KS1, A>();
     constexpr int NC = 4 * KS1 + 1;  // dW1 columns per neuron: s features | bias
     constexpr int kFdRegion = kFdRing * kX3ChunkFloats;
-    // the wave's dW1 | db1 partial [256 neurons][NCS] in LDS (NCS: the row stride that puts the
-    // two 16-lane groups of a ds_add_f32 on disjoint banks)
-    constexpr int NCS = NC == 5 ? 5 : 11;
-    static_assert(NC <= 9, "dW1 columns");
-    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + kFdWaves * 16 * 8 +
-                                                      kFdWaves * kUpdH * NCS];
+    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + kFdWaves * 16 * 8];
     float *ring = lds, *small = lds + kFdRegion;
     // the wave index as a scalar (readfirstlane): every wave-derived offset, the G2 tile and its
     // store guard become SGPR values (no per-lane 64-bit address arithmetic, no exec-masked stores)
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float *const srw = lds + kFdRegion + SMALL + wv * 128;  // [16 rows][8]
-    float *const dw1s = lds + kFdRegion + SMALL + kFdWaves * 128 + wv * kUpdH * NCS;
     const MfmaNet &net = g.net;
     mlp_small_to_lds(g.packed, net, small, true);  // small_r: W1, b1 x 2/ln 2, b2 x 2^(sw+SH)
-    for (int i = threadIdx.x & 63; i < kUpdH * NCS; i += 64) dw1s[i] = 0.f;
     __syncthreads();
 
     const int lane = threadIdx.x & 63, gq = lane >> 4, e = lane & 15;
@@ -249,6 +242,11 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
         for (int c = 0; c < 4; ++c) dW3p[a][c] = 0.f;
     }
     double lsum = 0.0;
+    float dW1p[2][2 * NC];  // [h][i]: neuron 16 (8 h + 2 gq + i / NC) + e, column i % NC
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] = 0.f;
     float g2max = 0.f;
     floatx4 dh1[16];  // dh1 -> g1 of the wave's tile
 
@@ -261,8 +259,8 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
     };
     // layer 1 of neuron tile t "neuron on lane": C[row 4 gq + q][neuron 16 t + e] (operands swapped)
     auto layer1_t = [&](int t, const float (&bo)[KS1]) {
-        const float *W1c = small_at(0);
-        const float *B1c = small_at(net.off_b1 - net.off_w1);
+        const float *W1c = small + 0;
+        const float *B1c = small + (net.off_b1 - net.off_w1);
         float w1[KS1];
 #pragma unroll
         for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[w1r_index(16 * t + e, 4 * kk + gq, KS1)];
@@ -273,40 +271,38 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
             c = __builtin_amdgcn_mfma_f32_16x16x4f32(bo[kk], w1[kk], c, 0, 0, 0);
         return c;
     };
-    // g1 / (4 x the tile's unscale) = dh1 * r (1 - r) of neuron tile t (1 - h1^2 = 4 r (1 - r),
-    // h1 = 1 - 2 r recomputed, r as in the forward's); neuron on lane: dh1[t][q] = row 4 gq + q
-    auto g1_tile = [&](int t, const float (&bo)[KS1]) {
-        const floatx4 pre = layer1_t(t, bo);
+    // dW1 | db1 += sum_rows g1 [s | 1]^T: the lane's 4 rows in registers (s rows from srw), then
+    // the 4 lane groups by a 2-stage permlane butterfly, per half of the neuron tiles
+    // (8 NC -> 2 NC values)
+    auto dw1_acc = [&](const float *srw) {
+        float sv[4][4 * KS1];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(pre[q]));
-            dh1[t][q] = dh1[t][q] * __builtin_fmaf(-r, r, r);
-        }
-    };
-    // dW1 | db1 += sum_rows g1 [s | 1]^T on the f32 MFMA instead of VALU products and lane
-    // butterflies: A[neuron][row] = the g1 registers above (K = the 4 rows of lane group gq),
-    // B[row][column] = [s | 1] x us (the tile's 4 x unscale folded into the 4 B registers instead
-    // of the 64 g1 values); four 16x16x4 steps give C[neuron 16 t + 4 gq + q][column e], columns
-    // 0 .. 4 KS1 - 1 the s features, 4 KS1 the bias, added into the wave's LDS partial (ds_add_f32:
-    // every address belongs to one lane of this wave, so the sums keep program order)
-    auto dw1_acc = [&](const float *srw, float us) {
-        float bq[4];
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float sv = srw[(4 * gq + q) * 8 + (e & 7)];
-            bq[q] = (e < 4 * KS1 ? sv : (e == 4 * KS1 ? 1.f : 0.f)) * us;
-        }
+            for (int kk = 0; kk < KS1; ++kk) {
+                const floatx4 v = *reinterpret_cast<const floatx4 *>(srw + (4 * gq + q) * 8 + 4 * kk);
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            floatx4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) c = __builtin_amdgcn_mfma_f32_16x16x4f32(dh1[t][q], bq[q], c, 0, 0, 0);
-            if (e < NC) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    __hip_atomic_fetch_add(dw1s + (16 * t + 4 * gq + q) * NCS + e, c[q], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+                for (int u = 0; u < 4; ++u) sv[q][4 * kk + u] = v[u];
             }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float v[8 * NC];
+#pragma unroll
+            for (int tt = 0; tt < 8; ++tt) {
+                const floatx4 gt = dh1[8 * h + tt];
+#pragma unroll
+                for (int f = 0; f < 4 * KS1; ++f) {
+                    float x = gt[0] * sv[0][f];
+#pragma unroll
+                    for (int q = 1; q < 4; ++q) x = __builtin_fmaf(gt[q], sv[q][f], x);
+                    v[tt * NC + f] = x;
+                }
+                v[tt * NC + 4 * KS1] = (gt[0] + gt[1]) + (gt[2] + gt[3]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4 * NC; ++i) v[i] = pair_sum_x32(v[i], v[i + 4 * NC]);
+#pragma unroll
+            for (int i = 0; i < 2 * NC; ++i) dW1p[h][i] += pair_sum_x16(v[i], v[i + 2 * NC]);
         }
     };
 
@@ -338,6 +334,21 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
             const int k = 4 * kk + gq;
             bobs[kk] = (valid && k < S) ? g.s[src * S + k] : 0.f;
             srw[e * 8 + k] = bobs[kk];  // this wave's s rows, for dW1
+        }
+        // the actor loss's row inputs, loaded now so that their latency hides under the forward
+        // GEMM (the critic's one v_target stays at its use: held across the GEMMs it spilled)
+        float in_a[A], in_lp[A], in_adv = 0.f;
+#pragma unroll
+        for (int a = 0; a < A; ++a) in_a[a] = in_lp[a] = 0.f;
+        if constexpr (LOSS == RLP_LOSS_ACTOR) {
+            if (valid) {
+                in_adv = g.adv[src];
+#pragma unroll
+                for (int a = 0; a < A; ++a) {
+                    in_a[a] = g.a[src * A + a];
+                    in_lp[a] = g.lp[src * A + a];
+                }
+            }
         }
         auto layer1 = [&](int t) {
             float w1[KS1];
@@ -394,17 +405,17 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
         float lrow = 0.f;
         if constexpr (LOSS == RLP_LOSS_ACTOR) {
             float t[A], d[A], lp_now = 0.f, lp_old = 0.f;
-            float adv = valid ? g.adv[src] : 0.f;
+            const float adv = in_adv;
 #pragma unroll
             for (int a = 0; a < A; ++a) {
                 t[a] = tanhf(z3[a]);
                 const float mean = t[a] * g.gain[a] + g.off[a];
-                const float act = valid ? g.a[src * A + a] : mean;
+                const float act = valid ? in_a[a] : mean;
                 d[a] = act - mean;
                 // Normal(mean, std).log_prob(act) (torch's expression, the division by 2 var and
                 // log(std) as launch constants)
                 lp_now += -(d[a] * d[a]) * (0.5f * g.inv_var[a]) - g.log_std[a] - 0.91893853320467274178f;
-                lp_old += valid ? g.lp[src * A + a] : 0.f;
+                lp_old += in_lp[a];
             }
             const float ratio = expf(lp_now - lp_old);
             const float lo = 1.f - g.eps_clip, hi = 1.f + g.eps_clip;
@@ -511,21 +522,35 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
             }
             split8(x, bh, bl);
         }, [](int) {});
-        // ---- g1 = dh1 * (1 - h1^2) and dW1 | db1 of this tile
+        // ---- g1 = dh1 * (1 - h1^2) and dW1 | db1 of this tile: the 16 neuron tiles' layer-1
+        // MFMAs first (their W1 / b1 reads in flight together), then the 64 independent tanh'
+        // chains — tile by tile, each tile's LDS reads, MFMA latency and transcendental chain were
+        // exposed in turn (r3x diag: g1 5.8k cycles per wave tile for ~2.5k of issue)
+        {
+            floatx4 pre[16];
 #pragma unroll
-        for (int t = 0; t < 16; ++t) g1_tile(t, bobs);
-        dw1_acc(srw, unscale4);
+            for (int t = 0; t < 16; ++t) pre[t] = layer1_t(t, bobs);
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(pre[t][q]));
+                    dh1[t][q] = dh1[t][q] * unscale4 * __builtin_fmaf(-r, r, r);
+                }
+        }
+        dw1_acc(srw);
     }
 
     // ---- per-wave partials: dW3 (lane's neurons) | db3 summed over the 16 row lanes | dW1 | db1
     float *out = g.part3 + (size_t)(blockIdx.x * kFdWaves + wv) * (A * H + A + H * S + H);
-    wave_sync_lds();  // the wave's LDS adds have landed
-    for (int i = lane; i < kUpdH * NC; i += 64) {
-        const int n = i / NC, f = i % NC;
-        const float v = dw1s[n * NCS + f];
-        if (f < S) out[A * H + A + n * S + f] = v;
-        else if (f == 4 * KS1) out[A * H + A + H * S + n] = v;
-    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2 * NC; ++i) {
+            const int n = 16 * (8 * h + 2 * gq + i / NC) + e, f = i % NC;
+            if (f < S) out[A * H + A + n * S + f] = dW1p[h][i];
+            else if (f == 4 * KS1) out[A * H + A + H * S + n] = dW1p[h][i];
+        }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) g2max = fmaxf(g2max, __shfl_xor(g2max, o));
     if (lane == 0) atomicMax(g.g2max, __float_as_uint(g2max));  // non-negative: uint order
