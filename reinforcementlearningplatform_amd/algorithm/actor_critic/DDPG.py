@@ -115,10 +115,13 @@ class DDPG:
         idx = (torch.rand(mem.batch_size, device=self.device) * self._gmax).long()
         idx.clamp_(max=mem.mem_size - 1)
         s, a, r, s_, done = K.replay_gather(mem.rb, idx, out=self._gbuf)
-        c, al = self._update_core(s, a, r, s_, done)
-        self._gloss[0].copy_(c)
-        self._gloss[1].copy_(al)
-        self.gpu_actor.copy_from_module()
+        if self._native is not None:  # losses straight into the graph's buffer
+            self._native.update(s, a, r, s_, done, out=self._gloss)
+        else:
+            c, al = self._update_core(s, a, r, s_, done)
+            self._gloss[0].copy_(c)
+            self._gloss[1].copy_(al)
+        self.gpu_actor.copy_from_module()  # (no copy when it aliases the native parameters)
 
     def _learn_graphed(self, iters):
         from .Soft_Actor_Critic import _capture

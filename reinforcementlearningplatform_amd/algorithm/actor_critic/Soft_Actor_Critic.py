@@ -167,10 +167,13 @@ class SAC:
         # alpha without an autograd edge to log_alpha: the reference's actor-loss gradient into
         # log_alpha is zeroed by alpha_optimizer.zero_grad() before it is used, so the values
         # are the same, and no autograd node outlives an iteration of the graph
-        c, al = self._update_core(s, a, r, s_, dw, self.log_alpha.detach().exp()
-                                  if self.adaptive_alpha else self.alpha)
-        self._gloss[0].copy_(c)
-        self._gloss[1].copy_(al)
+        if self._native is not None:  # losses straight into the graph's buffer
+            self._native.update(s, a, r, s_, dw, out=self._gloss)
+        else:
+            c, al = self._update_core(s, a, r, s_, dw, self.log_alpha.detach().exp()
+                                      if self.adaptive_alpha else self.alpha)
+            self._gloss[0].copy_(c)
+            self._gloss[1].copy_(al)
         self.gpu_actor.copy_from_actor()
 
     def _learn_graphed(self, iters):

@@ -212,13 +212,18 @@ class DDPGNativeUpdate:
             dst.lr, dst.beta1, dst.beta2, dst.eps = g["lr"], g["betas"][0], g["betas"][1], g["eps"]
         return c
 
-    def update(self, s, a, r, s_, end):
+    def update(self, s, a, r, s_, end, out=None):
+        """out: a float32 [2] device tensor to receive (critic loss, actor loss) — e.g. a
+        captured graph's loss buffer (no copies); else fresh tensors."""
         B = int(s.shape[0])
         if self.work is None or self.batch != B:
             self.work = K.ddpg_workspace(self.c_nets, B, s.device)
             self.batch = B
         f = lambda t: t.to(torch.float32).contiguous()
         s, a, r, s_, end = f(s), f(a), f(r).reshape(-1), f(s_), f(end).reshape(-1)
+        if out is not None:
+            K.ddpg_update(self.c_nets, self._cfg(B), s, a, r, s_, end, self.work, out)
+            return out[0], out[1]
         K.ddpg_update(self.c_nets, self._cfg(B), s, a, r, s_, end, self.work, self.losses)
         out = self.losses.clone()   # fresh tensors: self.losses is rewritten by the next call
         return out[0], out[1]

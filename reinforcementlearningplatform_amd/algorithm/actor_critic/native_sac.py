@@ -246,8 +246,9 @@ class SACNativeUpdate:
                 dst.lr, dst.beta1, dst.beta2, dst.eps = g["lr"], g["betas"][0], g["betas"][1], g["eps"]
         return c
 
-    def update(self, s, a, r, s_, dw, noise=None):
-        """noise: None (Philox) or [2][B][A] eps (s' draw, then s draw)."""
+    def update(self, s, a, r, s_, dw, noise=None, out=None):
+        """noise: None (Philox) or [2][B][A] eps (s' draw, then s draw). out: a float32 [2]
+        device tensor to receive (critic loss, actor loss) (no copies); else fresh tensors."""
         B = int(s.shape[0])
         if self.work is None or self.batch != B:
             self.work = K.sac_workspace(self.c_nets, B, s.device)
@@ -256,7 +257,10 @@ class SACNativeUpdate:
         s, a, r, s_, dw = f(s), f(a), f(r).reshape(-1), f(s_), f(dw).reshape(-1)
         nz = None if noise is None else f(noise)
         with torch.no_grad():
-            K.sac_update(self.c_nets, self._cfg(B), s, a, r, s_, dw, nz, self.work, self.losses)
+            K.sac_update(self.c_nets, self._cfg(B), s, a, r, s_, dw, nz, self.work,
+                         out if out is not None else self.losses)
+        if out is not None:
+            return out[0], out[1]
         out = self.losses.clone()   # fresh tensors: self.losses is rewritten by the next call
         return out[0], out[1]
 

@@ -332,14 +332,36 @@ class GPUNet:
             cnt = K.lib().rlp_mfma_packed_count(__import__("ctypes").byref(self.desc))
             self.packed = K.mfma_pack(self.desc, self.flat, out=self.packed) if cnt > 0 else None
 
+    def _params_region(self):
+        """The module's (weight, bias) tensors as one contiguous region of a single buffer (a
+        native update's flat parameters: module parameters are views of it), or None."""
+        ts = [t for l in self.linears for t in (l.weight, l.bias)]
+        if any(t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous()
+               for t in ts):
+            return None
+        base = ts[0].data_ptr()
+        off = 0
+        for t in ts:
+            if t.untyped_storage().data_ptr() != ts[0].untyped_storage().data_ptr() or \
+                    t.data_ptr() != base + 4 * off:
+                return None
+            off += t.numel()
+        st = ts[0].storage_offset()
+        return torch.as_strided(ts[0], (off,), (1,), st)
+
     def copy_from_module(self):
-        """refresh() in place (graph-capturable: the same flat / packed tensors)."""
+        """refresh() in place (graph-capturable: the same flat / packed tensors). When the
+        module's parameters are views of one flat buffer in this layout (a native update's), the
+        flat tensor aliases it and nothing is copied; otherwise one torch.cat launch."""
         with torch.no_grad():
-            off = 0
-            for l in self.linears:
-                for t in (l.weight, l.bias):
-                    self.flat[off:off + t.numel()].copy_(t.reshape(-1))
-                    off += t.numel()
+            region = self._params_region()
+            if region is not None and region.data_ptr() == self.flat.data_ptr():
+                pass  # aliased: already current
+            elif region is not None and region.numel() == self.flat.numel():
+                self.flat = region  # alias from now on (the first call runs before a capture)
+            else:
+                torch.cat([t.reshape(-1) for l in self.linears for t in (l.weight, l.bias)],
+                          out=self.flat)
             if self.packed is not None:
                 K.mfma_pack(self.desc, self.flat, out=self.packed)
 
@@ -486,17 +508,13 @@ class GPUSACActor:
         self.gain, self.off = a.gain.cpu().tolist(), a.off.cpu().tolist()
 
     def copy_from_actor(self):
-        """refresh() of the weights in place (graph-capturable: no new tensors)."""
+        """refresh() of the weights in place (graph-capturable: no new tensors; one launch)."""
         a = self.actor
         with torch.no_grad():
-            off = 0
-            for t in (a.fc1.weight, a.fc1.bias, a.fc2.weight, a.fc2.bias):
-                self.flat[off:off + t.numel()].copy_(t.reshape(-1))
-                off += t.numel()
-            for t in (a.mean_layer.weight, a.log_std_layer.weight, a.mean_layer.bias,
-                      a.log_std_layer.bias):
-                self.flat[off:off + t.numel()].copy_(t.reshape(-1))
-                off += t.numel()
+            torch.cat([t.reshape(-1) for t in (a.fc1.weight, a.fc1.bias, a.fc2.weight, a.fc2.bias,
+                                               a.mean_layer.weight, a.log_std_layer.weight,
+                                               a.mean_layer.bias, a.log_std_layer.bias)],
+                      out=self.flat)
 
     def head(self, s):
         return K.mlp_forward(self.desc, self.flat, s.to(self.device, torch.float32).contiguous())
