@@ -59,25 +59,27 @@ struct Epi {
 };
 
 constexpr int kDT = 64;            // output tile (M and N)
-constexpr int kDRc = 256;          // reduction rows one block stages at once
+constexpr int kDRc = 128;          // reduction rows one block stages at once (one LDS stage)
 constexpr int kDLd = kDRc + 4;     // LDS row: operand row-major along r, 4 banks apart per row
+constexpr int kDSlice = 256;       // reduction rows per slice of make_prob (two stages)
+constexpr int kDPf = kDT * kDRc / 4 / 256;  // float4 loads per thread of one panel's fast path (8)
 
 // extent of the panel's outer index u (A: rows m; B: columns n)
 __device__ __forceinline__ int e_rows(const Opnd &o, bool is_a) { return is_a ? o.rows : o.cols; }
 
-// Stage this block's panel of an operand into LDS as L[u][r] (row stride kDLd): u in [0, 64) the
-// outer index (A: m0 + u; B: n0 + u), r in [0, 256) the reduction index (r_lo + r; zero past rc).
+// A block's panel of an operand for one stage, as L[u][r] (row stride kDLd): u in [0, 64) the
+// outer index (A: m0 + u; B: n0 + u), r in [0, kDRc) the reduction index (r_lo + r; zero past rc).
 // Fast path (the panel lies inside one source, off the ones column, fully in range, and is
-// contiguous along r or along u with 16-byte alignment): 16 float4 loads per thread, all in
-// flight together. Otherwise the generic element loader in groups of 16.
-__device__ __forceinline__ void stage_panel(const Opnd &o, bool is_a, int u0, int ubound, int r_lo,
-                                            int rc, int nr, float *L) {
-    const int t = threadIdx.x;
-    // (i, j) of panel element (u, r)
-    auto ij = [&](int u, int r, int &i, int &j) {
-        i = is_a ? u0 + u : r_lo + r;
-        j = is_a ? r_lo + r : u0 + u;
-    };
+// contiguous along r or along u with 16-byte alignment): kDPf float4 loads per thread into
+// registers (panel_load, issued one stage ahead so they fly under the current stage's MFMAs),
+// written to LDS by panel_store. Otherwise the generic element loader, straight to LDS.
+struct PanelFast {
+    const float *base;
+    int u_stride, r_stride;
+    bool fast, rfast;
+};
+__device__ __forceinline__ PanelFast panel_plan(const Opnd &o, bool is_a, int u0, int ubound, int r_lo,
+                                                int rc) {
     const int i_lo = is_a ? u0 : r_lo, i_hi = is_a ? u0 + 64 : r_lo + rc;  // [lo, hi)
     const int j_lo = is_a ? r_lo : u0, j_hi = is_a ? r_lo + rc : u0 + 64;
     const int s_lo = o.split_rows ? i_lo : j_lo, s_hi = o.split_rows ? i_hi : j_hi;
@@ -94,34 +96,57 @@ __device__ __forceinline__ void stage_panel(const Opnd &o, bool is_a, int u0, in
     const bool ufast = u_stride == 1 && (r_stride & 3) == 0;
     const bool aligned = ((uintptr_t)p & 15) == 0 &&
                          (((is_a ? (u0 - ioff) * rs + (r_lo - joff) * cs : (r_lo - ioff) * rs + (u0 - joff) * cs)) & 3) == 0;
-    if (one_src && no_ones && inrange && aligned && (rfast || ufast)) {
-        const float *base = p + (int64_t)((is_a ? u0 : r_lo) - ioff) * rs + (int64_t)((is_a ? r_lo : u0) - joff) * cs;
-        floatx4 v[16];
-        if (rfast) {  // thread: r4 = 4 (t & 63), u = (t >> 6) + 4 q
-            const int r4 = 4 * (t & 63);
+    PanelFast f;
+    f.fast = one_src && no_ones && inrange && aligned && (rfast || ufast);
+    f.rfast = rfast;
+    f.base = p + (int64_t)((is_a ? u0 : r_lo) - ioff) * rs + (int64_t)((is_a ? r_lo : u0) - joff) * cs;
+    f.u_stride = u_stride;
+    f.r_stride = r_stride;
+    return f;
+}
+// rfast thread: r4 = 4 (t & 31), u = (t >> 5) + 8 q; ufast thread: u4 = 4 (t & 15), r = (t >> 4) + 16 q
+__device__ __forceinline__ void panel_load(const PanelFast &f, int rc, floatx4 (&v)[kDPf]) {
+    const int t = threadIdx.x;
+    if (f.rfast) {
+        const int r4 = 4 * (t & 31);
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int u = (t >> 6) + 4 * q;
-                v[q] = r4 < rc ? *(const floatx4 *)(base + (int64_t)u * u_stride + r4) : floatx4{0.f, 0.f, 0.f, 0.f};
-            }
-#pragma unroll
-            for (int q = 0; q < 16; ++q) *(floatx4 *)&L[((t >> 6) + 4 * q) * kDLd + r4] = v[q];
-        } else {      // thread: u4 = 4 (t & 15), r = (t >> 4) + 16 q
-            const int u4 = 4 * (t & 15);
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int r = (t >> 4) + 16 * q;
-                v[q] = r < rc ? *(const floatx4 *)(base + (int64_t)r * r_stride + u4) : floatx4{0.f, 0.f, 0.f, 0.f};
-            }
-#pragma unroll
-            for (int q = 0; q < 16; ++q)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) L[(u4 + k) * kDLd + (t >> 4) + 16 * q] = v[q][k];
+        for (int q = 0; q < kDPf; ++q) {
+            const int u = (t >> 5) + 8 * q;
+            v[q] = r4 < rc ? *(const floatx4 *)(f.base + (int64_t)u * f.u_stride + r4) : floatx4{0.f, 0.f, 0.f, 0.f};
         }
-        return;
+    } else {
+        const int u4 = 4 * (t & 15);
+#pragma unroll
+        for (int q = 0; q < kDPf; ++q) {
+            const int r = (t >> 4) + 16 * q;
+            v[q] = r < rc ? *(const floatx4 *)(f.base + (int64_t)r * f.r_stride + u4) : floatx4{0.f, 0.f, 0.f, 0.f};
+        }
     }
-    // generic element loader. Rows u past ubound are left as they are (their outputs are never
-    // stored); columns r in [rc, nr) are zeroed (they meet valid outputs in the MFMAs).
+}
+__device__ __forceinline__ void panel_store(const PanelFast &f, const floatx4 (&v)[kDPf], float *L) {
+    const int t = threadIdx.x;
+    if (f.rfast) {
+#pragma unroll
+        for (int q = 0; q < kDPf; ++q) *(floatx4 *)&L[((t >> 5) + 8 * q) * kDLd + 4 * (t & 31)] = v[q];
+    } else {
+        const int u4 = 4 * (t & 15);
+#pragma unroll
+        for (int q = 0; q < kDPf; ++q)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) L[(u4 + k) * kDLd + (t >> 4) + 16 * q] = v[q][k];
+    }
+}
+// generic element loader (the panel is not on the fast path). Rows u past ubound are left as they
+// are (their outputs are never stored); columns r in [rc, nr) are zeroed (they meet valid outputs
+// in the MFMAs).
+__device__ __forceinline__ void panel_generic(const Opnd &o, bool is_a, int u0, int ubound, int r_lo,
+                                              int rc, int nr, float *L) {
+    const int t = threadIdx.x;
+    // (i, j) of panel element (u, r)
+    auto ij = [&](int u, int r, int &i, int &j) {
+        i = is_a ? u0 + u : r_lo + r;
+        j = is_a ? r_lo + r : u0 + u;
+    };
     const int nu = ubound - u0 < 64 ? ubound - u0 : 64;
     if (nu <= 16) {  // few valid u (a last layer's W, an edge tile): thread = r, loop over u
         const int r = t;
@@ -160,13 +185,18 @@ __device__ __forceinline__ void stage_panel(const Opnd &o, bool is_a, int u0, in
     }
 }
 
-// C[M x N] = sum_r A(m, r) B(r, n) over r in [z * rchunk, min(R, (z + 1) * rchunk)), rchunk <= 256.
-// The block stages its whole reduction slice of both operands at once (all global loads in
-// flight together, 128 registers per lane, then one barrier): these GEMMs have <= 256-deep
-// slices, so one memory latency per launch instead of one per 16-deep tile. LDS holds A as
-// [m][r] and B as [n][r] (row stride 260 floats: the 16 x 4 fragment reads hit 64 distinct banks);
-// the reduction order is permuted so that each lane's operands for four consecutive MFMA steps
-// are contiguous (one 16-byte LDS read): step s, lane group g reads r = g * Q + s.
+// C[M x N] = sum_r A(m, r) B(r, n) over r in [z * rchunk, min(R, (z + 1) * rchunk)), rchunk <= 256
+// (make_prob; make_prob_long: longer). The block stages its slice 128 rows at a time: both
+// operands' panels of a stage in one burst of 16-byte loads (64 registers per lane), the next
+// stage's burst issued right after the current stage lands in LDS so that it flies under the
+// current stage's MFMAs. 67.6 KB of LDS per block: two blocks per CU, so a launch of more blocks
+// than CUs (a weight gradient beside its backward data pass, the twin critic's two chains)
+// overlaps one block's loads with the other's MFMAs instead of running in rounds of one block per
+// CU (DDPG learn(): the layer-1 weight-gradient + backward launch was 42 us in three rounds,
+// profiles/r4/r4e_ddpg_learn_timeline.txt). LDS holds A as [m][r] and B as [n][r] (row stride
+// 132 floats: the 16 x 4 fragment reads hit 64 distinct banks); the reduction order is permuted so
+// that each lane's operands for four consecutive MFMA steps are contiguous (one 16-byte LDS
+// read): step s, lane group g reads r = g * Q + s.
 struct Prob {
     Opnd A, B;
     Epi e;
@@ -174,23 +204,31 @@ struct Prob {
     int nx, ny, nz;  // column tiles, row tiles, reduction slices
 };
 
-// Up to two independent problems in one launch (the twin critic's chains, a layer's weight
-// gradient beside its backward data pass): the 1-D grid's first nx*ny*nz blocks run p0, the rest
-// p1 (one problem: gridDim.x = p0's block count).
-__global__ void __launch_bounds__(256) dense_gemm_kernel(Prob p0, Prob p1) {
+// Up to kMaxProbs independent problems in one launch (the twin critic's chains, a layer's weight
+// gradient beside its backward data pass, every layer's weight gradient of a net after the fused
+// data chain): the 1-D grid's blocks [start[i], start[i + 1]) run problem i.
+constexpr int kMaxProbs = 6;
+struct ProbSet {
+    Prob p[kMaxProbs];
+    int start[kMaxProbs + 1];
+    int n;
+};
+__global__ void __launch_bounds__(256) dense_gemm_kernel(ProbSet ps) {
     extern __shared__ float lds[];
     float *As = lds, *Bs = lds + kDT * kDLd;
-    const int nb0 = p0.nx * p0.ny * p0.nz;
-    const bool second = (int)blockIdx.x >= nb0;  // block-uniform
-    const Opnd A = second ? p1.A : p0.A, B = second ? p1.B : p0.B;
-    const Epi e = second ? p1.e : p0.e;
-    const int R = second ? p1.R : p0.R, rchunk = second ? p1.rchunk : p0.rchunk;
-    const int nx = second ? p1.nx : p0.nx, ny = second ? p1.ny : p0.ny;
-    const int bid = (int)blockIdx.x - (second ? nb0 : 0);
+    int pi = 0;  // block-uniform
+#pragma unroll
+    for (int k = 1; k < kMaxProbs; ++k)
+        if (k < ps.n && (int)blockIdx.x >= ps.start[k]) pi = k;
+    const Prob &q = ps.p[pi];
+    const Opnd A = q.A, B = q.B;
+    const Epi e = q.e;
+    const int R = q.R, rchunk = q.rchunk, nx = q.nx, ny = q.ny;
+    const int bid = (int)blockIdx.x - ps.start[pi];
     const int bx = bid % nx, by = (bid / nx) % ny, bz = bid / (nx * ny);
     const int m0 = by * kDT, n0 = bx * kDT;
-    // the block's reduction slice [r_lo, r_end), staged kDRc rows at a time (one stage unless the
-    // problem was built with make_prob_long: the PPO2 update's weight gradients over 2^18 rows)
+    // the block's reduction slice [r_lo, r_end), staged kDRc rows at a time; the next stage's
+    // fast-path panels are loaded into registers while the current stage's MFMAs run
     const int r_lo = bz * rchunk, r_end = min(R, r_lo + rchunk);
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
     const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
@@ -200,13 +238,25 @@ __global__ void __launch_bounds__(256) dense_gemm_kernel(Prob p0, Prob p1) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int g = l >> 4, c = l & 15;
+    const int ua = e_rows(A, true), ub = e_rows(B, false);
+    floatx4 va[kDPf], vb[kDPf];
+    int rc = min(r_end, r_lo + kDRc) - r_lo;
+    PanelFast fa = panel_plan(A, true, m0, ua, r_lo, rc), fb = panel_plan(B, false, n0, ub, r_lo, rc);
+    if (fa.fast) panel_load(fa, rc, va);
+    if (fb.fast) panel_load(fb, rc, vb);
     for (int rs = r_lo; rs < r_end || rs == r_lo; rs += kDRc) {
-        const int rc = min(r_end, rs + kDRc) - rs;
         const int Q = (rc + 15) / 16 * 4;  // MFMA steps (multiple of 4); rows g * Q + s, s < Q
         if (rs != r_lo) __syncthreads();   // the previous stage's fragments are read
-        stage_panel(A, true, m0, e_rows(A, true), rs, rc, 4 * Q, As);
-        stage_panel(B, false, n0, e_rows(B, false), rs, rc, 4 * Q, Bs);
+        if (fa.fast) panel_store(fa, va, As); else panel_generic(A, true, m0, ua, rs, rc, 4 * Q, As);
+        if (fb.fast) panel_store(fb, vb, Bs); else panel_generic(B, false, n0, ub, rs, rc, 4 * Q, Bs);
         __syncthreads();
+        const int rn = rs + kDRc, rcn = min(r_end, rn + kDRc) - rn;
+        if (rn < r_end) {  // next stage's loads, in flight under this stage's MFMAs
+            fa = panel_plan(A, true, m0, ua, rn, rcn);
+            fb = panel_plan(B, false, n0, ub, rn, rcn);
+            if (fa.fast) panel_load(fa, rcn, va);
+            if (fb.fast) panel_load(fb, rcn, vb);
+        }
         for (int s = 0; s < Q; s += 4) {
             floatx4 af[2], bf[2];
 #pragma unroll
@@ -222,6 +272,7 @@ __global__ void __launch_bounds__(256) dense_gemm_kernel(Prob p0, Prob p1) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][u], bf[j][u], acc[i][j], 0, 0, 0);
         }
         if (rc <= 0) break;
+        rc = rcn;
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -260,25 +311,40 @@ __global__ void __launch_bounds__(256) dense_gemm_kernel(Prob p0, Prob p1) {
             }
 }
 
-// grad[m][n] = sum over the splits of the partials, in split order; column N-1 is the bias.
+// grad[m][n] = sum over the splits of the partials; column N-1 is the bias. 64 outputs per block
+// x kWrSlices slices: each thread sums every kWrSlices-th split (8 loads in flight), then a
+// fixed-order LDS combine — deterministic; the PPO2 dense update's long reductions leave up to
+// 512 partials per element, which one thread per element walked with one latency each.
 // blockIdx.y = 1: the second problem of a twin launch (part1 -> gW1, gb1)
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float *__restrict__ part0, int splits,
-                                                           int M, int N, float *__restrict__ gW0,
-                                                           float *__restrict__ gb0,
-                                                           const float *__restrict__ part1,
-                                                           float *__restrict__ gW1,
-                                                           float *__restrict__ gb1) {
+constexpr int kWrSlices = 16;
+__global__ void __launch_bounds__(64 * kWrSlices) wgrad_reduce_kernel(const float *__restrict__ part0,
+                                                                      int splits, int M, int N,
+                                                                      float *__restrict__ gW0,
+                                                                      float *__restrict__ gb0,
+                                                                      const float *__restrict__ part1,
+                                                                      float *__restrict__ gW1,
+                                                                      float *__restrict__ gb1) {
     const float *part = blockIdx.y ? part1 : part0;
     float *gW = blockIdx.y ? gW1 : gW0, *gb = blockIdx.y ? gb1 : gb0;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= M * N) return;
+    const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + o;
     float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += part[(size_t)z * M * N + i];
+    if (i < M * N) {
+#pragma unroll 8
+        for (int z = sl; z < splits; z += kWrSlices) s += part[(size_t)z * M * N + i];
+    }
+    __shared__ float red[kWrSlices][64];
+    red[sl][o] = s;
+    __syncthreads();
+    if (sl != 0 || i >= M * N) return;
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < kWrSlices; ++k) t += red[k][o];
     const int m = i / N, n = i - m * N;
     if (n < N - 1)
-        gW[(size_t)m * (N - 1) + n] = s;
+        gW[(size_t)m * (N - 1) + n] = t;
     else
-        gb[m] = s;
+        gb[m] = t;
 }
 
 // TD target + critic MSE gradient (DDPG.py:83-89): y = r + (gamma * end) * Q'; dQ = d/dQ of
@@ -363,8 +429,8 @@ struct NetParts {
 };
 
 // One launch for what wgrad_reduce (per layer), Adam and the soft target update did in five: the
-// gradient element summed over its layer's partials in split order (wgrad_reduce's order, so the
-// same bits), stored to g, the Adam step on it, and — when tp is set — the soft target update
+// gradient element summed over its layer's partials in split order (DDPG / SAC: 16 splits of 256
+// batch rows), stored to g, the Adam step on it, and — when tp is set — the soft target update
 // with the new parameter, tp (1 - tau) + p tau (DDPG.py:113-118, Soft_Actor_Critic.py:126-127;
 // the target is not read again in the update).
 // Elements outside every layer (a module's unused parameters) keep the gradient in g.
@@ -385,6 +451,7 @@ __global__ void __launch_bounds__(256) adam_reduce_kernel(float *__restrict__ p,
             const int64_t idx = r < in * out ? (r / in) * (in + 1) + r % in : (r - in * out) * (in + 1) + in;
             const int64_t stride = out * (in + 1);
             float s = 0.f;
+#pragma unroll 8
             for (int zz = 0; zz < np.z[l]; ++zz) s += np.part[l][zz * stride + idx];
             gi = s;
             g[i] = s;
@@ -592,6 +659,298 @@ __global__ void __launch_bounds__(1024) sac_critic_loss_kernel(const float *__re
     }
 }
 
+// ---- fused forward of a three-layer chain -------------------------------------------------------
+// [K0 -> H1 -> H2 -> NO] with relu hidden layers (the DDPG demo nets, the SAC critics and actor
+// trunk), 16 rows per block, all three layers in one launch instead of three GEMM launches: the
+// block's input rows and both hidden activations stay in LDS between the layers (and go to HBM
+// once, for the backward's relu masks and weight gradients). Exact f32 products
+// (v_mfma_f32_16x16x4_f32). Eight waves per block (two per SIMD: one wave's loads and VALU under
+// the other's MFMAs). Layer 1 / 2: wave w owns the 16-column tiles t = w + 8 j, j < NT1 / NT2
+// (compile-time: every MFMA and load unconditional — a guarded tile made each MFMA a branch with a
+// vmcnt(0) in front, which serialised the weight loads: 43 us per DDPG chain at batch 4096); lane
+// (g, c) feeds A = the activation row c at k = kb + 4 g + u and B = W[16 t + c][kb + 4 g + u] for
+// the four steps u of a 16-deep k block, so both operands are 16-byte reads (LDS / the L2-resident
+// weights; the packed parameter buffers leave some W unaligned — global loads take that). The
+// weights of a 16-deep block load one 32-deep pass ahead of its MFMAs (two register sets, unrolled
+// by two: a register copy of an in-flight load would wait for it). Tiles past the width
+// read a clamped row and are not stored. Layer 3 (NO <= 8 outputs): the 64 lanes of a wave split
+// k, one wave per 2 rows, a shuffle tree per output.
+struct ChainArgs {
+    const float *x0, *x1;  // input columns [0, split) from x0 (row stride ld0), the rest from x1
+    int ld0, ld1, split, K0;
+    const float *W1, *b1, *W2, *b2, *W3, *b3;
+    const float *W3b;      // output rows [split3, NO) of layer 3 from W3b (the SAC actor's two heads)
+    int split3;            // (b3 may be null: no layer-3 bias)
+    int H1, H2, NO, B;
+    float *h1, *h2, *y;    // [B][H1], [B][H2], [B][NO]
+    int head;              // 0: y = z; 1: t = tanh(z) into aux, y = gain t + off; 2: y = tanh(z)
+                           // (h1 / h2 null: the hidden activations are not stored — inference)
+    const float *gain, *off;
+    float *aux;
+};
+constexpr int kChRows = 16, kChK0 = 64, kChH = 256, kChLd = kChH + 4;
+constexpr int kChWaves = 8, kChThreads = 64 * kChWaves, kChRpw = kChRows / kChWaves;  // rows per wave (layer 3)
+constexpr int kChMaxNt = kChH / 16 / kChWaves;  // 16-column tiles per wave at the widest layer
+
+// acc[j] += A (16 x 16, fragments f) x B (16 x 16 of tile j, fragments b[j]) over one 16-deep block
+template <int NT>
+__device__ __forceinline__ void chain_block(const floatx4 &f, const floatx4 (&b)[NT], floatx4 (&acc)[NT]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[u], b[j][u], acc[j], 0, 0, 0);
+}
+
+template <int NT1, int NT2>
+__global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, ChainArgs a1) {
+    const ChainArgs &a = blockIdx.y ? a1 : a0;
+    __shared__ __attribute__((aligned(16))) float xs[kChRows][kChK0 + 4];
+    __shared__ __attribute__((aligned(16))) float hs1[kChRows][kChLd];
+    __shared__ __attribute__((aligned(16))) float hs2[kChRows][kChLd];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
+    const int r0 = blockIdx.x * kChRows;
+    const int K8 = (a.K0 + 7) & ~7;  // zero-padded input columns: two 4-deep steps per pass
+    for (int i = t; i < kChRows * K8; i += kChThreads) {
+        const int rr = i / K8, k = i % K8, r = r0 + rr;
+        float v = 0.f;
+        if (r < a.B && k < a.K0) v = k < a.split ? a.x0[(int64_t)r * a.ld0 + k] : a.x1[(int64_t)r * a.ld1 + k - a.split];
+        xs[rr][k] = v;
+    }
+    __syncthreads();
+    // layer 1: k outer (one W1 element per tile and step, the next step's in flight)
+    {
+        int row[NT1];
+        floatx4 acc[NT1];
+#pragma unroll
+        for (int j = 0; j < NT1; ++j) {
+            const int n = 16 * (w + kChWaves * j) + c;
+            row[j] = n < a.H1 ? n : a.H1 - 1;
+            const float bb = a.b1[row[j]];
+            acc[j] = floatx4{bb, bb, bb, bb};
+        }
+        float wa[NT1], wb[NT1];
+        auto ld1 = [&](int k, float (&v)[NT1]) {  // k past K0: a clamped column (its x is 0)
+            const int kk = k < a.K0 ? k : a.K0 - 1;
+#pragma unroll
+            for (int j = 0; j < NT1; ++j) v[j] = a.W1[(int64_t)row[j] * a.K0 + kk];
+        };
+        ld1(g, wa);
+        for (int k4 = 0; k4 < K8; k4 += 8) {
+            ld1(k4 + 4 + g, wb);
+            const float x0 = xs[c][k4 + g];
+#pragma unroll
+            for (int j = 0; j < NT1; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, wa[j], acc[j], 0, 0, 0);
+            ld1(k4 + 8 + g, wa);
+            const float x1 = xs[c][k4 + 4 + g];
+#pragma unroll
+            for (int j = 0; j < NT1; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, wb[j], acc[j], 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < NT1; ++j) {
+            const int n = 16 * (w + kChWaves * j) + c;
+            if (n >= a.H1) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float v = fmaxf(acc[j][i], 0.f);
+                hs1[4 * g + i][n] = v;
+                if (a.h1 && r0 + 4 * g + i < a.B) a.h1[(int64_t)(r0 + 4 * g + i) * a.H1 + n] = v;
+            }
+        }
+    }
+    __syncthreads();
+    // layer 2 (H1 a multiple of 32)
+    {
+        int row[NT2];
+        floatx4 acc[NT2];
+#pragma unroll
+        for (int j = 0; j < NT2; ++j) {
+            const int n = 16 * (w + kChWaves * j) + c;
+            row[j] = n < a.H2 ? n : a.H2 - 1;
+            const float bb = a.b2[row[j]];
+            acc[j] = floatx4{bb, bb, bb, bb};
+        }
+        floatx4 ba[NT2], bb[NT2];
+        auto ld2 = [&](int kb, floatx4 (&v)[NT2]) {  // kb past H1: a clamped reload, unused
+            const int k = (kb < a.H1 ? kb : a.H1 - 16) + 4 * g;
+#pragma unroll
+            for (int j = 0; j < NT2; ++j) v[j] = *reinterpret_cast<const floatx4 *>(a.W2 + (int64_t)row[j] * a.H1 + k);
+        };
+        ld2(0, ba);
+        ld2(16, bb);
+        for (int kb = 0; kb < a.H1; kb += 32) {  // (sched barriers: the scheduler sinks the loads)
+            const floatx4 f0 = *reinterpret_cast<const floatx4 *>(&hs1[c][kb + 4 * g]);
+            const floatx4 f1 = *reinterpret_cast<const floatx4 *>(&hs1[c][kb + 16 + 4 * g]);
+            chain_block<NT2>(f0, ba, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            ld2(kb + 32, ba);
+            __builtin_amdgcn_sched_barrier(0);
+            chain_block<NT2>(f1, bb, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            ld2(kb + 48, bb);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < NT2; ++j) {
+            const int n = 16 * (w + kChWaves * j) + c;
+            if (n >= a.H2) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float v = fmaxf(acc[j][i], 0.f);
+                hs2[4 * g + i][n] = v;
+                if (a.h2 && r0 + 4 * g + i < a.B) a.h2[(int64_t)(r0 + 4 * g + i) * a.H2 + n] = v;
+            }
+        }
+    }
+    __syncthreads();
+    // layer 3: wave w, rows kChRpw w ..
+    for (int o = 0; o < a.NO; ++o) {
+        const float *w3 = o < a.split3 ? a.W3 + (int64_t)o * a.H2 : a.W3b + (int64_t)(o - a.split3) * a.H2;
+#pragma unroll
+        for (int i = 0; i < kChRpw; ++i) {
+            const int rr = kChRpw * w + i;
+            float z = 0.f;
+            for (int k = lane; k < a.H2; k += 64) z = __builtin_fmaf(hs2[rr][k], w3[k], z);
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) z += __shfl_xor(z, m);
+            const int r = r0 + rr;
+            if (lane == 0 && r < a.B) {
+                if (a.b3) z = z + a.b3[o];
+                if (a.head == 2) {
+                    z = tanhf(z);
+                } else if (a.head) {
+                    const float th = tanhf(z);
+                    a.aux[(int64_t)r * a.NO + o] = th;
+                    z = a.gain[o] * th + a.off[o];
+                }
+                a.y[(int64_t)r * a.NO + o] = z;
+            }
+        }
+    }
+}
+
+// The data-only backward of the same [K0 -> H1 -> H2 -> NO] relu chains (the critic's input
+// gradient of DDPG / SAC's actor pass: no weight gradients, so neither hidden gradient needs HBM):
+// dH2 = (dY W3) relu'(h2) and dH1 = (dH2 W2) relu'(h1) stay in LDS, dX[:, c0:c0+nc] = dH1 W1[:,
+// c0:c0+nc] with the tanh-affine backward of the actor's head when t is given (one launch instead
+// of three GEMMs). Layer 2: as chain3_fwd_kernel's (NT tiles of dH1 per wave, H2 a multiple of 32,
+// the next block's weights in flight), with B(k, n) = W2[k][n] (four 64-byte row segments per lane
+// instead of one 16-byte column read); the dX columns: the lane-split dot products of
+// chain3_fwd_kernel's layer 3.
+struct ChainBwdArgs {
+    const float *dy, *W1, *W2, *W3;  // dY [B][NO]; the layers' weights ([out][in])
+    const float *h1, *h2;            // relu outputs [B][H1], [B][H2] (the masks)
+    int K0, H1, H2, NO, B, c0, nc;
+    const float *t, *gain;           // t: tanh(z) of the actor's head [B][nc] (or null), gain [nc]
+    float *dx;                       // [B][nc] (nc = 0: none)
+    float *d2, *d1;                  // dH2 [B][H2], dH1 [B][H1] to HBM when set (the weight
+                                     // gradients' dY operands)
+};
+
+template <int NT>
+__global__ void __launch_bounds__(kChThreads) chain3_bwd_kernel(ChainBwdArgs a0, ChainBwdArgs a1) {
+    const ChainBwdArgs &a = blockIdx.y ? a1 : a0;
+    __shared__ __attribute__((aligned(16))) float gs2[kChRows][kChLd];
+    __shared__ __attribute__((aligned(16))) float gs1[kChRows][kChLd];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
+    const int r0 = blockIdx.x * kChRows;
+    // dH2 (an outer product for NO = 1: the GEMM path's single product per element)
+    for (int i = t; i < kChRows * a.H2; i += kChThreads) {
+        const int rr = i / a.H2, o = i % a.H2, r = r0 + rr;
+        float v = 0.f;
+        if (r < a.B && a.h2[(int64_t)r * a.H2 + o] > 0.f) {
+            v = a.dy[(int64_t)r * a.NO] * a.W3[o];
+            for (int j = 1; j < a.NO; ++j) v = __builtin_fmaf(a.dy[(int64_t)r * a.NO + j], a.W3[(int64_t)j * a.H2 + o], v);
+        }
+        gs2[rr][o] = v;
+        if (a.d2 && r < a.B) a.d2[(int64_t)r * a.H2 + o] = v;
+    }
+    __syncthreads();
+    {
+        int col[NT];
+        floatx4 acc[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n = 16 * (w + kChWaves * j) + c;
+            col[j] = n < a.H1 ? n : a.H1 - 1;
+            acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        floatx4 ba[NT], bb[NT];
+        auto ld = [&](int kb, floatx4 (&v)[NT]) {  // kb past H2: a clamped reload, unused
+            const int k = (kb < a.H2 ? kb : a.H2 - 16) + 4 * g;
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[j][u] = a.W2[(int64_t)(k + u) * a.H1 + col[j]];
+        };
+        ld(0, ba);
+        ld(16, bb);
+        for (int kb = 0; kb < a.H2; kb += 32) {  // (sched barriers: the scheduler sinks the loads)
+            const floatx4 f0 = *reinterpret_cast<const floatx4 *>(&gs2[c][kb + 4 * g]);
+            const floatx4 f1 = *reinterpret_cast<const floatx4 *>(&gs2[c][kb + 16 + 4 * g]);
+            chain_block<NT>(f0, ba, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(kb + 32, ba);
+            __builtin_amdgcn_sched_barrier(0);
+            chain_block<NT>(f1, bb, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(kb + 48, bb);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n = 16 * (w + kChWaves * j) + c;
+            if (n >= a.H1) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = r0 + 4 * g + i;
+                const float v = r < a.B && a.h1[(int64_t)r * a.H1 + n] > 0.f ? acc[j][i] : 0.f;
+                gs1[4 * g + i][n] = v;
+                if (a.d1 && r < a.B) a.d1[(int64_t)r * a.H1 + n] = v;
+            }
+        }
+    }
+    __syncthreads();
+    // dX columns: wave w, rows kChRpw w ..
+    for (int j = 0; j < a.nc; ++j) {
+#pragma unroll
+        for (int i = 0; i < kChRpw; ++i) {
+            const int rr = kChRpw * w + i;
+            float z = 0.f;
+            for (int k = lane; k < a.H1; k += 64)
+                z = __builtin_fmaf(gs1[rr][k], a.W1[(int64_t)k * a.K0 + a.c0 + j], z);
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) z += __shfl_xor(z, m);
+            const int r = r0 + rr;
+            if (lane == 0 && r < a.B) {
+                if (a.t) {  // torch: grad_t = da * gain; grad_z = grad_t * (1 - t*t)
+                    const float tt = a.t[(int64_t)r * a.nc + j];
+                    z = (z * a.gain[j]) * (1.f - tt * tt);
+                }
+                a.dx[(int64_t)r * a.nc + j] = z;
+            }
+        }
+    }
+}
+
+// launch helpers: the tile counts per wave as template arguments (hidden widths 32 .. 256: one or
+// two 16-column tiles per wave)
+static_assert(kChMaxNt == 2, "chain launch tables");
+using ChainFwdFn = void (*)(ChainArgs, ChainArgs);
+inline int chain_nt(int h) { return (h / 16 + kChWaves - 1) / kChWaves; }
+void chain_fwd_launch(const ChainArgs &c0, const ChainArgs &c1, int nchains, hipStream_t s) {
+    static const ChainFwdFn tab[2][2] = {{chain3_fwd_kernel<1, 1>, chain3_fwd_kernel<1, 2>},
+                                         {chain3_fwd_kernel<2, 1>, chain3_fwd_kernel<2, 2>}};
+    const ChainFwdFn f = tab[chain_nt(c0.H1) - 1][chain_nt(c0.H2) - 1];
+    f<<<dim3((c0.B + kChRows - 1) / kChRows, nchains), kChThreads, 0, s>>>(c0, c1);
+}
+void chain_bwd_launch(const ChainBwdArgs &c0, const ChainBwdArgs &c1, int nchains, hipStream_t s) {
+    const dim3 grid((c0.B + kChRows - 1) / kChRows, nchains);
+    if (chain_nt(c0.H1) == 1)
+        chain3_bwd_kernel<1><<<grid, kChThreads, 0, s>>>(c0, c1);
+    else
+        chain3_bwd_kernel<2><<<grid, kChThreads, 0, s>>>(c0, c1);
+}
+
 // ---- host side ------------------------------------------------------------------------------
 
 inline Opnd mat(const float *p, int rows, int cols, int ld) {  // row-major rows x cols
@@ -604,28 +963,41 @@ inline Opnd transposed(const float *p, int rows, int cols, int ld) {  // (i, j) 
     return Opnd{p, p, 1, ld, 1, ld, rows, cols, cols, -1, 0};
 }
 
-constexpr size_t kDenseLds = 2 * kDT * kDLd * sizeof(float);  // 133 120 B
+constexpr size_t kDenseLds = 2 * kDT * kDLd * sizeof(float);  // 67 584 B: two blocks per CU
 
 // splits >= ceil(R / 256) slices of the reduction (each <= 256 rows); returns the slice count
 // a problem's reduction slicing (splits >= ceil(R / 256) slices, each <= 256 rows) and tiling
 inline Prob make_prob(const Opnd &A, const Opnd &B, const Epi &e, int R, int splits) {
-    const int need = (R + kDRc - 1) / kDRc;
+    const int need = (R + kDSlice - 1) / kDSlice;
     const int sp = splits > need ? splits : need;
     const int rchunk = ((R + sp - 1) / sp + 15) / 16 * 16;
     const int nz = R > 0 ? (R + rchunk - 1) / rchunk : 1;
     return Prob{A, B, e, R, rchunk, (e.N + kDT - 1) / kDT, (e.M + kDT - 1) / kDT, nz};
 }
 
-// one problem, or two (q1 != nullptr) in one launch; returns p0's slice count
-int gemm_launch(const Prob &q0, const Prob *q1, hipStream_t s) {
+// problems qs[0 .. n) in one launch (n <= kMaxProbs)
+void gemm_multi(const Prob *qs, int n, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)dense_gemm_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDenseLds);
         attr = true;
     }
-    const int nb = q0.nx * q0.ny * q0.nz + (q1 ? q1->nx * q1->ny * q1->nz : 0);
-    dense_gemm_kernel<<<nb, 256, kDenseLds, s>>>(q0, q1 ? *q1 : q0);
+    ProbSet ps{};
+    int nb = 0;
+    for (int i = 0; i < n; ++i) {
+        ps.p[i] = qs[i];
+        ps.start[i] = nb;
+        nb += qs[i].nx * qs[i].ny * qs[i].nz;
+    }
+    ps.start[n] = nb;
+    ps.n = n;
+    dense_gemm_kernel<<<nb, 256, kDenseLds, s>>>(ps);
+}
+// one problem, or two (q1 != nullptr) in one launch; returns p0's slice count
+int gemm_launch(const Prob &q0, const Prob *q1, hipStream_t s) {
+    const Prob qs[2] = {q0, q1 ? *q1 : q0};
+    gemm_multi(qs, q1 ? 2 : 1, s);
     return q0.nz;
 }
 int gemm_impl(const Opnd &A, const Opnd &B, const Epi &e, const Opnd *A1, const Opnd *B1,
@@ -684,7 +1056,7 @@ Prob wgrad_prob(const float *dy, const Opnd &x, const Layer &L, int B, float *pa
 }
 void wgrad_reduce(const Layer &L, const float *part, int z, float *gW, float *gb, hipStream_t s) {
     const int tot = L.out * (L.in + 1);
-    wgrad_reduce_kernel<<<(tot + 255) / 256, 256, 0, s>>>(part, z, L.out, L.in + 1, gW, gb, part, gW, gb);
+    wgrad_reduce_kernel<<<(tot + 63) / 64, 64 * kWrSlices, 0, s>>>(part, z, L.out, L.in + 1, gW, gb, part, gW, gb);
 }
 
 // record a layer's partials (its own region) in np for adam_reduce_kernel
@@ -769,7 +1141,7 @@ int64_t hidden_sum(const rlp_dense_net &n) {
 constexpr int kWgradRows = 256;  // batch rows per weight-gradient split
 
 struct DdpgWs {  // float offsets into the workspace
-    int64_t ta, tc, c, pa, pc, ta_t, pa_t, g0, g1, dq, part, total;
+    int64_t ta, tc, c, pa, pc, ta_t, pa_t, g0, g1, g2, dq, part, total;
 };
 DdpgWs ddpg_ws(const rlp_ddpg_nets &n, int B) {
     DdpgWs w{};
@@ -785,6 +1157,7 @@ DdpgWs ddpg_ws(const rlp_ddpg_nets &n, int B) {
     const int mw = max_width(n.actor) > max_width(n.critic) ? max_width(n.actor) : max_width(n.critic);
     w.g0 = take((int64_t)B * mw);
     w.g1 = take((int64_t)B * mw);
+    w.g2 = take((int64_t)B * mw);
     w.dq = take((int64_t)B * n.actor.dims[n.actor.n_layers]);
     const int splits = (B + kWgradRows - 1) / kWgradRows;
     // every layer's weight-gradient partials at once (left for adam_reduce_kernel)
@@ -801,8 +1174,48 @@ DdpgWs ddpg_ws(const rlp_ddpg_nets &n, int B) {
 
 // forward of a whole net: layer l's output at act + off_l (row-major [B][dims[l+1]]); the first
 // layer reads x (a strided / concatenated view)
+// the fused chain takes the net: three layers, relu hidden widths multiples of 32 up to 256, at
+// most 64 inputs (a plain or column-concatenated row-major view) and 4 outputs
+bool chain3_ok(const rlp_dense_net &n, const Opnd &x) {
+    return n.n_layers == 3 && n.dims[0] <= kChK0 && n.dims[1] <= kChH && n.dims[1] % 32 == 0 &&
+           n.dims[2] <= kChH && n.dims[2] % 32 == 0 && n.dims[3] <= 4 && x.cs0 == 1 && x.cs1 == 1 &&
+           !x.split_rows && x.ones < 0 && x.cols == n.dims[0];
+}
+ChainArgs chain3_args(const rlp_dense_net &n, const float *params, const Opnd &x, int B, float *act,
+                      bool actor_head, const float *gain, const float *off, float *tanh_out) {
+    ChainArgs c{};
+    c.x0 = x.p0; c.x1 = x.p1; c.ld0 = x.rs0; c.ld1 = x.rs1; c.split = x.split; c.K0 = n.dims[0];
+    const Layer L1 = layer_of(n, params, 0), L2 = layer_of(n, params, 1), L3 = layer_of(n, params, 2);
+    c.W1 = L1.W; c.b1 = L1.b; c.W2 = L2.W; c.b2 = L2.b; c.W3 = L3.W; c.b3 = L3.b; c.W3b = L3.W;
+    c.H1 = n.dims[1]; c.H2 = n.dims[2]; c.NO = n.dims[3]; c.split3 = c.NO; c.B = B;
+    c.h1 = act; c.h2 = act + (int64_t)B * c.H1; c.y = c.h2 + (int64_t)B * c.H2;
+    c.head = actor_head ? 1 : 0; c.gain = gain; c.off = off; c.aux = tanh_out;
+    return c;
+}
+// the data-only backward chain: three layers, relu hidden widths multiples of 32 up to 256
+bool chain3_bwd_ok(const rlp_dense_net &n) {
+    return n.n_layers == 3 && n.dims[1] <= kChH && n.dims[1] % 32 == 0 && n.dims[2] <= kChH &&
+           n.dims[2] % 32 == 0 && n.dims[3] <= 4;
+}
+ChainBwdArgs chain3_bwd_args(const rlp_dense_net &n, const float *params, const float *act, int B,
+                             const float *dy, int c0, int nc, const float *t_in, const float *gain,
+                             float *dx, float *d2 = nullptr, float *d1 = nullptr) {
+    ChainBwdArgs c{};
+    c.dy = dy;
+    c.W1 = layer_of(n, params, 0).W; c.W2 = layer_of(n, params, 1).W; c.W3 = layer_of(n, params, 2).W;
+    c.K0 = n.dims[0]; c.H1 = n.dims[1]; c.H2 = n.dims[2]; c.NO = n.dims[3]; c.B = B;
+    c.h1 = act; c.h2 = act + (int64_t)B * c.H1;
+    c.c0 = c0; c.nc = nc; c.t = t_in; c.gain = gain; c.dx = dx; c.d2 = d2; c.d1 = d1;
+    return c;
+}
+
 void net_fwd(const rlp_dense_net &n, const float *params, const Opnd &x, int B, float *act,
              bool actor_head, const float *gain, const float *off, float *tanh_out, hipStream_t s) {
+    if (chain3_ok(n, x)) {  // one launch for the three layers
+        const ChainArgs c = chain3_args(n, params, x, B, act, actor_head, gain, off, tanh_out);
+        chain_fwd_launch(c, c, 1, s);
+        return;
+    }
     int64_t o = 0;
     Opnd in = x;
     for (int l = 0; l < n.n_layers; ++l) {
@@ -830,6 +1243,11 @@ void net_bwd(const rlp_dense_net &n, const float *params, float *grad, const Opn
              const float *act, const float *dy_top, float *g0, float *g1, float *part, int splits,
              int c0, int nc, const float *t_in, const float *gain, float *dx, hipStream_t s,
              NetParts *np = nullptr) {
+    if (!grad && dx && chain3_bwd_ok(n)) {  // the input gradient alone: one launch
+        const ChainBwdArgs c = chain3_bwd_args(n, params, act, B, dy_top, c0, nc, t_in, gain, dx);
+        chain_bwd_launch(c, c, 1, s);
+        return;
+    }
     const float *dy = dy_top;
     float *dn = dy_top == g0 ? g1 : g0;
     int64_t po = 0;
@@ -874,6 +1292,13 @@ bool same_dims(const rlp_dense_net &a, const rlp_dense_net &b) {
 void twin_fwd(const rlp_dense_net &n1, const rlp_dense_net &n2, const float *params, const Opnd &x,
               int B, float *act1, float *act2, hipStream_t s, const float *params2 = nullptr,
               const Opnd *x2 = nullptr) {
+    if (same_dims(n1, n2) && chain3_ok(n1, x) && chain3_ok(n2, x2 ? *x2 : x)) {  // both chains, one launch
+        const ChainArgs c1 = chain3_args(n1, params, x, B, act1, false, nullptr, nullptr, nullptr);
+        const ChainArgs c2 = chain3_args(n2, params2 ? params2 : params, x2 ? *x2 : x, B, act2, false,
+                                         nullptr, nullptr, nullptr);
+        chain_fwd_launch(c1, c2, 2, s);
+        return;
+    }
     int64_t o = 0;
     Opnd in1 = x, in2 = x2 ? *x2 : x;
     for (int l = 0; l < n1.n_layers; ++l) {
@@ -901,6 +1326,12 @@ void twin_bwd(const rlp_dense_net &n1, const rlp_dense_net &n2, const float *par
               const Opnd &x, int B, const float *act1, const float *act2, const float *dy1,
               const float *dy2, float *const d[4], float *part1, float *part2, int splits, int c0,
               int nc, float *dx1, float *dx2, hipStream_t s, NetParts *np = nullptr) {
+    if (!grad && dx1 && dx2 && same_dims(n1, n2) && chain3_bwd_ok(n1)) {  // both chains, one launch
+        const ChainBwdArgs c1 = chain3_bwd_args(n1, params, act1, B, dy1, c0, nc, nullptr, nullptr, dx1);
+        const ChainBwdArgs c2 = chain3_bwd_args(n2, params, act2, B, dy2, c0, nc, nullptr, nullptr, dx2);
+        chain_bwd_launch(c1, c2, 2, s);
+        return;
+    }
     const float *y1 = dy1, *y2 = dy2;
     int pp = 0;
     int64_t po = 0;
@@ -927,7 +1358,7 @@ void twin_bwd(const rlp_dense_net &n1, const rlp_dense_net &n2, const float *par
                 parts_add(np, p2, z, L2.in, L2.out, n2.offset[l]);
             } else {
                 const int tot = L1.out * (L1.in + 1);
-                wgrad_reduce_kernel<<<dim3((tot + 255) / 256, 2), 256, 0, s>>>(
+                wgrad_reduce_kernel<<<dim3((tot + 63) / 64, 2), 64 * kWrSlices, 0, s>>>(
                     p1, z, L1.out, L1.in + 1, grad + n1.offset[l], grad + n1.offset[l] + (int64_t)L1.in * L1.out,
                     p2, grad + n2.offset[l], grad + n2.offset[l] + (int64_t)L2.in * L2.out);
             }
@@ -955,11 +1386,82 @@ void twin_bwd(const rlp_dense_net &n1, const rlp_dense_net &n2, const float *par
     }
 }
 
+// dY -> every layer's weight-gradient partials (left in np for adam_reduce_kernel) of a
+// three-layer relu chain: the data chain writes dH2 / dH1 to d2 / d1, then all three dW | db
+// products in one launch (instead of three launches that each paired a layer's weight gradient
+// with its backward data GEMM). Partial regions in net_bwd's order (the last layer first).
+bool chain_grad(const rlp_dense_net &n, const float *params, const Opnd &x, int B, const float *act,
+                const float *dy, float *d2, float *d1, float *part, int splits, NetParts *np,
+                hipStream_t s) {
+    if (!np || !d2 || !d1 || !chain3_bwd_ok(n) || np->n + 3 > kMaxParts) return false;
+    const ChainBwdArgs c = chain3_bwd_args(n, params, act, B, dy, 0, 0, nullptr, nullptr, nullptr, d2, d1);
+    chain_bwd_launch(c, c, 1, s);
+    const float *dys[3] = {dy, d2, d1};  // layers 2, 1, 0
+    Prob q[3];
+    int64_t po = 0;
+    for (int k = 0; k < 3; ++k) {
+        const int l = 2 - k;
+        const Layer L = layer_of(n, params, l);
+        const Opnd xin = l == 0 ? x : mat(layer_out(n, act, B, l - 1), B, L.in, L.in);
+        q[k] = wgrad_prob(dys[k], xin, L, B, part + po, splits, -1);
+        parts_add(np, part + po, q[k].nz, L.in, L.out, n.offset[l]);
+        po += (int64_t)splits * L.out * (L.in + 1);
+    }
+    gemm_multi(q, 3, s);
+    return true;
+}
+
+// the same for two same-shaped chains (the SAC critic's Q1 / Q2: one data-chain launch, six
+// weight-gradient problems in one launch; regions per layer Q1 then Q2, as twin_bwd's)
+bool twin_chain_grad(const rlp_dense_net &n1, const rlp_dense_net &n2, const float *params, const Opnd &x,
+                     int B, const float *act1, const float *act2, const float *dy1, const float *dy2,
+                     float *const d[4], float *part, int splits, NetParts *np, hipStream_t s) {
+    if (!np || !same_dims(n1, n2) || !chain3_bwd_ok(n1) || np->n + 6 > kMaxParts) return false;
+    const ChainBwdArgs c1 = chain3_bwd_args(n1, params, act1, B, dy1, 0, 0, nullptr, nullptr, nullptr, d[0], d[1]);
+    const ChainBwdArgs c2 = chain3_bwd_args(n2, params, act2, B, dy2, 0, 0, nullptr, nullptr, nullptr, d[2], d[3]);
+    chain_bwd_launch(c1, c2, 2, s);
+    const float *dys[2][3] = {{dy1, d[0], d[1]}, {dy2, d[2], d[3]}};
+    const rlp_dense_net *ns[2] = {&n1, &n2};
+    const float *acts[2] = {act1, act2};
+    Prob q[6];
+    int64_t po = 0;
+    for (int k = 0; k < 3; ++k) {
+        const int l = 2 - k;
+        for (int h = 0; h < 2; ++h) {
+            const rlp_dense_net &nn = *ns[h];
+            const Layer L = layer_of(nn, params, l);
+            const Opnd xin = l == 0 ? x : mat(layer_out(nn, acts[h], B, l - 1), B, L.in, L.in);
+            q[2 * k + h] = wgrad_prob(dys[h][k], xin, L, B, part + po, splits, -1);
+            parts_add(np, part + po, q[2 * k + h].nz, L.in, L.out, nn.offset[l]);
+            po += (int64_t)splits * L.out * (L.in + 1);
+        }
+    }
+    gemm_multi(q, 6, s);
+    return true;
+}
+
 // rlp_mlp_forward on the tiled GEMM (one launch per layer) for large batches: y = MLP(x) for
 // the plain Linear-stack layout (W_l [out][in] then b_l), activations RLP_ACT_*; the hidden
 // activations in stream-ordered scratch
 int dense_mlp_forward(const rlp_mlp_desc &d, const float *params, const float *x, float *y, int n,
                       hipStream_t s) {
+    if (d.n_layers == 3 && d.act[0] == RLP_ACT_RELU && d.act[1] == RLP_ACT_RELU &&
+        (d.act[2] == RLP_ACT_NONE || d.act[2] == RLP_ACT_TANH) && d.dims[0] <= kChK0 &&
+        d.dims[1] <= kChH && d.dims[1] % 32 == 0 && d.dims[2] <= kChH && d.dims[2] % 32 == 0 &&
+        d.dims[3] <= 8) {  // the DDPG / SAC actors' batched inference: one chain launch
+        ChainArgs c{};
+        const int64_t o1 = (int64_t)d.dims[0] * d.dims[1] + d.dims[1];
+        const int64_t o2 = o1 + (int64_t)d.dims[1] * d.dims[2] + d.dims[2];
+        c.x0 = c.x1 = x; c.ld0 = c.ld1 = d.dims[0]; c.split = d.dims[0]; c.K0 = d.dims[0];
+        c.W1 = params; c.b1 = params + (int64_t)d.dims[0] * d.dims[1];
+        c.W2 = params + o1; c.b2 = c.W2 + (int64_t)d.dims[1] * d.dims[2];
+        c.W3 = c.W3b = params + o2; c.b3 = c.W3 + (int64_t)d.dims[2] * d.dims[3];
+        c.H1 = d.dims[1]; c.H2 = d.dims[2]; c.NO = d.dims[3]; c.split3 = c.NO; c.B = n;
+        c.y = y; c.head = d.act[2] == RLP_ACT_TANH ? 2 : 0;
+        chain_fwd_launch(c, c, 1, s);
+        RLP_CHECK_LAUNCH("rlp_mlp_forward (chain)");
+        return RLP_OK;
+    }
     int maxw = 0;
     for (int l = 1; l < d.n_layers; ++l) maxw = d.dims[l] > maxw ? d.dims[l] : maxw;
     float *buf = nullptr;
@@ -1015,7 +1517,7 @@ int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const fl
     const DdpgWs w = ddpg_ws(n, B);
     float *ta = work + w.ta, *tc = work + w.tc, *c = work + w.c, *pa = work + w.pa, *pc = work + w.pc;
     float *ta_t = work + w.ta_t, *pa_t = work + w.pa_t, *g0 = work + w.g0, *g1 = work + w.g1;
-    float *dq = work + w.dq, *part = work + w.part;
+    float *g2 = work + w.g2, *dq = work + w.dq, *part = work + w.part;
     const int splits = (B + kWgradRows - 1) / kWgradRows;
     const int La = n.actor.n_layers, Lc = n.critic.n_layers;
 
@@ -1030,8 +1532,9 @@ int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const fl
                                        layer_out(n.critic, c, B, Lc - 1), B, cfg->gamma, g0, losses,
                                        n.steps);
     NetParts cp{};
-    net_bwd(n.critic, n.critic.params, n.critic_grad, sa, B, c, g0, g0, g1, part, splits, 0, 0, nullptr,
-            nullptr, nullptr, st, &cp);
+    if (!chain_grad(n.critic, n.critic.params, sa, B, c, g0, g1, g2, part, splits, &cp, st))
+        net_bwd(n.critic, n.critic.params, n.critic_grad, sa, B, c, g0, g0, g1, part, splits, 0, 0,
+                nullptr, nullptr, nullptr, st, &cp);
     // critic Adam + its soft target update (DDPG.py:113-115; the target critic is not read again)
     adam_reduce(n.critic.params, n.critic_grad, n.critic_m, n.critic_v, n.critic.n_params, cp,
                 cfg->critic_adam, n.steps + 1, n.target_critic.params, cfg->critic_tau, st);
@@ -1046,7 +1549,7 @@ int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const fl
     // dq now holds dL/dz of the actor's head ([B][A]); back through the actor
     const Opnd s_in = mat(s, B, S, S);
     NetParts ap{};
-    {
+    if (!chain_grad(n.actor, n.actor.params, s_in, B, pa, dq, g0, g1, part, splits, &ap, st)) {
         float *dy = dq, *d0 = g0, *d1 = g1;
         int64_t po = 0;
         for (int l = La - 1; l >= 0; --l) {
@@ -1120,6 +1623,20 @@ SacWs sac_ws(const rlp_sac_nets &n, int B) {
 
 // trunk (relu after every layer) then the head GEMM z = h [Wm; Wl]^T (biases added by the head kernel)
 void sac_actor_fwd(const rlp_sac_nets &n, const float *x, int B, float *act, float *z, hipStream_t s) {
+    const rlp_dense_net &t = n.actor;
+    if (t.n_layers == 2 && t.dims[0] <= kChK0 && t.dims[1] <= kChH && t.dims[1] % 32 == 0 &&
+        t.dims[2] <= kChH && t.dims[2] % 32 == 0) {  // trunk + both heads in one launch
+        const int A = n.action_dim;
+        const Layer L1 = layer_of(t, t.params, 0), L2 = layer_of(t, t.params, 1);
+        ChainArgs c{};
+        c.x0 = c.x1 = x; c.ld0 = c.ld1 = t.dims[0]; c.split = t.dims[0]; c.K0 = t.dims[0];
+        c.W1 = L1.W; c.b1 = L1.b; c.W2 = L2.W; c.b2 = L2.b;
+        c.W3 = t.params + n.mean_offset; c.W3b = t.params + n.log_std_offset; c.split3 = A; c.b3 = nullptr;
+        c.H1 = t.dims[1]; c.H2 = t.dims[2]; c.NO = 2 * A; c.B = B;
+        c.h1 = act; c.h2 = act + (int64_t)B * c.H1; c.y = z;
+        chain_fwd_launch(c, c, 1, s);
+        return;
+    }
     Opnd in = mat(x, B, n.actor.dims[0], n.actor.dims[0]);
     int64_t o = 0;
     for (int l = 0; l < n.actor.n_layers; ++l) {
@@ -1303,7 +1820,9 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
                                                layer_out(n.q2, W(w.c2), B, Lq2 - 1), W(w.y), B,
                                                W(w.g1), W(w.g2), losses);
     NetParts cp{};
-    if (twin) {
+    if (twin && twin_chain_grad(n.q1, n.q2, n.q1.params, bx, B, W(w.c1), W(w.c2), W(w.g1), W(w.g2), dd,
+                                W(w.part), splits, &cp, st)) {
+    } else if (twin) {
         twin_bwd(n.q1, n.q2, n.q1.params, n.critic_grad, bx, B, W(w.c1), W(w.c2), W(w.g1), W(w.g2), dd,
                  W(w.part), W(w.part2), splits, 0, 0, nullptr, nullptr, st, &cp);
     } else {
@@ -1418,6 +1937,7 @@ __global__ void __launch_bounds__(256) chunk_sum_kernel(const float *__restrict_
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     float s = 0.f;
+#pragma unroll 4
     for (int c = 0; c < nchunks; ++c) s += slots[(size_t)c * n + i];
     grad[i] = s;
 }

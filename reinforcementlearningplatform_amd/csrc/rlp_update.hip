@@ -808,6 +808,10 @@ ppo2_reduce_kernel(MfmaNet net, const float *__restrict__ part, int nw,
         if (i < H * S + H) { src = part3; off = A * H + A + i; stride = p3; cnt = n3; }       // W1, b1
         else if (i < H * S + H + H * H + H) { src = part; off = i - (H * S + H); stride = pw; cnt = nw; }  // W2, b2
         else { src = part3; off = i - (H * S + 2 * H + H * H); stride = p3; cnt = n3; }        // W3, b3
+        // (unrolled: the loads of 8 partials in flight at once, the adds still in partial order —
+        // the W1 / W3 outputs walk 2 048 / kRedSplit FD partials each, one exposed load latency
+        // per partial without it)
+#pragma unroll 8
         for (int b = sl; b < cnt; b += kRedSplit) acc += src[(size_t)b * stride + off];
     }
     __shared__ float red[kRedSplit][64];

@@ -252,6 +252,29 @@ def assert_f32_class(name, native, torch32, truth_n, truth_t, floor_rel=2e-7):
     assert en <= 4 * e32 + floor, (name, en, e32, floor)
 
 
+ADAM_LR = {"actor": 1e-4, "critic": 3e-4}   # make_agent's Actor / Critic learning rates
+ADAM_EPS = 1e-8                              # torch.optim.Adam's default eps (DDPG.py's optimisers)
+
+
+def assert_adam_tracks(name, native, torch32, gmin, lr, steps, rtol=1e-4, atol=2e-6):
+    """Parameters after `steps` Adam steps agree to rtol / atol, except where a gradient sat in
+    Adam's eps regime: the step is lr m / (sqrt(v_hat) + eps) with sqrt(v_hat) ~ |g|, so for
+    |g| ~ eps it is a steep function of g and two f32 summation orders of a gradient that
+    cancels to ~1e-7 of max|g| move the element apart by a fraction of lr (the one element of the
+    critic's 68 609 that does so at batch 1000: |g| = 6e-9, steps 0.37 / 0.39 lr). Such elements
+    (min over the steps of the torch |g| below 10 eps) may differ by at most 2 lr per step, and
+    there may be only a few."""
+    d = (native - torch32).abs()
+    bad = d > atol + rtol * torch32.abs()
+    nbad = int(bad.sum())
+    if nbad == 0:
+        return
+    assert nbad <= max(2, native.numel() // 10000), (name, nbad)
+    assert bool((gmin[bad] < 10 * ADAM_EPS).all()), (name, "outside Adam's eps regime",
+                                                     gmin[bad].max().item(), d.max().item())
+    assert float(d[bad].max()) <= 2 * lr * steps, (name, d.max().item())
+
+
 @pytest.mark.parametrize("B", [4096, 1000])
 def test_native_ddpg_tracks_torch_update(B):
     """rlp_ddpg_update against the torch autograd + Adam path from the same weights over 5
@@ -265,6 +288,7 @@ def test_native_ddpg_tracks_torch_update(B):
     av0 = n_agent.critic.action_value.weight.detach().clone()
     tav0 = n_agent.target_critic.action_value.weight.detach().clone()
     import copy
+    gmin = {}
     for it in range(5):
         batch = _batch(B, it)
         before = [copy.deepcopy(getattr(t_agent, k)) for k in
@@ -276,13 +300,18 @@ def test_native_ddpg_tracks_torch_update(B):
         if it == 0:   # the same start: both gradients against float64, f32-class bound
             tn = ddpg_f64_grads(before, n_agent.critic, batch)
             tt = ddpg_f64_grads(before, t_agent.critic, batch)
-            for k in ("critic", "actor"):
-                gt = torch.cat([p.grad.reshape(-1) if p.grad is not None else torch.zeros_like(p).reshape(-1)
-                                for p in getattr(t_agent, k).parameters()])
+        for k in ("critic", "actor"):
+            gt = torch.cat([p.grad.reshape(-1) if p.grad is not None else torch.zeros_like(p).reshape(-1)
+                            for p in getattr(t_agent, k).parameters()])
+            gmin[k] = gt.abs() if it == 0 else torch.minimum(gmin[k], gt.abs())
+            if it == 0:
                 assert_f32_class(k, n_agent._native.grad[k].cpu(), gt.cpu(), tn[k], tt[k])
     for k in ("actor", "target_actor", "critic", "target_critic"):
-        torch.testing.assert_close(_flat(getattr(n_agent, k)), _flat(getattr(t_agent, k)),
-                                   rtol=1e-4, atol=2e-6, msg=k)
+        a, b = _flat(getattr(n_agent, k)), _flat(getattr(t_agent, k))
+        if k in ADAM_LR:
+            assert_adam_tracks(k, a, b, gmin[k], ADAM_LR[k], 5)
+        else:
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=2e-6, msg=lambda m, k=k: f"{k}: {m}")
     assert torch.equal(n_agent.critic.action_value.weight, av0)
     tav = n_agent.target_critic.action_value.weight
     assert not torch.equal(tav, tav0)
