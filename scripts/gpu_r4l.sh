@@ -2,7 +2,8 @@
 # Round-4 call l: the full GPU suite on exp10 (exp9 + eight-wave chains), then the off-policy /
 # demo legs on exp7 (chains, SAC actor chain), exp8 (+ the actors' batched-inference chain),
 # exp9 (+ multi-problem GEMM launches and the weight-gradient chains) and exp10, and exp10's
-# learn() timelines.
+# learn() timelines. Call n: V=exp12 AB="base exp11 exp12" (exp11: two 16-row tiles per forward
+# block for batched inference; exp12: + the SAC actor's backward as one data chain + one launch).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; TAG=${TAG:-r4l}; mkdir -p "$OUT/$TAG"
@@ -15,7 +16,7 @@ rc=$?; echo "tests rc=$rc"; tail -12 "$OUT/$TAG/tests.log"
 case $rc in 0|1) ;; *) exit $rc;; esac
 LEGS="--steps 3 --warmup 1 --no-cpu-baseline --e2e 0 --e2e-k30 0 --demo-e2e 1 --uav 0 --hbm 0 --fp32-leg 0 --oa 0 --ddpg 1 --sac 1"
 for v in ${AB:-exp7 exp8 exp9 exp10}; do
-  export RLP_LIBRARY=$ROOT/$LIBD/$v/librlp.so
+  if [ $v = base ]; then unset RLP_LIBRARY; else export RLP_LIBRARY=$ROOT/$LIBD/$v/librlp.so; fi
   (cd /tmp && timeout -k 10 300 python3 "$ROOT/bench.py" $LEGS) > "$OUT/$TAG/bench_$v.log" 2>&1
   rc=$?; echo "bench $v rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done

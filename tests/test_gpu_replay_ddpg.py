@@ -144,11 +144,12 @@ def test_ddpg_update_matches_reference(golden, native):
 
 def test_batched_actor_and_noise():
     agent = make_agent()
-    s = torch.rand(5000, 4, device="cuda") * 4 - 2
-    a0 = agent.choose_action(s, is_optimal=True)
-    with torch.no_grad():
-        ref = agent.actor(s)
-    torch.testing.assert_close(a0, ref, rtol=1e-5, atol=2e-6)   # ReLU net through librlp
+    for n in (40_001, 5000):   # the fused inference chain with two / one 16-row tiles per block
+        s = torch.rand(n, 4, device="cuda") * 4 - 2
+        a0 = agent.choose_action(s, is_optimal=True)
+        with torch.no_grad():
+            ref = agent.actor(s)
+        torch.testing.assert_close(a0, ref, rtol=1e-5, atol=2e-6)   # ReLU net through librlp
     sig = np.array([0.5, 0.5], np.float32)
     a1 = agent.choose_action(s, sigma=sig)
     z = ((a1 - ref) / 0.5)[(a1.abs() < 2.9).all(1)]             # unclipped rows
