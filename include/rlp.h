@@ -247,7 +247,10 @@ typedef struct rlp_mlp_desc {
 int64_t rlp_mlp_param_count(const rlp_mlp_desc *desc);
 
 /* Batched forward y[n][out] = MLP(x[n][in]) (nn.Sequential / driver forward()), fp32, MFMA
- * (v_mfma_f32_16x16x4_f32) for every layer; rows with mask[i]==0 are skipped (mask nullable). */
+ * (v_mfma_f32_16x16x4_f32) for every layer; rows with mask[i]==0 are skipped (mask nullable).
+ * Unmasked batches of >= 2048 rows run on the tiled GEMM, one launch per layer — or, for the
+ * DDPG / SAC actors' shape (three layers, relu, relu, tanh / none, <= 64 inputs, hidden widths
+ * multiples of 32 up to 256, <= 8 outputs), all three layers in one fused launch. */
 int rlp_mlp_forward(const rlp_mlp_desc *desc, const float *params, const float *x, float *y, int n,
                     const uint8_t *mask, rlp_stream_t stream);
 

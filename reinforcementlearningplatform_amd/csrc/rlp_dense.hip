@@ -701,16 +701,17 @@ __device__ __forceinline__ void chain_block(const floatx4 &f, const floatx4 (&b)
         for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[u], b[j][u], acc[j], 0, 0, 0);
 }
 
-template <int NT1, int NT2>
+template <int NT1, int NT2, int RT>
 __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, ChainArgs a1) {
+    constexpr int ROWS = kChRows * RT, RPW = ROWS / kChWaves;  // block rows, layer-3 rows per wave
     const ChainArgs &a = blockIdx.y ? a1 : a0;
-    __shared__ __attribute__((aligned(16))) float xs[kChRows][kChK0 + 4];
-    __shared__ __attribute__((aligned(16))) float hs1[kChRows][kChLd];
-    __shared__ __attribute__((aligned(16))) float hs2[kChRows][kChLd];
+    __shared__ __attribute__((aligned(16))) float xs[ROWS][kChK0 + 4];
+    __shared__ __attribute__((aligned(16))) float hs1[ROWS][kChLd];
+    __shared__ __attribute__((aligned(16))) float hs2[ROWS][kChLd];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
-    const int r0 = blockIdx.x * kChRows;
+    const int r0 = blockIdx.x * ROWS;
     const int K8 = (a.K0 + 7) & ~7;  // zero-padded input columns: two 4-deep steps per pass
-    for (int i = t; i < kChRows * K8; i += kChThreads) {
+    for (int i = t; i < ROWS * K8; i += kChThreads) {
         const int rr = i / K8, k = i % K8, r = r0 + rr;
         float v = 0.f;
         if (r < a.B && k < a.K0) v = k < a.split ? a.x0[(int64_t)r * a.ld0 + k] : a.x1[(int64_t)r * a.ld1 + k - a.split];
@@ -720,13 +721,14 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
     // layer 1: k outer (one W1 element per tile and step, the next step's in flight)
     {
         int row[NT1];
-        floatx4 acc[NT1];
+        floatx4 acc[RT][NT1];
 #pragma unroll
         for (int j = 0; j < NT1; ++j) {
             const int n = 16 * (w + kChWaves * j) + c;
             row[j] = n < a.H1 ? n : a.H1 - 1;
             const float bb = a.b1[row[j]];
-            acc[j] = floatx4{bb, bb, bb, bb};
+#pragma unroll
+            for (int q = 0; q < RT; ++q) acc[q][j] = floatx4{bb, bb, bb, bb};
         }
         float wa[NT1], wb[NT1];
         auto ld1 = [&](int k, float (&v)[NT1]) {  // k past K0: a clamped column (its x is 0)
@@ -737,37 +739,47 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
         ld1(g, wa);
         for (int k4 = 0; k4 < K8; k4 += 8) {
             ld1(k4 + 4 + g, wb);
-            const float x0 = xs[c][k4 + g];
 #pragma unroll
-            for (int j = 0; j < NT1; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, wa[j], acc[j], 0, 0, 0);
+            for (int q = 0; q < RT; ++q) {
+                const float x0 = xs[16 * q + c][k4 + g];
+#pragma unroll
+                for (int j = 0; j < NT1; ++j) acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, wa[j], acc[q][j], 0, 0, 0);
+            }
             ld1(k4 + 8 + g, wa);
-            const float x1 = xs[c][k4 + 4 + g];
 #pragma unroll
-            for (int j = 0; j < NT1; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, wb[j], acc[j], 0, 0, 0);
+            for (int q = 0; q < RT; ++q) {
+                const float x1 = xs[16 * q + c][k4 + 4 + g];
+#pragma unroll
+                for (int j = 0; j < NT1; ++j) acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, wb[j], acc[q][j], 0, 0, 0);
+            }
         }
 #pragma unroll
         for (int j = 0; j < NT1; ++j) {
             const int n = 16 * (w + kChWaves * j) + c;
             if (n >= a.H1) continue;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float v = fmaxf(acc[j][i], 0.f);
-                hs1[4 * g + i][n] = v;
-                if (a.h1 && r0 + 4 * g + i < a.B) a.h1[(int64_t)(r0 + 4 * g + i) * a.H1 + n] = v;
-            }
+            for (int q = 0; q < RT; ++q)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rr = 16 * q + 4 * g + i;
+                    const float v = fmaxf(acc[q][j][i], 0.f);
+                    hs1[rr][n] = v;
+                    if (a.h1 && r0 + rr < a.B) a.h1[(int64_t)(r0 + rr) * a.H1 + n] = v;
+                }
         }
     }
     __syncthreads();
-    // layer 2 (H1 a multiple of 32)
+    // layer 2 (H1 a multiple of 32); each B fragment feeds the RT row tiles
     {
         int row[NT2];
-        floatx4 acc[NT2];
+        floatx4 acc[RT][NT2];
 #pragma unroll
         for (int j = 0; j < NT2; ++j) {
             const int n = 16 * (w + kChWaves * j) + c;
             row[j] = n < a.H2 ? n : a.H2 - 1;
             const float bb = a.b2[row[j]];
-            acc[j] = floatx4{bb, bb, bb, bb};
+#pragma unroll
+            for (int q = 0; q < RT; ++q) acc[q][j] = floatx4{bb, bb, bb, bb};
         }
         floatx4 ba[NT2], bb[NT2];
         auto ld2 = [&](int kb, floatx4 (&v)[NT2]) {  // kb past H1: a clamped reload, unused
@@ -778,13 +790,19 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
         ld2(0, ba);
         ld2(16, bb);
         for (int kb = 0; kb < a.H1; kb += 32) {  // (sched barriers: the scheduler sinks the loads)
-            const floatx4 f0 = *reinterpret_cast<const floatx4 *>(&hs1[c][kb + 4 * g]);
-            const floatx4 f1 = *reinterpret_cast<const floatx4 *>(&hs1[c][kb + 16 + 4 * g]);
-            chain_block<NT2>(f0, ba, acc);
+            floatx4 f0[RT], f1[RT];
+#pragma unroll
+            for (int q = 0; q < RT; ++q) {
+                f0[q] = *reinterpret_cast<const floatx4 *>(&hs1[16 * q + c][kb + 4 * g]);
+                f1[q] = *reinterpret_cast<const floatx4 *>(&hs1[16 * q + c][kb + 16 + 4 * g]);
+            }
+#pragma unroll
+            for (int q = 0; q < RT; ++q) chain_block<NT2>(f0[q], ba, acc[q]);
             __builtin_amdgcn_sched_barrier(0);
             ld2(kb + 32, ba);
             __builtin_amdgcn_sched_barrier(0);
-            chain_block<NT2>(f1, bb, acc);
+#pragma unroll
+            for (int q = 0; q < RT; ++q) chain_block<NT2>(f1[q], bb, acc[q]);
             __builtin_amdgcn_sched_barrier(0);
             ld2(kb + 48, bb);
             __builtin_amdgcn_sched_barrier(0);
@@ -794,20 +812,23 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
             const int n = 16 * (w + kChWaves * j) + c;
             if (n >= a.H2) continue;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float v = fmaxf(acc[j][i], 0.f);
-                hs2[4 * g + i][n] = v;
-                if (a.h2 && r0 + 4 * g + i < a.B) a.h2[(int64_t)(r0 + 4 * g + i) * a.H2 + n] = v;
-            }
+            for (int q = 0; q < RT; ++q)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rr = 16 * q + 4 * g + i;
+                    const float v = fmaxf(acc[q][j][i], 0.f);
+                    hs2[rr][n] = v;
+                    if (a.h2 && r0 + rr < a.B) a.h2[(int64_t)(r0 + rr) * a.H2 + n] = v;
+                }
         }
     }
     __syncthreads();
-    // layer 3: wave w, rows kChRpw w ..
+    // layer 3: wave w, rows RPW w ..
     for (int o = 0; o < a.NO; ++o) {
         const float *w3 = o < a.split3 ? a.W3 + (int64_t)o * a.H2 : a.W3b + (int64_t)(o - a.split3) * a.H2;
 #pragma unroll
-        for (int i = 0; i < kChRpw; ++i) {
-            const int rr = kChRpw * w + i;
+        for (int i = 0; i < RPW; ++i) {
+            const int rr = RPW * w + i;
             float z = 0.f;
             for (int k = lane; k < a.H2; k += 64) z = __builtin_fmaf(hs2[rr][k], w3[k], z);
 #pragma unroll
@@ -844,6 +865,8 @@ struct ChainBwdArgs {
     float *dx;                       // [B][nc] (nc = 0: none)
     float *d2, *d1;                  // dH2 [B][H2], dH1 [B][H1] to HBM when set (the weight
                                      // gradients' dY operands)
+    const float *W3b;                // rows [split3, NO) of W3 from W3b (the SAC actor's heads)
+    int split3;
 };
 
 template <int NT>
@@ -859,7 +882,10 @@ __global__ void __launch_bounds__(kChThreads) chain3_bwd_kernel(ChainBwdArgs a0,
         float v = 0.f;
         if (r < a.B && a.h2[(int64_t)r * a.H2 + o] > 0.f) {
             v = a.dy[(int64_t)r * a.NO] * a.W3[o];
-            for (int j = 1; j < a.NO; ++j) v = __builtin_fmaf(a.dy[(int64_t)r * a.NO + j], a.W3[(int64_t)j * a.H2 + o], v);
+            for (int j = 1; j < a.NO; ++j) {
+                const float *w3 = j < a.split3 ? a.W3 + (int64_t)j * a.H2 : a.W3b + (int64_t)(j - a.split3) * a.H2;
+                v = __builtin_fmaf(a.dy[(int64_t)r * a.NO + j], w3[o], v);
+            }
         }
         gs2[rr][o] = v;
         if (a.d2 && r < a.B) a.d2[(int64_t)r * a.H2 + o] = v;
@@ -937,11 +963,16 @@ __global__ void __launch_bounds__(kChThreads) chain3_bwd_kernel(ChainBwdArgs a0,
 static_assert(kChMaxNt == 2, "chain launch tables");
 using ChainFwdFn = void (*)(ChainArgs, ChainArgs);
 inline int chain_nt(int h) { return (h / 16 + kChWaves - 1) / kChWaves; }
+constexpr int kChBigRows = 16384;  // rows from which a forward block takes two row tiles
 void chain_fwd_launch(const ChainArgs &c0, const ChainArgs &c1, int nchains, hipStream_t s) {
-    static const ChainFwdFn tab[2][2] = {{chain3_fwd_kernel<1, 1>, chain3_fwd_kernel<1, 2>},
-                                         {chain3_fwd_kernel<2, 1>, chain3_fwd_kernel<2, 2>}};
-    const ChainFwdFn f = tab[chain_nt(c0.H1) - 1][chain_nt(c0.H2) - 1];
-    f<<<dim3((c0.B + kChRows - 1) / kChRows, nchains), kChThreads, 0, s>>>(c0, c1);
+    // two 16-row tiles per block when the rows fill every CU twice over (batched inference: each
+    // layer-2 weight fragment then feeds twice the MFMAs, half the weight reads from L2)
+    static const ChainFwdFn tab[2][2][2] = {
+        {{chain3_fwd_kernel<1, 1, 1>, chain3_fwd_kernel<1, 2, 1>}, {chain3_fwd_kernel<2, 1, 1>, chain3_fwd_kernel<2, 2, 1>}},
+        {{chain3_fwd_kernel<1, 1, 2>, chain3_fwd_kernel<1, 2, 2>}, {chain3_fwd_kernel<2, 1, 2>, chain3_fwd_kernel<2, 2, 2>}}};
+    const int rt = c0.B >= kChBigRows ? 2 : 1;
+    const ChainFwdFn f = tab[rt - 1][chain_nt(c0.H1) - 1][chain_nt(c0.H2) - 1];
+    f<<<dim3((c0.B + kChRows * rt - 1) / (kChRows * rt), nchains), kChThreads, 0, s>>>(c0, c1);
 }
 void chain_bwd_launch(const ChainBwdArgs &c0, const ChainBwdArgs &c1, int nchains, hipStream_t s) {
     const dim3 grid((c0.B + kChRows - 1) / kChRows, nchains);
@@ -1206,6 +1237,7 @@ ChainBwdArgs chain3_bwd_args(const rlp_dense_net &n, const float *params, const 
     c.K0 = n.dims[0]; c.H1 = n.dims[1]; c.H2 = n.dims[2]; c.NO = n.dims[3]; c.B = B;
     c.h1 = act; c.h2 = act + (int64_t)B * c.H1;
     c.c0 = c0; c.nc = nc; c.t = t_in; c.gain = gain; c.dx = dx; c.d2 = d2; c.d1 = d1;
+    c.W3b = c.W3; c.split3 = c.NO;
     return c;
 }
 
@@ -1778,33 +1810,61 @@ int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float
         const Layer Ll{P + n.log_std_offset, P + n.log_std_offset + (int64_t)A * H, H, A};
         float *apart = W(w.apart);
         const int64_t hreg = (int64_t)splits * A * (H + 1);
-        {  // both heads' weight gradients in one launch, partials left for the actor's Adam
-            const Prob qm = wgrad_prob(W(w.gz), hx, Lm, B, apart, splits, 2 * A);
-            const Prob ql = wgrad_prob(W(w.gz) + A, hx, Ll, B, apart + hreg, splits, 2 * A);
-            const int z = gemm_launch(qm, &ql, st);
-            parts_add(&ap, apart, z, H, A, n.mean_offset);
-            parts_add(&ap, apart + hreg, z, H, A, n.log_std_offset);
-        }
         int64_t po = 2 * hreg;
-        // dh = (gz [Wm; Wl]) * relu'(h)
-        Epi e{};
-        e.y = W(w.d0); e.ldy = H; e.kind = kEpiReluBack; e.M = B; e.N = H; e.mask = h_last; e.ldm = H;
-        gemm(mat(W(w.gz), B, 2 * A, 2 * A), Opnd{Lm.W, Ll.W, H, 1, H, 1, 2 * A, H, A, -1, 1}, B, H,
-             2 * A, 1, e, st);
-        float *dy = W(w.d0), *dn = W(w.d1);
-        for (int l = Lt - 1; l >= 0; --l) {
-            const Layer L = layer_of(n.actor, P, l);
-            const Opnd xin = l == 0 ? mat(s, B, S, S) : mat(layer_out(n.actor, W(w.ta), B, l - 1), B, L.in, L.in);
-            float *gW = G + n.actor.offset[l], *gb = gW + (int64_t)L.in * L.out;
-            float *pl = apart + po;
-            po += (int64_t)splits * L.out * (L.in + 1);
-            if (l > 0) {
-                dense_wgrad_bwd(dy, xin, L, B, pl, splits, gW, gb, 0, L.in, kEpiReluBack,
-                                layer_out(n.actor, W(w.ta), B, l - 1), L.in, nullptr, dn, st, &ap,
-                                n.actor.offset[l]);
-                float *tmp = dy; dy = dn; dn = tmp;
-            } else {
-                dense_wgrad(dy, xin, L, B, pl, splits, gW, gb, st, -1, &ap, n.actor.offset[l]);
+        const rlp_dense_net &t = n.actor;
+        if (Lt == 2 && t.dims[1] <= kChH && t.dims[1] % 32 == 0 && t.dims[2] <= kChH &&
+            t.dims[2] % 32 == 0 && ap.n + 4 <= kMaxParts) {
+            // the heads' and the trunk's backward as one data chain (dh = (gz [Wm; Wl]) relu'(h2),
+            // dh1 = (dh W2) relu'(h1)), then the four weight gradients in one launch
+            ChainBwdArgs c{};
+            c.dy = W(w.gz); c.NO = 2 * A; c.W3 = Lm.W; c.W3b = Ll.W; c.split3 = A;
+            c.W1 = layer_of(t, P, 0).W; c.W2 = layer_of(t, P, 1).W;
+            c.K0 = t.dims[0]; c.H1 = t.dims[1]; c.H2 = t.dims[2]; c.B = B;
+            c.h1 = W(w.ta); c.h2 = h_last; c.d2 = W(w.d0); c.d1 = W(w.d1);
+            chain_bwd_launch(c, c, 1, st);
+            Prob q[4];
+            q[0] = wgrad_prob(W(w.gz), hx, Lm, B, apart, splits, 2 * A);
+            q[1] = wgrad_prob(W(w.gz) + A, hx, Ll, B, apart + hreg, splits, 2 * A);
+            parts_add(&ap, apart, q[0].nz, H, A, n.mean_offset);
+            parts_add(&ap, apart + hreg, q[1].nz, H, A, n.log_std_offset);
+            const float *dys[2] = {W(w.d0), W(w.d1)};  // layers 1, 0
+            for (int k = 0; k < 2; ++k) {
+                const int l = 1 - k;
+                const Layer L = layer_of(t, P, l);
+                const Opnd xin = l == 0 ? mat(s, B, S, S) : mat(W(w.ta), B, L.in, L.in);
+                q[2 + k] = wgrad_prob(dys[k], xin, L, B, apart + po, splits, -1);
+                parts_add(&ap, apart + po, q[2 + k].nz, L.in, L.out, t.offset[l]);
+                po += (int64_t)splits * L.out * (L.in + 1);
+            }
+            gemm_multi(q, 4, st);
+        } else {
+            {  // both heads' weight gradients in one launch, partials left for the actor's Adam
+                const Prob qm = wgrad_prob(W(w.gz), hx, Lm, B, apart, splits, 2 * A);
+                const Prob ql = wgrad_prob(W(w.gz) + A, hx, Ll, B, apart + hreg, splits, 2 * A);
+                const int z = gemm_launch(qm, &ql, st);
+                parts_add(&ap, apart, z, H, A, n.mean_offset);
+                parts_add(&ap, apart + hreg, z, H, A, n.log_std_offset);
+            }
+            // dh = (gz [Wm; Wl]) * relu'(h)
+            Epi e{};
+            e.y = W(w.d0); e.ldy = H; e.kind = kEpiReluBack; e.M = B; e.N = H; e.mask = h_last; e.ldm = H;
+            gemm(mat(W(w.gz), B, 2 * A, 2 * A), Opnd{Lm.W, Ll.W, H, 1, H, 1, 2 * A, H, A, -1, 1}, B, H,
+                 2 * A, 1, e, st);
+            float *dy = W(w.d0), *dn = W(w.d1);
+            for (int l = Lt - 1; l >= 0; --l) {
+                const Layer L = layer_of(n.actor, P, l);
+                const Opnd xin = l == 0 ? mat(s, B, S, S) : mat(layer_out(n.actor, W(w.ta), B, l - 1), B, L.in, L.in);
+                float *gW = G + n.actor.offset[l], *gb = gW + (int64_t)L.in * L.out;
+                float *pl = apart + po;
+                po += (int64_t)splits * L.out * (L.in + 1);
+                if (l > 0) {
+                    dense_wgrad_bwd(dy, xin, L, B, pl, splits, gW, gb, 0, L.in, kEpiReluBack,
+                                    layer_out(n.actor, W(w.ta), B, l - 1), L.in, nullptr, dn, st, &ap,
+                                    n.actor.offset[l]);
+                    float *tmp = dy; dy = dn; dn = tmp;
+                } else {
+                    dense_wgrad(dy, xin, L, B, pl, splits, gW, gb, st, -1, &ap, n.actor.offset[l]);
+                }
             }
         }
     }
@@ -1862,7 +1922,7 @@ namespace rlp {
 //             partial per slice), dX = dY W with the tanh backward (1 - h^2) epilogue
 // Every chunk's gradient lands in its own slot; the slots are summed in chunk order (fixed order
 // throughout: the same bits on every run and rank).
-constexpr int kPpoChunk = 1 << 18;
+constexpr int kPpoChunk = 1 << 18;  // (2^20-row chunks: the same SOI / 1.5 % faster UGV-OA iterations, r4n)
 
 inline Prob make_prob_long(const Opnd &A, const Opnd &B, const Epi &e, int R, int nz) {
     if (nz < 1) nz = 1;
