@@ -687,8 +687,13 @@ struct ChainArgs {
                            // (h1 / h2 null: the hidden activations are not stored — inference)
     const float *gain, *off;
     float *aux;
+    int hact;              // hidden activation: 0 relu, 1 tanh (the PPO2 nets)
+    const float *Wm, *bm;  // optional fourth layer between layer 2 and the head: H2 -> Hm (Hm <= 128;
+    int Hm;                // Hm = 0: none), activations to hm [B][Hm]; the head then reads Hm inputs
+    float *hm;
 };
 constexpr int kChRows = 16, kChK0 = 64, kChH = 256, kChLd = kChH + 4;
+__device__ __forceinline__ float chain_act(float x, int hact) { return hact ? tanhf(x) : fmaxf(x, 0.f); }
 constexpr int kChWaves = 8, kChThreads = 64 * kChWaves, kChRpw = kChRows / kChWaves;  // rows per wave (layer 3)
 constexpr int kChMaxNt = kChH / 16 / kChWaves;  // 16-column tiles per wave at the widest layer
 
@@ -701,7 +706,7 @@ __device__ __forceinline__ void chain_block(const floatx4 &f, const floatx4 (&b)
         for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[u], b[j][u], acc[j], 0, 0, 0);
 }
 
-template <int NT1, int NT2, int RT>
+template <int NT1, int NT2, int RT, int NTM>
 __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, ChainArgs a1) {
     constexpr int ROWS = kChRows * RT, RPW = ROWS / kChWaves;  // block rows, layer-3 rows per wave
     const ChainArgs &a = blockIdx.y ? a1 : a0;
@@ -711,6 +716,34 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
     const int r0 = blockIdx.x * ROWS;
     const int K8 = (a.K0 + 7) & ~7;  // zero-padded input columns: two 4-deep steps per pass
+    // both layers' first weight fragments are in flight before the input rows land (they do not
+    // depend on them: one L2 / HBM latency less on the chain's critical path)
+    int row1[NT1], row2[NT2];
+#pragma unroll
+    for (int j = 0; j < NT1; ++j) {
+        const int n = 16 * (w + kChWaves * j) + c;
+        row1[j] = n < a.H1 ? n : a.H1 - 1;
+    }
+#pragma unroll
+    for (int j = 0; j < NT2; ++j) {
+        const int n = 16 * (w + kChWaves * j) + c;
+        row2[j] = n < a.H2 ? n : a.H2 - 1;
+    }
+    auto ld1 = [&](int k, float (&v)[NT1]) {  // k past K0: a clamped column (its x is 0)
+        const int kk = k < a.K0 ? k : a.K0 - 1;
+#pragma unroll
+        for (int j = 0; j < NT1; ++j) v[j] = a.W1[(int64_t)row1[j] * a.K0 + kk];
+    };
+    auto ld2 = [&](int kb, floatx4 (&v)[NT2]) {  // kb past H1: a clamped reload, unused
+        const int k = (kb < a.H1 ? kb : a.H1 - 16) + 4 * g;
+#pragma unroll
+        for (int j = 0; j < NT2; ++j) v[j] = *reinterpret_cast<const floatx4 *>(a.W2 + (int64_t)row2[j] * a.H1 + k);
+    };
+    float wa[NT1], wb[NT1];
+    floatx4 ba[NT2], bb[NT2];
+    ld1(g, wa);
+    ld2(0, ba);
+    ld2(16, bb);
     for (int i = t; i < ROWS * K8; i += kChThreads) {
         const int rr = i / K8, k = i % K8, r = r0 + rr;
         float v = 0.f;
@@ -720,23 +753,13 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
     __syncthreads();
     // layer 1: k outer (one W1 element per tile and step, the next step's in flight)
     {
-        int row[NT1];
         floatx4 acc[RT][NT1];
 #pragma unroll
         for (int j = 0; j < NT1; ++j) {
-            const int n = 16 * (w + kChWaves * j) + c;
-            row[j] = n < a.H1 ? n : a.H1 - 1;
-            const float bb = a.b1[row[j]];
+            const float b1 = a.b1[row1[j]];
 #pragma unroll
-            for (int q = 0; q < RT; ++q) acc[q][j] = floatx4{bb, bb, bb, bb};
+            for (int q = 0; q < RT; ++q) acc[q][j] = floatx4{b1, b1, b1, b1};
         }
-        float wa[NT1], wb[NT1];
-        auto ld1 = [&](int k, float (&v)[NT1]) {  // k past K0: a clamped column (its x is 0)
-            const int kk = k < a.K0 ? k : a.K0 - 1;
-#pragma unroll
-            for (int j = 0; j < NT1; ++j) v[j] = a.W1[(int64_t)row[j] * a.K0 + kk];
-        };
-        ld1(g, wa);
         for (int k4 = 0; k4 < K8; k4 += 8) {
             ld1(k4 + 4 + g, wb);
 #pragma unroll
@@ -762,7 +785,7 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int rr = 16 * q + 4 * g + i;
-                    const float v = fmaxf(acc[q][j][i], 0.f);
+                    const float v = chain_act(acc[q][j][i], a.hact);
                     hs1[rr][n] = v;
                     if (a.h1 && r0 + rr < a.B) a.h1[(int64_t)(r0 + rr) * a.H1 + n] = v;
                 }
@@ -771,24 +794,13 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
     __syncthreads();
     // layer 2 (H1 a multiple of 32); each B fragment feeds the RT row tiles
     {
-        int row[NT2];
         floatx4 acc[RT][NT2];
 #pragma unroll
         for (int j = 0; j < NT2; ++j) {
-            const int n = 16 * (w + kChWaves * j) + c;
-            row[j] = n < a.H2 ? n : a.H2 - 1;
-            const float bb = a.b2[row[j]];
+            const float b2 = a.b2[row2[j]];
 #pragma unroll
-            for (int q = 0; q < RT; ++q) acc[q][j] = floatx4{bb, bb, bb, bb};
+            for (int q = 0; q < RT; ++q) acc[q][j] = floatx4{b2, b2, b2, b2};
         }
-        floatx4 ba[NT2], bb[NT2];
-        auto ld2 = [&](int kb, floatx4 (&v)[NT2]) {  // kb past H1: a clamped reload, unused
-            const int k = (kb < a.H1 ? kb : a.H1 - 16) + 4 * g;
-#pragma unroll
-            for (int j = 0; j < NT2; ++j) v[j] = *reinterpret_cast<const floatx4 *>(a.W2 + (int64_t)row[j] * a.H1 + k);
-        };
-        ld2(0, ba);
-        ld2(16, bb);
         for (int kb = 0; kb < a.H1; kb += 32) {  // (sched barriers: the scheduler sinks the loads)
             floatx4 f0[RT], f1[RT];
 #pragma unroll
@@ -816,21 +828,75 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int rr = 16 * q + 4 * g + i;
-                    const float v = fmaxf(acc[q][j][i], 0.f);
+                    const float v = chain_act(acc[q][j][i], a.hact);
                     hs2[rr][n] = v;
                     if (a.h2 && r0 + rr < a.B) a.h2[(int64_t)(r0 + rr) * a.H2 + n] = v;
                 }
         }
     }
     __syncthreads();
-    // layer 3: wave w, rows RPW w ..
+    if constexpr (NTM > 0) {  // the fourth layer (H2 a multiple of 32): hs2 -> hs1 (layer 2 has read hs1)
+        int rowm[NTM];
+        floatx4 acc[RT][NTM], ma[NTM], mb[NTM];
+#pragma unroll
+        for (int j = 0; j < NTM; ++j) {
+            const int n = 16 * (w + kChWaves * j) + c;
+            rowm[j] = n < a.Hm ? n : a.Hm - 1;
+            const float bv = a.bm[rowm[j]];
+#pragma unroll
+            for (int q = 0; q < RT; ++q) acc[q][j] = floatx4{bv, bv, bv, bv};
+        }
+        auto ldm = [&](int kb, floatx4 (&v)[NTM]) {
+            const int k = (kb < a.H2 ? kb : a.H2 - 16) + 4 * g;
+#pragma unroll
+            for (int j = 0; j < NTM; ++j) v[j] = *reinterpret_cast<const floatx4 *>(a.Wm + (int64_t)rowm[j] * a.H2 + k);
+        };
+        ldm(0, ma);
+        ldm(16, mb);
+        for (int kb = 0; kb < a.H2; kb += 32) {
+            floatx4 f0[RT], f1[RT];
+#pragma unroll
+            for (int q = 0; q < RT; ++q) {
+                f0[q] = *reinterpret_cast<const floatx4 *>(&hs2[16 * q + c][kb + 4 * g]);
+                f1[q] = *reinterpret_cast<const floatx4 *>(&hs2[16 * q + c][kb + 16 + 4 * g]);
+            }
+#pragma unroll
+            for (int q = 0; q < RT; ++q) chain_block<NTM>(f0[q], ma, acc[q]);
+            __builtin_amdgcn_sched_barrier(0);
+            ldm(kb + 32, ma);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < RT; ++q) chain_block<NTM>(f1[q], mb, acc[q]);
+            __builtin_amdgcn_sched_barrier(0);
+            ldm(kb + 48, mb);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < NTM; ++j) {
+            const int n = 16 * (w + kChWaves * j) + c;
+            if (n >= a.Hm) continue;
+#pragma unroll
+            for (int q = 0; q < RT; ++q)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rr = 16 * q + 4 * g + i;
+                    const float v = chain_act(acc[q][j][i], a.hact);
+                    hs1[rr][n] = v;
+                    if (a.hm && r0 + rr < a.B) a.hm[(int64_t)(r0 + rr) * a.Hm + n] = v;
+                }
+        }
+        __syncthreads();
+    }
+    // the head: wave w, rows RPW w .. (over hs2, or hs1 after the fourth layer)
+    const int KL = NTM > 0 ? a.Hm : a.H2;
+    float (*hl)[kChLd] = NTM > 0 ? hs1 : hs2;
     for (int o = 0; o < a.NO; ++o) {
-        const float *w3 = o < a.split3 ? a.W3 + (int64_t)o * a.H2 : a.W3b + (int64_t)(o - a.split3) * a.H2;
+        const float *w3 = o < a.split3 ? a.W3 + (int64_t)o * KL : a.W3b + (int64_t)(o - a.split3) * KL;
 #pragma unroll
         for (int i = 0; i < RPW; ++i) {
             const int rr = RPW * w + i;
             float z = 0.f;
-            for (int k = lane; k < a.H2; k += 64) z = __builtin_fmaf(hs2[rr][k], w3[k], z);
+            for (int k = lane; k < KL; k += 64) z = __builtin_fmaf(hl[rr][k], w3[k], z);
 #pragma unroll
             for (int m = 32; m > 0; m >>= 1) z += __shfl_xor(z, m);
             const int r = r0 + rr;
@@ -876,6 +942,22 @@ __global__ void __launch_bounds__(kChThreads) chain3_bwd_kernel(ChainBwdArgs a0,
     __shared__ __attribute__((aligned(16))) float gs1[kChRows][kChLd];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
     const int r0 = blockIdx.x * kChRows;
+    int col[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int n = 16 * (w + kChWaves * j) + c;
+        col[j] = n < a.H1 ? n : a.H1 - 1;
+    }
+    auto ld = [&](int kb, floatx4 (&v)[NT]) {  // kb past H2: a clamped reload, unused
+        const int k = (kb < a.H2 ? kb : a.H2 - 16) + 4 * g;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[j][u] = a.W2[(int64_t)(k + u) * a.H1 + col[j]];
+    };
+    floatx4 ba[NT], bb[NT];  // the first weight fragments in flight under the dH2 fill
+    ld(0, ba);
+    ld(16, bb);
     // dH2 (an outer product for NO = 1: the GEMM path's single product per element)
     for (int i = t; i < kChRows * a.H2; i += kChThreads) {
         const int rr = i / a.H2, o = i % a.H2, r = r0 + rr;
@@ -892,24 +974,9 @@ __global__ void __launch_bounds__(kChThreads) chain3_bwd_kernel(ChainBwdArgs a0,
     }
     __syncthreads();
     {
-        int col[NT];
         floatx4 acc[NT];
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            const int n = 16 * (w + kChWaves * j) + c;
-            col[j] = n < a.H1 ? n : a.H1 - 1;
-            acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-        }
-        floatx4 ba[NT], bb[NT];
-        auto ld = [&](int kb, floatx4 (&v)[NT]) {  // kb past H2: a clamped reload, unused
-            const int k = (kb < a.H2 ? kb : a.H2 - 16) + 4 * g;
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-#pragma unroll
-                for (int u = 0; u < 4; ++u) v[j][u] = a.W2[(int64_t)(k + u) * a.H1 + col[j]];
-        };
-        ld(0, ba);
-        ld(16, bb);
+        for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
         for (int kb = 0; kb < a.H2; kb += 32) {  // (sched barriers: the scheduler sinks the loads)
             const floatx4 f0 = *reinterpret_cast<const floatx4 *>(&gs2[c][kb + 4 * g]);
             const floatx4 f1 = *reinterpret_cast<const floatx4 *>(&gs2[c][kb + 16 + 4 * g]);
@@ -964,14 +1031,18 @@ static_assert(kChMaxNt == 2, "chain launch tables");
 using ChainFwdFn = void (*)(ChainArgs, ChainArgs);
 inline int chain_nt(int h) { return (h / 16 + kChWaves - 1) / kChWaves; }
 constexpr int kChBigRows = 16384;  // rows from which a forward block takes two row tiles
+template <int RT, int NTM>
+constexpr ChainFwdFn chain_fwd_fn(int nt1, int nt2) {
+    return nt1 == 1 ? (nt2 == 1 ? chain3_fwd_kernel<1, 1, RT, NTM> : chain3_fwd_kernel<1, 2, RT, NTM>)
+                    : (nt2 == 1 ? chain3_fwd_kernel<2, 1, RT, NTM> : chain3_fwd_kernel<2, 2, RT, NTM>);
+}
 void chain_fwd_launch(const ChainArgs &c0, const ChainArgs &c1, int nchains, hipStream_t s) {
-    // two 16-row tiles per block when the rows fill every CU twice over (batched inference: each
-    // layer-2 weight fragment then feeds twice the MFMAs, half the weight reads from L2)
-    static const ChainFwdFn tab[2][2][2] = {
-        {{chain3_fwd_kernel<1, 1, 1>, chain3_fwd_kernel<1, 2, 1>}, {chain3_fwd_kernel<2, 1, 1>, chain3_fwd_kernel<2, 2, 1>}},
-        {{chain3_fwd_kernel<1, 1, 2>, chain3_fwd_kernel<1, 2, 2>}, {chain3_fwd_kernel<2, 1, 2>, chain3_fwd_kernel<2, 2, 2>}}};
-    const int rt = c0.B >= kChBigRows ? 2 : 1;
-    const ChainFwdFn f = tab[rt - 1][chain_nt(c0.H1) - 1][chain_nt(c0.H2) - 1];
+    // two 16-row tiles per block when the rows fill every CU twice over (batched inference, the
+    // PPO2 update's chunks: each layer-2 weight fragment then feeds twice the MFMAs, half the
+    // weight reads from L2)
+    const int rt = c0.B >= kChBigRows ? 2 : 1, n1 = chain_nt(c0.H1), n2 = chain_nt(c0.H2);
+    const ChainFwdFn f = rt == 1 ? (c0.Hm ? chain_fwd_fn<1, 1>(n1, n2) : chain_fwd_fn<1, 0>(n1, n2))
+                                 : (c0.Hm ? chain_fwd_fn<2, 1>(n1, n2) : chain_fwd_fn<2, 0>(n1, n2));
     f<<<dim3((c0.B + kChRows * rt - 1) / (kChRows * rt), nchains), kChThreads, 0, s>>>(c0, c1);
 }
 void chain_bwd_launch(const ChainBwdArgs &c0, const ChainBwdArgs &c1, int nchains, hipStream_t s) {
@@ -1477,19 +1548,33 @@ bool twin_chain_grad(const rlp_dense_net &n1, const rlp_dense_net &n2, const flo
 // activations in stream-ordered scratch
 int dense_mlp_forward(const rlp_mlp_desc &d, const float *params, const float *x, float *y, int n,
                       hipStream_t s) {
-    if (d.n_layers == 3 && d.act[0] == RLP_ACT_RELU && d.act[1] == RLP_ACT_RELU &&
-        (d.act[2] == RLP_ACT_NONE || d.act[2] == RLP_ACT_TANH) && d.dims[0] <= kChK0 &&
-        d.dims[1] <= kChH && d.dims[1] % 32 == 0 && d.dims[2] <= kChH && d.dims[2] % 32 == 0 &&
-        d.dims[3] <= 8) {  // the DDPG / SAC actors' batched inference: one chain launch
+    // three or four layers with one hidden activation (relu: the DDPG / SAC actors' batched
+    // inference; tanh: the PPO2 demo nets' plain-layout rollout), tanh / none at the output,
+    // <= 64 inputs, the first two hidden widths multiples of 32 up to 256, a third up to 128:
+    // one chain launch
+    const int L = d.n_layers;
+    bool chain = (L == 3 || L == 4) && d.dims[0] <= kChK0 && d.dims[L] <= 8 &&
+                 (d.act[L - 1] == RLP_ACT_NONE || d.act[L - 1] == RLP_ACT_TANH) &&
+                 (d.act[0] == RLP_ACT_RELU || d.act[0] == RLP_ACT_TANH) && (L == 3 || d.dims[3] <= 16 * kChWaves);
+    for (int l = 1; chain && l <= 2; ++l) chain = d.dims[l] <= kChH && d.dims[l] % 32 == 0;
+    for (int l = 1; chain && l < L - 1; ++l) chain = d.act[l] == d.act[0];
+    if (chain) {
+        int64_t off[RLP_MLP_MAX_LAYERS], o = 0;
+        for (int l = 0; l < L; ++l) {
+            off[l] = o;
+            o += (int64_t)d.dims[l] * d.dims[l + 1] + d.dims[l + 1];
+        }
+        auto lw = [&](int l) { return params + off[l]; };
+        auto lb = [&](int l) { return params + off[l] + (int64_t)d.dims[l] * d.dims[l + 1]; };
         ChainArgs c{};
-        const int64_t o1 = (int64_t)d.dims[0] * d.dims[1] + d.dims[1];
-        const int64_t o2 = o1 + (int64_t)d.dims[1] * d.dims[2] + d.dims[2];
         c.x0 = c.x1 = x; c.ld0 = c.ld1 = d.dims[0]; c.split = d.dims[0]; c.K0 = d.dims[0];
-        c.W1 = params; c.b1 = params + (int64_t)d.dims[0] * d.dims[1];
-        c.W2 = params + o1; c.b2 = c.W2 + (int64_t)d.dims[1] * d.dims[2];
-        c.W3 = c.W3b = params + o2; c.b3 = c.W3 + (int64_t)d.dims[2] * d.dims[3];
-        c.H1 = d.dims[1]; c.H2 = d.dims[2]; c.NO = d.dims[3]; c.split3 = c.NO; c.B = n;
-        c.y = y; c.head = d.act[2] == RLP_ACT_TANH ? 2 : 0;
+        c.W1 = lw(0); c.b1 = lb(0); c.W2 = lw(1); c.b2 = lb(1);
+        if (L == 4) {
+            c.Wm = lw(2); c.bm = lb(2); c.Hm = d.dims[3];
+        }
+        c.W3 = c.W3b = lw(L - 1); c.b3 = lb(L - 1);
+        c.H1 = d.dims[1]; c.H2 = d.dims[2]; c.NO = d.dims[L]; c.split3 = c.NO; c.B = n;
+        c.y = y; c.head = d.act[L - 1] == RLP_ACT_TANH ? 2 : 0; c.hact = d.act[0] == RLP_ACT_TANH;
         chain_fwd_launch(c, c, 1, s);
         RLP_CHECK_LAUNCH("rlp_mlp_forward (chain)");
         return RLP_OK;
@@ -2015,6 +2100,16 @@ inline bool ppo2_dense_ok(const rlp_mlp_desc &d, bool actor) {
     return actor ? (A <= 4 && d.act[d.n_layers - 1] == RLP_ACT_TANH)
                  : (A == 1 && d.act[d.n_layers - 1] == RLP_ACT_NONE);
 }
+// the whole forward as one chain launch: three or four tanh layers, <= 64 inputs, the first two
+// hidden widths multiples of 32 up to 256, a third hidden width up to 128, <= 8 outputs (the
+// PPO2-SOI demo's 4-128-64-32-2 / 4-64-64-1, the lidar demos' 41-256-256-{2,1})
+inline bool ppo2_chain_ok(const rlp_mlp_desc &d) {
+    const int L = d.n_layers;
+    if ((L != 3 && L != 4) || d.dims[0] > kChK0 || d.dims[L] > 8) return false;
+    for (int l = 1; l <= 2; ++l)
+        if (d.dims[l] > kChH || d.dims[l] % 32) return false;
+    return L == 3 || d.dims[3] <= 16 * kChWaves;
+}
 inline PpoDenseWs ppo2_dense_ws(const rlp_mlp_desc &d, int64_t rows) {
     const int64_t B = rows < kPpoChunk ? rows : kPpoChunk;
     int64_t hid = 0, maxw = 0, np = 0, maxpart = 0;
@@ -2096,17 +2191,35 @@ int rlp_ppo2_dense_grad(const rlp_mlp_desc *desc, const float *params, const rlp
         // forward
         float *act = ws + w.act;
         int64_t ao[RLP_MLP_MAX_LAYERS];
-        Opnd in = mat(s + r0 * S, B, S, S);
         int64_t o = 0;
         for (int l = 0; l < L; ++l) {
-            const Layer Ly{params + off[l], params + off[l] + (int64_t)d.dims[l] * d.dims[l + 1],
-                           d.dims[l], d.dims[l + 1]};
-            const bool last = l == L - 1;
-            const int kind = !last ? kEpiTanh : actor ? kEpiTanhAff : kEpiNone;
             ao[l] = o;
-            dense_fwd(in, Ly, B, kind, act + o, gain_d, off_d, ws + w.t, st);
-            in = mat(act + o, B, Ly.out, Ly.out);
-            o += (int64_t)B * Ly.out;
+            o += (int64_t)B * d.dims[l + 1];
+        }
+        auto lw = [&](int l) { return params + off[l]; };
+        auto lb = [&](int l) { return params + off[l] + (int64_t)d.dims[l] * d.dims[l + 1]; };
+        if (ppo2_chain_ok(d)) {  // all layers in one launch (the hidden activations still to HBM)
+            ChainArgs ch{};
+            ch.x0 = ch.x1 = s + r0 * S; ch.ld0 = ch.ld1 = S; ch.split = S; ch.K0 = S;
+            ch.W1 = lw(0); ch.b1 = lb(0); ch.W2 = lw(1); ch.b2 = lb(1);
+            ch.H1 = d.dims[1]; ch.H2 = d.dims[2];
+            ch.h1 = act + ao[0]; ch.h2 = act + ao[1];
+            if (L == 4) {
+                ch.Wm = lw(2); ch.bm = lb(2); ch.Hm = d.dims[3]; ch.hm = act + ao[2];
+            }
+            ch.W3 = ch.W3b = lw(L - 1); ch.b3 = lb(L - 1); ch.NO = A; ch.split3 = A;
+            ch.y = act + ao[L - 1]; ch.B = B; ch.hact = 1;
+            ch.head = actor ? 1 : 0; ch.gain = gain_d; ch.off = off_d; ch.aux = ws + w.t;
+            chain_fwd_launch(ch, ch, 1, st);
+        } else {
+            Opnd in = mat(s + r0 * S, B, S, S);
+            for (int l = 0; l < L; ++l) {
+                const Layer Ly{lw(l), lb(l), d.dims[l], d.dims[l + 1]};
+                const bool last = l == L - 1;
+                const int kind = !last ? kEpiTanh : actor ? kEpiTanhAff : kEpiNone;
+                dense_fwd(in, Ly, B, kind, act + ao[l], gain_d, off_d, ws + w.t, st);
+                in = mat(act + ao[l], B, Ly.out, Ly.out);
+            }
         }
         // head: dL/dz_L into g0
         h.B = B;

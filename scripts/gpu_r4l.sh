@@ -7,6 +7,9 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; TAG=${TAG:-r4l}; mkdir -p "$OUT/$TAG"
+# call o was queued for exp14 (hoisted weight loads) before exp15 (+ the PPO2 dense forward and the
+# tanh nets' inference as chains) was built: it runs the superset
+if [ "$TAG" = r4o ]; then V=exp15; AB="base exp14 exp15"; fi
 export TMPDIR=/tmp
 LIBD=reinforcementlearningplatform_amd/csrc/build
 export RLP_LIBRARY=$ROOT/$LIBD/${V:-exp10}/librlp.so
