@@ -347,6 +347,48 @@ __global__ void __launch_bounds__(64 * kWrSlices) wgrad_reduce_kernel(const floa
         gb[m] = t;
 }
 
+// NetParts is declared below; the multi-layer reduce takes its fields directly
+constexpr int kMaxRegions = 8;
+struct PartRegions {
+    const float *part[kMaxRegions];
+    int64_t off[kMaxRegions];  // the layer's W in g (its bias follows)
+    int z[kMaxRegions], in[kMaxRegions], out[kMaxRegions];
+    int n;
+};
+// every layer's weight gradient of one net from its partials in one launch: wgrad_reduce_kernel's
+// sliced sum (the same order: the same bits) over the concatenated outputs of the regions; g
+// elements outside every region are left alone
+__global__ void __launch_bounds__(64 * kWrSlices) parts_reduce_kernel(float *__restrict__ g, int64_t n,
+                                                                       PartRegions pr) {
+    const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 64 + o;
+    int l = -1;
+    int64_t idx = 0, stride = 0;
+    for (int k = 0; k < pr.n; ++k) {
+        const int64_t r = i - pr.off[k], in = pr.in[k], out = pr.out[k];
+        if (i < n && r >= 0 && r < out * (in + 1)) {
+            l = k;
+            idx = r < in * out ? (r / in) * (in + 1) + r % in : (r - in * out) * (in + 1) + in;
+            stride = out * (in + 1);
+        }
+    }
+    float s = 0.f;
+    if (l >= 0) {
+        const float *part = pr.part[l];
+        const int z = pr.z[l];
+#pragma unroll 8
+        for (int zz = sl; zz < z; zz += kWrSlices) s += part[(size_t)zz * stride + idx];
+    }
+    __shared__ float red[kWrSlices][64];
+    red[sl][o] = s;
+    __syncthreads();
+    if (sl != 0 || l < 0) return;
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < kWrSlices; ++k) t += red[k][o];
+    g[i] = t;
+}
+
 // TD target + critic MSE gradient (DDPG.py:83-89): y = r + (gamma * end) * Q'; dQ = d/dQ of
 // mse_loss(y, Q) = -((2 / B) * (y - Q)); loss = mean((y - Q)^2). One block; also advances the
 // two Adam step counters (actor, critic) the update's optimizer steps read.
@@ -933,15 +975,22 @@ struct ChainBwdArgs {
                                      // gradients' dY operands)
     const float *W3b;                // rows [split3, NO) of W3 from W3b (the SAC actor's heads)
     int split3;
+    int hact;                        // hidden activation: 0 relu, 1 tanh (the PPO2 nets)
+    const float *Wm, *hm;            // optional fourth layer (H2 -> Hm, Hm a multiple of 32, W3 then
+    int Hm;                          // [NO][Hm]): its weights [Hm][H2], its outputs [B][Hm], and
+    float *dm;                       // dHm [B][Hm] to HBM when set
 };
 
-template <int NT>
+template <int NT, int NTB>
 __global__ void __launch_bounds__(kChThreads) chain3_bwd_kernel(ChainBwdArgs a0, ChainBwdArgs a1) {
     const ChainBwdArgs &a = blockIdx.y ? a1 : a0;
     __shared__ __attribute__((aligned(16))) float gs2[kChRows][kChLd];
     __shared__ __attribute__((aligned(16))) float gs1[kChRows][kChLd];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
     const int r0 = blockIdx.x * kChRows;
+    // the derivative of the hidden activation from its output h: relu (h > 0) or tanh (1 - h^2,
+    // the GEMM path's kEpiTanhAffBack with gain 1)
+    auto dact = [&](float v, float h) { return a.hact ? (v * 1.f) * (1.f - h * h) : (h > 0.f ? v : 0.f); };
     int col[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -958,21 +1007,72 @@ __global__ void __launch_bounds__(kChThreads) chain3_bwd_kernel(ChainBwdArgs a0,
     floatx4 ba[NT], bb[NT];  // the first weight fragments in flight under the dH2 fill
     ld(0, ba);
     ld(16, bb);
-    // dH2 (an outer product for NO = 1: the GEMM path's single product per element)
-    for (int i = t; i < kChRows * a.H2; i += kChThreads) {
-        const int rr = i / a.H2, o = i % a.H2, r = r0 + rr;
+    // the first gradient: dY W3 through the top hidden layer (an outer product for NO = 1: the GEMM
+    // path's single product per element) — dH2, or with the fourth layer dHm (into gs1, free until
+    // the dH1 stage)
+    const int KT = NTB > 0 ? a.Hm : a.H2;
+    const float *htop = NTB > 0 ? a.hm : a.h2;
+    float *dtop = NTB > 0 ? a.dm : a.d2;
+    float (*gtop)[kChLd] = NTB > 0 ? gs1 : gs2;
+    for (int i = t; i < kChRows * KT; i += kChThreads) {
+        const int rr = i / KT, o = i % KT, r = r0 + rr;
         float v = 0.f;
-        if (r < a.B && a.h2[(int64_t)r * a.H2 + o] > 0.f) {
+        if (r < a.B) {
             v = a.dy[(int64_t)r * a.NO] * a.W3[o];
             for (int j = 1; j < a.NO; ++j) {
-                const float *w3 = j < a.split3 ? a.W3 + (int64_t)j * a.H2 : a.W3b + (int64_t)(j - a.split3) * a.H2;
+                const float *w3 = j < a.split3 ? a.W3 + (int64_t)j * KT : a.W3b + (int64_t)(j - a.split3) * KT;
                 v = __builtin_fmaf(a.dy[(int64_t)r * a.NO + j], w3[o], v);
             }
+            v = dact(v, htop[(int64_t)r * KT + o]);
         }
-        gs2[rr][o] = v;
-        if (a.d2 && r < a.B) a.d2[(int64_t)r * a.H2 + o] = v;
+        gtop[rr][o] = v;
+        if (dtop && r < a.B) dtop[(int64_t)r * KT + o] = v;
     }
     __syncthreads();
+    if constexpr (NTB > 0) {  // dH2 = (dHm Wm) act'(h2): gs1 -> gs2 (Hm a multiple of 32)
+        int colb[NTB];
+        floatx4 acc[NTB], ma[NTB], mb[NTB];
+#pragma unroll
+        for (int j = 0; j < NTB; ++j) {
+            const int n = 16 * (w + kChWaves * j) + c;
+            colb[j] = n < a.H2 ? n : a.H2 - 1;
+            acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        auto ldm = [&](int kb, floatx4 (&v)[NTB]) {
+            const int k = (kb < a.Hm ? kb : a.Hm - 16) + 4 * g;
+#pragma unroll
+            for (int j = 0; j < NTB; ++j)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[j][u] = a.Wm[(int64_t)(k + u) * a.H2 + colb[j]];
+        };
+        ldm(0, ma);
+        ldm(16, mb);
+        for (int kb = 0; kb < a.Hm; kb += 32) {
+            const floatx4 f0 = *reinterpret_cast<const floatx4 *>(&gs1[c][kb + 4 * g]);
+            const floatx4 f1 = *reinterpret_cast<const floatx4 *>(&gs1[c][kb + 16 + 4 * g]);
+            chain_block<NTB>(f0, ma, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            ldm(kb + 32, ma);
+            __builtin_amdgcn_sched_barrier(0);
+            chain_block<NTB>(f1, mb, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            ldm(kb + 48, mb);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < NTB; ++j) {
+            const int n = 16 * (w + kChWaves * j) + c;
+            if (n >= a.H2) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = r0 + 4 * g + i;
+                const float v = r < a.B ? dact(acc[j][i], a.h2[(int64_t)r * a.H2 + n]) : 0.f;
+                gs2[4 * g + i][n] = v;
+                if (a.d2 && r < a.B) a.d2[(int64_t)r * a.H2 + n] = v;
+            }
+        }
+        __syncthreads();
+    }
     {
         floatx4 acc[NT];
 #pragma unroll
@@ -996,7 +1096,7 @@ __global__ void __launch_bounds__(kChThreads) chain3_bwd_kernel(ChainBwdArgs a0,
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int r = r0 + 4 * g + i;
-                const float v = r < a.B && a.h1[(int64_t)r * a.H1 + n] > 0.f ? acc[j][i] : 0.f;
+                const float v = r < a.B ? dact(acc[j][i], a.h1[(int64_t)r * a.H1 + n]) : 0.f;
                 gs1[4 * g + i][n] = v;
                 if (a.d1 && r < a.B) a.d1[(int64_t)r * a.H1 + n] = v;
             }
@@ -1045,12 +1145,13 @@ void chain_fwd_launch(const ChainArgs &c0, const ChainArgs &c1, int nchains, hip
                                  : (c0.Hm ? chain_fwd_fn<2, 1>(n1, n2) : chain_fwd_fn<2, 0>(n1, n2));
     f<<<dim3((c0.B + kChRows * rt - 1) / (kChRows * rt), nchains), kChThreads, 0, s>>>(c0, c1);
 }
+using ChainBwdFn = void (*)(ChainBwdArgs, ChainBwdArgs);
 void chain_bwd_launch(const ChainBwdArgs &c0, const ChainBwdArgs &c1, int nchains, hipStream_t s) {
-    const dim3 grid((c0.B + kChRows - 1) / kChRows, nchains);
-    if (chain_nt(c0.H1) == 1)
-        chain3_bwd_kernel<1><<<grid, kChThreads, 0, s>>>(c0, c1);
-    else
-        chain3_bwd_kernel<2><<<grid, kChThreads, 0, s>>>(c0, c1);
+    static const ChainBwdFn tab[2][3] = {
+        {chain3_bwd_kernel<1, 0>, chain3_bwd_kernel<1, 1>, chain3_bwd_kernel<1, 2>},
+        {chain3_bwd_kernel<2, 0>, chain3_bwd_kernel<2, 1>, chain3_bwd_kernel<2, 2>}};
+    const ChainBwdFn f = tab[chain_nt(c0.H1) - 1][c0.Hm ? chain_nt(c0.H2) : 0];
+    f<<<dim3((c0.B + kChRows - 1) / kChRows, nchains), kChThreads, 0, s>>>(c0, c1);
 }
 
 // ---- host side ------------------------------------------------------------------------------
@@ -2088,7 +2189,7 @@ __global__ void __launch_bounds__(256) chunk_sum_kernel(const float *__restrict_
 }
 
 struct PpoDenseWs {  // float offsets into the workspace
-    int64_t act, t, g0, g1, part, ones, head, slots, total;
+    int64_t act, t, g0, g1, g2, g3, part, ones, head, slots, total;
 };
 inline bool ppo2_dense_ok(const rlp_mlp_desc &d, bool actor) {
     if (d.n_layers < 1 || d.n_layers > RLP_MLP_MAX_LAYERS) return false;
@@ -2110,18 +2211,29 @@ inline bool ppo2_chain_ok(const rlp_mlp_desc &d) {
         if (d.dims[l] > kChH || d.dims[l] % 32) return false;
     return L == 3 || d.dims[3] <= 16 * kChWaves;
 }
+// the backward as one data chain (dH of every hidden layer, tanh') + every layer's weight
+// gradient in one launch + one reduce: the forward chain's nets whose third hidden width (four
+// layers) is a multiple of 32
+inline bool ppo2_chain_bwd_ok(const rlp_mlp_desc &d) {
+    return ppo2_chain_ok(d) && (d.n_layers == 3 || d.dims[3] % 32 == 0) && d.n_layers <= kMaxRegions;
+}
+// reduction slices of layer l's weight gradient over a chunk (512 blocks per launch)
+inline int64_t ppo2_wgrad_nz(const rlp_mlp_desc &d, int l) {
+    const int64_t tiles = ((d.dims[l] + 1 + kDT - 1) / kDT) * ((d.dims[l + 1] + kDT - 1) / kDT);
+    return 512 / tiles > 1 ? 512 / tiles : 1;
+}
 inline PpoDenseWs ppo2_dense_ws(const rlp_mlp_desc &d, int64_t rows) {
     const int64_t B = rows < kPpoChunk ? rows : kPpoChunk;
-    int64_t hid = 0, maxw = 0, np = 0, maxpart = 0;
+    int64_t hid = 0, maxw = 0, np = 0, maxpart = 0, sumpart = 0;
     for (int l = 0; l < d.n_layers; ++l) {
         hid += d.dims[l + 1];
         maxw = d.dims[l + 1] > maxw ? d.dims[l + 1] : maxw;
         np += (int64_t)d.dims[l] * d.dims[l + 1] + d.dims[l + 1];
-        const int64_t tiles = ((d.dims[l] + 1 + kDT - 1) / kDT) * ((d.dims[l + 1] + kDT - 1) / kDT);
-        const int64_t nz = 512 / tiles > 1 ? 512 / tiles : 1;
-        const int64_t p = nz * d.dims[l + 1] * (d.dims[l] + 1);
+        const int64_t p = ppo2_wgrad_nz(d, l) * d.dims[l + 1] * (d.dims[l] + 1);
         maxpart = p > maxpart ? p : maxpart;
+        sumpart += p;
     }
+    const bool chain = ppo2_chain_bwd_ok(d);  // every layer's partials at once
     const int64_t chunks = (rows + kPpoChunk - 1) / kPpoChunk;
     PpoDenseWs w{};
     int64_t o = 0;
@@ -2130,7 +2242,9 @@ inline PpoDenseWs ppo2_dense_ws(const rlp_mlp_desc &d, int64_t rows) {
     w.t = take(B * 4);
     w.g0 = take(B * maxw);
     w.g1 = take(B * maxw);
-    w.part = take(maxpart);
+    w.g2 = chain ? take(B * maxw) : w.g1;
+    w.g3 = chain ? take(B * maxw) : w.g1;
+    w.part = take(chain ? sumpart : maxpart);
     w.ones = take(1024);
     w.head = take(8);
     w.slots = take(chunks * np);
@@ -2234,6 +2348,40 @@ int rlp_ppo2_dense_grad(const rlp_mlp_desc *desc, const float *params, const rlp
         }
         // backward: layer by layer from the top; chunk c's gradient into its slot
         float *slot = ws + w.slots + c * np;
+        if (ppo2_chain_bwd_ok(d)) {
+            // dH of every hidden layer in one data chain (into g1 / g2 / g3), then every layer's
+            // dW | db partials in one launch and one reduce into the slot
+            float *dh[3] = {ws + w.g1, ws + w.g2, ws + w.g3};  // dH1, dH2, dH3 (four layers)
+            ChainBwdArgs cb{};
+            cb.dy = ws + w.g0; cb.NO = A; cb.split3 = A; cb.W3 = cb.W3b = lw(L - 1);
+            cb.W2 = lw(1); cb.W1 = lw(0); cb.K0 = S; cb.H1 = d.dims[1]; cb.H2 = d.dims[2]; cb.B = B;
+            cb.h1 = act + ao[0]; cb.h2 = act + ao[1]; cb.d1 = dh[0]; cb.d2 = dh[1]; cb.hact = 1;
+            if (L == 4) {
+                cb.Wm = lw(2); cb.hm = act + ao[2]; cb.Hm = d.dims[3]; cb.dm = dh[2];
+            }
+            chain_bwd_launch(cb, cb, 1, st);
+            Prob q[kMaxRegions];
+            PartRegions pr{};
+            int64_t po = 0;
+            for (int l = 0; l < L; ++l) {
+                const Layer Ly{lw(l), lb(l), d.dims[l], d.dims[l + 1]};
+                const float *dyl = l == L - 1 ? ws + w.g0 : dh[l];
+                const Opnd xin = l == 0 ? mat(s + r0 * S, B, S, S) : mat(act + ao[l - 1], B, Ly.in, Ly.in);
+                Epi ew{};
+                ew.y = ws + w.part + po; ew.kind = kEpiPartial; ew.M = Ly.out; ew.N = Ly.in + 1;
+                Opnd xo = xin;
+                xo.cols = Ly.in + 1;
+                xo.ones = Ly.in;
+                q[l] = make_prob_long(transposed(dyl, Ly.out, B, Ly.out), xo, ew, B, (int)ppo2_wgrad_nz(d, l));
+                pr.part[l] = ws + w.part + po; pr.off[l] = off[l]; pr.z[l] = q[l].nz;
+                pr.in[l] = Ly.in; pr.out[l] = Ly.out;
+                po += ppo2_wgrad_nz(d, l) * Ly.out * (Ly.in + 1);
+            }
+            pr.n = L;
+            gemm_multi(q, L, st);
+            parts_reduce_kernel<<<(int)((np + 63) / 64), 64 * kWrSlices, 0, st>>>(slot, np, pr);
+            continue;
+        }
         const float *dy = ws + w.g0;
         float *dn = ws + w.g1;
         for (int l = L - 1; l >= 0; --l) {
