@@ -701,11 +701,12 @@ __global__ void __launch_bounds__(1024) sac_critic_loss_kernel(const float *__re
     }
 }
 
-// ---- fused forward of a three-layer chain -------------------------------------------------------
-// [K0 -> H1 -> H2 -> NO] with relu hidden layers (the DDPG demo nets, the SAC critics and actor
-// trunk), 16 rows per block, all three layers in one launch instead of three GEMM launches: the
-// block's input rows and both hidden activations stay in LDS between the layers (and go to HBM
-// once, for the backward's relu masks and weight gradients). Exact f32 products
+// ---- fused forward of a three- or four-layer chain ----------------------------------------------
+// [K0 -> H1 -> H2 (-> Hm) -> NO] with relu or tanh hidden layers (the DDPG demo nets, the SAC
+// critics and actor trunk + heads, the PPO2 demo nets), 16 or 32 rows per block, all layers in one
+// launch instead of one GEMM launch per layer: the block's input rows and the hidden activations
+// stay in LDS between the layers (and go to HBM once, for the backward's masks and weight
+// gradients; not at all for batched inference). Exact f32 products
 // (v_mfma_f32_16x16x4_f32). Eight waves per block (two per SIMD: one wave's loads and VALU under
 // the other's MFMAs). Layer 1 / 2: wave w owns the 16-column tiles t = w + 8 j, j < NT1 / NT2
 // (compile-time: every MFMA and load unconditional — a guarded tile made each MFMA a branch with a
@@ -748,13 +749,13 @@ __device__ __forceinline__ void chain_block(const floatx4 &f, const floatx4 (&b)
         for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[u], b[j][u], acc[j], 0, 0, 0);
 }
 
-template <int NT1, int NT2, int RT, int NTM>
+template <int NT1, int NT2, int RT, int NTM, int LD = kChLd, int KX = kChK0>
 __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, ChainArgs a1) {
     constexpr int ROWS = kChRows * RT, RPW = ROWS / kChWaves;  // block rows, layer-3 rows per wave
     const ChainArgs &a = blockIdx.y ? a1 : a0;
-    __shared__ __attribute__((aligned(16))) float xs[ROWS][kChK0 + 4];
-    __shared__ __attribute__((aligned(16))) float hs1[ROWS][kChLd];
-    __shared__ __attribute__((aligned(16))) float hs2[ROWS][kChLd];
+    __shared__ __attribute__((aligned(16))) float xs[ROWS][KX + 4];
+    __shared__ __attribute__((aligned(16))) float hs1[ROWS][LD];
+    __shared__ __attribute__((aligned(16))) float hs2[ROWS][LD];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
     const int r0 = blockIdx.x * ROWS;
     const int K8 = (a.K0 + 7) & ~7;  // zero-padded input columns: two 4-deep steps per pass
@@ -931,7 +932,7 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
     }
     // the head: wave w, rows RPW w .. (over hs2, or hs1 after the fourth layer)
     const int KL = NTM > 0 ? a.Hm : a.H2;
-    float (*hl)[kChLd] = NTM > 0 ? hs1 : hs2;
+    float (*hl)[LD] = NTM > 0 ? hs1 : hs2;
     for (int o = 0; o < a.NO; ++o) {
         const float *w3 = o < a.split3 ? a.W3 + (int64_t)o * KL : a.W3b + (int64_t)(o - a.split3) * KL;
 #pragma unroll
@@ -957,11 +958,12 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
     }
 }
 
-// The data-only backward of the same [K0 -> H1 -> H2 -> NO] relu chains (the critic's input
-// gradient of DDPG / SAC's actor pass: no weight gradients, so neither hidden gradient needs HBM):
-// dH2 = (dY W3) relu'(h2) and dH1 = (dH2 W2) relu'(h1) stay in LDS, dX[:, c0:c0+nc] = dH1 W1[:,
-// c0:c0+nc] with the tanh-affine backward of the actor's head when t is given (one launch instead
-// of three GEMMs). Layer 2: as chain3_fwd_kernel's (NT tiles of dH1 per wave, H2 a multiple of 32,
+// The backward data pass of the same chains: dH2 = (dY W3) act'(h2) and dH1 = (dH2 W2) act'(h1)
+// (with a fourth layer dHm = (dY W3) act'(hm) first, then dH2 = (dHm Wm) act'(h2)) stay in LDS
+// and, when asked (d2 / d1 / dm), go to HBM as the weight gradients' dY operands; dX[:, c0:c0+nc]
+// = dH1 W1[:, c0:c0+nc] with the tanh-affine backward of the actor's head when t is given (the
+// critic's input gradient of DDPG / SAC's actor pass). One launch instead of one or two GEMMs per
+// layer. Layer 2: as chain3_fwd_kernel's (NT tiles of dH1 per wave, H2 a multiple of 32,
 // the next block's weights in flight), with B(k, n) = W2[k][n] (four 64-byte row segments per lane
 // instead of one 16-byte column read); the dX columns: the lane-split dot products of
 // chain3_fwd_kernel's layer 3.
@@ -1131,6 +1133,7 @@ static_assert(kChMaxNt == 2, "chain launch tables");
 using ChainFwdFn = void (*)(ChainArgs, ChainArgs);
 inline int chain_nt(int h) { return (h / 16 + kChWaves - 1) / kChWaves; }
 constexpr int kChBigRows = 16384;  // rows from which a forward block takes two row tiles
+constexpr int kChNarrow = 128;     // widths up to which one 16-column tile per wave covers a layer
 template <int RT, int NTM>
 constexpr ChainFwdFn chain_fwd_fn(int nt1, int nt2) {
     return nt1 == 1 ? (nt2 == 1 ? chain3_fwd_kernel<1, 1, RT, NTM> : chain3_fwd_kernel<1, 2, RT, NTM>)
@@ -1141,8 +1144,13 @@ void chain_fwd_launch(const ChainArgs &c0, const ChainArgs &c1, int nchains, hip
     // PPO2 update's chunks: each layer-2 weight fragment then feeds twice the MFMAs, half the
     // weight reads from L2)
     const int rt = c0.B >= kChBigRows ? 2 : 1, n1 = chain_nt(c0.H1), n2 = chain_nt(c0.H2);
-    const ChainFwdFn f = rt == 1 ? (c0.Hm ? chain_fwd_fn<1, 1>(n1, n2) : chain_fwd_fn<1, 0>(n1, n2))
-                                 : (c0.Hm ? chain_fwd_fn<2, 1>(n1, n2) : chain_fwd_fn<2, 0>(n1, n2));
+    ChainFwdFn f = rt == 1 ? (c0.Hm ? chain_fwd_fn<1, 1>(n1, n2) : chain_fwd_fn<1, 0>(n1, n2))
+                           : (c0.Hm ? chain_fwd_fn<2, 1>(n1, n2) : chain_fwd_fn<2, 0>(n1, n2));
+    // nets no wider than 128 with at most 8 inputs (the PPO2-SOI demo's) with two row tiles:
+    // half-width LDS rows and an 8-column input tile, four blocks per CU instead of two (35
+    // instead of 75 KB)
+    if (rt == 2 && c0.H1 <= kChNarrow && c0.H2 <= kChNarrow && c0.Hm <= kChNarrow && c0.K0 <= 8)
+        f = c0.Hm ? chain3_fwd_kernel<1, 1, 2, 1, kChNarrow + 4, 8> : chain3_fwd_kernel<1, 1, 2, 0, kChNarrow + 4, 8>;
     f<<<dim3((c0.B + kChRows * rt - 1) / (kChRows * rt), nchains), kChThreads, 0, s>>>(c0, c1);
 }
 using ChainBwdFn = void (*)(ChainBwdArgs, ChainBwdArgs);
