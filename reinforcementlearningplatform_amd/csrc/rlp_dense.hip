@@ -718,6 +718,10 @@ __global__ void __launch_bounds__(1024) sac_critic_loss_kernel(const float *__re
 // by two: a register copy of an in-flight load would wait for it). Tiles past the width
 // read a clamped row and are not stored. Layer 3 (NO <= 8 outputs): the 64 lanes of a wave split
 // k, one wave per 2 rows, a shuffle tree per output.
+// a 16-byte weight read at 4-byte alignment: the packed parameter buffers put some layers' W at
+// offsets that are not multiples of 4 floats (the SAC critic's Q2 chain); gfx950's global loads
+// take unaligned addresses, and this type tells the compiler so instead of promising 16
+typedef float floatx4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 struct ChainArgs {
     const float *x0, *x1;  // input columns [0, split) from x0 (row stride ld0), the rest from x1
     int ld0, ld1, split, K0;
@@ -780,7 +784,7 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
     auto ld2 = [&](int kb, floatx4 (&v)[NT2]) {  // kb past H1: a clamped reload, unused
         const int k = (kb < a.H1 ? kb : a.H1 - 16) + 4 * g;
 #pragma unroll
-        for (int j = 0; j < NT2; ++j) v[j] = *reinterpret_cast<const floatx4 *>(a.W2 + (int64_t)row2[j] * a.H1 + k);
+        for (int j = 0; j < NT2; ++j) v[j] = *reinterpret_cast<const floatx4_a4 *>(a.W2 + (int64_t)row2[j] * a.H1 + k);
     };
     float wa[NT1], wb[NT1];
     floatx4 ba[NT2], bb[NT2];
@@ -892,7 +896,7 @@ __global__ void __launch_bounds__(kChThreads) chain3_fwd_kernel(ChainArgs a0, Ch
         auto ldm = [&](int kb, floatx4 (&v)[NTM]) {
             const int k = (kb < a.H2 ? kb : a.H2 - 16) + 4 * g;
 #pragma unroll
-            for (int j = 0; j < NTM; ++j) v[j] = *reinterpret_cast<const floatx4 *>(a.Wm + (int64_t)rowm[j] * a.H2 + k);
+            for (int j = 0; j < NTM; ++j) v[j] = *reinterpret_cast<const floatx4_a4 *>(a.Wm + (int64_t)rowm[j] * a.H2 + k);
         };
         ldm(0, ma);
         ldm(16, mb);
