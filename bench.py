@@ -82,11 +82,14 @@ PEAK_F16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS   # f16/bf16 dense MFMA = 16x 
 PEAK_F16X3_TFLOPS = PEAK_F16_MFMA_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0
 # the rollout kernel each --physics mode launches (rlp_rollout.hip; the name rocprof reports)
-ROLLOUT_KERNEL = {"shared": "rlp::rollout_sp_kernel<KIND,256,SUB,4>",
-                  "cu": "rlp::rollout_sp_kernel<KIND,256,2,8>",
+# (template arguments as rocprof prints them: KIND, H, SUB, waves per block, waves per SIMD)
+ROLLOUT_KERNEL = {"shared": "rlp::rollout_sp_kernel<KIND,256,SUB,4,2>",
+                  "cu": "rlp::rollout_sp_kernel<KIND,256,2,8,2>",
                   "cu4": "rlp::rollout_sp_kernel<KIND,256,2,4,1>",
                   "lanes": "rlp::rollout_kernel<KIND,256,SUB,true>"}
 
+TRAFFIC_SOURCE = ("looked up from profiles/pmc_traffic.json (a committed rocprofv3 FETCH_SIZE / "
+                  "WRITE_SIZE pass of this workload and kernel), not measured in this run")
 PHYSICS_MODES = {"auto": -1, "lanes": 0, "shared": 1, "cu": 3, "cu4": 5}
 
 
@@ -131,6 +134,84 @@ def orthogonal_params(desc, gains, seed):
 def mlp_flops(desc):
     ds = desc.layer_dims()
     return sum(2 * ds[i] * ds[i + 1] for i in range(desc.n_layers))
+
+
+def dims_flops(dims):
+    """Forward FLOP per row of a Linear stack with layer widths `dims`."""
+    return sum(2 * dims[i] * dims[i + 1] for i in range(len(dims) - 1))
+
+
+def update_flops_per_row(dims):
+    """Algorithmic FLOP per row of one optimiser step's gradient of a Linear stack (what
+    loss.backward() does after the forward): forward sum 2 in out, backward data pass through every
+    layer but the first (sum_{l >= 1} 2 in out), weight + bias gradients sum 2 (in + 1) out."""
+    L = len(dims) - 1
+    return (dims_flops(dims) + sum(2 * dims[i] * dims[i + 1] for i in range(1, L))
+            + sum(2 * (dims[i] + 1) * dims[i + 1] for i in range(L)))
+
+
+def _wgrad_flops(dims):
+    return sum(2 * (dims[i] + 1) * dims[i + 1] for i in range(len(dims) - 1))
+
+
+def ddpg_learn_flops(S=4, A=2, H=256):
+    """Algorithmic FLOP per batch row of one DDPG learn() (DDPG.py:72-109) with the SOI driver's
+    nets (actor [S,H,H,A], critic cat(s,a) [S+A,H,H,1]): target actor + target critic forward; the
+    critic's forward, backward data pass (layers >= 1) and weight gradients; the actor's forward,
+    the updated critic's forward on (s, mu(s)), its backward data pass down to the action columns,
+    the actor's backward data pass (layers >= 1) and weight gradients."""
+    da, dc = [S, H, H, A], [S + A, H, H, 1]
+    fa, fc = dims_flops(da), dims_flops(dc)
+    critic = fc + (fc - 2 * dc[0] * H) + _wgrad_flops(dc)
+    actor = fa + fc + (fc - 2 * dc[0] * H + 2 * A * H) + (fa - 2 * S * H) + _wgrad_flops(da)
+    return fa + fc + critic + actor
+
+
+def sac_learn_flops(S=41, A=2, h=(128, 64)):
+    """Algorithmic FLOP per batch row of one SAC learn() (Soft_Actor_Critic.py:70-129) with the SAC
+    demo nets (actor trunk [S,128,64] + mean / log_std heads [64 -> A]; twin critics
+    cat(s,a) [S+A,128,64,1]): the actor on s' and the twin target critics; the twin critics'
+    forward, backward data (layers >= 1) and weight gradients; the actor on s, the twin critics on
+    (s, a~pi(s)) and their backward data pass down to the action columns, the actor's backward data
+    pass (layers >= 1) and weight gradients (trunk and both heads)."""
+    dt, dc = [S, *h], [S + A, *h, 1]
+    fa = dims_flops(dt) + 2 * (2 * h[-1] * A)
+    wa = _wgrad_flops(dt) + 2 * 2 * (h[-1] + 1) * A
+    fc = dims_flops(dc)
+    target = fa + 2 * fc
+    critic = 2 * fc + 2 * (fc - 2 * dc[0] * h[0]) + 2 * _wgrad_flops(dc)
+    actor = fa + 2 * fc + 2 * (fc - 2 * dc[0] * h[0] + 2 * A * h[0]) + (fa - 2 * S * h[0]) + wa
+    return target + critic + actor
+
+
+def learn_roofline(flop_per_row, batch, learn_ms):
+    ach = flop_per_row * batch / (learn_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": ach, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": ach / PEAK_FP32_MFMA_TFLOPS, "flop_per_learn": flop_per_row * batch,
+            "peak_basis": "f32 MFMA dense (the update's v_mfma_f32_16x16x4_f32 GEMMs)",
+            "note": "one learn() of `batch` rows is a chain of small dependent launches in one HIP "
+                    "graph: latency-bound at this batch, far from the roof"}
+
+
+def _net_dims(module):
+    lin = [m for m in module.modules() if isinstance(m, torch.nn.Linear)]
+    return [lin[0].in_features] + [l.out_features for l in lin]
+
+
+def update_roofline(learner, rows, k_epochs, update_ms):
+    """achieved TFLOP/s of the K-epoch update of one PPO2 iteration (both nets, full batch),
+    priced against the arithmetic the update runs: the f16x3 kernels' 838.9 TF ceiling
+    (rlp_ppo2_grad) or the f32 MFMA peak (rlp_ppo2_dense_grad, torch)."""
+    per_row = update_flops_per_row(_net_dims(learner.actor)) + update_flops_per_row(_net_dims(learner.critic))
+    flop = per_row * rows * k_epochs
+    dense = [getattr(getattr(learner, k, None), "dense", True) for k in ("net_a", "net_c")]
+    f16x3 = type(learner).__name__ == "NativePPO2Learner" and not any(dense)
+    peak = PEAK_F16X3_TFLOPS if f16x3 else PEAK_FP32_MFMA_TFLOPS
+    ach = flop / (update_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
+            "flop_per_iteration": flop, "update_ms": update_ms,
+            "peak_basis": "f16x3 ceiling (f16 MFMA / 3)" if f16x3 else "f32 MFMA dense",
+            "flop_basis": "K x rows x (forward + backward data + weight gradients) of both nets"}
 
 
 def _template_args(name):
@@ -238,6 +319,7 @@ def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
                                                                                    VecPPO2)
     from reinforcementlearningplatform_amd.utils.classes import PPOActor_Gaussian, PPOCritic
     pkg, cls_name = E2E_ENVS[seg.env]
+    uevs = []
     env_cls = getattr(importlib.import_module(
         f"reinforcementlearningplatform_amd.environment.{pkg}.{cls_name}"), cls_name)
     env = env_cls(n_envs=seg.n, seed=seg.seed, env_id0=seg.env_id0)
@@ -261,7 +343,11 @@ def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
         if ev is not None:
             ev[1].record()
         vec.advantages()
+        if ev is not None:
+            ev[2].record()
         vec.update()
+        if ev is not None:
+            ev[3].record()
     one()
     dist_on = torch.distributed.is_available() and torch.distributed.is_initialized()
     if dist_on:
@@ -269,7 +355,7 @@ def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(iters):
-        evs.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+        evs.append(tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)))
         one(evs[-1])
     if dist_on:
         torch.distributed.barrier()
@@ -279,9 +365,11 @@ def e2e_iterations(seg, iters, k_epochs=6, learner="native"):
         t = torch.tensor([dt], device="cuda")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
-    rollout_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    info = {"rollout_ms": rollout_ms, "learner": type(vec.learner).__name__,
-            "norm_scope": "global" if vec.global_norm else "rank"}
+    rollout_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    update_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+    info = {"rollout_ms": rollout_ms, "update_ms": update_ms, "learner": type(vec.learner).__name__,
+            "norm_scope": "global" if vec.global_norm else "rank",
+            "update_roofline": update_roofline(vec.learner, seg.n * seg.T, k_epochs, update_ms)}
     if dist_on:
         info["allreduce"] = allreduce_probe(vec)
     del vec, env
@@ -392,7 +480,11 @@ def demo_nets_e2e_leg(rank, which, iters=2, seed=19):
         if ev is not None:
             ev[1].record()
         vec.advantages()
+        if ev is not None:
+            ev[2].record()
         vec.update()
+        if ev is not None:
+            ev[3].record()
     one()
     dist_on = torch.distributed.is_available() and torch.distributed.is_initialized()
     if dist_on:
@@ -400,7 +492,7 @@ def demo_nets_e2e_leg(rank, which, iters=2, seed=19):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(iters):
-        evs.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+        evs.append(tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)))
         one(evs[-1])
     if dist_on:
         torch.distributed.barrier()
@@ -411,11 +503,16 @@ def demo_nets_e2e_leg(rank, which, iters=2, seed=19):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     lr = vec.learner
+    update_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+    nets = [getattr(lr, k, None) for k in ("net_a", "net_c")]
+    kinds = ["rlp_ppo2_dense_grad (exact f32 MFMA GEMMs)" if m.dense else "rlp_ppo2_grad (f16x3 FD + wgrad)"
+             for m in nets if m is not None]
     out = {"value": n * T * iters / dt, "unit": "env-steps/s", "s_per_iteration": dt / iters,
-           "rollout_ms": float(np.mean([a.elapsed_time(b) for a, b in evs])), "envs_per_gpu": n,
+           "rollout_ms": float(np.mean([e[0].elapsed_time(e[1]) for e in evs])),
+           "update_ms": update_ms, "envs_per_gpu": n,
            "T": T, "K_epochs": c["K"], "learner": type(lr).__name__,
-           "update": ("rlp_ppo2_dense_grad (exact f32 MFMA GEMMs) + rlp_adam_step"
-                      if getattr(lr, "net_a", None) is not None and lr.net_a.dense else "other"),
+           "update": (" / ".join(dict.fromkeys(kinds)) + " + rlp_adam_step") if kinds else "torch",
+           "update_roofline": update_roofline(lr, n * T, c["K"], update_ms),
            "rollout": "plain-layout nets (per-step rlp_mlp_forward + sample/step kernel)"
                       if vec.plain else "fused / lidar per-step path",
            "config": f"{env.name} PPO2, actor {[env.state_dim, *c['actor'], env.action_dim]} / "
@@ -493,7 +590,13 @@ def soi_ddpg_leg(rank, n=65536, steps=20, warmup=3, batch=4096, capacity=1 << 20
             out["learn_ms"] = ev[0].elapsed_time(ev[1]) / steps
     return {"value": out["with_learn"], "unit": "env-steps/s", "env_only": out["env_only"],
             "with_learn_torch_update": out["with_learn_torch_update"], "learn_ms": out["learn_ms"],
+            "learn_roofline": learn_roofline(ddpg_learn_flops(), batch, out["learn_ms"]),
             "envs_per_gpu": n, "replay_capacity": capacity, "batch": batch, "learn_iters_per_step": 1,
+            "update_to_data": {"sampled_rows_per_transition": batch / n, "reference": 64,
+                               "reference_basis": "DDPG-4-SecondOrderIntegration/train.py:180,237: "
+                                                  "one 64-row learn() per env step",
+                               "ratio_vs_reference": batch / n / 64,
+                               "note": "throughput at a lower sample reuse than the reference driver"},
             "config": "SecondOrderIntegration (DDPG copy) DDPG, replay in HBM, nets [4,256,256,2] "
                       "relu / Q [6,256,256,1] relu; native DDPG update (rlp_ddpg_update, f32 MFMA) "
                       "in one HIP graph per learn(); with_learn_torch_update = the same loop with "
@@ -563,21 +666,34 @@ def ugvoa_ppo2_leg(rank, n=16384, T=64, iters=3, seed=17):
     need = torch.ones(n, dtype=torch.uint8, device="cuda")
     bufs = K.rollout_buffers(kind, T, n)
     step0 = [0]
+    ws = [None]   # the lidar path's scratch, allocated once (rlp_rollout_workspace_bytes)
 
     def seg():
         cfg = K.make_rollout_cfg(T, n, seed, step0[0], rank * n, std, lo, hi,
                                  A.RLP_SUCCESS_DONE_AND_FLAG_NE, A.timeout_flag(kind))
-        K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs)
+        ws[0] = K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs, workspace=ws[0])
         step0[0] += T
     seg()
     torch.cuda.synchronize()
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(iters)]
     t0 = time.perf_counter()
-    for _ in range(iters):
+    for i in range(iters):
+        evs[i][0].record()
         seg()
+        evs[i][1].record()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    seg_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    flop = n * T * (mlp_flops(ad) + mlp_flops(cd)) + n * mlp_flops(cd)
+    ach = flop / (seg_ms * 1e-3) / 1e12
     return {"value": n * T * iters / dt, "unit": "env-steps/s", "envs_per_gpu": n, "T": T,
             "ms_per_segment": dt / iters * 1e3, "episodes_per_segment": int(bufs["done"].sum()),
+            "roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_FP32_MFMA_TFLOPS,
+                         "unit": "TFLOP/s", "frac": ach / PEAK_FP32_MFMA_TFLOPS,
+                         "flop_per_segment": flop, "segment_ms": seg_ms,
+                         "peak_basis": "f32 MFMA dense (the per-step packed forwards: f32 MFMA)",
+                         "note": "whole segment (T x {critic + actor forward, sample, lidar env "
+                                 "step, resets} launches) against the nets' FLOPs"},
             "config": "UGVForwardObstacleAvoidance (PPO2 copy, 37-beam lidar, 10 circles) PPO2 "
                       "rollout, nets [41,256,256,2] / [41,256,256,1] tanh (rlp_rollout)"}
 
@@ -627,8 +743,14 @@ def ugvoa_sac_leg(rank, n=16384, steps=20, warmup=3, batch=4096, capacity=1 << 2
             out["learn_ms"] = ev[0].elapsed_time(ev[1]) / steps
     return {"value": out["with_learn"], "unit": "env-steps/s", "env_only": out["env_only"],
             "with_learn_torch_update": out["with_learn_torch_update"], "learn_ms": out["learn_ms"],
+            "learn_roofline": learn_roofline(sac_learn_flops(S, Ad), batch, out["learn_ms"]),
             "envs_per_gpu": n, "replay_capacity": capacity, "batch": batch,
             "learn_iters_per_step": 1,
+            "update_to_data": {"sampled_rows_per_transition": batch / n, "reference": 256,
+                               "reference_basis": "SAC-4-UGVForward/train.py:206,263: one 256-row "
+                                                  "learn() per env step",
+                               "ratio_vs_reference": batch / n / 256,
+                               "note": "throughput at a lower sample reuse than the reference driver"},
             "config": "UGVForwardObstacleAvoidance (env-dir copy, 37-beam lidar, 10 circles) SAC, "
                       "replay in HBM, demo nets; native SAC update (rlp_sac_update, f32 MFMA) in one "
                       "HIP graph per learn() (sample, gather, update, actor refresh); "
@@ -841,6 +963,8 @@ def main():
     ap.add_argument("--ddpg", type=int, default=1, help="also time SOI DDPG with the HBM replay (config 3)")
     ap.add_argument("--oa", type=int, default=1, help="also time UGVForwardObstacleAvoidance env steps (lidar)")
     ap.add_argument("--sac", type=int, default=1, help="also time UGVForwardObstacleAvoidance SAC (config 5 shard)")
+    ap.add_argument("--offpolicy-steps", type=int, default=20,
+                    help="timed vector steps of the DDPG / SAC legs (short runs for counter passes)")
     ap.add_argument("--physics", default="auto", choices=list(PHYSICS_MODES),
                     help="rollout kernel: env state in LDS + full-lane physics waves (two 4-wave "
                          "blocks per CU, one 8-wave block per CU, or one 4-wave block per CU; auto: "
@@ -941,6 +1065,7 @@ def main():
         "roofline": {"bound": "mfma", "kernel": (rollout_kernel_name(args.physics, n, args.env, args.sub) if args.precision == "f16x3"
                                                 else "rlp::rollout_kernel<KIND,256,SUB,false>"), "achieved": achieved,
                      "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+                     "traffic_source": TRAFFIC_SOURCE,
                      "peak_basis": basis, "avg_launch_ms": rollout_ms, "flop_per_launch": flop_launch},
     }
     if prec == _native.MLP_F16X3 and args.fp32_leg:
@@ -993,6 +1118,7 @@ def main():
                          "achieved": uach, "peak": upeak, "unit": "TFLOP/s", "frac": uach / upeak,
                          "traffic": pmc_traffic("uav_ppo2_rollout", un, uT,
                                                 rollout_kernel_name(uphys, un, "uav", args.sub)),
+                         "traffic_source": TRAFFIC_SOURCE,
                          "avg_launch_ms": ums, "flop_per_launch": uflop}}
         del useg
         _native.set_rollout_physics(PHYSICS_MODES[args.physics])
@@ -1003,7 +1129,7 @@ def main():
             v["hbm_frac_pmc"] = (None if v["traffic"] is None else
                                  v["traffic"] / (v["avg_launch_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS)
     if args.ddpg and args.env == "cartpole":
-        d = soi_ddpg_leg(rank)
+        d = soi_ddpg_leg(rank, steps=args.offpolicy_steps, warmup=min(3, args.offpolicy_steps))
         if dist is not None:
             t = torch.tensor([d["value"], d["env_only"]], device="cuda", dtype=torch.float64)
             dist.all_reduce(t)   # independent replicas: sum of the ranks' rates
@@ -1024,7 +1150,7 @@ def main():
             d["value"] = float(t[0])
         out["ugvoa_ppo2_rollout"] = d
     if args.sac and args.env == "cartpole":
-        d = ugvoa_sac_leg(rank)
+        d = ugvoa_sac_leg(rank, steps=args.offpolicy_steps, warmup=min(3, args.offpolicy_steps))
         if dist is not None:
             t = torch.tensor([d["value"], d["env_only"]], device="cuda", dtype=torch.float64)
             dist.all_reduce(t)   # independent env shards / replicas: sum of the ranks' rates

@@ -18,7 +18,9 @@
  *  - Return value: RLP_OK (0) on success; RLP_EINVAL / RLP_EUNSUPPORTED on bad arguments;
  *    -(int)hipError_t for a HIP launch error. Nothing throws or aborts across the ABI.
  *    rlp_last_error_string() returns a thread-local description of the last failure.
- *  - The library allocates no device memory. Callers own every buffer.
+ *  - The library allocates no device memory. Callers own every buffer; calls that need scratch
+ *    take a caller-owned workspace sized by a *_workspace_* query and return RLP_EINVAL when it is
+ *    too small (checked on the host before any launch).
  */
 #ifndef RLP_H_
 #define RLP_H_
@@ -37,7 +39,7 @@ typedef void *rlp_stream_t; /* hipStream_t */
 #define RLP_EUNSUPPORTED (-1001)
 #define RLP_ENOMEM (-1002)  /* a stream-ordered scratch allocation failed */
 
-#define RLP_ABI_VERSION 1
+#define RLP_ABI_VERSION 2  /* 2: caller-owned rollout / mlp_forward workspaces (round 5) */
 
 /* ------------------------------------------------------------------------------------------ */
 /* Environment kinds. Each kind is one specific reference env copy (copies diverge). */
@@ -250,9 +252,13 @@ int64_t rlp_mlp_param_count(const rlp_mlp_desc *desc);
  * (v_mfma_f32_16x16x4_f32) for every layer; rows with mask[i]==0 are skipped (mask nullable).
  * Unmasked batches of >= 2048 rows run on the tiled GEMM, one launch per layer — or, for the
  * DDPG / SAC actors' shape (three layers, relu, relu, tanh / none, <= 64 inputs, hidden widths
- * multiples of 32 up to 256, <= 8 outputs), all three layers in one fused launch. */
+ * multiples of 32 up to 256, <= 8 outputs), all three layers in one fused launch. The per-layer
+ * path keeps two hidden activations in `workspace` (device, rlp_mlp_forward_workspace_bytes(desc,
+ * n) bytes; 0 — and workspace nullable — for every other path). */
+int64_t rlp_mlp_forward_workspace_bytes(const rlp_mlp_desc *desc, int n);
 int rlp_mlp_forward(const rlp_mlp_desc *desc, const float *params, const float *x, float *y, int n,
-                    const uint8_t *mask, rlp_stream_t stream);
+                    const uint8_t *mask, void *workspace, int64_t workspace_bytes,
+                    rlp_stream_t stream);
 
 /* Size (floats) and packing of the MFMA-fragment layout used by rlp_rollout for a
  * [S -> H -> H -> A] tanh network (H in {64,128,256}). Returns RLP_EUNSUPPORTED otherwise. */
@@ -328,6 +334,10 @@ typedef struct rlp_rollout_cfg {
      * whose actor ends in tanh (the PPO2-SOI demo's 4-128-64-32-2 / 4-64-64-1): per step
      * rlp_mlp_forward's kernels + one sample / env-step / append kernel, same draws and buffers */
     int32_t net_layout;
+    /* device scratch of the multi-launch paths (net_layout 1, RLP_ENV_UGV_OBSTACLE_AVOIDANCE):
+     * rlp_rollout_workspace_bytes(...) bytes, nullable when that is 0 (the fused kernels) */
+    void *workspace;
+    int64_t workspace_bytes;
 } rlp_rollout_cfg;
 
 /* state: [D][n] f64 in/out, carried across segments. need_reset: [n] u8 in/out (1 = env is
@@ -340,6 +350,10 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
                 const rlp_mlp_desc *actor_desc, const float *actor_packed,
                 const rlp_mlp_desc *critic_desc, const float *critic_packed,
                 const rlp_rollout_cfg *cfg, const rlp_rollout_bufs *bufs, rlp_stream_t stream);
+/* bytes of cfg->workspace that rlp_rollout needs for this kind, nets and cfg (T, n, net_layout):
+ * 0 for the fused kernels; RLP_EINVAL on bad arguments. Host-only. */
+int64_t rlp_rollout_workspace_bytes(int kind, const rlp_mlp_desc *actor_desc,
+                                    const rlp_mlp_desc *critic_desc, const rlp_rollout_cfg *cfg);
 
 /* Batched forward of an MFMA-packed [S->H->H->A] net (H = 256): y[rows][A] (last-layer act
  * applied). Proximal_Policy_Optimization2.evaluate (:63-67) / critic(s) in learn() (:91-92). */
@@ -413,7 +427,8 @@ int rlp_adv_normalize(float *adv, int64_t count, double *adv_stats, int parts, r
  *                    constant, so the entropy term has no parameter gradient)
  *   RLP_LOSS_CRITIC: mean((v_target - V(s))^2)  (:155-156)
  * `index` (nullable) gathers the rows of a mini-batch (:110-111 BatchSampler); `loss_sum` (+=)
- * receives the summed per-row loss (divide by rows for the reported loss). `packed` is
+ * receives the summed per-row loss (divide by rows for the reported loss), summed from per-wave
+ * partials in a fixed order (gradient and loss run-to-run identical). `packed` is
  * rlp_mfma_pack(params). The hidden-layer GEMMs use the f16x3 split (RLP_MLP_F16X3 accuracy),
  * the weight-gradient GEMMs exact f32 MFMA. `workspace` holds rlp_ppo2_workspace_floats(). */
 #define RLP_LOSS_ACTOR 0
@@ -443,7 +458,8 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
  * (rlp_ppo2_dense_workspace_floats), fixed summation order (run-to-run identical). Three- and
  * four-layer nets with <= 64 inputs and hidden widths 32k <= 256 (the demos' shapes) run each
  * 2^18-row chunk as five launches (forward chain, loss head, backward chain, every layer's weight
- * gradient, one reduce); other stacks one GEMM launch per layer and pass. */
+ * gradient, one reduce); other stacks one GEMM launch per layer and pass. The loss is summed from
+ * per-block partials in a fixed order too (gradient and loss_sum run-to-run identical). */
 int64_t rlp_ppo2_dense_workspace_floats(const rlp_mlp_desc *desc, int64_t rows);
 int rlp_ppo2_dense_grad(const rlp_mlp_desc *desc, const float *params, const rlp_ppo2_loss_cfg *cfg,
                         const float *s, const float *a, const float *a_logprob, const float *adv,

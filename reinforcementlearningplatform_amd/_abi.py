@@ -131,7 +131,9 @@ class RolloutCfg(C.Structure):
                 ("std", C.c_float * 4), ("a_min", C.c_float * 4), ("a_max", C.c_float * 4),
                 # per-call kernel selection (include/rlp.h): 0 = library default, else value + 1
                 ("mlp_precision", C.c_int32), ("physics", C.c_int32), ("sub", C.c_int32),
-                ("net_layout", C.c_int32)]
+                ("net_layout", C.c_int32),
+                # caller-owned device scratch (rlp_rollout_workspace_bytes)
+                ("workspace", C.c_void_p), ("workspace_bytes", C.c_int64)]
 
 
 class RolloutBufs(C.Structure):

@@ -11,6 +11,7 @@ import torch  # import first: its libamdhip64 is the runtime librlp.so binds to 
 from . import _abi
 
 _LIB_NAME = "librlp.so"
+ABI_VERSION = 2  # include/rlp.h RLP_ABI_VERSION
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
 
@@ -34,13 +35,15 @@ def _declare(lib):
         "rlp_env_observe": (i32, [i32, vp, vp, i32, vp, vp]),
         "rlp_env_step": (i32, [i32, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]),
         "rlp_mlp_param_count": (i64, [vp]),
-        "rlp_mlp_forward": (i32, [vp, vp, vp, vp, i32, vp, vp]),
+        "rlp_mlp_forward_workspace_bytes": (i64, [vp, i32]),
+        "rlp_mlp_forward": (i32, [vp, vp, vp, vp, i32, vp, vp, i64, vp]),
         "rlp_mfma_packed_count": (i64, [vp]),
         "rlp_mfma_pack": (i32, [vp, vp, vp, vp]),
         "rlp_policy_sample": (i32, [vp, i32, i32, vp, vp, vp, vp, u64, u64, u64, vp, vp, vp]),
         "rlp_sac_sample": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, vp, i32, vp, u64, u64, u64, vp, vp,
                                  vp]),
         "rlp_rollout": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "rlp_rollout_workspace_bytes": (i64, [i32, vp, vp, vp]),
         "rlp_mfma_forward": (i32, [vp, vp, vp, vp, i64, vp]),
         "rlp_value_fixup": (i32, [vp, vp, vp, vp, vp, vp, i64, vp]),
         "rlp_set_rollout_sub": (i32, [i32]),
@@ -87,8 +90,9 @@ def lib():
                            f"reinforcementlearningplatform_amd/csrc` or __graft_entry__.build()")
         _lib = C.CDLL(path)
         _declare(_lib)
-        if _lib.rlp_abi_version() != 1:
-            raise RLPError("librlp ABI version mismatch")
+        if _lib.rlp_abi_version() != ABI_VERSION:
+            raise RLPError(f"librlp ABI version {_lib.rlp_abi_version()} != {ABI_VERSION} (rebuild "
+                           f"librlp.so: make -C reinforcementlearningplatform_amd/csrc)")
         for i, (name, size) in enumerate(_abi.check_struct_sizes().items()):
             if _lib.rlp_struct_size(i) != size:
                 raise RLPError(f"struct layout mismatch for {name}: C {_lib.rlp_struct_size(i)} "

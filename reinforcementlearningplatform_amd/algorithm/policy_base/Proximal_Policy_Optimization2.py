@@ -61,8 +61,8 @@ class Proximal_Policy_Optimization2:
         self.seed = int(seed) if seed is not None else int(np.random.randint(0, 2 ** 31 - 1))
         self.sample_counter = 0
         self.cnt = 0
-        from .native_ppo2 import NativePPO2Learner, dense_fits, native_fits
-        fits = all(native_fits(m) or dense_fits(m, a)
+        from .native_ppo2 import NativePPO2Learner, dense_fits
+        fits = all(dense_fits(m, a)
                    for m, a in ((self.actor, True), (self.critic, False)))
         self.learner = learner or ("native" if fits else "torch")
         self.native = None

@@ -39,11 +39,14 @@ def _linears(module):
     return lin, dims
 
 
-def native_fits(module):
+def native_fits(module, is_actor):
     """True when librlp's f16x3 update kernels (rlp_ppo2_grad) take the net: a
-    [S<=8 -> 256 -> 256 -> A<=4] Linear stack."""
+    [S<=8 -> 256 -> 256 -> A<=4] Linear stack whose forward is what those kernels differentiate —
+    tanh hidden layers, the actor's tanh(z) * gain + off head or the critic's linear head (the same
+    probe-forward check as dense_fits: a ReLU 256-256 net has the shape but not the arithmetic)."""
     lin, dims = _linears(module)
-    return len(lin) == 3 and dims[1] == 256 and dims[2] == 256 and dims[0] <= 8 and dims[3] <= 4
+    shape = len(lin) == 3 and dims[1] == 256 and dims[2] == 256 and dims[0] <= 8 and dims[3] <= 4
+    return shape and dense_fits(module, is_actor)
 
 
 def dense_fits(module, is_actor):
@@ -78,17 +81,22 @@ def dense_fits(module, is_actor):
     return ref.shape == h.shape and bool(torch.allclose(ref, h, rtol=1e-5, atol=1e-6))
 
 
+def _update_kind(module, is_actor):
+    """'f16x3' (rlp_ppo2_grad) or 'dense' (rlp_ppo2_dense_grad); ValueError for any other net."""
+    if native_fits(module, is_actor):
+        return "f16x3"
+    if dense_fits(module, is_actor):
+        return "dense"
+    raise ValueError(f"NativePPO2Learner: needs a Linear/Tanh stack (got {_linears(module)[1]} or a "
+                     f"forward that is not tanh hidden layers + "
+                     f"{'tanh * gain + off' if is_actor else 'linear'} output)")
+
+
 class _Net:
     def __init__(self, module, is_actor, device):
         lin, dims = _linears(module)
-        if native_fits(module):
-            self.dense = False  # rlp_ppo2_grad (f16x3 FD + wgrad kernels)
-        elif dense_fits(module, is_actor):
-            self.dense = True   # rlp_ppo2_dense_grad (tiled f32 MFMA GEMMs)
-        else:
-            raise ValueError(f"NativePPO2Learner: needs a Linear/Tanh stack (got {dims} or a "
-                             f"forward that is not tanh hidden layers + "
-                             f"{'tanh * gain + off' if is_actor else 'linear'} output)")
+        # f16x3: rlp_ppo2_grad (FD + wgrad kernels); dense: rlp_ppo2_dense_grad (f32 MFMA GEMMs)
+        self.dense = _update_kind(module, is_actor) == "dense"
         acts = [_abi.RLP_ACT_TANH] * (len(lin) - 1) + [
             _abi.RLP_ACT_TANH if is_actor else _abi.RLP_ACT_NONE]
         self.desc = _abi.MLPDesc.make(dims, acts)
@@ -119,6 +127,8 @@ class NativePPO2Learner:
             v = getattr(self.actor, name, None)
             if torch.is_tensor(v):
                 setattr(self.actor, name, v.to(self.device))
+        _update_kind(self.actor, True)    # both nets checked before any device work
+        _update_kind(self.critic, False)
         self.net_a = _Net(self.actor, True, self.device)
         self.net_c = _Net(self.critic, False, self.device)
         self.pg = process_group

@@ -187,11 +187,11 @@ class VecPPO2:
             self.msg['K_epochs'] = self.msg['k_epo']
         if learner not in ("auto", "native", "torch"):
             raise ValueError(f"VecPPO2: learner {learner!r} (auto | native | torch)")
-        from .native_ppo2 import NativePPO2Learner, dense_fits, native_fits
+        from .native_ppo2 import NativePPO2Learner, dense_fits
         if learner == "auto":  # librlp's update: f16x3 kernels for [S<=8 -> 256 -> 256 -> A<=4],
             # exact-f32 dense GEMMs for other Linear/Tanh stacks (the lidar env's 41-input nets,
             # the PPO2-SOI demo's 4-128-64-32 / 4-64-64 nets); anything else: torch autograd
-            fits = all(native_fits(m) or dense_fits(m, a) for m, a in ((actor, True), (critic, False)))
+            fits = all(dense_fits(m, a) for m, a in ((actor, True), (critic, False)))
             learner = "native" if fits else "torch"
         cls = NativePPO2Learner if learner == "native" else PPO2Learner
         self.learner = cls(actor, critic, self.msg, process_group, self.device)
@@ -254,9 +254,10 @@ class VecPPO2:
         cfg = K.make_rollout_cfg(self.T, self.n, self.seed, self.step0, self.env_id0,
                                  self.std_list(), self.lo, self.hi, self.rule, self.flag,
                                  plain=self.plain)
-        K.rollout(self.kind, self.params, self.env.state, self.need, self.gpu_actor.desc,
-                  self._net_buf(self.gpu_actor), self.gpu_critic.desc,
-                  self._net_buf(self.gpu_critic), cfg, self.bufs)
+        self._rollout_ws = K.rollout(self.kind, self.params, self.env.state, self.need,
+                                     self.gpu_actor.desc, self._net_buf(self.gpu_actor),
+                                     self.gpu_critic.desc, self._net_buf(self.gpu_critic), cfg,
+                                     self.bufs, workspace=getattr(self, "_rollout_ws", None))
         self.step0 += self.T
         self.total_steps += self.T * self.n * self.world
 

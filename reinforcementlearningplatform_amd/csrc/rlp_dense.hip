@@ -1656,22 +1656,33 @@ bool twin_chain_grad(const rlp_dense_net &n1, const rlp_dense_net &n2, const flo
     return true;
 }
 
-// rlp_mlp_forward on the tiled GEMM (one launch per layer) for large batches: y = MLP(x) for
-// the plain Linear-stack layout (W_l [out][in] then b_l), activations RLP_ACT_*; the hidden
-// activations in stream-ordered scratch
-int dense_mlp_forward(const rlp_mlp_desc &d, const float *params, const float *x, float *y, int n,
-                      hipStream_t s) {
-    // three or four layers with one hidden activation (relu: the DDPG / SAC actors' batched
-    // inference; tanh: the PPO2 demo nets' plain-layout rollout), tanh / none at the output,
-    // <= 64 inputs, the first two hidden widths multiples of 32 up to 256, a third up to 128:
-    // one chain launch
+// three or four layers with one hidden activation (relu: the DDPG / SAC actors' batched
+// inference; tanh: the PPO2 demo nets' plain-layout rollout), tanh / none at the output, <= 64
+// inputs, the first two hidden widths multiples of 32 up to 256, a third up to 128: one chain launch
+bool mlp_chain_ok(const rlp_mlp_desc &d) {
     const int L = d.n_layers;
     bool chain = (L == 3 || L == 4) && d.dims[0] <= kChK0 && d.dims[L] <= 8 &&
                  (d.act[L - 1] == RLP_ACT_NONE || d.act[L - 1] == RLP_ACT_TANH) &&
                  (d.act[0] == RLP_ACT_RELU || d.act[0] == RLP_ACT_TANH) && (L == 3 || d.dims[3] <= 16 * kChWaves);
     for (int l = 1; chain && l <= 2; ++l) chain = d.dims[l] <= kChH && d.dims[l] % 32 == 0;
     for (int l = 1; chain && l < L - 1; ++l) chain = d.act[l] == d.act[0];
-    if (chain) {
+    return chain;
+}
+// floats of dense_mlp_forward's scratch (two hidden activations of the per-layer path; 0 for a chain)
+int64_t dense_mlp_scratch_floats(const rlp_mlp_desc &d, int n) {
+    if (mlp_chain_ok(d) || d.n_layers < 2) return 0;
+    int maxw = 0;
+    for (int l = 1; l < d.n_layers; ++l) maxw = d.dims[l] > maxw ? d.dims[l] : maxw;
+    return 2 * (int64_t)n * maxw;
+}
+
+// rlp_mlp_forward on the tiled GEMM (one launch per layer) for large batches: y = MLP(x) for
+// the plain Linear-stack layout (W_l [out][in] then b_l), activations RLP_ACT_*; the hidden
+// activations in the caller's scratch (dense_mlp_scratch_floats)
+int dense_mlp_forward(const rlp_mlp_desc &d, const float *params, const float *x, float *y, int n,
+                      float *scratch, hipStream_t s) {
+    const int L = d.n_layers;
+    if (mlp_chain_ok(d)) {
         int64_t off[RLP_MLP_MAX_LAYERS], o = 0;
         for (int l = 0; l < L; ++l) {
             off[l] = o;
@@ -1694,10 +1705,7 @@ int dense_mlp_forward(const rlp_mlp_desc &d, const float *params, const float *x
     }
     int maxw = 0;
     for (int l = 1; l < d.n_layers; ++l) maxw = d.dims[l] > maxw ? d.dims[l] : maxw;
-    float *buf = nullptr;
-    if (d.n_layers > 1 &&
-        hipMallocAsync((void **)&buf, sizeof(float) * 2 * (size_t)n * maxw, s) != hipSuccess)
-        return fail(RLP_ENOMEM, "rlp_mlp_forward: scratch");
+    float *buf = scratch;
     const float *in = x;
     int64_t off = 0;
     for (int l = 0; l < d.n_layers; ++l) {
@@ -1709,7 +1717,6 @@ int dense_mlp_forward(const rlp_mlp_desc &d, const float *params, const float *x
         dense_fwd(mat(in, n, K, K), L, n, kind, out, nullptr, nullptr, nullptr, s);
         in = out;
     }
-    if (buf) (void)hipFreeAsync(buf, s);
     RLP_CHECK_LAUNCH("rlp_mlp_forward (dense)");
     return RLP_OK;
 }
@@ -2136,7 +2143,7 @@ struct PpoDenseArgs {
     float inv_rows, eps_clip, ent_row;
     float gain[4], log_std[4], inv_var[4];
     float *dy;                   // [B][A]: dL/dz_L
-    double *loss_sum;
+    double *lpart;               // per-block loss partials (summed in order by loss_sum_kernel)
 };
 
 template <bool ACTOR>
@@ -2173,7 +2180,19 @@ __global__ void __launch_bounds__(256) ppo2_dense_head_kernel(PpoDenseArgs h) {
     __shared__ double red[4];
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
     __syncthreads();
-    if (threadIdx.x == 0 && h.loss_sum) atomicAdd(h.loss_sum, (red[0] + red[1]) + (red[2] + red[3]));
+    if (threadIdx.x == 0) h.lpart[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// *loss_sum += the head blocks' partials, in block order then a fixed shuffle / LDS tree
+__global__ void __launch_bounds__(256) loss_sum_kernel(const double *__restrict__ lpart, int64_t n,
+                                                       double *loss_sum) {
+    double l = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += 256) l += lpart[i];
+    for (int o = 1; o < 64; o <<= 1) l += __shfl_xor(l, o);
+    __shared__ double red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
+    __syncthreads();
+    if (threadIdx.x == 0) *loss_sum += (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // the workspace's constant vectors: 1024 ones (the hidden layers' tanh backward through the
@@ -2201,7 +2220,7 @@ __global__ void __launch_bounds__(256) chunk_sum_kernel(const float *__restrict_
 }
 
 struct PpoDenseWs {  // float offsets into the workspace
-    int64_t act, t, g0, g1, g2, g3, part, ones, head, slots, total;
+    int64_t act, t, g0, g1, g2, g3, part, ones, head, slots, lpart, total;
 };
 inline bool ppo2_dense_ok(const rlp_mlp_desc &d, bool actor) {
     if (d.n_layers < 1 || d.n_layers > RLP_MLP_MAX_LAYERS) return false;
@@ -2260,6 +2279,7 @@ inline PpoDenseWs ppo2_dense_ws(const rlp_mlp_desc &d, int64_t rows) {
     w.ones = take(1024);
     w.head = take(8);
     w.slots = take(chunks * np);
+    w.lpart = take(2 * ((rows + 255) / 256));  // f64 loss partial per head block
     w.total = o;
     return w;
 }
@@ -2297,7 +2317,7 @@ int rlp_ppo2_dense_grad(const rlp_mlp_desc *desc, const float *params, const rlp
         np += (int64_t)d.dims[l] * d.dims[l + 1] + d.dims[l + 1];
     }
     PpoDenseArgs h{};
-    h.A = A; h.inv_rows = 1.f / (float)rows; h.eps_clip = cfg->eps_clip; h.loss_sum = loss_sum;
+    h.A = A; h.inv_rows = 1.f / (float)rows; h.eps_clip = cfg->eps_clip;
     PpoConsts pc{};
     float ent = 0.f;
     for (int k = 0; k < A && actor; ++k) {
@@ -2350,6 +2370,7 @@ int rlp_ppo2_dense_grad(const rlp_mlp_desc *desc, const float *params, const rlp
         // head: dL/dz_L into g0
         h.B = B;
         h.dy = ws + w.g0;
+        h.lpart = reinterpret_cast<double *>(ws + w.lpart) + r0 / 256;
         if (actor) {
             h.t = ws + w.t; h.mean = act + ao[L - 1];
             h.a = a + r0 * A; h.lp = a_logprob + r0 * A; h.adv = adv + r0;
@@ -2425,6 +2446,9 @@ int rlp_ppo2_dense_grad(const rlp_mlp_desc *desc, const float *params, const rlp
         }
     }
     chunk_sum_kernel<<<(int)((np + 255) / 256), 256, 0, st>>>(ws + w.slots, (int)nchunks, np, grad);
+    if (loss_sum)
+        loss_sum_kernel<<<1, 256, 0, st>>>(reinterpret_cast<const double *>(ws + w.lpart),
+                                           (rows + 255) / 256, loss_sum);
     RLP_CHECK_LAUNCH("rlp_ppo2_dense_grad");
     return RLP_OK;
 }

@@ -277,8 +277,26 @@ using namespace rlp;
 
 namespace rlp {
 int dense_mlp_forward(const rlp_mlp_desc &d, const float *params, const float *x, float *y, int n,
-                      hipStream_t s);  // rlp_dense.hip
+                      float *scratch, hipStream_t s);  // rlp_dense.hip
+int64_t dense_mlp_scratch_floats(const rlp_mlp_desc &d, int n);  // rlp_dense.hip (0: chain path)
 constexpr int kMlpDenseRows = 2048;
+
+// the path rlp_mlp_forward takes for (desc, n, masked): true = rlp_dense.hip's tiled GEMM / chain
+bool mlp_dense_path(const rlp_mlp_desc &d, int n, bool masked) {
+    int maxw = 0;
+    bool acts_ok = true;
+    for (int l = 0; l <= d.n_layers; ++l) maxw = d.dims[l] > maxw ? d.dims[l] : maxw;
+    for (int l = 0; l < d.n_layers; ++l)
+        acts_ok &= d.act[l] == RLP_ACT_RELU || d.act[l] == RLP_ACT_TANH || d.act[l] == RLP_ACT_NONE;
+    // (the GEMM's element offsets are 32-bit: rows x width < 2^31)
+    return !masked && n >= kMlpDenseRows && acts_ok && (int64_t)n * maxw < (int64_t(1) << 31);
+}
+bool mlp_desc_ok(const rlp_mlp_desc *d) {
+    if (!d || d->n_layers < 1 || d->n_layers > RLP_MLP_MAX_LAYERS) return false;
+    for (int l = 0; l <= d->n_layers; ++l)
+        if (d->dims[l] < 1 || d->dims[l] > kMlpMaxW) return false;
+    return true;
+}
 }  // namespace rlp
 
 extern "C" {
@@ -291,8 +309,14 @@ int64_t rlp_mlp_param_count(const rlp_mlp_desc *desc) {
     return c;
 }
 
+int64_t rlp_mlp_forward_workspace_bytes(const rlp_mlp_desc *desc, int n) {
+    if (!mlp_desc_ok(desc) || n < 0) return RLP_EINVAL;
+    return mlp_dense_path(*desc, n, false) ? 4 * dense_mlp_scratch_floats(*desc, n) : 0;
+}
+
 int rlp_mlp_forward(const rlp_mlp_desc *desc, const float *params, const float *x, float *y,
-                    int n, const uint8_t *mask, rlp_stream_t stream) {
+                    int n, const uint8_t *mask, void *workspace, int64_t workspace_bytes,
+                    rlp_stream_t stream) {
     RLP_REQUIRE(desc && params && x && y, "rlp_mlp_forward: null argument");
     RLP_REQUIRE(desc->n_layers >= 1 && desc->n_layers <= RLP_MLP_MAX_LAYERS,
                 "rlp_mlp_forward: n_layers %d", desc->n_layers);
@@ -305,13 +329,14 @@ int rlp_mlp_forward(const rlp_mlp_desc *desc, const float *params, const float *
     if (n <= 0) return n == 0 ? RLP_OK : RLP_EINVAL;
     // large unmasked batches (the off-policy drivers' acting forward over every env) on the tiled
     // GEMM of rlp_dense.hip: one launch per layer, weights staged once per 64-row tile
-    bool acts_ok = true;
-    for (int l = 0; l < desc->n_layers; ++l)
-        acts_ok &= desc->act[l] == RLP_ACT_RELU || desc->act[l] == RLP_ACT_TANH ||
-                   desc->act[l] == RLP_ACT_NONE;
-    // (the GEMM's element offsets are 32-bit: rows x width < 2^31)
-    if (!mask && n >= kMlpDenseRows && acts_ok && (int64_t)n * maxw < (int64_t(1) << 31))
-        return dense_mlp_forward(*desc, params, x, y, n, as_stream(stream));
+    if (mlp_dense_path(*desc, n, mask != nullptr)) {
+        const int64_t need = 4 * dense_mlp_scratch_floats(*desc, n);
+        RLP_REQUIRE(workspace_bytes >= need && (need == 0 || workspace),
+                    "rlp_mlp_forward: workspace of %lld bytes, need %lld "
+                    "(rlp_mlp_forward_workspace_bytes)", (long long)workspace_bytes, (long long)need);
+        return dense_mlp_forward(*desc, params, x, y, n, static_cast<float *>(workspace),
+                                 as_stream(stream));
+    }
     // row stride: multiple of 32 (+2) so the B-operand reads (16 rows x 2 k per half-wave) hit
     // 32 distinct banks
     const int ldw = ((maxw + 31) / 32) * 32 + 2;

@@ -725,9 +725,13 @@ __global__ void __launch_bounds__(256) oa_boot_kernel(int T, int n, const float 
     if (!b.done[k]) b.value_next[k] = v[i];
 }
 
+inline int64_t rollout_oa_ws_bytes(int n) {
+    return (int64_t)n * (int64_t)(sizeof(double) + sizeof(int32_t) + sizeof(float));
+}
+
 static int rollout_oa(const void *params, double *state, uint8_t *need_reset, const float *actor,
                       const MfmaNet &an, const float *critic, const MfmaNet &cn,
-                      const RolloutArgs &ra, const rlp_rollout_bufs &b, hipStream_t s) {
+                      const RolloutArgs &ra, const rlp_rollout_bufs &b, void *ws, hipStream_t s) {
     const auto &p = *static_cast<const OA::P *>(params);
     if (an.S != OA::S || cn.S != OA::S || an.A != OA::A || cn.A != 1)
         return fail(RLP_EINVAL, "rlp_rollout: net dims (S=%d,A=%d / S=%d,A=%d) != env (S=%d,A=%d)",
@@ -735,10 +739,7 @@ static int rollout_oa(const void *params, double *state, uint8_t *need_reset, co
     if (an.H != 256 || cn.H != 256)
         return fail(RLP_EUNSUPPORTED, "rlp_rollout: hidden width %d/%d (built for 256)", an.H, cn.H);
     const int n = ra.n, T = ra.T, nb = (n + 255) / 256;
-    // per-call scratch (stream-ordered): the step's f64 reward, i32 flag, the bootstrap V
-    void *ws = nullptr;
-    const size_t wsz = (size_t)n * (sizeof(double) + sizeof(int32_t) + sizeof(float));
-    if (hipMallocAsync(&ws, wsz, s) != hipSuccess) return fail(RLP_ENOMEM, "rlp_rollout: scratch");
+    // the caller's scratch (rollout_oa_ws_bytes): the step's f64 reward, i32 flag, the bootstrap V
     double *r64 = static_cast<double *>(ws);
     int32_t *f32 = reinterpret_cast<int32_t *>(r64 + n);
     float *vb = reinterpret_cast<float *>(f32 + n);
@@ -767,7 +768,6 @@ static int rollout_oa(const void *params, double *state, uint8_t *need_reset, co
                                       nullptr, nullptr, 0, s);
         if (rc == RLP_OK) oa_boot_kernel<<<nb, 256, 0, s>>>(T, n, vb, b);
     }
-    (void)hipFreeAsync(ws, s);
     if (rc != RLP_OK) return rc;
     RLP_CHECK_LAUNCH("rlp_rollout (UGVForwardObstacleAvoidance)");
     return RLP_OK;
@@ -862,11 +862,19 @@ __global__ void __launch_bounds__(256) plain_step_kernel(typename Env<KIND>::P p
     for (int d = 0; d < E::D; ++d) state[(size_t)d * n + i] = s[d];
 }
 
+// the plain path's scratch: the bootstrap V, then rlp_mlp_forward's workspace (shared by the two
+// nets' forwards, which run one after the other on the stream)
+inline int64_t rollout_plain_ws_bytes(const rlp_mlp_desc &ad, const rlp_mlp_desc &cd, int n) {
+    const int64_t wa = rlp_mlp_forward_workspace_bytes(&ad, n), wc = rlp_mlp_forward_workspace_bytes(&cd, n);
+    if (wa < 0 || wc < 0) return RLP_EINVAL;
+    return ((int64_t)n * 4 + 255) / 256 * 256 + (wa > wc ? wa : wc);
+}
+
 template <int KIND>
 static int rollout_plain(const void *params, double *state, uint8_t *need_reset,
                          const rlp_mlp_desc &ad, const float *actor, const rlp_mlp_desc &cd,
                          const float *critic, const RolloutArgs &ra, const rlp_rollout_bufs &b,
-                         hipStream_t s) {
+                         void *ws, int64_t ws_bytes, hipStream_t s) {
     using E = Env<KIND>;
     const auto &p = *static_cast<const typename E::P *>(params);
     if (ad.dims[0] != E::S || cd.dims[0] != E::S || ad.dims[ad.n_layers] != E::A ||
@@ -876,23 +884,24 @@ static int rollout_plain(const void *params, double *state, uint8_t *need_reset,
     if (ad.act[ad.n_layers - 1] != RLP_ACT_TANH)
         return fail(RLP_EUNSUPPORTED, "rlp_rollout: the actor's last layer must be tanh");
     const int n = ra.n, T = ra.T, nb = (n + 255) / 256;
-    float *vb = nullptr;  // the bootstrap V (stream-ordered scratch)
-    if (hipMallocAsync((void **)&vb, sizeof(float) * (size_t)n, s) != hipSuccess)
-        return fail(RLP_ENOMEM, "rlp_rollout: scratch of %d floats", n);
+    float *vb = static_cast<float *>(ws);  // the bootstrap V
+    void *mws = static_cast<char *>(ws) + ((int64_t)n * 4 + 255) / 256 * 256;
+    const int64_t mwb = ws_bytes - ((int64_t)n * 4 + 255) / 256 * 256;
     plain_begin_kernel<KIND><<<nb, 256, 0, s>>>(p, state, need_reset, ra, b.obs);
     int rc = RLP_OK;
     for (int t = 0; t < T && rc == RLP_OK; ++t) {
         const size_t k0 = (size_t)t * n;
         const float *obs_t = b.obs + k0 * E::S;
-        rc = rlp_mlp_forward(&cd, critic, obs_t, b.value + k0, n, nullptr, s);
-        if (rc == RLP_OK) rc = rlp_mlp_forward(&ad, actor, obs_t, b.action + k0 * E::A, n, nullptr, s);
+        rc = rlp_mlp_forward(&cd, critic, obs_t, b.value + k0, n, nullptr, mws, mwb, s);
+        if (rc == RLP_OK)
+            rc = rlp_mlp_forward(&ad, actor, obs_t, b.action + k0 * E::A, n, nullptr, mws, mwb, s);
         if (rc == RLP_OK) plain_step_kernel<KIND><<<nb, 256, 0, s>>>(p, state, need_reset, ra, t, b);
     }
     if (rc == RLP_OK) {  // V(s'_{T-1}) of the envs still running
-        rc = rlp_mlp_forward(&cd, critic, b.obs_next + (size_t)(T - 1) * n * E::S, vb, n, nullptr, s);
+        rc = rlp_mlp_forward(&cd, critic, b.obs_next + (size_t)(T - 1) * n * E::S, vb, n, nullptr,
+                             mws, mwb, s);
         if (rc == RLP_OK) oa_boot_kernel<<<nb, 256, 0, s>>>(T, n, vb, b);
     }
-    (void)hipFreeAsync(vb, s);
     if (rc != RLP_OK) return rc;
     RLP_CHECK_LAUNCH("rlp_rollout (plain-layout nets)");
     return RLP_OK;
@@ -957,6 +966,14 @@ int rlp_value_fixup(const rlp_mlp_desc *critic_desc, const float *critic_packed,
                                     1, as_stream(stream));
 }
 
+int64_t rlp_rollout_workspace_bytes(int kind, const rlp_mlp_desc *actor_desc,
+                                    const rlp_mlp_desc *critic_desc, const rlp_rollout_cfg *cfg) {
+    if (!actor_desc || !critic_desc || !cfg || cfg->n < 0 || cfg->T < 1) return RLP_EINVAL;
+    if (cfg->net_layout == 1) return rollout_plain_ws_bytes(*actor_desc, *critic_desc, cfg->n);
+    if (cfg->net_layout != 0) return RLP_EINVAL;
+    return kind == RLP_ENV_UGV_OBSTACLE_AVOIDANCE ? rollout_oa_ws_bytes(cfg->n) : 0;
+}
+
 int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_reset,
                 const rlp_mlp_desc *actor_desc, const float *actor_packed,
                 const rlp_mlp_desc *critic_desc, const float *critic_packed,
@@ -1004,12 +1021,20 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
     const int sub = cfg->sub ? cfg->sub : g_rollout_sub;
     const int prec = cfg->mlp_precision ? cfg->mlp_precision - 1 : g_mlp_precision;
     const int physics = cfg->physics == 8 ? -1 : cfg->physics ? cfg->physics - 1 : g_rollout_shared_physics;
+    {  // the caller's workspace, checked before any launch
+        const int64_t need = rlp_rollout_workspace_bytes(kind, actor_desc, critic_desc, cfg);
+        RLP_REQUIRE(need >= 0, "rlp_rollout: workspace query failed (net descs)");
+        RLP_REQUIRE(cfg->workspace_bytes >= need && (need == 0 || cfg->workspace),
+                    "rlp_rollout: workspace of %lld bytes, need %lld (rlp_rollout_workspace_bytes)",
+                    (long long)cfg->workspace_bytes, (long long)need);
+    }
     if (cfg->net_layout == 1) {
         switch (kind) {
 #define RLP_PLAIN(K)                                                                              \
     case K:                                                                                       \
         return rollout_plain<K>(env_params, state, need_reset, *actor_desc, actor_packed,        \
-                                *critic_desc, critic_packed, ra, b, s);
+                                *critic_desc, critic_packed, ra, b, cfg->workspace,              \
+                                cfg->workspace_bytes, s);
             RLP_PLAIN(RLP_ENV_CARTPOLE)
             RLP_PLAIN(RLP_ENV_CARTPOLE_ANGLEONLY)
             RLP_PLAIN(RLP_ENV_SOI)
@@ -1041,7 +1066,8 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
                                                           actor_packed, an, critic_packed, cn, ra,
                                                           b, sub, prec, physics, s);
     case RLP_ENV_UGV_OBSTACLE_AVOIDANCE:
-        return rollout_oa(env_params, state, need_reset, actor_packed, an, critic_packed, cn, ra, b, s);
+        return rollout_oa(env_params, state, need_reset, actor_packed, an, critic_packed, cn, ra, b,
+                          cfg->workspace, s);
     }
     return fail(RLP_EINVAL, "rlp_rollout: unknown env kind %d", kind);
 }

@@ -37,7 +37,7 @@ struct Ppo2Args {
     float *g2t;         // [tiles][256][64]
     unsigned *g2max;    // bits of max|g2| (atomicMax)
     float *part3;       // [grid * 4][A*256 + A + 256*S + 256]: per-wave dW3 | db3 | dW1 | db1
-    double *loss_sum;
+    double *lpart;      // [FD waves]: per-wave loss partials (summed in order by the reduce)
 };
 
 // block barrier for LDS hand-offs only: drains this wave's LDS ops, not its global loads (HIP's
@@ -567,7 +567,7 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
     }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) lsum += __shfl_xor(lsum, o);
-    if (lane == 0 && g.loss_sum) atomicAdd(g.loss_sum, lsum);
+    if (lane == 0) g.lpart[blockIdx.x * kFdWaves + wv] = lsum;
 }
 
 struct WArgs {
@@ -794,7 +794,8 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
 constexpr int kRedSplit = 16;
 __global__ void __launch_bounds__(64 * kRedSplit)
 ppo2_reduce_kernel(MfmaNet net, const float *__restrict__ part, int nw,
-                   const float *__restrict__ part3, int n3, float *grad) {
+                   const float *__restrict__ part3, int n3, float *grad,
+                   const double *__restrict__ lpart, double *loss_sum) {
     const int H = net.H, S = net.S, A = net.A;
     const int64_t total = (int64_t)H * S + H + (int64_t)H * H + H + (int64_t)A * H + A;
     const int pw = H * H + H, p3 = A * H + A + H * S + H;
@@ -822,6 +823,20 @@ ppo2_reduce_kernel(MfmaNet net, const float *__restrict__ part, int nw,
 #pragma unroll
         for (int k = 0; k < kRedSplit; ++k) t += red[k][o];
         grad[i] = t;
+    }
+    // block 0 also sums the FD waves' loss partials in a fixed order (run-to-run identical loss)
+    if (blockIdx.x == 0 && loss_sum) {
+        double l = 0.0;
+        for (int w = threadIdx.x; w < n3; w += 64 * kRedSplit) l += lpart[w];
+        for (int k = 1; k < 64; k <<= 1) l += __shfl_xor(l, k);
+        __shared__ double lred[kRedSplit];
+        if ((threadIdx.x & 63) == 0) lred[threadIdx.x >> 6] = l;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double t = 0.0;
+            for (int k = 0; k < kRedSplit; ++k) t += lred[k];
+            *loss_sum += t;
+        }
     }
 }
 
@@ -906,7 +921,8 @@ int64_t rlp_ppo2_workspace_floats(const rlp_mlp_desc *desc, int64_t rows) {
     const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
     const int64_t grid = ppo2_grid();  // wgrad: one block per CU; FD: two
     return tiles * kUpdTileFloats + grid * (kUpdH * kUpdH + kUpdH) +
-           2 * grid * 4 * (net.A * kUpdH + net.A + kUpdH * net.S + kUpdH) + 16;
+           2 * grid * 4 * (net.A * kUpdH + net.A + kUpdH * net.S + kUpdH) + 16 +
+           2 * grid * kFdWaves;  // g2max (16 floats), the FD waves' f64 loss partials
 }
 
 int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_loss_cfg *cfg,
@@ -954,7 +970,7 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
                                            (net.A * kUpdH + net.A + kUpdH * net.S + kUpdH));
     if (hipMemsetAsync(g.g2max, 0, sizeof(unsigned), st) != hipSuccess)
         return fail(RLP_EINVAL, "rlp_ppo2_grad: memset");
-    g.loss_sum = loss_sum;
+    g.lpart = reinterpret_cast<double *>(reinterpret_cast<float *>(g.g2max) + 16);
 #define RLP_FD(KS1, A_, L) ppo2_fd_kernel<KS1, A_, L><<<gfd, 64 * kFdWaves, 0, st>>>(g)
     if (actor) {
         if (net.ks1 == 1) {
@@ -975,8 +991,8 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (wgrad)");
     const int64_t total = (int64_t)net.H * net.S + net.H + (int64_t)net.H * net.H + net.H +
                           (int64_t)net.A * net.H + net.A;
-    ppo2_reduce_kernel<<<(int)((total + 63) / 64), 64 * kRedSplit, 0, st>>>(net, partw, grid,
-                                                                          g.part3, gfd * kFdWaves, grad);
+    ppo2_reduce_kernel<<<(int)((total + 63) / 64), 64 * kRedSplit, 0, st>>>(
+        net, partw, grid, g.part3, gfd * kFdWaves, grad, g.lpart, loss_sum);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (reduce)");
     return RLP_OK;
 }

@@ -53,13 +53,21 @@ def env_step(kind, params, state, action, want_obs_cur=True):
     return oc, on, r, f, d
 
 
-def mlp_forward(desc, params, x, mask=None, out=None):
+def mlp_forward(desc, params, x, mask=None, out=None, workspace=None):
+    """rlp_mlp_forward; the per-layer GEMM path's scratch (rlp_mlp_forward_workspace_bytes) is
+    `workspace` (a uint8 device tensor) when it is large enough, else allocated here."""
     n = x.shape[0]
     outn = desc.dims[desc.n_layers]
     out = out if out is not None else torch.empty((n, outn), dtype=torch.float32, device=x.device)
     x_ = x.contiguous()
-    check(lib().rlp_mlp_forward(C.byref(desc), ptr(params), ptr(x_), ptr(out), n,
-                                ptr(mask), stream_ptr()), "rlp_mlp_forward")
+    need = int(lib().rlp_mlp_forward_workspace_bytes(C.byref(desc), n)) if mask is None else 0
+    if need < 0:
+        check(need, "rlp_mlp_forward_workspace_bytes")
+    if need > 0 and (workspace is None or workspace.numel() < need):
+        workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
+    check(lib().rlp_mlp_forward(C.byref(desc), ptr(params), ptr(x_), ptr(out), n, ptr(mask),
+                                ptr(workspace) if need > 0 else None, need, stream_ptr()),
+          "rlp_mlp_forward")
     return out
 
 
@@ -143,12 +151,29 @@ def rollout_buffers(kind, T, n, device=None):
                                                                     device=dev))
 
 
+def rollout_workspace_bytes(kind, actor_desc, critic_desc, cfg):
+    need = int(lib().rlp_rollout_workspace_bytes(kind, C.byref(actor_desc), C.byref(critic_desc),
+                                                 C.byref(cfg)))
+    if need < 0:
+        check(need, "rlp_rollout_workspace_bytes")
+    return need
+
+
 def rollout(kind, params, state, need_reset, actor_desc, actor_packed, critic_desc, critic_packed,
-            cfg, bufs):
+            cfg, bufs, workspace=None):
+    """rlp_rollout. The multi-launch paths' scratch (rlp_rollout_workspace_bytes: the plain-layout
+    nets and the lidar env) is `workspace` (uint8 device tensor) when large enough, else allocated
+    here; the workspace used is returned so a driver loop can keep it (allocated once)."""
+    need = rollout_workspace_bytes(kind, actor_desc, critic_desc, cfg)
+    if need > 0 and (workspace is None or workspace.numel() < need):
+        workspace = torch.empty(need, dtype=torch.uint8, device=state.device)
+    cfg.workspace = workspace.data_ptr() if need > 0 else None
+    cfg.workspace_bytes = workspace.numel() if need > 0 else 0
     cb = _abi.RolloutBufs(**{k: v.data_ptr() for k, v in bufs.items()})
     check(lib().rlp_rollout(kind, C.byref(params), ptr(state), ptr(need_reset), C.byref(actor_desc),
                             ptr(actor_packed), C.byref(critic_desc), ptr(critic_packed),
                             C.byref(cfg), C.byref(cb), stream_ptr()), "rlp_rollout")
+    return workspace
 
 
 def make_rollout_cfg(T, n, seed, step0, env_id0, std, a_min, a_max, success_rule, success_flag,

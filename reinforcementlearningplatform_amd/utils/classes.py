@@ -327,8 +327,10 @@ class GPUNet:
     def refresh(self):
         """Re-read the module's parameters (call after every optimiser step)."""
         with torch.no_grad():
-            self.flat = torch.cat([t.detach().reshape(-1).to(self.device, torch.float32)
-                                   for l in self.linears for t in (l.weight, l.bias)]).contiguous()
+            region = self._params_region() if self.flat is not None else None
+            if region is None or region.data_ptr() != self.flat.data_ptr():  # aliased: current
+                self.flat = torch.cat([t.detach().reshape(-1).to(self.device, torch.float32)
+                                       for l in self.linears for t in (l.weight, l.bias)]).contiguous()
             cnt = K.lib().rlp_mfma_packed_count(__import__("ctypes").byref(self.desc))
             self.packed = K.mfma_pack(self.desc, self.flat, out=self.packed) if cnt > 0 else None
 
@@ -336,7 +338,9 @@ class GPUNet:
         """The module's (weight, bias) tensors as one contiguous region of a single buffer (a
         native update's flat parameters: module parameters are views of it), or None."""
         ts = [t for l in self.linears for t in (l.weight, l.bias)]
-        if any(t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous()
+        # against the flat buffer's device: self.device may be an index-less torch.device('cuda')
+        # while the parameters report cuda:0
+        if any(t.device != self.flat.device or t.dtype != torch.float32 or not t.is_contiguous()
                for t in ts):
             return None
         base = ts[0].data_ptr()
@@ -347,7 +351,8 @@ class GPUNet:
                 return None
             off += t.numel()
         st = ts[0].storage_offset()
-        return torch.as_strided(ts[0], (off,), (1,), st)
+        # detached: the alias is plain data (no autograd view of the parameters)
+        return torch.as_strided(ts[0].detach(), (off,), (1,), st)
 
     def copy_from_module(self):
         """refresh() in place (graph-capturable: the same flat / packed tensors). When the

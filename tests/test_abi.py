@@ -53,6 +53,45 @@ def test_bad_arguments_return_status():
     assert lib.rlp_mlp_param_count(C.byref(d)) == d.param_count() == 67329
 
 
+def test_workspaces_are_caller_owned_and_checked():
+    """The multi-launch paths take a caller-owned workspace (no per-call device allocation):
+    the queries size it, and a too-small one is refused on the host before any launch."""
+    lib = _native.lib()
+    dev = C.c_void_p(1 << 20)  # never dereferenced: the calls must fail before any launch
+    n = 4096
+    # rlp_mlp_forward's per-layer GEMM path (widths not multiples of 32: no fused chain)
+    d = _abi.MLPDesc.make([4, 100, 100, 1], [1, 1, 0])
+    need = lib.rlp_mlp_forward_workspace_bytes(C.byref(d), n)
+    assert need == 2 * n * 100 * 4
+    assert lib.rlp_mlp_forward(C.byref(d), dev, dev, dev, n, None, None, 0, None) == _abi.RLP_EINVAL
+    assert b"workspace" in lib.rlp_last_error_string()
+    assert lib.rlp_mlp_forward(C.byref(d), dev, dev, dev, n, None, dev, need - 4, None) == _abi.RLP_EINVAL
+    chain = _abi.MLPDesc.make([4, 128, 64, 32, 2], [1, 1, 1, 1])   # the PPO2-SOI demo actor
+    assert lib.rlp_mlp_forward_workspace_bytes(C.byref(chain), n) == 0
+    assert lib.rlp_mlp_forward_workspace_bytes(C.byref(d), 100) == 0      # small batches: no GEMM
+    # rlp_rollout: the plain-layout nets and the lidar env need scratch, the fused kernels none
+    crit = _abi.MLPDesc.make([4, 64, 64, 1], [1, 1, 0])
+    cfg = _abi.RolloutCfg()
+    cfg.T, cfg.n, cfg.net_layout = 8, n, 1
+    cfg.std[0] = cfg.std[1] = 1.0
+    need = lib.rlp_rollout_workspace_bytes(_abi.RLP_ENV_SOI, C.byref(chain), C.byref(crit), C.byref(cfg))
+    assert need >= 4 * n
+    p = _abi.soi_params("env")
+    bufs = _abi.RolloutBufs(*([dev.value] * 10))
+    for ws, wsb in ((None, 0), (dev, need - 1)):
+        cfg.workspace, cfg.workspace_bytes = ws, wsb
+        rc = lib.rlp_rollout(_abi.RLP_ENV_SOI, C.byref(p), dev, dev, C.byref(chain), dev,
+                             C.byref(crit), dev, C.byref(cfg), C.byref(bufs), None)
+        assert rc == _abi.RLP_EINVAL and b"workspace" in lib.rlp_last_error_string()
+    cfg.net_layout = 0
+    big = _abi.MLPDesc.make([41, 256, 256, 2], [1, 1, 1])
+    bigc = _abi.MLPDesc.make([41, 256, 256, 1], [1, 1, 0])
+    assert lib.rlp_rollout_workspace_bytes(_abi.RLP_ENV_UGV_OBSTACLE_AVOIDANCE, C.byref(big),
+                                           C.byref(bigc), C.byref(cfg)) == 16 * n
+    assert lib.rlp_rollout_workspace_bytes(_abi.RLP_ENV_CARTPOLE, C.byref(big), C.byref(bigc),
+                                           C.byref(cfg)) == 0
+
+
 def test_product_never_imports_oracle():
     pkg = os.path.join(ROOT, "reinforcementlearningplatform_amd")
     for dp, _, fs in os.walk(pkg):

@@ -14,6 +14,8 @@
     against the oracle: physics exact / 1e-9, the oracle's double-accumulated policy and critic on
     the kernel's observations; VecPPO2 runs whole iterations on them.
 """
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -159,8 +161,10 @@ def test_dense_grad_vs_float64(net, rows):
     lrn.grads(s, a, lp, adv, vt)
     gn = [lrn.net_a.grad.double().cpu().numpy(), lrn.net_c.grad.double().cpu().numpy()]
     g2 = [lrn.net_a.grad.clone(), lrn.net_c.grad.clone()]
+    loss1 = lrn.loss.clone()
     lrn.grads(s, a, lp, adv, vt)
     assert torch.equal(g2[0], lrn.net_a.grad) and torch.equal(g2[1], lrn.net_c.grad)  # fixed order
+    assert torch.equal(loss1, lrn.loss)   # the loss sums too (per-block partials, fixed order)
     t64 = _loss_grads(_as(actor, torch.float64, "cuda"), _as(critic, torch.float64, "cuda"),
                       *(x.double() for x in (s, a, lp, adv, vt)))
     t32 = _loss_grads(_as(actor, torch.float32, "cuda"), _as(critic, torch.float32, "cuda"),
@@ -266,12 +270,24 @@ def test_vec_ppo2_soi_demo_nets():
     assert agent.plain and type(agent.learner).__name__ == "NativePPO2Learner"
     assert agent.learner.net_a.dense and agent.learner.net_c.dense
     a0 = None
-    for it in range(3):
-        out = agent.iteration()
-        assert torch.isfinite(out["actor_loss"]) and torch.isfinite(out["critic_loss"])
-        if it == 0:
-            a0 = agent.bufs["action"].clone()
-        # V(s') of done && !success rows came from the critic, the others from the rollout
+    checked = 0
+    for it in range(4):   # 4 x 64 steps: the envs still running at 250 steps (time_max 5 s) time out
+        agent.rollout()
+        agent.advantages()
+        # V(s') of the done && !success rows (time-outs) comes from the masked generic forward:
+        # the critic on obs_next, against a float64 torch forward of the same critic
         b = agent.bufs
         assert torch.isfinite(b["value_next"]).all()
+        m = (b["done"].bool() & ~b["success"].bool()).view(-1)
+        if m.any():
+            x = b["obs_next"].view(-1, env.state_dim)[m].double()
+            ref = copy.deepcopy(agent.critic).double()(x).view(-1)
+            got = b["value_next"].view(-1)[m].double()
+            torch.testing.assert_close(got, ref, rtol=1e-5, atol=2e-6)
+            checked += int(m.sum())
+        al, cl = agent.update()
+        assert torch.isfinite(al) and torch.isfinite(cl)
+        if it == 0:
+            a0 = agent.bufs["action"].clone()
+    assert checked > 0
     assert not torch.equal(a0, agent.bufs["action"])

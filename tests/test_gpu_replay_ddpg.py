@@ -201,8 +201,12 @@ def test_ddpg_graphed_update_is_one_adam_step():
         pg = torch.cat([p.detach().reshape(-1) for p in m_g.parameters()])
         assert torch.isfinite(pg).all() and not torch.equal(pe, pg)
         assert float((pe - pg).abs().max()) <= 1.5 * lr
+    # the GPU actor aliases the native update's actor parameters: no copy launch in the graph
+    assert g_agent._native is not None
+    assert g_agent.gpu_actor.flat.data_ptr() == g_agent._native.nets["actor"].flat.data_ptr()
     flat = g_agent.gpu_actor.flat.clone()
     g_agent.gpu_actor.refresh()
+    assert g_agent.gpu_actor.flat.data_ptr() == g_agent._native.nets["actor"].flat.data_ptr()
     torch.testing.assert_close(flat, g_agent.gpu_actor.flat, rtol=0, atol=0)
     for _ in range(5):
         g_agent.learn(is_reward_ascent=False, iter=2)

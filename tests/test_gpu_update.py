@@ -85,6 +85,11 @@ def test_ppo2_grads_vs_torch(S, A, N):
             assert en <= 4 * e32 + 2e-6 * scale, (name, i, en, e32, scale)
     la, lc = (nl.loss / N).cpu().tolist()
     assert abs(la - al64) <= 1e-5 * (abs(al64) + 1) and abs(lc - cl64) <= 1e-5 * (abs(cl64) + 1)
+    # run-to-run identical: gradients and the loss sums (per-wave partials, fixed-order reduce)
+    g0, l0 = (nl.net_a.grad.clone(), nl.net_c.grad.clone()), nl.loss.clone()
+    nl.grads(dev(s), dev(a), dev(lp), dev(adv), dev(vt))
+    assert torch.equal(g0[0], nl.net_a.grad) and torch.equal(g0[1], nl.net_c.grad)
+    assert torch.equal(l0, nl.loss)
 
 
 def test_ppo2_grads_minibatch_index():
