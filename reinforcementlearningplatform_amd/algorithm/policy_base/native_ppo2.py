@@ -24,6 +24,9 @@ msg keys beyond the reference's ppo_msg (all optional):
   grad_clip_norm  clip_grad_norm_'s max_norm (PPO2 0.5, :150; DPPO2 CartPole/SOI copies 0.2)
   adam_betas      (0.9, 0.999) for torch.optim.Adam; SharedAdam's default is (0.9, 0.99)
                   (utils/classes.py:676-679), which every DPPO2 driver uses
+  update_kernels  'auto' (f16x3 FD + wgrad kernels where they take the net: [S -> 256 -> 256 -> A],
+                  S <= 8 or the lidar demos' 41; exact-f32 dense GEMMs otherwise) or 'dense' (the
+                  dense GEMM path for every net: A/B and tests)
 """
 import numpy as np
 import torch
@@ -41,11 +44,14 @@ def _linears(module):
 
 def native_fits(module, is_actor):
     """True when librlp's f16x3 update kernels (rlp_ppo2_grad) take the net: a
-    [S<=8 -> 256 -> 256 -> A<=4] Linear stack whose forward is what those kernels differentiate —
+    [S -> 256 -> 256 -> A<=4] Linear stack, S <= 8 (the drivers' envs) or 41..44 (the lidar demos'
+    4 + 37 inputs: layer 1 on the exact-f32 GEMM beside the f16x3 kernels), whose forward is what
+    those kernels differentiate —
     tanh hidden layers, the actor's tanh(z) * gain + off head or the critic's linear head (the same
     probe-forward check as dense_fits: a ReLU 256-256 net has the shape but not the arithmetic)."""
     lin, dims = _linears(module)
-    shape = len(lin) == 3 and dims[1] == 256 and dims[2] == 256 and dims[0] <= 8 and dims[3] <= 4
+    shape = (len(lin) == 3 and dims[1] == 256 and dims[2] == 256 and dims[3] <= 4
+             and (dims[0] <= 8 or 41 <= dims[0] <= 44))
     return shape and dense_fits(module, is_actor)
 
 
@@ -81,9 +87,12 @@ def dense_fits(module, is_actor):
     return ref.shape == h.shape and bool(torch.allclose(ref, h, rtol=1e-5, atol=1e-6))
 
 
-def _update_kind(module, is_actor):
-    """'f16x3' (rlp_ppo2_grad) or 'dense' (rlp_ppo2_dense_grad); ValueError for any other net."""
-    if native_fits(module, is_actor):
+def _update_kind(module, is_actor, kernels="auto"):
+    """'f16x3' (rlp_ppo2_grad) or 'dense' (rlp_ppo2_dense_grad); ValueError for any other net.
+    kernels='dense' takes the dense GEMM path for nets both paths take (A/B, tests)."""
+    if kernels not in ("auto", "dense"):
+        raise ValueError(f"NativePPO2Learner: update_kernels {kernels!r} (auto | dense)")
+    if kernels == "auto" and native_fits(module, is_actor):
         return "f16x3"
     if dense_fits(module, is_actor):
         return "dense"
@@ -93,10 +102,12 @@ def _update_kind(module, is_actor):
 
 
 class _Net:
-    def __init__(self, module, is_actor, device):
+    def __init__(self, module, is_actor, device, kernels="auto"):
         lin, dims = _linears(module)
         # f16x3: rlp_ppo2_grad (FD + wgrad kernels); dense: rlp_ppo2_dense_grad (f32 MFMA GEMMs)
-        self.dense = _update_kind(module, is_actor) == "dense"
+        self.dense = _update_kind(module, is_actor, kernels) == "dense"
+        # the 41-input nets' f16x3 path takes contiguous rows (mini-batches gathered first)
+        self.ext = not self.dense and dims[0] > 8
         acts = [_abi.RLP_ACT_TANH] * (len(lin) - 1) + [
             _abi.RLP_ACT_TANH if is_actor else _abi.RLP_ACT_NONE]
         self.desc = _abi.MLPDesc.make(dims, acts)
@@ -127,10 +138,11 @@ class NativePPO2Learner:
             v = getattr(self.actor, name, None)
             if torch.is_tensor(v):
                 setattr(self.actor, name, v.to(self.device))
-        _update_kind(self.actor, True)    # both nets checked before any device work
-        _update_kind(self.critic, False)
-        self.net_a = _Net(self.actor, True, self.device)
-        self.net_c = _Net(self.critic, False, self.device)
+        kernels = msg.get('update_kernels', 'auto')
+        _update_kind(self.actor, True, kernels)    # both nets checked before any device work
+        _update_kind(self.critic, False, kernels)
+        self.net_a = _Net(self.actor, True, self.device, kernels)
+        self.net_c = _Net(self.critic, False, self.device, kernels)
         self.pg = process_group
         self.distributed = process_group is not None or (
             torch.distributed.is_available() and torch.distributed.is_initialized()
@@ -181,10 +193,11 @@ class NativePPO2Learner:
         return self.ws
 
     def _net_grad(self, net, cfg, s, index, ws, loss, **kw):
-        if net.dense:   # plain layout, contiguous rows: gather the mini-batch first
-            if index is not None:
-                s = s.index_select(0, index)
-                kw = {k: v.index_select(0, index) for k, v in kw.items()}
+        if (net.dense or net.ext) and index is not None:   # contiguous rows: gather the mini-batch
+            s = s.index_select(0, index)
+            kw = {k: v.index_select(0, index) for k, v in kw.items()}
+            index = None
+        if net.dense:   # plain layout
             K.ppo2_dense_grad(net.desc, net.flat, cfg, s, grad=net.grad, loss_sum=loss,
                               workspace=ws, **kw)
         else:

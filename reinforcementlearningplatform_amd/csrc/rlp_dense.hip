@@ -18,6 +18,8 @@
 // (. * gain) * (1 - t^2).
 #include "rlp_common.hpp"
 
+#include <mutex>
+
 namespace rlp {
 
 // element (i, j) of a rows x cols matrix: columns (rows, with split_rows) [0, split) from p0, the
@@ -67,6 +69,19 @@ constexpr int kDPf = kDT * kDRc / 4 / 256;  // float4 loads per thread of one pa
 // extent of the panel's outer index u (A: rows m; B: columns n)
 __device__ __forceinline__ int e_rows(const Opnd &o, bool is_a) { return is_a ? o.rows : o.cols; }
 
+// LDS column of reduction index r in a stage of Q MFMA steps per lane group (Q a multiple of 4,
+// <= 32; r < 4 Q): lane group g reads the Q consecutive indices [g Q, g Q + Q) as columns
+// [32 g, 32 g + Q), and rows u with bit 3 set swap the 32-column halves (XOR 32). Then every
+// 16-lane group of a ds_read_b128 fragment read (rows c = 0..15 at 4 banks apart, two lane groups
+// g) hits 64 distinct banks for any Q: with the plain g Q offsets a 128-row stage (Q = 32) put
+// lane groups g and g + 1 on the same banks (2-way), and the transposing stores below were 8-way
+// (profiles/r5/r5d_pmc_shapes.txt: SQ_LDS_BANK_CONFLICT 0.74-0.78 of the LDS cycles).
+__device__ __forceinline__ int lds_col(int r, int Q) {
+    const int g = (r >= Q) + (r >= 2 * Q) + (r >= 3 * Q);  // r / Q (r < 4 Q) without a division
+    return 32 * g + (r - g * Q);
+}
+__device__ __forceinline__ int lds_swz(int u) { return (u & 8) << 2; }
+
 // A block's panel of an operand for one stage, as L[u][r] (row stride kDLd): u in [0, 64) the
 // outer index (A: m0 + u; B: n0 + u), r in [0, kDRc) the reduction index (r_lo + r; zero past rc).
 // Fast path (the panel lies inside one source, off the ones column, fully in range, and is
@@ -104,7 +119,9 @@ __device__ __forceinline__ PanelFast panel_plan(const Opnd &o, bool is_a, int u0
     f.r_stride = r_stride;
     return f;
 }
-// rfast thread: r4 = 4 (t & 31), u = (t >> 5) + 8 q; ufast thread: u4 = 4 (t & 15), r = (t >> 4) + 16 q
+// rfast thread: r4 = 4 (t & 31), u = (t >> 5) + 8 q; ufast thread: u4 = 4 (t >> 4), r = (t & 15) + 16 q
+// (a half-wave of the transposing store then writes two u quads x 16 r: 32 distinct banks; the
+// former u4 = 4 (t & 15) mapping wrote 16 u quads x 2 r, 8-way conflicts)
 __device__ __forceinline__ void panel_load(const PanelFast &f, int rc, floatx4 (&v)[kDPf]) {
     const int t = threadIdx.x;
     if (f.rfast) {
@@ -115,25 +132,38 @@ __device__ __forceinline__ void panel_load(const PanelFast &f, int rc, floatx4 (
             v[q] = r4 < rc ? *(const floatx4 *)(f.base + (int64_t)u * f.u_stride + r4) : floatx4{0.f, 0.f, 0.f, 0.f};
         }
     } else {
-        const int u4 = 4 * (t & 15);
+        const int u4 = 4 * (t >> 4);
 #pragma unroll
         for (int q = 0; q < kDPf; ++q) {
-            const int r = (t >> 4) + 16 * q;
+            const int r = (t & 15) + 16 * q;
             v[q] = r < rc ? *(const floatx4 *)(f.base + (int64_t)r * f.r_stride + u4) : floatx4{0.f, 0.f, 0.f, 0.f};
         }
     }
 }
-__device__ __forceinline__ void panel_store(const PanelFast &f, const floatx4 (&v)[kDPf], float *L) {
+// the stage's panel into L (columns lds_col; reduction indices past 4 Q are never read: skipped)
+__device__ __forceinline__ void panel_store(const PanelFast &f, const floatx4 (&v)[kDPf], float *L, int Q) {
     const int t = threadIdx.x;
     if (f.rfast) {
+        const int r4 = 4 * (t & 31);
+        const int col = r4 < 4 * Q ? lds_col(r4, Q) : -1;
+        if (col >= 0) {
 #pragma unroll
-        for (int q = 0; q < kDPf; ++q) *(floatx4 *)&L[((t >> 5) + 8 * q) * kDLd + 4 * (t & 31)] = v[q];
+            for (int q = 0; q < kDPf; ++q) {
+                const int u = (t >> 5) + 8 * q;
+                *(floatx4 *)&L[u * kDLd + (col ^ lds_swz(u))] = v[q];
+            }
+        }
     } else {
-        const int u4 = 4 * (t & 15);
+        const int u4 = 4 * (t >> 4), sw = lds_swz(u4);
 #pragma unroll
-        for (int q = 0; q < kDPf; ++q)
+        for (int q = 0; q < kDPf; ++q) {
+            const int r = (t & 15) + 16 * q;
+            if (r < 4 * Q) {
+                const int col = lds_col(r, Q) ^ sw;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) L[(u4 + k) * kDLd + (t >> 4) + 16 * q] = v[q][k];
+                for (int k = 0; k < 4; ++k) L[(u4 + k) * kDLd + col] = v[q][k];
+            }
+        }
     }
 }
 // generic element loader (the panel is not on the fast path). Rows u past ubound are left as they
@@ -159,9 +189,10 @@ __device__ __forceinline__ void panel_generic(const Opnd &o, bool is_a, int u0, 
                 const bool ok = u < nu && r < rc;
                 v[u] = opnd_ld(o, ok ? i : 0x7fffffff, ok ? j : 0x7fffffff);
             }
+            const int col = lds_col(r, nr / 4);
 #pragma unroll
             for (int u = 0; u < 16; ++u)
-                if (u < nu) L[u * kDLd + r] = v[u];
+                if (u < nu) L[u * kDLd + (col ^ lds_swz(u))] = v[u];
         }
         return;
     }
@@ -181,7 +212,7 @@ __device__ __forceinline__ void panel_generic(const Opnd &o, bool is_a, int u0, 
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-            if (r0 + 4 * k < nr) L[u * kDLd + r0 + 4 * k] = v[k];
+            if (r0 + 4 * k < nr) L[u * kDLd + (lds_col(r0 + 4 * k, nr / 4) ^ lds_swz(u))] = v[k];
     }
 }
 
@@ -194,9 +225,9 @@ __device__ __forceinline__ void panel_generic(const Opnd &o, bool is_a, int u0, 
 // overlaps one block's loads with the other's MFMAs instead of running in rounds of one block per
 // CU (DDPG learn(): the layer-1 weight-gradient + backward launch was 42 us in three rounds,
 // profiles/r4/r4e_ddpg_learn_timeline.txt). LDS holds A as [m][r] and B as [n][r] (row stride
-// 132 floats: the 16 x 4 fragment reads hit 64 distinct banks); the reduction order is permuted so
-// that each lane's operands for four consecutive MFMA steps are contiguous (one 16-byte LDS
-// read): step s, lane group g reads r = g * Q + s.
+// 132 floats, columns lds_col / lds_swz: conflict-free fragment reads and stores); the reduction
+// order is permuted so that each lane's operands for four consecutive MFMA steps are contiguous
+// (one 16-byte LDS read): step s, lane group g reads r = g * Q + s.
 struct Prob {
     Opnd A, B;
     Epi e;
@@ -247,8 +278,8 @@ __global__ void __launch_bounds__(256) dense_gemm_kernel(ProbSet ps) {
     for (int rs = r_lo; rs < r_end || rs == r_lo; rs += kDRc) {
         const int Q = (rc + 15) / 16 * 4;  // MFMA steps (multiple of 4); rows g * Q + s, s < Q
         if (rs != r_lo) __syncthreads();   // the previous stage's fragments are read
-        if (fa.fast) panel_store(fa, va, As); else panel_generic(A, true, m0, ua, rs, rc, 4 * Q, As);
-        if (fb.fast) panel_store(fb, vb, Bs); else panel_generic(B, false, n0, ub, rs, rc, 4 * Q, Bs);
+        if (fa.fast) panel_store(fa, va, As, Q); else panel_generic(A, true, m0, ua, rs, rc, 4 * Q, As);
+        if (fb.fast) panel_store(fb, vb, Bs, Q); else panel_generic(B, false, n0, ub, rs, rc, 4 * Q, Bs);
         __syncthreads();
         const int rn = rs + kDRc, rcn = min(r_end, rn + kDRc) - rn;
         if (rn < r_end) {  // next stage's loads, in flight under this stage's MFMAs
@@ -257,12 +288,13 @@ __global__ void __launch_bounds__(256) dense_gemm_kernel(ProbSet ps) {
             if (fa.fast) panel_load(fa, rcn, va);
             if (fb.fast) panel_load(fb, rcn, vb);
         }
+        const int fcol = (32 * g) ^ lds_swz(c);  // lane group g's columns (rows wm + 16 i + c: c's bit 3)
         for (int s = 0; s < Q; s += 4) {
             floatx4 af[2], bf[2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) af[i] = *(const floatx4 *)&As[(wm + 16 * i + c) * kDLd + g * Q + s];
+            for (int i = 0; i < 2; ++i) af[i] = *(const floatx4 *)&As[(wm + 16 * i + c) * kDLd + fcol + s];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) bf[j] = *(const floatx4 *)&Bs[(wn + 16 * j + c) * kDLd + g * Q + s];
+            for (int j = 0; j < 2; ++j) bf[j] = *(const floatx4 *)&Bs[(wn + 16 * j + c) * kDLd + fcol + s];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -1190,13 +1222,24 @@ inline Prob make_prob(const Opnd &A, const Opnd &B, const Epi &e, int R, int spl
     return Prob{A, B, e, R, rchunk, (e.N + kDT - 1) / kDT, (e.M + kDT - 1) / kDT, nz};
 }
 
-// problems qs[0 .. n) in one launch (n <= kMaxProbs)
+// The kernel's dynamic LDS (67.6 KB) is above the 64 KiB default: the attribute is set once per
+// process (std::call_once: thread-safe), and a failure is reported at every launch.
+static_assert(sizeof(ProbSet) <= 4096 - 256, "ProbSet kernarg within the 4 KiB kernarg segment");
+static hipError_t dense_gemm_attr() {
+    static std::once_flag once;
+    static hipError_t rc = hipSuccess;
+    std::call_once(once, [] {
+        rc = hipFuncSetAttribute((const void *)dense_gemm_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDenseLds);
+    });
+    return rc;
+}
+
+// problems qs[0 .. n) in one launch (0 < n <= kMaxProbs)
 void gemm_multi(const Prob *qs, int n, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void *)dense_gemm_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDenseLds);
-        attr = true;
+    if (n < 1 || n > kMaxProbs || dense_gemm_attr() != hipSuccess) {
+        fail(RLP_EINVAL, "dense GEMM: %d problems (max %d) or LDS attribute not set", n, kMaxProbs);
+        return;
     }
     ProbSet ps{};
     int nb = 0;
@@ -2282,6 +2325,46 @@ inline PpoDenseWs ppo2_dense_ws(const rlp_mlp_desc &d, int64_t rows) {
     w.lpart = take(2 * ((rows + 255) / 256));  // f64 loss partial per head block
     w.total = o;
     return w;
+}
+
+// ---- layer 1 of the 41-input nets for rlp_ppo2_grad (rlp_update.hip, "EXT" kernels) -----------
+// The f16x3 FD / wgrad kernels take h1 = tanh(s W1^T + b1) from HBM and hand g1 = dL/dz1 back;
+// both layer-1 products run here on the exact-f32 tiled GEMM in row chunks of kExtChunk (32-bit
+// element offsets): the forward with the tanh epilogue, dW1 | db1 = G1^T [s | 1] as long
+// reduction slices whose partials (every chunk's, in chunk order) one fixed-order reduce sums.
+constexpr int64_t kExtChunk = 1 << 22;
+constexpr int kExtSlices = 128;  // reduction slices per chunk (x 4 tiles = 512 blocks)
+int64_t ppo2_ext_floats(int S, int H, int64_t rows) {
+    const int64_t chunks = (rows + kExtChunk - 1) / kExtChunk;
+    return chunks * kExtSlices * (int64_t)H * (S + 1);
+}
+void ppo2_ext_h1(const float *W1, int ldw, const float *b1, int S, int H, const float *s,
+                 int64_t rows, float *h1, hipStream_t st) {
+    for (int64_t r0 = 0; r0 < rows; r0 += kExtChunk) {
+        const int B = (int)(rows - r0 < kExtChunk ? rows - r0 : kExtChunk);
+        Epi e{};
+        e.y = h1 + r0 * H; e.ldy = H; e.bias = b1; e.kind = kEpiTanh; e.M = B; e.N = H;
+        // B(r = input k, n = neuron j) = W1[j][k], row stride ldw (the packed W1 block)
+        const Prob q = make_prob(mat(s + r0 * S, B, S, S), Opnd{W1, W1, 1, ldw, 1, ldw, S, H, H, -1, 0},
+                                 e, S, 1);
+        gemm_multi(&q, 1, st);
+    }
+}
+void ppo2_ext_dw1(const float *g1, const float *s, int S, int H, int64_t rows, float *part,
+                  float *gW, float *gb, hipStream_t st) {
+    int z = 0;
+    for (int64_t r0 = 0; r0 < rows; r0 += kExtChunk) {
+        const int B = (int)(rows - r0 < kExtChunk ? rows - r0 : kExtChunk);
+        Epi e{};
+        e.y = part + (int64_t)z * H * (S + 1); e.kind = kEpiPartial; e.M = H; e.N = S + 1;
+        Opnd x = mat(s + r0 * S, B, S, S);
+        x.cols = S + 1;
+        x.ones = S;
+        const Prob q = make_prob_long(transposed(g1 + r0 * H, H, B, H), x, e, B, kExtSlices);
+        gemm_multi(&q, 1, st);
+        z += q.nz;
+    }
+    wgrad_reduce(Layer{nullptr, nullptr, S, H}, part, z, gW, gb, st);
 }
 
 }  // namespace rlp

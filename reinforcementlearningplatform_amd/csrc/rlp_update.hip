@@ -36,8 +36,11 @@ struct Ppo2Args {
     float log_std[4], inv_var[4];  // per-launch constants of the Normal log-prob and its gradient
     float *g2t;         // [tiles][256][64]
     unsigned *g2max;    // bits of max|g2| (atomicMax)
-    float *part3;       // [grid * 4][A*256 + A + 256*S + 256]: per-wave dW3 | db3 | dW1 | db1
+    float *part3;       // [FD waves][p3]: per-wave dW3 | db3 | dW1 | db1 (EXT: dW3 | db3)
+    int p3;             // floats per wave partial: A*256 + A + 256*S + 256 (EXT: A*256 + A)
     double *lpart;      // [FD waves]: per-wave loss partials (summed in order by the reduce)
+    const float *h1;    // EXT: [rows][256] tanh(W1 s + b1) (exact f32, rlp_dense.hip)
+    float *g1;          // EXT: [rows][256] dL/dz1, the dense dW1 | db1 GEMM's operand
 };
 
 // block barrier for LDS hand-offs only: drains this wave's LDS ops, not its global loads (HIP's
@@ -212,24 +215,36 @@ constexpr int kFdWaves = 8;
 constexpr int kFdRows = 16 * kFdWaves;
 constexpr int kFdRing = 3;  // W2 chunk-ring slots (one group in flight while one is read)
 
+// KS1 = 0 ("EXT", the lidar demos' 41-input nets): layer 1 lives outside the kernel — h1 =
+// tanh(W1 s + b1) comes from g.h1 (one exact-f32 GEMM per step, rlp_dense.hip), g1 = dL/dz1 goes to
+// g.g1 for the dense dW1 | db1 GEMM; the kernel keeps the 256 x 256 layer's f16x3 forward and
+// backward, the loss head and dW3 | db3. (Eleven f32 K-steps of layer 1 in-kernel, twice per tile,
+// would cost as much MFMA pipe as the f16 GEMMs, and dW1's 256 x 42 partials do not fit in registers.)
 template <int KS1, int A, int LOSS>
 __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
-    constexpr int H = kUpdH, SMALL = mlp_small_floats<H, KS1, A>();
-    constexpr int NC = 4 * KS1 + 1;  // dW1 columns per neuron: s features | bias
+    constexpr bool EXT = KS1 == 0;
+    constexpr int KS = EXT ? 1 : KS1;
+    constexpr int H = kUpdH, SMALL = EXT ? 2 * H + A * H + 8 : mlp_small_floats<H, KS1, A>();
+    constexpr int NC = 4 * KS + 1;  // dW1 columns per neuron: s features | bias
     constexpr int kFdRegion = kFdRing * kX3ChunkFloats;
-    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + kFdWaves * 16 * 8];
+    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + (EXT ? 4 : kFdWaves * 16 * 8)];
     float *ring = lds, *small = lds + kFdRegion;
     // the wave index as a scalar (readfirstlane): every wave-derived offset, the G2 tile and its
     // store guard become SGPR values (no per-lane 64-bit address arithmetic, no exec-masked stores)
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float *const srw = lds + kFdRegion + SMALL + wv * 128;  // [16 rows][8]
+    float *const srw = lds + kFdRegion + SMALL + (EXT ? 0 : wv * 128);  // [16 rows][8]
     const MfmaNet &net = g.net;
-    mlp_small_to_lds(g.packed, net, small, true);  // small_r: W1, b1 x 2/ln 2, b2 x 2^(sw+SH)
+    // small_r: W1, b1 x 2/ln 2, b2 x 2^(sw+SH) (EXT: from b1 on, W1 is not used)
+    const int sb = EXT ? net.off_b1 : net.off_w1;
+    {
+        const gptr<float> src = as_global(g.packed) + net.off_small_r + (sb - net.off_w1);
+        for (int i = threadIdx.x; i < net.small_count - (sb - net.off_w1); i += blockDim.x) small[i] = src[i];
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63, gq = lane >> 4, e = lane & 15;
     const int S = net.S;
-    const float *info = small + (net.off_info - net.off_w1);
+    const float *info = small + (net.off_info - sb);
     const float sw = info[0];
     const float k_out = 2.8853900817779268f * info[2];
     float *const my_part = ring + wv * (16 / kFdWaves) * 256;
@@ -258,16 +273,16 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
         return small + smo + off;
     };
     // layer 1 of neuron tile t "neuron on lane": C[row 4 gq + q][neuron 16 t + e] (operands swapped)
-    auto layer1_t = [&](int t, const float (&bo)[KS1]) {
+    auto layer1_t = [&](int t, const float (&bo)[KS]) {
         const float *W1c = small + 0;
-        const float *B1c = small + (net.off_b1 - net.off_w1);
-        float w1[KS1];
+        const float *B1c = small + (net.off_b1 - sb);
+        float w1[KS];
 #pragma unroll
-        for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[w1r_index(16 * t + e, 4 * kk + gq, KS1)];
+        for (int kk = 0; kk < KS; ++kk) w1[kk] = W1c[w1r_index(16 * t + e, 4 * kk + gq, KS)];
         const float b1 = B1c[16 * t + e];
         floatx4 c = {b1, b1, b1, b1};
 #pragma unroll
-        for (int kk = 0; kk < KS1; ++kk)
+        for (int kk = 0; kk < KS; ++kk)
             c = __builtin_amdgcn_mfma_f32_16x16x4f32(bo[kk], w1[kk], c, 0, 0, 0);
         return c;
     };
@@ -275,11 +290,11 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
     // the 4 lane groups by a 2-stage permlane butterfly, per half of the neuron tiles
     // (8 NC -> 2 NC values)
     auto dw1_acc = [&](const float *srw) {
-        float sv[4][4 * KS1];
+        float sv[4][4 * KS];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int kk = 0; kk < KS1; ++kk) {
+            for (int kk = 0; kk < KS; ++kk) {
                 const floatx4 v = *reinterpret_cast<const floatx4 *>(srw + (4 * gq + q) * 8 + 4 * kk);
 #pragma unroll
                 for (int u = 0; u < 4; ++u) sv[q][4 * kk + u] = v[u];
@@ -291,13 +306,13 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
             for (int tt = 0; tt < 8; ++tt) {
                 const floatx4 gt = dh1[8 * h + tt];
 #pragma unroll
-                for (int f = 0; f < 4 * KS1; ++f) {
+                for (int f = 0; f < 4 * KS; ++f) {
                     float x = gt[0] * sv[0][f];
 #pragma unroll
                     for (int q = 1; q < 4; ++q) x = __builtin_fmaf(gt[q], sv[q][f], x);
                     v[tt * NC + f] = x;
                 }
-                v[tt * NC + 4 * KS1] = (gt[0] + gt[1]) + (gt[2] + gt[3]);
+                v[tt * NC + 4 * KS] = (gt[0] + gt[1]) + (gt[2] + gt[3]);
             }
 #pragma unroll
             for (int i = 0; i < 4 * NC; ++i) v[i] = pair_sum_x32(v[i], v[i + 4 * NC]);
@@ -321,20 +336,26 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
         asm volatile("" : "+s"(smo));
         const float *sm = small + smo;
         const float *W1c = sm;
-        const float *B1c = sm + (net.off_b1 - net.off_w1);
-        const float *B2c = sm + (net.off_b2 - net.off_w1);
-        const float *W3c = sm + (net.off_w3 - net.off_w1);
-        const float *b3c = sm + (net.off_b3 - net.off_w1);
+        const float *B1c = sm + (net.off_b1 - sb);
+        const float *B2c = sm + (net.off_b2 - sb);
+        const float *W3c = sm + (net.off_w3 - sb);
+        const float *b3c = sm + (net.off_b3 - sb);
         const int64_t r = bt * kFdRows + 16 * wv + e;
         const bool valid = r < g.rows;
         const int64_t src = valid ? (g.index ? g.index[r] : r) : 0;
-        float bobs[KS1];
+        float bobs[KS];
 #pragma unroll
-        for (int kk = 0; kk < KS1; ++kk) {
+        for (int kk = 0; kk < KS; ++kk) {
             const int k = 4 * kk + gq;
-            bobs[kk] = (valid && k < S) ? g.s[src * S + k] : 0.f;
-            srw[e * 8 + k] = bobs[kk];  // this wave's s rows, for dW1
+            if constexpr (EXT) {
+                bobs[kk] = 0.f;
+            } else {
+                bobs[kk] = (valid && k < S) ? g.s[src * S + k] : 0.f;
+                srw[e * 8 + k] = bobs[kk];  // this wave's s rows, for dW1
+            }
         }
+        // EXT: this lane's h1 row (rows past the end read row 0: their g3 is zero)
+        const float *h1r = EXT ? g.h1 + (size_t)src * H : nullptr;
         // the actor loss's row inputs, loaded now so that their latency hides under the forward
         // GEMM (the critic's one v_target stays at its use: held across the GEMMs it spilled)
         float in_a[A], in_lp[A], in_adv = 0.f;
@@ -351,12 +372,12 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
             }
         }
         auto layer1 = [&](int t) {
-            float w1[KS1];
+            float w1[KS];
 #pragma unroll
-            for (int kk = 0; kk < KS1; ++kk) w1[kk] = W1c[w1r_index(16 * t + e, 4 * kk + gq, KS1)];
+            for (int kk = 0; kk < KS; ++kk) w1[kk] = W1c[w1r_index(16 * t + e, 4 * kk + gq, KS)];
             floatx4 c = *reinterpret_cast<const floatx4 *>(B1c + 16 * t + 4 * gq);
 #pragma unroll
-            for (int kk = 0; kk < KS1; ++kk)
+            for (int kk = 0; kk < KS; ++kk)
                 c = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[kk], bobs[kk], c, 0, 0, 0);
             return c;
         };
@@ -371,11 +392,23 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const float pre = i < 4 ? p0[i] : p1[i - 4];
-                const float ex = __builtin_amdgcn_exp2f(pre);  // pre = 2 h1 / ln 2 (small_r)
-                x[i] = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + ex), kX3HScale);
+                if constexpr (EXT) {
+                    x[i] = pre * kX3HScale;  // h1 itself (exact power-of-two scale)
+                } else {
+                    const float ex = __builtin_amdgcn_exp2f(pre);  // pre = 2 h1 / ln 2 (small_r)
+                    x[i] = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + ex), kX3HScale);
+                }
             }
             split8(x, bh, bl);
-        }, [&](int P) { p0 = layer1(2 * P); p1 = layer1(2 * P + 1); });
+        }, [&](int P) {
+            if constexpr (EXT) {  // neurons 32 P + 4 gq .. + 3 and 32 P + 16 + 4 gq .. + 3 of the row
+                p0 = *reinterpret_cast<const floatx4 *>(h1r + 32 * P + 4 * gq);
+                p1 = *reinterpret_cast<const floatx4 *>(h1r + 32 * P + 16 + 4 * gq);
+            } else {
+                p0 = layer1(2 * P);
+                p1 = layer1(2 * P + 1);
+            }
+        });
         // ---- h2 = tanh(z2), z3 = W3 h2 + b3 (every lane group ends with its row's z3)
         float z3[A];
 #pragma unroll
@@ -526,7 +559,23 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
         // MFMAs first (their W1 / b1 reads in flight together), then the 64 independent tanh'
         // chains — tile by tile, each tile's LDS reads, MFMA latency and transcendental chain were
         // exposed in turn (r3x diag: g1 5.8k cycles per wave tile for ~2.5k of issue)
-        {
+        if constexpr (EXT) {  // g1 from the stored h1, to g.g1 (rows 4 gq + q, neuron 16 t + e)
+            const float unscale = __builtin_amdgcn_ldexpf(1.f, ex - 14) / sw;
+            const int64_t r0 = bt * kFdRows + 16 * wv + 4 * gq;
+            float hv[16][4];
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    hv[t][q] = r0 + q < g.rows ? g.h1[(size_t)(r0 + q) * H + 16 * t + e] : 0.f;
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float v = dh1[t][q] * unscale * __builtin_fmaf(-hv[t][q], hv[t][q], 1.f);
+                    if (r0 + q < g.rows) g.g1[(size_t)(r0 + q) * H + 16 * t + e] = v;
+                }
+        } else {
             floatx4 pre[16];
 #pragma unroll
             for (int t = 0; t < 16; ++t) pre[t] = layer1_t(t, bobs);
@@ -537,20 +586,22 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
                     const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(pre[t][q]));
                     dh1[t][q] = dh1[t][q] * unscale4 * __builtin_fmaf(-r, r, r);
                 }
+            dw1_acc(srw);
         }
-        dw1_acc(srw);
     }
 
     // ---- per-wave partials: dW3 (lane's neurons) | db3 summed over the 16 row lanes | dW1 | db1
-    float *out = g.part3 + (size_t)(blockIdx.x * kFdWaves + wv) * (A * H + A + H * S + H);
+    float *out = g.part3 + (size_t)(blockIdx.x * kFdWaves + wv) * g.p3;
+    if constexpr (!EXT) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int i = 0; i < 2 * NC; ++i) {
-            const int n = 16 * (8 * h + 2 * gq + i / NC) + e, f = i % NC;
-            if (f < S) out[A * H + A + n * S + f] = dW1p[h][i];
-            else if (f == 4 * KS1) out[A * H + A + H * S + n] = dW1p[h][i];
-        }
+            for (int i = 0; i < 2 * NC; ++i) {
+                const int n = 16 * (8 * h + 2 * gq + i / NC) + e, f = i % NC;
+                if (f < S) out[A * H + A + n * S + f] = dW1p[h][i];
+                else if (f == 4 * KS1) out[A * H + A + H * S + n] = dW1p[h][i];
+            }
+    }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) g2max = fmaxf(g2max, __shfl_xor(g2max, o));
     if (lane == 0) atomicMax(g.g2max, __float_as_uint(g2max));  // non-negative: uint order
@@ -579,6 +630,7 @@ struct WArgs {
     const float *g2t;
     const unsigned *g2max;
     float *part;  // [grid][H*H + H]: dW2 | db2
+    const float *h1;  // EXT (KS1 = 0): [rows][256] tanh(W1 s + b1), read instead of recomputed
 };
 
 // B fragments of h1 for one 64-row tile: [ks 2][nt 16][hi, lo][64 lanes][8 halfs] (64 KiB):
@@ -596,23 +648,26 @@ struct WArgs {
 // v_mfma_f32_32x32x16_f16 form (half the MFMA issue slots), the pinning without the fences (8 %
 // slower), the build spread over four steps, the younger waves at s_setprio 1.
 constexpr int kWgWaves = 8;
+// KS1 = 0 (EXT, the 41-input nets): the fragments come from the stored h1 (g.h1 of the FD kernel)
+// instead of a layer-1 recompute; each build's 8 values are loaded one build ahead.
 template <int KS1>
 __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
-    constexpr int W = kWgWaves, H = kUpdH, SP = 4 * KS1, NT = 64 * W, JT = 16 / W;
+    constexpr bool EXT = KS1 == 0;
+    constexpr int W = kWgWaves, H = kUpdH, SP = EXT ? 4 : 4 * KS1, NT = 64 * W, JT = 16 / W;
     constexpr int SV = (kUpdRows * SP + NT - 1) / NT;
     constexpr int FRAG = 2 * 16 * 2 * 64 * 8;  // halfs of one tile's h1 fragments (64 KiB)
     constexpr int FPW = 32 / W;                // fragments (ks, nt) built per wave and tile
     // double-buffered: tile i's MFMAs read hfrag[i & 1] while its waves build tile i + step's
     // fragments into hfrag[(i + 1) & 1] from srow[(i + 1) & 1]
-    __shared__ float srow[2][kUpdRows][SP];
-    __shared__ float w1s[H][SP + 1];
-    __shared__ float b1s[H];
+    __shared__ float srow[2][EXT ? 1 : kUpdRows][SP];
+    __shared__ float w1s[EXT ? 1 : H][SP + 1];
+    __shared__ float b1s[EXT ? 1 : H];
     __shared__ __attribute__((aligned(16))) _Float16 hfrag[2][FRAG];
     const MfmaNet &net = w.net;
     const int S = net.S;
     const int lane = threadIdx.x & 63, gq = lane >> 4, e = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    {
+    if constexpr (!EXT) {
         // small_r: W1, b1 x 2/ln 2 (h1 as in the FD forward)
         const float *W1c = w.packed + net.off_small_r;
         const float *B1c = w.packed + net.off_small_r + (net.off_b1 - net.off_w1);
@@ -638,6 +693,7 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
     }
     const int64_t ntiles = (w.rows + kUpdRows - 1) / kUpdRows;
     auto load_s = [&](int64_t tile, float (&sv)[SV]) {  // this thread's s values of a tile
+        if constexpr (EXT) return;
 #pragma unroll
         for (int u = 0; u < SV; ++u) {
             const int i = threadIdx.x + NT * u, rr = i / SP, k = i % SP;
@@ -647,6 +703,7 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
         }
     };
     auto store_s = [&](int buf, const float (&sv)[SV]) {
+        if constexpr (EXT) return;
 #pragma unroll
         for (int u = 0; u < SV; ++u) {
             const int i = threadIdx.x + NT * u;
@@ -678,6 +735,27 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
         *reinterpret_cast<half8 *>(&hfrag[buf][(((ks * 16 + nt) * 2 + 0) * 64 + lane) * 8]) = hh8;
         *reinterpret_cast<half8 *>(&hfrag[buf][(((ks * 16 + nt) * 2 + 1) * 64 + lane) * 8]) = hl8;
     };
+    // EXT: the 8 h1 values of fragment F of a tile (rows 32 ks + 16 hh + 4 gq + q, neuron 16 nt + e;
+    // rows past the end 0: their g2 is zero), then the same split and stores
+    auto load_hv = [&](int64_t tile, int F, float (&hv)[8]) {
+        const int ks = F >> 4, nt = F & 15;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t r = tile * kUpdRows + 32 * ks + 16 * hh + 4 * gq + q;
+                hv[4 * hh + q] = (tile < ntiles && r < w.rows) ? w.h1[(size_t)r * H + 16 * nt + e] : 0.f;
+            }
+    };
+    auto build_frag_ext = [&](int buf, int F, const float (&hv)[8]) {
+        float x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = hv[i] * kX3HScale;
+        half8 hh8, hl8;
+        split8(x, hh8, hl8);
+        *reinterpret_cast<half8 *>(&hfrag[buf][((F * 2 + 0) * 64 + lane) * 8]) = hh8;
+        *reinterpret_cast<half8 *>(&hfrag[buf][((F * 2 + 1) * 64 + lane) * 8]) = hl8;
+    };
     const float *g2base = w.g2t;
     asm volatile("" : "+s"(g2base));
     // A operands of one K step: g2(rows 32 ks + 4 gq + i and 32 ks + 16 + 4 gq + i,
@@ -704,8 +782,18 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
         store_s(0, sv);
     }
     lds_barrier();
+    float hvn[8];  // EXT: the next build's h1 values, in flight one build ahead
+    if constexpr (EXT) {
 #pragma unroll 1
-    for (int u = 0; u < FPW; ++u) build_frag(0, FPW * wv + u);
+        for (int u = 0; u < FPW; ++u) {
+            load_hv(tile, FPW * wv + u, hvn);
+            build_frag_ext(0, FPW * wv + u, hvn);
+        }
+        load_hv(tile + gridDim.x, FPW * wv, hvn);
+    } else {
+#pragma unroll 1
+        for (int u = 0; u < FPW; ++u) build_frag(0, FPW * wv + u);
+    }
     float svn[SV];
     load_s(tile + gridDim.x, svn);
     floatx4 gv[JT][2];
@@ -758,7 +846,14 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
                 // the next tile's fragments, spread over this tile's MFMAs (FPW per wave)
                 if (F % (32 / FPW) == (32 / FPW) - 1) {
                     __builtin_amdgcn_sched_barrier(0);  // (the build stays a region of its own)
-                    build_frag(nxt, FPW * wv + F / (32 / FPW));
+                    const int u = F / (32 / FPW);
+                    if constexpr (EXT) {
+                        build_frag_ext(nxt, FPW * wv + u, hvn);
+                        if (u + 1 < FPW) load_hv(tile + gridDim.x, FPW * wv + u + 1, hvn);
+                        else load_hv(tile + 2 * (int64_t)gridDim.x, FPW * wv, hvn);
+                    } else {
+                        build_frag(nxt, FPW * wv + u);
+                    }
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 if (F + 1 < 32) {
@@ -794,13 +889,15 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
 constexpr int kRedSplit = 16;
 __global__ void __launch_bounds__(64 * kRedSplit)
 ppo2_reduce_kernel(MfmaNet net, const float *__restrict__ part, int nw,
-                   const float *__restrict__ part3, int n3, float *grad,
-                   const double *__restrict__ lpart, double *loss_sum) {
+                   const float *__restrict__ part3, int n3, int p3, float *grad,
+                   const double *__restrict__ lpart, double *loss_sum, int w1_ext) {
     const int H = net.H, S = net.S, A = net.A;
     const int64_t total = (int64_t)H * S + H + (int64_t)H * H + H + (int64_t)A * H + A;
-    const int pw = H * H + H, p3 = A * H + A + H * S + H;
+    const int pw = H * H + H;
     const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;
-    const int64_t i = (int64_t)blockIdx.x * 64 + o;
+    // EXT nets: W1 | b1 come from the dense dW1 GEMM's own reduce (not in the FD partials)
+    const int64_t i0 = w1_ext ? (int64_t)H * S + H : 0;
+    const int64_t i = i0 + (int64_t)blockIdx.x * 64 + o;
     float acc = 0.f;
     if (i < total) {
         const float *src;
@@ -908,6 +1005,44 @@ static int ppo2_grid() {  // CUs of the device (cached: device properties are sl
     return cus;
 }
 
+// the 41-input nets' layer 1 on the dense GEMM (rlp_dense.hip): h1 = tanh(s W1^T + b1) and
+// dW1 | db1 = G1^T [s | 1] (fixed-order partials + reduce into gW / gb)
+int64_t ppo2_ext_floats(int S, int H, int64_t rows);
+void ppo2_ext_h1(const float *W1, int ldw, const float *b1, int S, int H, const float *s,
+                 int64_t rows, float *h1, hipStream_t st);
+void ppo2_ext_dw1(const float *g1, const float *s, int S, int H, int64_t rows, float *part,
+                  float *gW, float *gb, hipStream_t st);
+
+// floats of a net's rlp_ppo2_grad workspace, in this order: G2 tiles | wgrad partials | FD
+// partials | g2max (16) | FD loss partials (f64) | EXT: h1 | g1 | dW1 partials
+struct Ppo2Ws {
+    int64_t g2t, partw, part3, g2max, lpart, h1, g1, dw1, total;
+    int p3;
+};
+inline bool ppo2_ext(const MfmaNet &net) { return net.ks1 > 2; }
+inline bool ppo2_net_ok(const MfmaNet &net) { return net.H == kUpdH && (net.ks1 <= 2 || net.ks1 == 11); }
+inline Ppo2Ws ppo2_ws(const MfmaNet &net, int64_t rows) {
+    const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
+    const int64_t grid = ppo2_grid();  // wgrad: one block per CU; FD: one 8-wave block per CU
+    const bool ext = ppo2_ext(net);
+    Ppo2Ws w{};
+    w.p3 = ext ? net.A * kUpdH + net.A : net.A * kUpdH + net.A + kUpdH * net.S + kUpdH;
+    int64_t o = 0;
+    auto take = [&](int64_t k) { int64_t r = o; o += (k + 63) / 64 * 64; return r; };
+    w.g2t = take(tiles * kUpdTileFloats);
+    w.partw = take(grid * (kUpdH * kUpdH + kUpdH));
+    w.part3 = take(grid * kFdWaves * (int64_t)w.p3);
+    w.g2max = take(16);
+    w.lpart = take(2 * grid * kFdWaves);
+    if (ext) {
+        w.h1 = take(rows * kUpdH);
+        w.g1 = take(rows * kUpdH);
+        w.dw1 = take(ppo2_ext_floats(net.S, kUpdH, rows));
+    }
+    w.total = o;
+    return w;
+}
+
 }  // namespace rlp
 
 using namespace rlp;
@@ -916,13 +1051,8 @@ extern "C" {
 
 int64_t rlp_ppo2_workspace_floats(const rlp_mlp_desc *desc, int64_t rows) {
     MfmaNet net;
-    if (!desc || !mfma_net_from_desc(*desc, &net) || net.H != kUpdH || net.ks1 > 2 || rows < 0)
-        return RLP_EINVAL;
-    const int64_t tiles = (rows + kUpdRows - 1) / kUpdRows;
-    const int64_t grid = ppo2_grid();  // wgrad: one block per CU; FD: two
-    return tiles * kUpdTileFloats + grid * (kUpdH * kUpdH + kUpdH) +
-           2 * grid * 4 * (net.A * kUpdH + net.A + kUpdH * net.S + kUpdH) + 16 +
-           2 * grid * kFdWaves;  // g2max (16 floats), the FD waves' f64 loss partials
+    if (!desc || !mfma_net_from_desc(*desc, &net) || !ppo2_net_ok(net) || rows < 0) return RLP_EINVAL;
+    return ppo2_ws(net, rows > 0 ? rows : 1).total;
 }
 
 int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_loss_cfg *cfg,
@@ -931,8 +1061,11 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
                   double *loss_sum, float *workspace, rlp_stream_t stream) {
     RLP_REQUIRE(desc && packed && cfg && s && grad && workspace, "rlp_ppo2_grad: null argument");
     MfmaNet net;
-    if (!mfma_net_from_desc(*desc, &net) || net.H != kUpdH || net.ks1 > 2)
-        return fail(RLP_EUNSUPPORTED, "rlp_ppo2_grad: need a [S<=8 -> 256 -> 256 -> A] tanh net");
+    if (!mfma_net_from_desc(*desc, &net) || !ppo2_net_ok(net))
+        return fail(RLP_EUNSUPPORTED, "rlp_ppo2_grad: need a [S<=8 or 41..44 -> 256 -> 256 -> A] tanh net");
+    const bool ext = ppo2_ext(net);
+    RLP_REQUIRE(!ext || !index, "rlp_ppo2_grad: %d-input nets take contiguous rows (gather the "
+                "mini-batch first)", net.S);
     const bool actor = cfg->kind == RLP_LOSS_ACTOR;
     RLP_REQUIRE(actor || cfg->kind == RLP_LOSS_CRITIC, "rlp_ppo2_grad: loss kind %d", cfg->kind);
     if (actor) {
@@ -963,16 +1096,27 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
         ent += 0.5f + 0.91893853320467274178f + logf(cfg->std[k]);  // Normal.entropy()
     }
     g.ent_row = cfg->entropy_coef * ent;
-    g.g2t = workspace;
-    float *partw = workspace + tiles * kUpdTileFloats;
-    g.part3 = partw + (int64_t)gfull * (kUpdH * kUpdH + kUpdH);
-    g.g2max = reinterpret_cast<unsigned *>(g.part3 + (int64_t)2 * gfull * 4 *
-                                           (net.A * kUpdH + net.A + kUpdH * net.S + kUpdH));
+    const Ppo2Ws wl = ppo2_ws(net, rows);
+    (void)gfull;
+    g.g2t = workspace + wl.g2t;
+    float *partw = workspace + wl.partw;
+    g.part3 = workspace + wl.part3;
+    g.p3 = wl.p3;
+    g.g2max = reinterpret_cast<unsigned *>(workspace + wl.g2max);
     if (hipMemsetAsync(g.g2max, 0, sizeof(unsigned), st) != hipSuccess)
         return fail(RLP_EINVAL, "rlp_ppo2_grad: memset");
-    g.lpart = reinterpret_cast<double *>(reinterpret_cast<float *>(g.g2max) + 16);
+    g.lpart = reinterpret_cast<double *>(workspace + wl.lpart);
+    if (ext) {  // h1 of every row for the FD forward, g1 back from it
+        g.h1 = workspace + wl.h1;
+        g.g1 = workspace + wl.g1;
+        ppo2_ext_h1(packed + net.off_w1, 4 * net.ks1, packed + net.off_b1, net.S, kUpdH, s, rows,
+                    workspace + wl.h1, st);
+    }
 #define RLP_FD(KS1, A_, L) ppo2_fd_kernel<KS1, A_, L><<<gfd, 64 * kFdWaves, 0, st>>>(g)
-    if (actor) {
+    if (ext) {
+        if (!actor) RLP_FD(0, 1, 1);
+        else if (net.A == 1) RLP_FD(0, 1, 0); else if (net.A == 2) RLP_FD(0, 2, 0); else if (net.A == 3) RLP_FD(0, 3, 0); else RLP_FD(0, 4, 0);
+    } else if (actor) {
         if (net.ks1 == 1) {
             if (net.A == 1) RLP_FD(1, 1, 0); else if (net.A == 2) RLP_FD(1, 2, 0); else if (net.A == 3) RLP_FD(1, 3, 0); else RLP_FD(1, 4, 0);
         } else {
@@ -985,14 +1129,19 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (fd)");
     WArgs w{};
     w.packed = packed; w.net = net; w.s = s; w.index = index; w.rows = rows;
-    w.g2t = g.g2t; w.g2max = g.g2max; w.part = partw;
-    if (net.ks1 == 1) ppo2_wgrad_kernel<1><<<grid, 64 * kWgWaves, 0, st>>>(w);
+    w.g2t = g.g2t; w.g2max = g.g2max; w.part = partw; w.h1 = g.h1;
+    if (ext) ppo2_wgrad_kernel<0><<<grid, 64 * kWgWaves, 0, st>>>(w);
+    else if (net.ks1 == 1) ppo2_wgrad_kernel<1><<<grid, 64 * kWgWaves, 0, st>>>(w);
     else ppo2_wgrad_kernel<2><<<grid, 64 * kWgWaves, 0, st>>>(w);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (wgrad)");
+    if (ext)  // dW1 | db1 = G1^T [s | 1] on the dense GEMM, into grad's W1 / b1
+        ppo2_ext_dw1(g.g1, s, net.S, kUpdH, rows, workspace + wl.dw1, grad,
+                     grad + (int64_t)kUpdH * net.S, st);
     const int64_t total = (int64_t)net.H * net.S + net.H + (int64_t)net.H * net.H + net.H +
                           (int64_t)net.A * net.H + net.A;
-    ppo2_reduce_kernel<<<(int)((total + 63) / 64), 64 * kRedSplit, 0, st>>>(
-        net, partw, grid, g.part3, gfd * kFdWaves, grad, g.lpart, loss_sum);
+    const int64_t nred = ext ? total - ((int64_t)net.H * net.S + net.H) : total;
+    ppo2_reduce_kernel<<<(int)((nred + 63) / 64), 64 * kRedSplit, 0, st>>>(
+        net, partw, grid, g.part3, gfd * kFdWaves, g.p3, grad, g.lpart, loss_sum, ext ? 1 : 0);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (reduce)");
     return RLP_OK;
 }

@@ -7,7 +7,7 @@ import ctypes as C
 import torch
 
 from . import _abi
-from ._native import check, lib, ptr, stream_ptr
+from ._native import RLPError, check, lib, ptr, stream_ptr
 
 
 def dims(kind):
@@ -289,8 +289,14 @@ def ppo2_grad(desc, packed, cfg, s, a=None, a_logprob=None, adv=None, v_target=N
     dev = s.device
     grad = grad if grad is not None else torch.empty(desc.param_count(), dtype=torch.float32,
                                                      device=dev)
+    need = int(lib().rlp_ppo2_workspace_floats(C.byref(desc), rows))
+    if need < 0:   # not a net rlp_ppo2_grad takes: let the call report why
+        need = 0
     if workspace is None:
         workspace = ppo2_workspace(desc, rows, dev)
+    elif workspace.numel() < need:
+        raise RLPError(f"rlp_ppo2_grad: workspace of {workspace.numel()} floats, need {need} "
+                       f"(rlp_ppo2_workspace_floats)")
     # converted tensors are bound to locals so they outlive the (asynchronous) launch
     s_, a_, lp_, adv_, vt_, idx_ = (None if t is None else t.contiguous()
                                     for t in (s, a, a_logprob, adv, v_target, index))
@@ -316,6 +322,11 @@ def ppo2_dense_grad(desc, params, cfg, s, a=None, a_logprob=None, adv=None, v_ta
                                                      device=dev)
     if workspace is None:
         workspace = ppo2_dense_workspace(desc, rows, dev)
+    else:
+        need = int(lib().rlp_ppo2_dense_workspace_floats(C.byref(desc), rows))
+        if workspace.numel() < need:
+            raise RLPError(f"rlp_ppo2_dense_grad: workspace of {workspace.numel()} floats, need "
+                           f"{need} (rlp_ppo2_dense_workspace_floats)")
     s_, a_, lp_, adv_, vt_ = (None if t is None else t.contiguous()
                               for t in (s, a, a_logprob, adv, v_target))
     check(lib().rlp_ppo2_dense_grad(C.byref(desc), ptr(params), C.byref(cfg), ptr(s_), ptr(a_),

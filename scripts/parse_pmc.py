@@ -26,11 +26,12 @@ for f in files:
             name = row.get("Kernel_Name", "")
             short = name.split("(")[0].replace("void ", "")[:60]
             v = float(row["Counter_Value"])
-            vals[short][row["Counter_Name"]].append(v)
+            reps = int(row.get("N") or 1)   # aggregated rows (scripts/pmc_filter.py): mean x N
+            vals[short][row["Counter_Name"]].extend([v] * reps)
             if by_grid and by_grid.search(name):
                 key = (name.split("(")[0].replace("void ", "")[:90], int(row["Grid_Size"]),
                        int(row["Workgroup_Size"]), int(row["LDS_Block_Size"]))
-                shapes[key][row["Counter_Name"]].append(v)
+                shapes[key][row["Counter_Name"]].extend([v] * reps)
 for k, cs in sorted(vals.items()):
     print(k)
     for c, v in sorted(cs.items()):

@@ -1056,6 +1056,73 @@ def gen_ppo2_soi_learn():
     print("ppo2_soi_learn", {k: float(np.abs(v).max()) for k, v in grads.items()})
 
 
+def gen_ppo2_ugvoa_learn():
+    """learn() with the PPO2-UGVForwardObstacleAvoidance demo's nets and K (actor / critic
+    41 -> 256 -> 256 -> 2 / -> 1 tanh, demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/
+    train.py:39-125; ppo_msg :144-162: K_epochs 25, a_lr 1e-4, c_lr 1e-3, full batch; init_std
+    per action dim = range / 6, :164) on a 1 200-row buffer (the demo's buffer_size =
+    time_max / dt * 4 = 15 / 0.05 * 4): the reference's first-step p.grad, the GAE / v_target /
+    normalised advantages learn() computed, and the after-weights of the 25 epochs. Inputs:
+    4 state features in [-2, 2] and 37 lidar ranges in [0, 2] (the laser_dis range)."""
+    g = np.random.default_rng(20267)
+    with quiet():
+        drv_oa = load("demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py",
+                      "ref_ppo2_ugvoa_train")
+    torch.manual_seed(37)
+    S, A = 41, 2
+    lo, hi = np.array([-3., -2 * np.pi]), np.array([3., 2 * np.pi])
+    std0 = (hi - lo) / 2 / 3
+    actor = drv_oa.PPOActor_Gaussian(state_dim=S, action_dim=A, a_min=lo, a_max=hi, init_std=std0,
+                                     use_orthogonal_init=True)
+    critic = drv_oa.PPOCritic(state_dim=S, use_orthogonal_init=True)
+    with torch.no_grad():   # a last layer large enough for a non-trivial tanh'(z)
+        torch.nn.init.orthogonal_(actor.mean_layer.weight, gain=1.0)
+    B, K = 1200, 25
+    ppo_msg = {'gamma': 0.99, 'K_epochs': K, 'eps_clip': 0.2, 'buffer_size': B, 'state_dim': S,
+               'action_dim': A, 'a_lr': 1e-4, 'c_lr': 1e-3, 'set_adam_eps': True, 'lmd': 0.95,
+               'use_adv_norm': True, 'mini_batch_size': 64, 'entropy_coef': 0.01,
+               'use_grad_clip': False, 'use_lr_decay': False, 'max_train_steps': int(5e6),
+               'using_mini_batch': False}
+    env_msg = {'state_dim': S, 'action_dim': A, 'name': 'UGVForwardObstacleAvoidance',
+               'action_range': np.stack([lo, hi], 1)}
+    agent = ppo2_mod.Proximal_Policy_Optimization2(env_msg, ppo_msg, actor=actor, critic=critic)
+    s, a, lp, r, s2, done, success = _learn_buffer(g, B, S, actor, 0.3)
+    s[:, 4:] = (s[:, 4:] + 2) / 2          # lidar ranges in [0, 2]
+    s2[:, 4:] = np.clip((s2[:, 4:] + 2) / 2, 0, 2)
+    with torch.no_grad():   # the buffer's actions / log-probs for these inputs
+        mean = actor(torch.tensor(s, dtype=torch.float))
+        at = torch.clamp(mean + actor.std * torch.tensor(g.normal(size=mean.shape), dtype=torch.float),
+                         actor.a_min, actor.a_max)
+        a = at.numpy().astype(np.float64)
+        lp = torch.distributions.Normal(mean, actor.std).log_prob(at).numpy().astype(np.float64)
+    lp = lp + 0.3 * g.normal(size=lp.shape)
+    for i in range(B):
+        agent.buffer.append(s=s[i], a=a[i], log_prob=lp[i], r=r[i], s_=s2[i], done=done[i],
+                            success=success[i], index=i)
+    before_a, before_c = _flat(actor), _flat(critic)
+    with torch.no_grad():
+        vs = critic(torch.tensor(s, dtype=torch.float))
+    rec, grads = {}, {}
+    _grad_tap(grads, "actor", agent.optimizer_actor, list(actor.parameters()))
+    _grad_tap(grads, "critic", agent.optimizer_critic, list(critic.parameters()))
+    real = ppo2_mod.torch
+    ppo2_mod.torch = _TorchProbe(rec)
+    try:
+        agent.learn(0, buf_num=1)
+    finally:
+        ppo2_mod.torch = real
+    adv = torch.tensor(rec["gae_list"]).view(-1, 1)
+    v_target = adv + vs
+    adv_n = (adv - adv.mean()) / (adv.std() + 1e-5)
+    np.savez_compressed(os.path.join(OUT, "ppo2_ugvoa_learn.npz"), s=s, a=a, a_lp=lp, r=r, s_=s2,
+                        done=done, success=success, before_actor=before_a, before_critic=before_c,
+                        after_actor=_flat(actor), after_critic=_flat(critic),
+                        adv_norm=adv_n.numpy()[:, 0], v_target=v_target.numpy()[:, 0],
+                        grad_actor=grads["actor"], grad_critic=grads["critic"],
+                        std=std0.astype(np.float32), a_min=lo, a_max=hi, K=np.int32(K))
+    print("ppo2_ugvoa_learn", {k: float(np.abs(v).max()) for k, v in grads.items()})
+
+
 def gen_dppo2_learn():
     """Two consecutive Worker.learn() iterations of the DPPO2-CartPole copy (SharedAdam with the
     driver's lr / eps, k_epo = 6, use_grad_clip=True, clip 0.2), the local nets reloaded from the
@@ -1235,6 +1302,7 @@ if __name__ == "__main__":
     gen_sac_grad()
     gen_ppo2_learn()
     gen_ppo2_soi_learn()
+    gen_ppo2_ugvoa_learn()
     gen_dppo2_learn()
     gen_ppo2_transcript("cartpole")
     gen_ppo2_transcript("angleonly")

@@ -172,8 +172,9 @@ def _oa_env(n_envs, seed, **kw):
 def test_vec_ppo2_iterations(cls, kwargs):
     """VecPPO2 iterations (rlp_rollout + advantages + K epochs); the lidar env's 41-input nets
     (the PPO2-UGVForwardObstacleAvoidance demo shape) roll out through rlp_rollout's per-step
-    kernel sequence and update on librlp's dense-GEMM gradient (learner='auto' picks the native
-    learner for every Linear/Tanh stack)."""
+    kernel sequence and update on librlp's f16x3 kernels with layer 1 on the exact-f32 GEMM
+    (learner='auto' picks the native learner for every Linear/Tanh stack; mini-batches of the
+    41-input nets are gathered before the gradient)."""
     env = cls(n_envs=4096, seed=5, **kwargs)
     ar = np.array(env.action_range)
     actor = PPOActor_Gaussian(env.state_dim, env.action_dim, ar[:, 0], ar[:, 1],
@@ -182,7 +183,7 @@ def test_vec_ppo2_iterations(cls, kwargs):
     agent = VecPPO2(env, actor, critic, {'K_epochs': 2, 'using_mini_batch': True,
                                          'mini_batch_size': 32768}, T=32)
     assert type(agent.learner).__name__ == "NativePPO2Learner"
-    assert agent.learner.net_a.dense == (env.state_dim > 8)
+    assert not agent.learner.net_a.dense and agent.learner.net_a.ext == (env.state_dim > 8)
     for _ in range(3):
         out = agent.iteration()
     assert torch.isfinite(out["actor_loss"]) and torch.isfinite(out["critic_loss"])

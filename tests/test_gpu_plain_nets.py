@@ -138,8 +138,10 @@ NETS = {"soi": (lambda: SoiActor(), lambda: SoiCritic(), 4, 2),
 
 
 @pytest.mark.parametrize("rows", [1000, 300_000])
-@pytest.mark.parametrize("net", sorted(NETS))
-def test_dense_grad_vs_float64(net, rows):
+@pytest.mark.parametrize("net,kernels", [("lidar", "auto"), ("lidar", "dense"), ("soi", "auto")])
+def test_dense_grad_vs_float64(net, kernels, rows):
+    """rlp_ppo2_dense_grad (kernels 'dense', and the SOI nets' 'auto') and, for the lidar nets'
+    'auto', rlp_ppo2_grad's f16x3 FD / wgrad kernels with layer 1 on the exact-f32 GEMM."""
     mk_a, mk_c, S, Ad = NETS[net]
     torch.manual_seed(7)
     actor, critic = mk_a(), mk_c()
@@ -156,8 +158,10 @@ def test_dense_grad_vs_float64(net, rows):
     vt = torch.randn(rows, 1, device="cuda", generator=g)
     lp = _off_kinks(actor, s, a, lp)
     lrn = NativePPO2Learner(_as(actor, torch.float32, "cuda"), _as(critic, torch.float32, "cuda"),
-                            dict(DEFAULT_PPO_MSG), device="cuda")
-    assert lrn.net_a.dense and lrn.net_c.dense
+                            dict(DEFAULT_PPO_MSG, update_kernels=kernels), device="cuda")
+    f16x3 = net == "lidar" and kernels == "auto"
+    assert lrn.net_a.dense != f16x3 and lrn.net_c.dense != f16x3
+    assert lrn.net_a.ext == f16x3 and lrn.net_c.ext == f16x3
     lrn.grads(s, a, lp, adv, vt)
     gn = [lrn.net_a.grad.double().cpu().numpy(), lrn.net_c.grad.double().cpu().numpy()]
     g2 = [lrn.net_a.grad.clone(), lrn.net_c.grad.clone()]
@@ -170,7 +174,7 @@ def test_dense_grad_vs_float64(net, rows):
     t32 = _loss_grads(_as(actor, torch.float32, "cuda"), _as(critic, torch.float32, "cuda"),
                       s, a, lp, adv, vt)
     for i, name in enumerate(("actor", "critic")):
-        _f32_class(f"{net} {rows} {name}", gn[i], t32[i], t64[i])
+        _f32_class(f"{net} {kernels} {rows} {name}", gn[i], t32[i], t64[i])
 
 
 def test_dense_learner_matches_reference_soi_learn(golden):
@@ -207,6 +211,47 @@ def test_dense_learner_matches_reference_soi_learn(golden):
     for name, m in (("actor", actor), ("critic", critic)):
         got = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
         np.testing.assert_allclose(got, g[f"after_{name}"], rtol=1e-5, atol=2e-6, err_msg=name)
+
+
+def test_learner_matches_reference_ugvoa_learn(golden):
+    """The PPO2-UGVForwardObstacleAvoidance demo's 41 -> 256 -> 256 nets with the demo's K = 25
+    (tests/golden/ppo2_ugvoa_learn.npz, made by running the reference's learn()): first-step
+    gradients within 4x the reference's own f32 error of float64, and the after-weights of the 25
+    full-batch epochs (rtol 1e-5 / atol 2e-6 per 3 Adam steps, growing with sqrt(steps) as in
+    tests/test_learn_golden.py)."""
+    g = golden("ppo2_ugvoa_learn")
+    K = int(g["K"])
+    lo, hi = tuple(float(x) for x in g["a_min"]), tuple(float(x) for x in g["a_max"])
+
+    def nets(device):
+        actor = SoiActor(a_min=lo, a_max=hi, init_std=g["std"], S=41, widths=(256, 256))
+        critic = SoiCritic(S=41, widths=(256, 256))
+        _load(actor, g["before_actor"])
+        _load(critic, g["before_critic"])
+        return actor.to(device), critic.to(device)
+    t = lambda k, w=1: torch.as_tensor(g[k], dtype=torch.float32, device="cuda").reshape(-1, w)
+    s, a, lp, adv, vt = t("s", 41), t("a", 2), t("a_lp", 2), t("adv_norm"), t("v_target")
+    msg = dict(DEFAULT_PPO_MSG, K_epochs=K, gamma=0.99, a_lr=1e-4, c_lr=1e-3)
+    actor, critic = nets("cuda")
+    lrn = NativePPO2Learner(actor, critic, msg, device="cuda")
+    lrn.grads(s, a, lp, adv, vt)
+    a64, c64 = (_as(m, torch.float64, "cpu") for m in nets("cpu"))
+    t64 = _loss_grads(a64, c64, *(x.double().cpu() for x in (s, a, lp, adv, vt)))
+    for name, net, truth in (("actor", lrn.net_a, t64[0]), ("critic", lrn.net_c, t64[1])):
+        ref = g[f"grad_{name}"].astype(np.float64)
+        e32 = np.abs(ref - truth).max()
+        en = np.abs(net.grad.double().cpu().numpy() - truth).max()
+        floor = 2e-6 * np.abs(truth).max()
+        print(f"ugvoa {name}: native {en:.3e} reference f32 {e32:.3e} floor {floor:.3e}")
+        assert en <= 4 * e32 + floor, (name, en, e32)
+    actor, critic = nets("cuda")
+    lrn = NativePPO2Learner(actor, critic, msg, device="cuda")
+    lrn.update(s, a, lp, adv, vt)
+    torch.cuda.synchronize()
+    atol = 2e-6 * np.sqrt(K / 3)
+    for name, m in (("actor", actor), ("critic", critic)):
+        got = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+        np.testing.assert_allclose(got, g[f"after_{name}"], rtol=1e-5, atol=atol, err_msg=name)
 
 
 # ---------------------------------------------------------------------------------------------

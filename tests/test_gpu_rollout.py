@@ -42,10 +42,11 @@ def nets(S, Ad, seed, H=256):
     return ad, init(ad, 1.0), cd, init(cd, 1.0)
 
 
-def test_lidar_env_nets_pack_and_forward_but_update_rejects():
+def test_lidar_env_nets_pack_forward_and_update():
     """41-input nets (the lidar env's PPO2 demos) pack for the MFMA forward (layer 1 on 11
-    K-steps), which matches the oracle's double-accumulated MLP; the native PPO2 update, built for
-    <= 8 inputs, rejects them with a clean error (their update runs on the torch learner)."""
+    K-steps), which matches the oracle's double-accumulated MLP; the native f16x3 update takes
+    them with contiguous rows (layer 1 on the exact-f32 GEMM; precision: test_gpu_plain_nets.py)
+    and refuses a gather index or a too-small workspace with a clean error before any launch."""
     from oracle import oracle
     kind = A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE
     D, S, Ad = A.ENV_DIMS[kind]
@@ -57,10 +58,13 @@ def test_lidar_env_nets_pack_and_forward_but_update_rejects():
         ref = oracle.mlp_forward(d, prm, x)
         np.testing.assert_allclose(y, ref, rtol=1e-5, atol=2e-6)
     pk = K.mfma_pack(cd, dev(cp))
-    ws = torch.empty(1 << 20, device="cuda")
-    with pytest.raises(_native.RLPError, match="S<=8"):
-        K.ppo2_grad(cd, pk, K.ppo2_loss_cfg(A.RLP_LOSS_CRITIC), dev(x), v_target=dev(x[:, 0].copy()),
-                    grad=torch.empty(cd.param_count(), device="cuda"), workspace=ws)
+    cfg, vt = K.ppo2_loss_cfg(A.RLP_LOSS_CRITIC), dev(x[:, 0].copy())
+    with pytest.raises(_native.RLPError, match="workspace"):
+        K.ppo2_grad(cd, pk, cfg, dev(x), v_target=vt, workspace=torch.empty(1 << 20, device="cuda"))
+    with pytest.raises(_native.RLPError, match="contiguous rows"):
+        K.ppo2_grad(cd, pk, cfg, dev(x), v_target=vt, index=torch.arange(100, device="cuda"))
+    g = K.ppo2_grad(cd, pk, cfg, dev(x), v_target=vt)
+    assert torch.isfinite(g).all() and float(g.abs().max()) > 0
 
 
 def test_rollout_invariants_at_bench_size():
