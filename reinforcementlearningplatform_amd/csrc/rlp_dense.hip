@@ -2329,42 +2329,172 @@ inline PpoDenseWs ppo2_dense_ws(const rlp_mlp_desc &d, int64_t rows) {
 
 // ---- layer 1 of the 41-input nets for rlp_ppo2_grad (rlp_update.hip, "EXT" kernels) -----------
 // The f16x3 FD / wgrad kernels take h1 = tanh(s W1^T + b1) from HBM and hand g1 = dL/dz1 back;
-// both layer-1 products run here on the exact-f32 tiled GEMM in row chunks of kExtChunk (32-bit
-// element offsets): the forward with the tanh epilogue, dW1 | db1 = G1^T [s | 1] as long
-// reduction slices whose partials (every chunk's, in chunk order) one fixed-order reduce sums.
-constexpr int64_t kExtChunk = 1 << 22;
-constexpr int kExtSlices = 128;  // reduction slices per chunk (x 4 tiles = 512 blocks)
+// the two layer-1 products run here as exact-f32 MFMA kernels of their own (v_mfma_f32_16x16x4_f32,
+// f32 accumulation, as torch's f32 GEMM). Both are HBM-bound (1 KiB of h1 written / of g1 read per
+// row against 164 B of s): the s rows of a tile are one contiguous span, loaded coalesced and
+// transposed into LDS (the tiled GEMM's generic loader spent 46 VALU per MFMA on the 41-float rows:
+// 1.9 ms for the forward of 2^20 rows, profiles/r5/r5f_ext_pmc_shapes.txt).
+constexpr int kL1Rows = 64;        // rows per forward tile (16 per wave)
+constexpr int kL1Ld = 256 + 16;    // LDS row of 256 floats: lane groups g, g + 1 16 banks apart
+constexpr int kL1SLd = kL1Rows + 16;
+constexpr int kL1WRows = 32;       // rows per weight-gradient step
+constexpr int kL1WLd = 48;         // s tile row (features | 1 | 0 pad): 16 banks between rows
+constexpr int kL1WBlocks = 512;    // weight-gradient blocks (per-block partials, fixed-order reduce)
+
+// row / column of flat index f of a [*][S] row-major span, without an integer division:
+// (f + 0.5) / S lies at least 0.5 / S from an integer, far beyond the float rounding for f < 2^20
+__device__ __forceinline__ int l1_row(int f, float invS) { return (int)(((float)f + 0.5f) * invS); }
+
+// h1[row][256] = tanh(W1 s_row + b1) for 64-row tiles (grid-stride), W1^T and the tile's s^T in
+// LDS. Wave w: rows 16 w .. 16 w + 15, all 16 neuron tiles (C = [neuron][row], 64 accumulators);
+// lane (g, e) stores neurons 16 t + 4 g .. + 3 of row e as one float4.
+template <int KS>
+__global__ void __launch_bounds__(256) l1_fwd_kernel(const float *__restrict__ s, int S, int64_t rows,
+                                                     const float *__restrict__ W1, int ldw,
+                                                     const float *__restrict__ b1, float *__restrict__ h1) {
+    __shared__ float w1t[4 * KS][kL1Ld];        // [k][neuron]
+    __shared__ float st[4 * KS][kL1SLd];        // [k][row]
+    const int t = threadIdx.x, lane = t & 63, g = lane >> 4, e = lane & 15, w = t >> 6;
+    for (int i = t; i < 4 * KS * 256; i += 256) {
+        const int n = i / (4 * KS), k = i - n * (4 * KS);
+        w1t[k][n] = k < S ? W1[(int64_t)n * ldw + k] : 0.f;
+    }
+    const float invS = 1.f / (float)S;
+    const int64_t ntiles = (rows + kL1Rows - 1) / kL1Rows;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t r0 = tile * kL1Rows;
+        const int nr = (int)(rows - r0 < kL1Rows ? rows - r0 : kL1Rows);
+        __syncthreads();  // the previous tile's s^T is read
+        for (int f = t; f < kL1Rows * 4 * KS; f += 256) {  // zero the padding columns / rows first
+            const int k = f / kL1Rows, r = f - k * kL1Rows;
+            if (k >= S || r >= nr) st[k][r] = 0.f;
+        }
+        const float *src = s + r0 * S;
+        for (int f = t; f < nr * S; f += 256) {  // the tile's contiguous span, coalesced
+            const int r = l1_row(f, invS);
+            st[f - r * S][r] = src[f];
+        }
+        __syncthreads();
+        floatx4 acc[16];
+#pragma unroll
+        for (int nt = 0; nt < 16; ++nt) {
+            const floatx4 b = *reinterpret_cast<const floatx4 *>(b1 + 16 * nt + 4 * g);
+            acc[nt] = b;
+        }
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            const float bv = st[4 * kk + g][16 * w + e];
+#pragma unroll
+            for (int nt = 0; nt < 16; ++nt)
+                acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1t[4 * kk + g][16 * nt + e], bv, acc[nt], 0, 0, 0);
+        }
+        const int r = 16 * w + e;
+        if (r < nr) {
+            float *dst = h1 + (r0 + r) * 256 + 4 * g;
+#pragma unroll
+            for (int nt = 0; nt < 16; ++nt) {
+                floatx4 v;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = tanhf(acc[nt][q]);
+                *reinterpret_cast<floatx4 *>(dst + 16 * nt) = v;
+            }
+        }
+    }
+}
+
+// part[b][256][S + 1] = sum over block b's rows of g1[row] (x) [s_row | 1]: dW1 | db1 partials.
+// Wave w owns neurons 64 w .. 64 w + 63 (4 tiles) x FT feature tiles (C = [neuron][feature]);
+// 32-row steps, the next step's g1 rows loaded into registers under the current step's MFMAs.
+template <int FT>
+__global__ void __launch_bounds__(256) l1_wgrad_kernel(const float *__restrict__ g1,
+                                                       const float *__restrict__ s, int S, int64_t rows,
+                                                       int64_t rpb, float *__restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float gt[kL1WRows][kL1Ld];  // [row][neuron]
+    __shared__ float sx[kL1WRows][kL1WLd];                              // [row][feature | 1]
+    const int t = threadIdx.x, lane = t & 63, g = lane >> 4, e = lane & 15, w = t >> 6;
+    const int64_t lo = blockIdx.x * rpb, hi = lo + rpb < rows ? lo + rpb : rows;
+    const float invS = 1.f / (float)S;
+    floatx4 acc[4][FT];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    constexpr int NV = kL1WRows * 256 / 4 / 256;  // float4 of g1 per thread and step (8)
+    floatx4 v[NV];
+    auto load = [&](int64_t r0) {
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            const int i = t + 256 * u, r = i >> 6;
+            v[u] = r0 + r < hi ? *reinterpret_cast<const floatx4 *>(g1 + (r0 + r) * 256 + 4 * (i & 63))
+                               : floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    if (lo < hi) load(lo);
+    for (int64_t r0 = lo; r0 < hi; r0 += kL1WRows) {
+        const int nr = (int)(hi - r0 < kL1WRows ? hi - r0 : kL1WRows);
+        __syncthreads();  // the previous step's tiles are read
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            const int i = t + 256 * u;
+            *reinterpret_cast<floatx4 *>(&gt[i >> 6][4 * (i & 63)]) = v[u];
+        }
+        for (int f = t; f < kL1WRows * kL1WLd; f += 256) {  // ones column, zero padding
+            const int r = f / kL1WLd, c = f - r * kL1WLd;
+            if (c >= S) sx[r][c] = (c == S && r < nr) ? 1.f : 0.f;
+            else if (r >= nr) sx[r][c] = 0.f;
+        }
+        const float *src = s + r0 * S;
+        for (int f = t; f < nr * S; f += 256) {
+            const int r = l1_row(f, invS);
+            sx[r][f - r * S] = src[f];
+        }
+        __syncthreads();
+        if (r0 + kL1WRows < hi) load(r0 + kL1WRows);  // next step, under this step's MFMAs
+#pragma unroll
+        for (int k0 = 0; k0 < kL1WRows; k0 += 4) {
+            float bv[FT];
+#pragma unroll
+            for (int j = 0; j < FT; ++j) bv[j] = sx[k0 + g][16 * j + e];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float av = gt[k0 + g][64 * w + 16 * i + e];
+#pragma unroll
+                for (int j = 0; j < FT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+    // C layout: lane (g, e) holds neurons 64 w + 16 i + 4 g + q, feature 16 j + e
+    float *out = part + (int64_t)blockIdx.x * 256 * (S + 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FT; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = 64 * w + 16 * i + 4 * g + q, c = 16 * j + e;
+                if (c <= S) out[n * (S + 1) + c] = acc[i][j][q];
+            }
+}
+
 int64_t ppo2_ext_floats(int S, int H, int64_t rows) {
-    const int64_t chunks = (rows + kExtChunk - 1) / kExtChunk;
-    return chunks * kExtSlices * (int64_t)H * (S + 1);
+    (void)rows;
+    return (int64_t)kL1WBlocks * H * (S + 1);
 }
 void ppo2_ext_h1(const float *W1, int ldw, const float *b1, int S, int H, const float *s,
                  int64_t rows, float *h1, hipStream_t st) {
-    for (int64_t r0 = 0; r0 < rows; r0 += kExtChunk) {
-        const int B = (int)(rows - r0 < kExtChunk ? rows - r0 : kExtChunk);
-        Epi e{};
-        e.y = h1 + r0 * H; e.ldy = H; e.bias = b1; e.kind = kEpiTanh; e.M = B; e.N = H;
-        // B(r = input k, n = neuron j) = W1[j][k], row stride ldw (the packed W1 block)
-        const Prob q = make_prob(mat(s + r0 * S, B, S, S), Opnd{W1, W1, 1, ldw, 1, ldw, S, H, H, -1, 0},
-                                 e, S, 1);
-        gemm_multi(&q, 1, st);
-    }
+    (void)H;
+    const int64_t ntiles = (rows + kL1Rows - 1) / kL1Rows;
+    const int grid = (int)(ntiles < 4096 ? ntiles : 4096);
+    l1_fwd_kernel<11><<<grid, 256, 0, st>>>(s, S, rows, W1, ldw, b1, h1);
 }
 void ppo2_ext_dw1(const float *g1, const float *s, int S, int H, int64_t rows, float *part,
                   float *gW, float *gb, hipStream_t st) {
-    int z = 0;
-    for (int64_t r0 = 0; r0 < rows; r0 += kExtChunk) {
-        const int B = (int)(rows - r0 < kExtChunk ? rows - r0 : kExtChunk);
-        Epi e{};
-        e.y = part + (int64_t)z * H * (S + 1); e.kind = kEpiPartial; e.M = H; e.N = S + 1;
-        Opnd x = mat(s + r0 * S, B, S, S);
-        x.cols = S + 1;
-        x.ones = S;
-        const Prob q = make_prob_long(transposed(g1 + r0 * H, H, B, H), x, e, B, kExtSlices);
-        gemm_multi(&q, 1, st);
-        z += q.nz;
-    }
-    wgrad_reduce(Layer{nullptr, nullptr, S, H}, part, z, gW, gb, st);
+    int64_t rpb = (rows + kL1WBlocks - 1) / kL1WBlocks;
+    rpb = (rpb + kL1WRows - 1) / kL1WRows * kL1WRows;
+    const int nb = (int)((rows + rpb - 1) / rpb);
+    l1_wgrad_kernel<3><<<nb, 256, 0, st>>>(g1, s, S, rows, rpb, part);
+    wgrad_reduce(Layer{nullptr, nullptr, S, H}, part, nb, gW, gb, st);
 }
 
 }  // namespace rlp
