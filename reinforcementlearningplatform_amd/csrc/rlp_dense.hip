@@ -2263,7 +2263,7 @@ __global__ void __launch_bounds__(256) chunk_sum_kernel(const float *__restrict_
 }
 
 struct PpoDenseWs {  // float offsets into the workspace
-    int64_t act, t, g0, g1, g2, g3, part, ones, head, slots, lpart, total;
+    int64_t act, t, g0, g1, g2, g3, part, ones, head, slots, lpart, fg_part, fg_lpart, total;
 };
 inline bool ppo2_dense_ok(const rlp_mlp_desc &d, bool actor) {
     if (d.n_layers < 1 || d.n_layers > RLP_MLP_MAX_LAYERS) return false;
@@ -2296,6 +2296,25 @@ inline int64_t ppo2_wgrad_nz(const rlp_mlp_desc &d, int l) {
     const int64_t tiles = ((d.dims[l] + 1 + kDT - 1) / kDT) * ((d.dims[l + 1] + kDT - 1) / kDT);
     return 512 / tiles > 1 ? 512 / tiles : 1;
 }
+// the shapes fg_grad_kernel takes: <= 8 inputs, hidden (128, 64, 32) or (64, 64), head <= 4
+// (actor) / 1 (critic) — the PPO2-SOI demo's nets
+inline int ppo2_fused_kind(const rlp_mlp_desc &d) {
+    const int L = d.n_layers;
+    if (d.dims[0] > 8 || d.dims[L] > 4) return 0;
+    if (L == 4 && d.dims[1] == 128 && d.dims[2] == 64 && d.dims[3] == 32) return 1;
+    if (L == 3 && d.dims[1] == 64 && d.dims[2] == 64) return 2;
+    return 0;
+}
+inline int dense_cus() {  // CUs of the device (cached)
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0, n = 0;
+        cus = (hipGetDevice(&dev) == hipSuccess &&
+               hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+                  ? n : 256;
+    }
+    return cus;
+}
 inline PpoDenseWs ppo2_dense_ws(const rlp_mlp_desc &d, int64_t rows) {
     const int64_t B = rows < kPpoChunk ? rows : kPpoChunk;
     int64_t hid = 0, maxw = 0, np = 0, maxpart = 0, sumpart = 0;
@@ -2323,8 +2342,271 @@ inline PpoDenseWs ppo2_dense_ws(const rlp_mlp_desc &d, int64_t rows) {
     w.head = take(8);
     w.slots = take(chunks * np);
     w.lpart = take(2 * ((rows + 255) / 256));  // f64 loss partial per head block
+    if (ppo2_fused_kind(d)) {  // fg_grad_kernel: one partial gradient and loss per block
+        w.fg_part = take((int64_t)dense_cus() * np);
+        w.fg_lpart = take(2 * (int64_t)dense_cus());
+    }
     w.total = o;
     return w;
+}
+
+// ---- fused per-row gradient for the PPO2-SOI demo's small nets ---------------------------------
+// actor 4 -> 128 -> 64 -> 32 -> 2 / critic 4 -> 64 -> 64 -> 1 (demonstration/PPO2/
+// PPO2-4-SecondOrderIntegration/train.py:37-125): per 32-row step ONE block runs the forward, the
+// loss head, the backward data passes and the weight-gradient accumulation, every activation and
+// hidden gradient in LDS (the chunked path sends them through HBM five launches per chunk:
+// forward chain, head, backward chain, weight-gradient GEMM, reduce; 18 TF/s, r5h). Exact f32
+// MFMA (v_mfma_f32_16x16x4_f32) throughout; one 8-wave block per CU over a static row stride; the
+// weight gradient of the block's rows stays in the MFMA accumulators (each wave owns a fixed set
+// of 16 x 16 dW | db tiles) and is written once as the block's partial, summed over blocks in a
+// fixed order (run-to-run identical, as the chunked path).
+// LDS rows are x + (17 - x) mod 32 floats long (== 17 mod 32): the three operand-read patterns
+// (lane (g, e) reading [16 e + ..][g] and [g][e + ..]) then hit at most two lanes per bank.
+constexpr int kFgRows = 32;
+constexpr int kFgWaves = 8;
+__host__ __device__ constexpr int fg_ld(int x) { return x + ((17 - x % 32) + 32) % 32; }
+
+template <int H1, int H2, int H3>
+struct FgShape {
+    static constexpr int L = H3 ? 4 : 3;
+    // padded widths: inputs <= 8, hidden H1, H2 (, H3), the head 16
+    __host__ __device__ static constexpr int width(int l) {
+        return l == 0 ? 8 : l == L ? 16 : l == 1 ? H1 : l == 2 ? H2 : H3;
+    }
+    // LDS (floats): X | H_1 .. H_{L-1} | Z | dA | dB | W_1 .. W_L | b_1 .. b_L
+    __host__ __device__ static constexpr int act_ld(int l) { return fg_ld(l == 0 ? 16 : l == L ? 16 : width(l) + 1); }
+    __host__ __device__ static constexpr int hmax() { return H1 > H2 ? H1 : H2; }
+    __host__ __device__ static constexpr int w_ld(int l) { return fg_ld(width(l - 1)); }   // W_l [width(l)][w_ld(l)]
+    __host__ __device__ static constexpr int off_act(int l) {  // X = 0, H_l = l, Z = L
+        int o = 0;
+        for (int i = 0; i < l; ++i) o += kFgRows * act_ld(i);
+        return o;
+    }
+    __host__ __device__ static constexpr int off_dA() { return off_act(L + 1); }
+    __host__ __device__ static constexpr int off_dB() { return off_dA() + kFgRows * fg_ld(hmax()); }
+    __host__ __device__ static constexpr int off_w(int l) {
+        int o = off_dB() + kFgRows * fg_ld(hmax());
+        for (int i = 1; i < l; ++i) o += width(i) * w_ld(i);
+        return o;
+    }
+    __host__ __device__ static constexpr int off_b(int l) {
+        int o = off_w(L + 1);
+        for (int i = 1; i < l; ++i) o += width(i);
+        return o;
+    }
+    __host__ __device__ static constexpr int floats() { return off_b(L + 1); }
+    // dW | db tiles of layer l: width(l) / 16 x ceil((in + 1) / 16) (in = 8 padded inputs for l = 1)
+    __host__ __device__ static constexpr int ntn(int l) { return l == 1 ? 1 : (width(l - 1) + 1 + 15) / 16; }
+    __host__ __device__ static constexpr int tiles(int l) { return width(l) / 16 * ntn(l); }
+    __host__ __device__ static constexpr int tile0(int l) {
+        int o = 0;
+        for (int i = 1; i < l; ++i) o += tiles(i);
+        return o;
+    }
+    __host__ __device__ static constexpr int tiles_total() { return tile0(L + 1); }
+    __host__ __device__ static constexpr int per_wave() { return (tiles_total() + kFgWaves - 1) / kFgWaves; }
+};
+
+struct FgArgs {
+    const float *params;       // plain layout (torch order)
+    const float *s, *a, *lp, *adv, *vt;
+    int64_t rows;
+    int S, A;                  // inputs (<= 8), actor outputs (<= 4; critic 1)
+    int dims[5];               // true widths: S, hidden..., out
+    int64_t off[4];            // W_l offsets in params (b_l follows W_l)
+    int64_t np;                // parameters
+    float inv_rows, eps_clip, ent_row;
+    float gain[4], off_[4], log_std[4], inv_var[4];
+    float *part;               // [grid][np]: the blocks' dW | db partials (torch order)
+    double *lpart;             // [grid]: the blocks' loss partials
+};
+
+template <int H1, int H2, int H3, bool ACTOR>
+__global__ void __launch_bounds__(64 * kFgWaves, 1) fg_grad_kernel(FgArgs g) {
+    using F = FgShape<H1, H2, H3>;
+    constexpr int L = F::L;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int t = threadIdx.x, lane = t & 63, gq = lane >> 4, e = lane & 15;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    // zero everything once (padding rows / columns are read as operands), then weights, biases
+    for (int i = t; i < F::floats(); i += 64 * kFgWaves) lds[i] = 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int l = 1; l <= L; ++l) {
+        const int in = g.dims[l - 1], out = g.dims[l];
+        const float *W = g.params + g.off[l - 1], *b = W + (int64_t)in * out;
+        for (int i = t; i < in * out; i += 64 * kFgWaves) {
+            const int o = i / in, k = i - o * in;
+            lds[F::off_w(l) + o * F::w_ld(l) + k] = W[i];
+        }
+        for (int i = t; i < out; i += 64 * kFgWaves) lds[F::off_b(l) + i] = b[i];
+    }
+    // the ones columns (bias of the next layer's weight gradient) of H_1 .. H_{L-1}
+#pragma unroll
+    for (int l = 1; l < L; ++l)
+        for (int r = t; r < kFgRows; r += 64 * kFgWaves) lds[F::off_act(l) + r * F::act_ld(l) + g.dims[l]] = 1.f;
+    floatx4 acc[F::per_wave()];
+#pragma unroll
+    for (int j = 0; j < F::per_wave(); ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    double lsum = 0.0;
+    const int S = g.S, A = g.A, ks0 = (S + 3) / 4;
+    const int64_t nsteps = (g.rows + kFgRows - 1) / kFgRows;
+    // one 16 x 16 output tile: acc over K / 4 MFMA steps, a(k) / b(k) the lane's operands
+    auto mm = [&](floatx4 c, int K, auto &&av, auto &&bv) {
+#pragma unroll 2
+        for (int k0 = 0; k0 < K; k0 += 4)
+            c = __builtin_amdgcn_mfma_f32_16x16x4f32(av(k0 + gq), bv(k0 + gq), c, 0, 0, 0);
+        return c;
+    };
+    for (int64_t step = blockIdx.x; step < nsteps; step += gridDim.x) {
+        const int64_t r0 = step * kFgRows;
+        const int nr = (int)(g.rows - r0 < kFgRows ? g.rows - r0 : kFgRows);
+        __syncthreads();  // the previous step's X / dZ reads are done
+        // X: s | 1 | 0 (rows past the end all zero)
+        for (int i = t; i < kFgRows * 16; i += 64 * kFgWaves) {
+            const int r = i >> 4, c = i & 15;
+            float v = 0.f;
+            if (r < nr) v = c < S ? g.s[(r0 + r) * S + c] : (c == S ? 1.f : 0.f);
+            lds[F::off_act(0) + r * F::act_ld(0) + c] = v;
+        }
+        // the head's row inputs (wave 0, lane = row)
+        float in_a[4] = {0.f, 0.f, 0.f, 0.f}, in_lp[4] = {0.f, 0.f, 0.f, 0.f}, in_x = 0.f;
+        if (wv == 0 && lane < nr) {
+            if constexpr (ACTOR) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < A) {
+                        in_a[k] = g.a[(r0 + lane) * A + k];
+                        in_lp[k] = g.lp[(r0 + lane) * A + k];
+                    }
+                in_x = g.adv[r0 + lane];
+            } else {
+                in_x = g.vt[r0 + lane];
+            }
+        }
+        __syncthreads();
+        // ---- forward: C[out][row] = W_l H_{l-1}^T + b, tanh (hidden) or z (last) -------------
+#pragma unroll
+        for (int l = 1; l <= L; ++l) {
+            const int M = F::width(l), K = l == 1 ? 4 * ks0 : F::width(l - 1);
+            const float *Wl = lds + F::off_w(l), *bl = lds + F::off_b(l);
+            const float *Hp = lds + F::off_act(l - 1);
+            float *Hc = lds + F::off_act(l);
+            const int lwp = F::w_ld(l), lhp = F::act_ld(l - 1), lhc = F::act_ld(l);
+            for (int tau = wv; tau < M / 16 * (kFgRows / 16); tau += kFgWaves) {
+                const int mt = tau >> 1, rt = tau & 1;
+                floatx4 c = {bl[16 * mt + 4 * gq], bl[16 * mt + 4 * gq + 1], bl[16 * mt + 4 * gq + 2],
+                             bl[16 * mt + 4 * gq + 3]};
+                c = mm(c, K, [&](int k) { return Wl[(16 * mt + e) * lwp + k]; },
+                       [&](int k) { return Hp[(16 * rt + e) * lhp + k]; });
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float v = c[q];
+                    Hc[(16 * rt + e) * lhc + 16 * mt + 4 * gq + q] = l < L ? tanhf(v) : v;
+                }
+            }
+            __syncthreads();
+        }
+        // ---- loss head: dZ_L in place of Z (wave 0, lane = row; padding rows / columns zero) --
+        if (wv == 0 && lane < kFgRows) {
+            float *z = lds + F::off_act(L) + lane * F::act_ld(L);
+            const bool valid = lane < nr;
+            double l = 0.0;
+            if constexpr (ACTOR) {
+                float lp_now = 0.f, lp_old = 0.f, d[4] = {0.f, 0.f, 0.f, 0.f}, tt[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k >= A) continue;
+                    tt[k] = tanhf(z[k]);
+                    d[k] = in_a[k] - (tt[k] * g.gain[k] + g.off_[k]);
+                    lp_now += -(d[k] * d[k]) * (0.5f * g.inv_var[k]) - g.log_std[k] - 0.91893853320467274178f;
+                    lp_old += in_lp[k];
+                }
+                const float adv = in_x;
+                const float ratio = expf(lp_now - lp_old);
+                const float lo = 1.f - g.eps_clip, hi = 1.f + g.eps_clip;
+                const float s1 = ratio * adv, rc = fminf(fmaxf(ratio, lo), hi), s2 = rc * adv;
+                const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);  // torch.min: a tie splits
+                const float w2 = s2 < s1 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+                const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;  // clamp backward
+                const float dl_dlp = -adv * (w1 + w2 * inr) * ratio * g.inv_rows;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < A) z[k] = valid ? dl_dlp * (d[k] * g.inv_var[k]) * g.gain[k] * (1.f - tt[k] * tt[k]) : 0.f;
+                l = valid ? (double)(-fminf(s1, s2) - g.ent_row) : 0.0;
+            } else {
+                const float diff = z[0] - in_x;
+                z[0] = valid ? 2.f * diff * g.inv_rows : 0.f;
+                l = valid ? (double)(diff * diff) : 0.0;
+            }
+            for (int k = ACTOR ? A : 1; k < 16; ++k) z[k] = 0.f;
+            lsum += l;
+        }
+        __syncthreads();
+        // ---- backward: per layer (top down) the weight-gradient tiles this wave owns
+        // (dW | db += dZ_l^T [H_{l-1} | 1], K = the step's rows) and the data pass
+        // dZ_{l-1} = (dZ_l W_l) * (1 - H_{l-1}^2) into the other gradient buffer
+#pragma unroll
+        for (int l = L; l >= 1; --l) {
+            const float *dZ = lds + (l == L ? F::off_act(L) : ((L - l) % 2 ? F::off_dA() : F::off_dB()));
+            const int ldz = l == L ? F::act_ld(L) : fg_ld(F::hmax());
+            const float *Hp = lds + F::off_act(l - 1);
+            const int lhp = F::act_ld(l - 1);
+#pragma unroll
+            for (int j = 0; j < F::per_wave(); ++j) {
+                const int T = wv + kFgWaves * j - F::tile0(l);
+                if (T < 0 || T >= F::tiles(l)) continue;
+                const int mt = T / F::ntn(l), nt = T - mt * F::ntn(l);
+                acc[j] = mm(acc[j], kFgRows, [&](int k) { return dZ[k * ldz + 16 * mt + e]; },
+                            [&](int k) { return Hp[k * lhp + 16 * nt + e]; });
+            }
+            if (l > 1) {
+                const int M = F::width(l), N = F::width(l - 1);
+                const float *Wl = lds + F::off_w(l);
+                const int lw = F::w_ld(l);
+                float *dP = lds + ((L - l + 1) % 2 ? F::off_dA() : F::off_dB());
+                const int ldp = fg_ld(F::hmax());
+                for (int tau = wv; tau < (kFgRows / 16) * (N / 16); tau += kFgWaves) {
+                    const int rt = tau % (kFgRows / 16), nt = tau / (kFgRows / 16);
+                    floatx4 c = {0.f, 0.f, 0.f, 0.f};
+                    c = mm(c, M, [&](int k) { return dZ[(16 * rt + e) * ldz + k]; },
+                           [&](int k) { return Wl[k * lw + 16 * nt + e]; });
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int r = 16 * rt + 4 * gq + q, n = 16 * nt + e;
+                        const float h = Hp[r * lhp + n];
+                        dP[r * ldp + n] = c[q] * __builtin_fmaf(-h, h, 1.f);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // ---- the block's partials: dW | db tiles in torch order, the loss
+    float *out = g.part + (int64_t)blockIdx.x * g.np;
+#pragma unroll
+    for (int j = 0; j < F::per_wave(); ++j) {
+        const int T = wv + kFgWaves * j;
+        if (T >= F::tiles_total()) continue;
+        int l = 1;
+#pragma unroll
+        for (int i = 2; i <= L; ++i)
+            if (T >= F::tile0(i)) l = i;
+        const int Tl = T - F::tile0(l), mt = Tl / F::ntn(l), nt = Tl - mt * F::ntn(l);
+        const int in = g.dims[l - 1], outw = g.dims[l];
+        float *W = out + g.off[l - 1], *b = W + (int64_t)in * outw;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int o = 16 * mt + 4 * gq + q, c = 16 * nt + e;
+            if (o >= outw) continue;
+            if (c < in) W[o * in + c] = acc[j][q];
+            else if (c == in) b[o] = acc[j][q];
+        }
+    }
+    if (wv == 0) {
+        for (int o = 1; o < 64; o <<= 1) lsum += __shfl_xor(lsum, o);
+        if (lane == 0) g.lpart[blockIdx.x] = lsum;
+    }
 }
 
 // ---- layer 1 of the 41-input nets for rlp_ppo2_grad (rlp_update.hip, "EXT" kernels) -----------
@@ -2541,6 +2823,41 @@ int rlp_ppo2_dense_grad(const rlp_mlp_desc *desc, const float *params, const rlp
         ent += 0.5f + 0.91893853320467274178f + logf(cfg->std[k]);  // Normal.entropy()
     }
     h.ent_row = cfg->entropy_coef * ent;
+    if (const int fk = ppo2_fused_kind(d)) {  // the SOI demo's nets: one fused launch + reduces
+        FgArgs f{};
+        f.params = params; f.s = s; f.a = a; f.lp = a_logprob; f.adv = adv; f.vt = v_target;
+        f.rows = rows; f.S = S; f.A = A;
+        for (int l = 0; l <= L; ++l) f.dims[l] = d.dims[l];
+        for (int l = 0; l < L; ++l) f.off[l] = off[l];
+        f.np = np; f.inv_rows = h.inv_rows; f.eps_clip = h.eps_clip; f.ent_row = h.ent_row;
+        for (int k = 0; k < 4; ++k) {
+            f.gain[k] = h.gain[k]; f.off_[k] = pc.off[k]; f.log_std[k] = h.log_std[k]; f.inv_var[k] = h.inv_var[k];
+        }
+        f.part = ws + w.fg_part;
+        f.lpart = reinterpret_cast<double *>(ws + w.fg_lpart);
+        const int64_t nsteps = (rows + kFgRows - 1) / kFgRows;
+        const int grid = (int)(nsteps < dense_cus() ? nsteps : dense_cus());
+        using K1 = FgShape<128, 64, 32>;
+        using K2 = FgShape<64, 64, 0>;
+        const size_t lds = sizeof(float) * (fk == 1 ? K1::floats() : K2::floats());
+        const void *fn = fk == 1 ? (actor ? (const void *)fg_grad_kernel<128, 64, 32, true>
+                                          : (const void *)fg_grad_kernel<128, 64, 32, false>)
+                                 : (actor ? (const void *)fg_grad_kernel<64, 64, 0, true>
+                                          : (const void *)fg_grad_kernel<64, 64, 0, false>);
+        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return fail(RLP_EINVAL, "rlp_ppo2_dense_grad: fused kernel LDS attribute (%zu B)", lds);
+        if (fk == 1) {
+            if (actor) fg_grad_kernel<128, 64, 32, true><<<grid, 64 * kFgWaves, lds, st>>>(f);
+            else fg_grad_kernel<128, 64, 32, false><<<grid, 64 * kFgWaves, lds, st>>>(f);
+        } else {
+            if (actor) fg_grad_kernel<64, 64, 0, true><<<grid, 64 * kFgWaves, lds, st>>>(f);
+            else fg_grad_kernel<64, 64, 0, false><<<grid, 64 * kFgWaves, lds, st>>>(f);
+        }
+        chunk_sum_kernel<<<(int)((np + 255) / 256), 256, 0, st>>>(f.part, grid, np, grad);
+        if (loss_sum) loss_sum_kernel<<<1, 256, 0, st>>>(f.lpart, grid, loss_sum);
+        RLP_CHECK_LAUNCH("rlp_ppo2_dense_grad (fused)");
+        return RLP_OK;
+    }
     ppo2_consts_kernel<<<1, 256, 0, st>>>(ws + w.ones, ws + w.head, pc);
     const float *gain_d = ws + w.head, *off_d = ws + w.head + 4;
     const int64_t nchunks = (rows + kPpoChunk - 1) / kPpoChunk;

@@ -219,3 +219,50 @@ def test_native_update_data_parallel_duplicated_batch_bit_exact():
         ref = torch.cat([nl.net_a.flat, nl.net_c.flat]).cpu().numpy()
         for r in (0, 1):
             np.testing.assert_array_equal(out[r][i], ref, err_msg=f"rank {r} {rule} clip={clip}")
+
+
+# ---------------------------------------------------------------------------------------------
+# Rows exactly at a clip kink (ratio = 1 -/+ eps_clip in float64). There the clipped surrogate's
+# gradient jumps: torch.min / clamp give a row either its full term or none, and which one two
+# correct float32 evaluations pick depends on the last ulp of their ratio. The native update must
+# give one of the two (the rest of the batch unchanged), for both kinks and advantage signs.
+# ---------------------------------------------------------------------------------------------
+def _kink_candidates(actor, critic, s, a, lp64, adv, vt, msg, row):
+    """float64 actor gradients with row `row`'s old log-prob 1e-6 to either side of the exact
+    float64 kink lp64[row] (beyond the float32 errors of lp and of the ratio, ~3e-7): one candidate
+    has the row inside the clip range, the other clipped."""
+    out = []
+    for delta in (-1e-6, 1e-6):
+        lp2 = lp64.clone()
+        lp2[row, 0] += delta
+        ga, _, _, _ = torch_grads(actor, critic, s, a, lp2, adv, vt, msg, torch.float64)
+        out.append(ga)
+    return out
+
+
+@pytest.mark.parametrize("kink,adv_sign", [(+1, +1), (+1, -1), (-1, +1), (-1, -1)])
+def test_ppo2_grad_at_clip_kink(kink, adv_sign):
+    msg = dict(DEFAULT_PPO_MSG)
+    eps = msg['eps_clip']
+    actor, critic, s, a, lp, adv, vt = make_case(4, 1, 257, seed=77)
+    row = 100
+    with torch.no_grad():   # the row's old log-prob puts its float64 ratio exactly on the kink
+        a64 = copy.deepcopy(actor).double()
+        lp_now = a64.get_dist(s.double()).log_prob(a.double())
+        lp64 = lp.clone().double()
+        lp64[row, 0] = lp_now[row, 0] - np.log(1 + kink * eps)
+        lp = lp64.float()
+        adv = adv.clone()
+        adv[row, 0] = adv_sign * (abs(float(adv[row, 0])) + 0.5)
+    cands = _kink_candidates(actor, critic, s, a, lp64, adv, vt, msg, row)
+    ga32, _, _, _ = torch_grads(actor, critic, s, a, lp, adv, vt, msg, torch.float32)
+    nl = NativePPO2Learner(copy.deepcopy(actor), copy.deepcopy(critic), msg, device="cuda")
+    dev = lambda t: t.cuda().contiguous()
+    nl.grads(dev(s), dev(a), dev(lp), dev(adv), dev(vt))
+    gn = nl.net_a.grad.double().cpu()
+    errs = [float((gn - c).abs().max()) for c in cands]
+    e32 = min(float((ga32 - c).abs().max()) for c in cands)
+    floor = 2e-6 * float(max(c.abs().max() for c in cands))
+    # the candidates differ by the row's whole term where the branches disagree (upper kink with
+    # adv > 0, lower kink with adv < 0), else they agree; the native gradient is one of them
+    assert min(errs) <= 4 * e32 + floor, (errs, e32, floor)
