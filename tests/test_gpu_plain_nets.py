@@ -177,6 +177,54 @@ def test_dense_grad_vs_float64(net, kernels, rows):
         _f32_class(f"{net} {kernels} {rows} {name}", gn[i], t32[i], t64[i])
 
 
+@pytest.mark.parametrize("kink,adv_sign", [(+1, +1), (-1, -1)])
+def test_soi_grad_at_clip_kink(kink, adv_sign):
+    """A row whose float64 ratio lies exactly on a clip kink, where the two branches of torch.min /
+    clamp give the row its whole term or none (upper kink with adv > 0, lower kink with adv < 0):
+    the fused SOI-net gradient is one of the two float64 candidates (the row's old log-prob 1e-6
+    inside / outside the kink), within 4x torch float32's error of it."""
+    mk_a, mk_c, S, Ad = NETS["soi"]
+    torch.manual_seed(11)
+    actor, critic = mk_a(), mk_c()
+    with torch.no_grad():
+        nn.init.orthogonal_(actor.mean_layer.weight, gain=1.0)
+    rows, row = 777, 300
+    g = torch.Generator(device="cuda").manual_seed(5)
+    s = torch.rand(rows, S, device="cuda", generator=g) * 4 - 2
+    with torch.no_grad():
+        mean = _as(actor, torch.float32, "cuda")(s)
+    a = (mean + 0.7 * torch.randn(rows, Ad, device="cuda", generator=g)).clamp(-3, 3)
+    lp = Normal(mean, 1.0).log_prob(a) + 0.3 * torch.randn(rows, Ad, device="cuda", generator=g)
+    adv = torch.randn(rows, 1, device="cuda", generator=g)
+    vt = torch.randn(rows, 1, device="cuda", generator=g)
+    lp = _off_kinks(actor, s, a, lp)
+    with torch.no_grad():
+        d = _as(actor, torch.float64, "cuda").get_dist(s.double())
+        lp_now = d.log_prob(a.double()).sum(1)
+        lp64 = lp.double().clone()
+        # the row's summed old log-prob on the kink: shift its first component
+        lp64[row, 0] += (lp_now[row] - np.log(1 + kink * 0.2)) - lp64[row].sum()
+        adv[row, 0] = adv_sign * (abs(float(adv[row, 0])) + 0.5)
+    lp = lp64.float()
+    a64, c64 = _as(actor, torch.float64, "cuda"), _as(critic, torch.float64, "cuda")
+    cands = []
+    for delta in (-1e-6, 1e-6):
+        l2 = lp64.clone()
+        l2[row, 0] += delta
+        cands.append(_loss_grads(a64, c64, s.double(), a.double(), l2, adv.double(), vt.double())[0])
+    t32 = _loss_grads(_as(actor, torch.float32, "cuda"), _as(critic, torch.float32, "cuda"),
+                      s, a, lp, adv, vt)[0]
+    lrn = NativePPO2Learner(_as(actor, torch.float32, "cuda"), _as(critic, torch.float32, "cuda"),
+                            dict(DEFAULT_PPO_MSG), device="cuda")
+    lrn.grads(s, a, lp, adv, vt)
+    gn = lrn.net_a.grad.double().cpu().numpy()
+    errs = [np.abs(gn - c).max() for c in cands]
+    e32 = min(np.abs(t32 - c).max() for c in cands)
+    floor = 2e-6 * max(np.abs(c).max() for c in cands)
+    assert np.abs(cands[0] - cands[1]).max() > 10 * floor   # the branches do differ here
+    assert min(errs) <= 4 * e32 + floor, (errs, e32, floor)
+
+
 def test_dense_learner_matches_reference_soi_learn(golden):
     """The PPO2-SOI demo's nets: NativePPO2Learner (dense path) from the reference's
     before-weights on its buffer (normalised advantages and v_target as learn() computed them):
