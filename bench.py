@@ -454,7 +454,8 @@ DEMO_E2E = {
 def demo_nets_e2e_leg(rank, which, iters=2, seed=19):
     """Whole PPO2 iterations (VecPPO2) for the PPO2 drivers whose nets the fused f16x3 kernels do
     not take: the rollout through rlp_rollout's plain-layout path (SOI) or its per-step lidar path
-    (UGV-OA), the K-epoch update through rlp_ppo2_dense_grad (exact f32 MFMA GEMMs) + Adam."""
+    (UGV-OA), the K-epoch update through rlp_ppo2_dense_grad (exact f32 MFMA: the fused per-row
+    kernel for the SOI nets) or, for the 41-input nets, rlp_ppo2_grad (f16x3) + Adam."""
     from reinforcementlearningplatform_amd.algorithm.policy_base.vec_ppo2 import VecPPO2
     c = DEMO_E2E[which]
     n, T = c["n"], c["T"]
@@ -505,7 +506,8 @@ def demo_nets_e2e_leg(rank, which, iters=2, seed=19):
     lr = vec.learner
     update_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
     nets = [getattr(lr, k, None) for k in ("net_a", "net_c")]
-    kinds = ["rlp_ppo2_dense_grad (exact f32 MFMA GEMMs)" if m.dense else "rlp_ppo2_grad (f16x3 FD + wgrad)"
+    kinds = [("rlp_ppo2_dense_grad (exact f32 MFMA, fused per-row kernel)" if m.fused else
+              "rlp_ppo2_dense_grad (exact f32 MFMA GEMMs)") if m.dense else "rlp_ppo2_grad (f16x3 FD + wgrad)"
              for m in nets if m is not None]
     out = {"value": n * T * iters / dt, "unit": "env-steps/s", "s_per_iteration": dt / iters,
            "rollout_ms": float(np.mean([e[0].elapsed_time(e[1]) for e in evs])),

@@ -108,6 +108,9 @@ class _Net:
         self.dense = _update_kind(module, is_actor, kernels) == "dense"
         # the 41-input nets' f16x3 path takes contiguous rows (mini-batches gathered first)
         self.ext = not self.dense and dims[0] > 8
+        # rlp_ppo2_dense_grad's fused per-row kernel takes the SOI demo's nets (rlp_dense.hip,
+        # ppo2_fused_kind); other dense nets go through its chunked GEMMs
+        self.fused = self.dense and dims[0] <= 8 and dims[-1] <= 4 and list(dims[1:-1]) in ([128, 64, 32], [64, 64])
         acts = [_abi.RLP_ACT_TANH] * (len(lin) - 1) + [
             _abi.RLP_ACT_TANH if is_actor else _abi.RLP_ACT_NONE]
         self.desc = _abi.MLPDesc.make(dims, acts)

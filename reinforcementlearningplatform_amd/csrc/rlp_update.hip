@@ -796,8 +796,11 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
     }
     float svn[SV];
     load_s(tile + gridDim.x, svn);
-    floatx4 gv[JT][2];
-    load_g2(tile, 0, gv);
+    // the g2 A operands of K steps 0 and 1, each loaded a whole tile ahead (two steps): one step of
+    // prefetch left 32 KiB in flight per CU, short of what hides an HBM miss under this load
+    floatx4 gv0[JT][2], gv1[JT][2];
+    load_g2(tile, 0, gv0);
+    load_g2(tile, 1, gv1);
     lds_barrier();
     for (int i = 0; tile < ntiles; tile += gridDim.x, ++i) {
         const int cur = i & 1, nxt = cur ^ 1;
@@ -811,6 +814,7 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
         for (int ks = 0; ks < 2; ++ks) {
             // A operands scaled by 2^sg and split
             half8 ah[JT], al[JT];
+            floatx4 (&gv)[JT][2] = ks == 0 ? gv0 : gv1;
 #pragma unroll
             for (int jt = 0; jt < JT; ++jt) {
                 float x[8];
@@ -821,10 +825,8 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
                 }
                 split8(x, ah[jt], al[jt]);
             }
-            // the next K step's g2 (this tile's second, or the next tile's first), in flight
-            // under this step's MFMAs
-            if (ks == 0) load_g2(tile, 1, gv);
-            else load_g2(tile + gridDim.x, 0, gv);
+            // the next tile's g2 of this K step, in flight under two steps of MFMAs
+            load_g2(tile + gridDim.x, ks, gv);
 #pragma unroll
             for (int nt = 0; nt < 16; ++nt) {
                 const int F = ks * 16 + nt;

@@ -30,6 +30,8 @@ for line in open(sys.argv[2]):
         if "e2e" in d:
             o["e2e"] = round(d["e2e"]["s_per_iteration"], 4)
             if "k30" in d["e2e"]: o["e2e_k30"] = round(d["e2e"]["k30"]["s_per_iteration"], 4)
+        for k in ("soi_ppo2_e2e", "ugvoa_ppo2_e2e"):
+            if k in d and "s_per_iteration" in d[k]: o[k] = round(d[k]["s_per_iteration"], 4)
         if "uav_ppo2_rollout" in d: o["uav_ms"] = round(d["uav_ppo2_rollout"]["roofline"]["avg_launch_ms"], 4)
         print("   ", json.dumps(o))
 PY

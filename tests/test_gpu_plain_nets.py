@@ -162,6 +162,7 @@ def test_dense_grad_vs_float64(net, kernels, rows):
     f16x3 = net == "lidar" and kernels == "auto"
     assert lrn.net_a.dense != f16x3 and lrn.net_c.dense != f16x3
     assert lrn.net_a.ext == f16x3 and lrn.net_c.ext == f16x3
+    assert lrn.net_a.fused == (net == "soi") and lrn.net_c.fused == (net == "soi")  # fg_grad_kernel
     lrn.grads(s, a, lp, adv, vt)
     gn = [lrn.net_a.grad.double().cpu().numpy(), lrn.net_c.grad.double().cpu().numpy()]
     g2 = [lrn.net_a.grad.clone(), lrn.net_c.grad.clone()]
