@@ -58,10 +58,12 @@ __device__ __forceinline__ void split2(float2v x, half2v &hi, half2v &lo) {
 __device__ __forceinline__ void split2_mix(float2v x, half2v &hi, half2v &lo) {
     hi = __builtin_convertvector(x, half2v);
     const unsigned h = __builtin_bit_cast(unsigned, hi);
-    unsigned l = 0;
+    // both halves of l are written, so its prior value is not an input (an early-clobber output:
+    // a "+v" operand initialised to 0 cost one v_mov per pair, 32 per 16-row GEMM operand build)
+    unsigned l;
     asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
         "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-        : "+v"(l) : "v"(h), "v"(x.x), "v"(x.y));
+        : "=&v"(l) : "v"(h), "v"(x.x), "v"(x.y));
     lo = __builtin_bit_cast(half2v, l);
 }
 

@@ -88,12 +88,13 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
     lds_barrier();  // every wave is done with the ring
 #pragma unroll
     for (int q = 0; q < RG - 1; ++q) issue(q);
-    half8 bh, bl;
+    // the B operands of phase P in buffer P & 1 (the loop is unrolled: no copies between phases)
+    half8 bbh[2], bbl[2];
     pre(0);
-    bop(0, bh, bl);
+    bop(0, bbh[0], bbl[0]);
 #pragma unroll
     for (int P = 0; P < 8; ++P) {
-        half8 nbh, nbl;
+        const half8 &bh = bbh[P & 1], &bl = bbl[P & 1];
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             const int c = 2 * P + hf;
@@ -112,7 +113,7 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
             }
             const float *slot = ring + (((c / CPB) % RG) * CPB + c % CPB) * kX3ChunkFloats + lane * 4;
             if (hf == 0 && P + 1 < 8) pre(P + 1);
-            if (hf == 1 && P + 1 < 8) bop(P + 1, nbh, nbl);
+            if (hf == 1 && P + 1 < 8) bop(P + 1, bbh[(P + 1) & 1], bbl[(P + 1) & 1]);
             // the chunk's 8 output tiles in four pairs, each pair's 4 fragments read while the
             // previous pair's 6 MFMAs run (two register buffers: the same 32 fragment registers;
             // pinned with sched_group_barrier). Same-box rocprof A/B (profiles/r3/r3s_fd_ab.txt):
@@ -152,10 +153,6 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
                     __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
                 }
             }
-        }
-        if (P + 1 < 8) {
-            bh = nbh;
-            bl = nbl;
         }
     }
 }
@@ -227,8 +224,11 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
     constexpr int H = kUpdH, SMALL = EXT ? 2 * H + A * H + 8 : mlp_small_floats<H, KS1, A>();
     constexpr int NC = 4 * KS + 1;  // dW1 columns per neuron: s features | bias
     constexpr int kFdRegion = kFdRing * kX3ChunkFloats;
-    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + (EXT ? 4 : kFdWaves * 16 * 8)];
+    __shared__ __attribute__((aligned(16))) float lds[kFdRegion + SMALL + (EXT ? 4 : kFdWaves * 16 * 8 + 4 * H)];
     float *ring = lds, *small = lds + kFdRegion;
+    // b1 x 2/ln 2 four times per neuron: the g1 recompute's swapped layer-1 tiles take their C
+    // operand {b1, b1, b1, b1} with one read (a broadcast from registers cost 4 v_mov per tile)
+    float *const b1q = lds + kFdRegion + SMALL + kFdWaves * 16 * 8;
     // the wave index as a scalar (readfirstlane): every wave-derived offset, the G2 tile and its
     // store guard become SGPR values (no per-lane 64-bit address arithmetic, no exec-masked stores)
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -239,6 +239,8 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
     {
         const gptr<float> src = as_global(g.packed) + net.off_small_r + (sb - net.off_w1);
         for (int i = threadIdx.x; i < net.small_count - (sb - net.off_w1); i += blockDim.x) small[i] = src[i];
+        if constexpr (!EXT)
+            for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) b1q[i] = src[(net.off_b1 - sb) + i / 4];
     }
     __syncthreads();
 
@@ -275,12 +277,10 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
     // layer 1 of neuron tile t "neuron on lane": C[row 4 gq + q][neuron 16 t + e] (operands swapped)
     auto layer1_t = [&](int t, const float (&bo)[KS]) {
         const float *W1c = small + 0;
-        const float *B1c = small + (net.off_b1 - sb);
         float w1[KS];
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) w1[kk] = W1c[w1r_index(16 * t + e, 4 * kk + gq, KS)];
-        const float b1 = B1c[16 * t + e];
-        floatx4 c = {b1, b1, b1, b1};
+        floatx4 c = *reinterpret_cast<const floatx4 *>(b1q + 4 * (16 * t + e));
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk)
             c = __builtin_amdgcn_mfma_f32_16x16x4f32(bo[kk], w1[kk], c, 0, 0, 0);
