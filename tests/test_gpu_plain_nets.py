@@ -137,7 +137,7 @@ NETS = {"soi": (lambda: SoiActor(), lambda: SoiCritic(), 4, 2),
                   lambda: SoiCritic(S=41, widths=(256, 256)), 41, 2)}
 
 
-@pytest.mark.parametrize("rows", [1000, 300_000])
+@pytest.mark.parametrize("rows", [1, 33, 1000, 300_000])
 @pytest.mark.parametrize("net,kernels", [("lidar", "auto"), ("lidar", "dense"), ("soi", "auto")])
 def test_dense_grad_vs_float64(net, kernels, rows):
     """rlp_ppo2_dense_grad (kernels 'dense', and the SOI nets' 'auto') and, for the lidar nets'
