@@ -210,7 +210,8 @@ constexpr int kDppRowMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kD
 // the second half of each block's waves at s_setprio 1.
 constexpr int kFdWaves = 8;
 constexpr int kFdRows = 16 * kFdWaves;
-constexpr int kFdRing = 3;  // W2 chunk-ring slots (one group in flight while one is read)
+constexpr int kFdRing = 4;  // W2 chunk-ring slots (two chunks in flight while one is read; 3: the
+                            // lidar nets' FD 2 % slower, the CartPole nets' the same, r5o_fd_ring_ab.txt)
 
 // KS1 = 0 ("EXT", the lidar demos' 41-input nets): layer 1 lives outside the kernel — h1 =
 // tanh(W1 s + b1) comes from g.h1 (one exact-f32 GEMM per step, rlp_dense.hip), g1 = dL/dz1 goes to
