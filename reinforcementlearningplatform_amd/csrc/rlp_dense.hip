@@ -2350,6 +2350,29 @@ inline PpoDenseWs ppo2_dense_ws(const rlp_mlp_desc &d, int64_t rows) {
     return w;
 }
 
+// tanh for the EXT layer 1 (l1_fwd_kernel: 0.56 -> 0.50 ms per 2^20 rows; in fg_grad_kernel,
+// which LDS bounds, it measured 1-2 % slower, so that kernel keeps tanhf; r5q_tanh_ab.txt):
+// ocml's tanhf shape (an odd polynomial near 0, 1 - 2 / (exp(2|x|) + 1) above) with the
+// polynomial carried to |x| < 0.8 and the exponential on v_exp_f32 directly (ocml rebuilds exp
+// from a split argument and ldexp: 27 VALU against 17). The polynomial x + x^3 P(x^2)
+// (coefficients fitted for relative error) is within 0.8 ulp of tanh in f32 Horner form; above
+// 0.8 the result is >= 0.66, so 1 - 2r has no cancellation: <= 2.3 ulp with 1-ulp v_exp_f32 /
+// v_rcp_f32 (ocml tanhf: <= 2 ulp).
+__device__ __forceinline__ float tanh_x3(float x) {
+    const float ax = fabsf(x), t = x * x;
+    float p = -0.0005696456741425663f;
+    p = __builtin_fmaf(p, t, 0.002847711636260569f);
+    p = __builtin_fmaf(p, t, -0.008504900349316143f);
+    p = __builtin_fmaf(p, t, 0.021770580912164706f);
+    p = __builtin_fmaf(p, t, -0.05395333174766384f);
+    p = __builtin_fmaf(p, t, 0.13333225206779578f);
+    p = __builtin_fmaf(p, t, -0.3333333065982628f);
+    const float sm = __builtin_fmaf(ax * t, p, ax);
+    const float ex = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);  // exp(2 |x|)
+    const float bg = __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(ex + 1.f), 1.f);
+    return __builtin_copysignf(ax < 0.8f ? sm : bg, x);
+}
+
 // ---- fused per-row gradient for the PPO2-SOI demo's small nets ---------------------------------
 // actor 4 -> 128 -> 64 -> 32 -> 2 / critic 4 -> 64 -> 64 -> 1 (demonstration/PPO2/
 // PPO2-4-SecondOrderIntegration/train.py:37-125): per 32-row step ONE block runs the forward, the
@@ -2677,7 +2700,7 @@ __global__ void __launch_bounds__(256) l1_fwd_kernel(const float *__restrict__ s
             for (int nt = 0; nt < 16; ++nt) {
                 floatx4 v;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = tanhf(acc[nt][q]);
+                for (int q = 0; q < 4; ++q) v[q] = tanh_x3(acc[nt][q]);
                 *reinterpret_cast<floatx4 *>(dst + 16 * nt) = v;
             }
         }
