@@ -2475,11 +2475,20 @@ __global__ void __launch_bounds__(64 * kFgWaves, 1) fg_grad_kernel(FgArgs g) {
     const int S = g.S, A = g.A, ks0 = (S + 3) / 4;
     const int64_t nsteps = (g.rows + kFgRows - 1) / kFgRows;
     // one 16 x 16 output tile: acc over K / 4 MFMA steps, a(k) / b(k) the lane's operands
+    // (the 4-layer actor: two accumulation chains, even and odd K steps, added at the end — one
+    // chain waits out the f32 MFMA's dependent-accumulator latency at every step: -2.5 %; the
+    // 3-layer critic measured 1.5 % slower with them, r5r_fg_chains_ab.txt)
     auto mm = [&](floatx4 c, int K, auto &&av, auto &&bv) {
+        floatx4 c1 = {0.f, 0.f, 0.f, 0.f};
+        int k0 = 0;
 #pragma unroll 2
-        for (int k0 = 0; k0 < K; k0 += 4)
+        for (; H3 > 0 && k0 + 8 <= K; k0 += 8) {
             c = __builtin_amdgcn_mfma_f32_16x16x4f32(av(k0 + gq), bv(k0 + gq), c, 0, 0, 0);
-        return c;
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av(k0 + 4 + gq), bv(k0 + 4 + gq), c1, 0, 0, 0);
+        }
+#pragma unroll 2
+        for (; k0 < K; k0 += 4) c = __builtin_amdgcn_mfma_f32_16x16x4f32(av(k0 + gq), bv(k0 + gq), c, 0, 0, 0);
+        return H3 > 0 ? c + c1 : c;
     };
     for (int64_t step = blockIdx.x; step < nsteps; step += gridDim.x) {
         const int64_t r0 = step * kFgRows;
