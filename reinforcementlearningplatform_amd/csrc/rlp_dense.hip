@@ -2471,6 +2471,21 @@ __global__ void __launch_bounds__(64 * kFgWaves, 1) fg_grad_kernel(FgArgs g) {
     floatx4 acc[F::per_wave()];
 #pragma unroll
     for (int j = 0; j < F::per_wave(); ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // layer 2's weight operands stay in registers for the whole launch (they are a fixed tile per
+    // wave: the forward's output tile 16 (wv / 2) and the data pass's input tiles 16 (wv / 2 + 4 i)),
+    // a third of the LDS operand reads gone: W2 [H2][H1] row-major in params
+    constexpr int NW2 = H1 / 64;   // data-pass tiles of layer 2 per wave
+    float w2f[H1 / 4], w2d[NW2][H2 / 4];
+    {
+        const float *W2 = g.params + g.off[1];
+        const int m2 = wv >> 1;
+#pragma unroll
+        for (int k4 = 0; k4 < H1 / 4; ++k4) w2f[k4] = W2[(16 * m2 + e) * H1 + 4 * k4 + gq];
+#pragma unroll
+        for (int i = 0; i < NW2; ++i)
+#pragma unroll
+            for (int k4 = 0; k4 < H2 / 4; ++k4) w2d[i][k4] = W2[(4 * k4 + gq) * H1 + 16 * (m2 + 4 * i) + e];
+    }
     double lsum = 0.0;
     const int S = g.S, A = g.A, ks0 = (S + 3) / 4;
     const int64_t nsteps = (g.rows + kFgRows - 1) / kFgRows;
@@ -2529,8 +2544,18 @@ __global__ void __launch_bounds__(64 * kFgWaves, 1) fg_grad_kernel(FgArgs g) {
                 const int mt = tau >> 1, rt = tau & 1;
                 floatx4 c = {bl[16 * mt + 4 * gq], bl[16 * mt + 4 * gq + 1], bl[16 * mt + 4 * gq + 2],
                              bl[16 * mt + 4 * gq + 3]};
-                c = mm(c, K, [&](int k) { return Wl[(16 * mt + e) * lwp + k]; },
-                       [&](int k) { return Hp[(16 * rt + e) * lhp + k]; });
+                if (l == 2) {  // one tile per wave (tau = wv), A operands from w2f
+                    floatx4 c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int k4 = 0; k4 < H1 / 4; k4 += 2) {
+                        c = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[k4], Hp[(16 * rt + e) * lhp + 4 * k4 + gq], c, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[k4 + 1], Hp[(16 * rt + e) * lhp + 4 * k4 + 4 + gq], c1, 0, 0, 0);
+                    }
+                    c = c + c1;
+                } else {
+                    c = mm(c, K, [&](int k) { return Wl[(16 * mt + e) * lwp + k]; },
+                           [&](int k) { return Hp[(16 * rt + e) * lhp + k]; });
+                }
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const float v = c[q];
@@ -2601,8 +2626,22 @@ __global__ void __launch_bounds__(64 * kFgWaves, 1) fg_grad_kernel(FgArgs g) {
                 for (int tau = wv; tau < (kFgRows / 16) * (N / 16); tau += kFgWaves) {
                     const int rt = tau % (kFgRows / 16), nt = tau / (kFgRows / 16);
                     floatx4 c = {0.f, 0.f, 0.f, 0.f};
-                    c = mm(c, M, [&](int k) { return dZ[(16 * rt + e) * ldz + k]; },
-                           [&](int k) { return Wl[k * lw + 16 * nt + e]; });
+                    if (l == 2) {  // tau = wv + 8 i, B operands from w2d[i]
+#pragma unroll
+                        for (int i = 0; i < NW2; ++i) {
+                            if (tau != wv + kFgWaves * i) continue;
+                            floatx4 c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                            for (int k4 = 0; k4 < H2 / 4; k4 += 2) {
+                                c = __builtin_amdgcn_mfma_f32_16x16x4f32(dZ[(16 * rt + e) * ldz + 4 * k4 + gq], w2d[i][k4], c, 0, 0, 0);
+                                c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(dZ[(16 * rt + e) * ldz + 4 * k4 + 4 + gq], w2d[i][k4 + 1], c1, 0, 0, 0);
+                            }
+                            c = c + c1;
+                        }
+                    } else {
+                        c = mm(c, M, [&](int k) { return dZ[(16 * rt + e) * ldz + k]; },
+                               [&](int k) { return Wl[k * lw + 16 * nt + e]; });
+                    }
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const int r = 16 * rt + 4 * gq + q, n = 16 * nt + e;
