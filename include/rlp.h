@@ -455,11 +455,14 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
  * `params` is the plain layout (rlp_mlp_param_count floats, torch order); rows are contiguous (a
  * mini-batch is gathered by the caller). Exact f32 MFMA products (v_mfma_f32_16x16x4_f32),
  * activations and the weight gradients' partials in `workspace`
- * (rlp_ppo2_dense_workspace_floats), fixed summation order (run-to-run identical). Three- and
- * four-layer nets with <= 64 inputs and hidden widths 32k <= 256 (the demos' shapes) run each
- * 2^18-row chunk as five launches (forward chain, loss head, backward chain, every layer's weight
- * gradient, one reduce); other stacks one GEMM launch per layer and pass. The loss is summed from
- * per-block partials in a fixed order too (gradient and loss_sum run-to-run identical). */
+ * (rlp_ppo2_dense_workspace_floats), fixed summation order (run-to-run identical). The SOI demo's
+ * two shapes (<= 8 inputs; hidden 128-64-32 or 64-64; <= 4 outputs) run as ONE fused per-row launch
+ * (forward, loss head, backward, weight-gradient partials with every activation in LDS) and two
+ * fixed-order sums; other three- and four-layer nets with <= 64 inputs and hidden widths
+ * 32k <= 256 run each 2^18-row chunk as five launches (forward chain, loss head, backward chain,
+ * every layer's weight gradient, one reduce); other stacks one GEMM launch per layer and pass. The
+ * loss is summed from per-block partials in a fixed order too (gradient and loss_sum run-to-run
+ * identical). */
 int64_t rlp_ppo2_dense_workspace_floats(const rlp_mlp_desc *desc, int64_t rows);
 int rlp_ppo2_dense_grad(const rlp_mlp_desc *desc, const float *params, const rlp_ppo2_loss_cfg *cfg,
                         const float *s, const float *a, const float *a_logprob, const float *adv,
