@@ -846,10 +846,14 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
                     acc2[jt][nt] = v;
                 }
                 __builtin_amdgcn_sched_group_barrier(0x008, 3 * JT, 0);
-                // the next tile's fragments, spread over this tile's MFMAs (FPW per wave)
-                if (F % (32 / FPW) == (32 / FPW) - 1) {
+                // the next tile's fragments, spread over this tile's MFMAs (FPW per wave); for the
+                // recomputed h1 the two waves of a SIMD (w, w + 4) build half a spacing apart, so one's
+                // build issues under the other's MFMAs (-2.5 %; the EXT loads +3 %, kept in step:
+                // r5y_wgrad_stagger_ab.txt; the builds grouped 2 or 4 per point: no gain, r5x)
+                constexpr int SP = 32 / FPW;
+                if (F % SP == (!EXT && wv >= 4 ? SP / 2 - 1 : SP - 1)) {
                     __builtin_amdgcn_sched_barrier(0);  // (the build stays a region of its own)
-                    const int u = F / (32 / FPW);
+                    const int u = F / SP;
                     if constexpr (EXT) {
                         build_frag_ext(nxt, FPW * wv + u, hvn);
                         if (u + 1 < FPW) load_hv(tile + gridDim.x, FPW * wv + u + 1, hvn);
