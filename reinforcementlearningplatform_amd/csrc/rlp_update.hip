@@ -662,7 +662,8 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
     // fragments into hfrag[(i + 1) & 1] from srow[(i + 1) & 1]
     __shared__ float srow[2][EXT ? 1 : kUpdRows][SP];
     __shared__ float w1s[EXT ? 1 : H][SP + 1];
-    __shared__ float b1s[EXT ? 1 : H];
+    // b1 four times per neuron: the swapped layer-1 tiles' C operand {b1, b1, b1, b1} in one read
+    __shared__ __attribute__((aligned(16))) float b1s[EXT ? 4 : 4 * H];
     __shared__ __attribute__((aligned(16))) _Float16 hfrag[2][FRAG];
     const MfmaNet &net = w.net;
     const int S = net.S;
@@ -674,7 +675,7 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
         const float *B1c = w.packed + net.off_small_r + (net.off_b1 - net.off_w1);
         for (int i = threadIdx.x; i < H * SP; i += blockDim.x)
             w1s[i / SP][i % SP] = W1c[w1r_index(i / SP, i % SP, KS1)];
-        for (int i = threadIdx.x; i < H; i += blockDim.x) b1s[i] = B1c[i];
+        for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) b1s[i] = B1c[i / 4];
     }
     // g2 scale: max|g2| * 2^sg in [2^13, 2^14)
     const float gm = __uint_as_float(*w.g2max);
@@ -719,8 +720,7 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
         float x[8];
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
-            const float b1 = b1s[16 * nt + e];
-            floatx4 c = {b1, b1, b1, b1};
+            floatx4 c = *reinterpret_cast<const floatx4 *>(&b1s[4 * (16 * nt + e)]);
 #pragma unroll
             for (int kk = 0; kk < KS1; ++kk)
                 c = __builtin_amdgcn_mfma_f32_16x16x4f32(srow[buf][32 * ks + 16 * hh + e][4 * kk + gq],
