@@ -2475,6 +2475,8 @@ __global__ void __launch_bounds__(64 * kFgWaves, 1) fg_grad_kernel(FgArgs g) {
     // wave: the forward's output tile 16 (wv / 2) and the data pass's input tiles 16 (wv / 2 + 4 i)),
     // a third of the LDS operand reads gone: W2 [H2][H1] row-major in params
     constexpr int NW2 = H1 / 64;   // data-pass tiles of layer 2 per wave
+    static_assert(H2 / 16 * (kFgRows / 16) == kFgWaves && (kFgRows / 16) * (H1 / 16) == kFgWaves * NW2,
+                  "layer 2: one forward tile and NW2 data-pass tiles per wave (tau = wv + 8 i)");
     float w2f[H1 / 4], w2d[NW2][H2 / 4];
     {
         const float *W2 = g.params + g.off[1];

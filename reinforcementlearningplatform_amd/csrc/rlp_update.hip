@@ -851,6 +851,7 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
                 // build issues under the other's MFMAs (-2.5 %; the EXT loads +3 %, kept in step:
                 // r5y_wgrad_stagger_ab.txt; the builds grouped 2 or 4 per point: no gain, r5x)
                 constexpr int SP = 32 / FPW;
+                static_assert(kWgWaves == 8, "the stagger pairs waves w and w + 4 (one SIMD)");
                 if (F % SP == (!EXT && wv >= 4 ? SP / 2 - 1 : SP - 1)) {
                     __builtin_amdgcn_sched_barrier(0);  // (the build stays a region of its own)
                     const int u = F / SP;
