@@ -7,7 +7,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); TAG=${TAG:-lab}; OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 export TMPDIR=/tmp
-BASE="--no-cpu-baseline --ddpg 0 --sac 0 --oa 0 --fp32-leg 0 --hbm 0 --uav 0 --e2e 0 --e2e-k30 0 --demo-e2e 0"
+BASE="--no-cpu-baseline --ddpg 0 --sac 0 --oa ${OA:-0} --fp32-leg 0 --hbm 0 --uav 0 --e2e 0 --e2e-k30 0 --demo-e2e 0"
 i=0
 for rep in $(seq 1 ${REPS:-1}); do
 for lib in ${LIBS:--}; do
@@ -32,6 +32,7 @@ for line in open(sys.argv[2]):
             if "k30" in d["e2e"]: o["e2e_k30"] = round(d["e2e"]["k30"]["s_per_iteration"], 4)
         for k in ("soi_ppo2_e2e", "ugvoa_ppo2_e2e"):
             if k in d and "s_per_iteration" in d[k]: o[k] = round(d[k]["s_per_iteration"], 4)
+        if "ugvoa_ppo2_rollout" in d: o["ugvoa_rollout"] = "%.4g" % d["ugvoa_ppo2_rollout"]["value"]
         if "uav_ppo2_rollout" in d: o["uav_ms"] = round(d["uav_ppo2_rollout"]["roofline"]["avg_launch_ms"], 4)
         print("   ", json.dumps(o))
 PY
