@@ -46,6 +46,7 @@ def _self_launch(argv):
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
     rc = 0
     live = list(procs)
+    failed_at = None
     while live:
         for p in list(live):
             code = p.poll()
@@ -53,9 +54,13 @@ def _self_launch(argv):
                 continue
             live.remove(p)
             if code != 0 and rc == 0:
-                rc = code
-                for q in live:   # one rank failed: the others would wait in a collective forever
-                    q.terminate()
+                rc, failed_at = code, time.monotonic()
+        # one rank failed: the others may be waiting in a collective forever. They get a grace
+        # period to fail (or finish) on their own first, so each reports its own error.
+        if failed_at is not None and time.monotonic() - failed_at > 30.0:
+            for q in live:
+                q.terminate()
+            failed_at = float("inf")
         time.sleep(0.2)
     return rc
 

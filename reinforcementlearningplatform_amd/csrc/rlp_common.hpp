@@ -26,6 +26,20 @@ int fail(int code, const char *fmt, ...);
 
 inline hipStream_t as_stream(rlp_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// CUs of the current device, read once per process (device properties are slow; a magic static,
+// so the first calls from several host threads initialise it once). Grid sizes and the workspace
+// sizes derived from them all read this one value, so they always agree. 256 (MI355X) if the
+// query fails.
+inline int device_cus() {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        return (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+                   ? n : 256;
+    }();
+    return cus;
+}
+
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 

@@ -2305,16 +2305,7 @@ inline int ppo2_fused_kind(const rlp_mlp_desc &d) {
     if (L == 3 && d.dims[1] == 64 && d.dims[2] == 64) return 2;
     return 0;
 }
-inline int dense_cus() {  // CUs of the device (cached)
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0, n = 0;
-        cus = (hipGetDevice(&dev) == hipSuccess &&
-               hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-                  ? n : 256;
-    }
-    return cus;
-}
+inline int dense_cus() { return device_cus(); }  // the fused kernel's workspace and grid
 inline PpoDenseWs ppo2_dense_ws(const rlp_mlp_desc &d, int64_t rows) {
     const int64_t B = rows < kPpoChunk ? rows : kPpoChunk;
     int64_t hid = 0, maxw = 0, np = 0, maxpart = 0, sumpart = 0;

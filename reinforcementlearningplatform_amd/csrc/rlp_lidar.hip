@@ -136,22 +136,14 @@ __global__ void __launch_bounds__(kOaThreads) oa_kernel(OA::P p, double *state, 
     }
 }
 
-static int g_oa_cus = 0;
-
 template <bool STEP>
 static int launch_oa(const OA::P &p, double *state, int n, const float *action, float *obs_cur,
                      float *obs_next, double *reward, int32_t *flag, uint8_t *done, hipStream_t st,
                      const uint8_t *keep = nullptr, const float *prev = nullptr) {
     if (p.n_obs < 0 || p.n_obs > OA::NOBS)
         return fail(RLP_EINVAL, "UGVForwardObstacleAvoidance: n_obs=%d (0..%d)", p.n_obs, OA::NOBS);
-    if (!g_oa_cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&g_oa_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            g_oa_cus = 256;
-    }
     // fewer envs per block when the batch is small, so every CU gets several blocks
-    if ((n + 63) / 64 >= 4 * g_oa_cus)
+    if ((n + 63) / 64 >= 4 * device_cus())
         oa_kernel<64, STEP><<<(n + 63) / 64, kOaThreads, 0, st>>>(p, state, n, action, obs_cur,
                                                                  obs_next, reward, flag, done, keep,
                                                                  prev);

@@ -517,18 +517,6 @@ packed_forward_kernel(const float *__restrict__ P, MfmaNet net, const float *__r
     }
 }
 
-static int device_cus() {  // CUs of the current device (cached: device properties are slow)
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            cus <= 0)
-            cus = 256;
-    }
-    return cus;
-}
-
 template <int MODE, int SUB>
 static int launch_packed_forward_sub(const MfmaNet &net, const float *P, const float *x, float *y,
                                      int64_t rows, const uint8_t *done, const uint8_t *success,
@@ -618,14 +606,7 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
     if (an.H != 256 || cn.H != 256)
         return fail(RLP_EUNSUPPORTED, "rlp_rollout: hidden width %d/%d (built for 256)", an.H, cn.H);
     if (prec == RLP_MLP_F16X3) {
-        static int cus = 0;
-        if (cus == 0) {
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                    hipSuccess || cus <= 0)
-                cus = 256;
-        }
+        const int cus = device_cus();
         // auto: one 8-wave block of 32-env waves per CU where the envs fill every CU; else one
         // 4-wave block of 32-env waves per CU (mode 5: 1 wave per SIMD with the VGPR + AGPR
         // budget). The UAV's physics spills at 256 registers (584 B per lane at 2 waves per SIMD,

@@ -1000,18 +1000,7 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
     }
 }
 
-static int ppo2_grid() {  // CUs of the device (cached: device properties are slow)
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-            cus = n;
-        else
-            cus = 256;
-    }
-    return cus;
-}
+static int ppo2_grid() { return device_cus(); }  // wgrad / FD: one block per CU
 
 // the 41-input nets' layer 1 on the dense GEMM (rlp_dense.hip): h1 = tanh(s W1^T + b1) and
 // dW1 | db1 = G1^T [s | 1] (fixed-order partials + reduce into gW / gb)
