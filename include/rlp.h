@@ -37,7 +37,7 @@ typedef void *rlp_stream_t; /* hipStream_t */
 #define RLP_OK 0
 #define RLP_EINVAL (-1000)
 #define RLP_EUNSUPPORTED (-1001)
-#define RLP_ENOMEM (-1002)  /* a stream-ordered scratch allocation failed */
+#define RLP_ENOMEM (-1002)  /* unused since ABI version 2 (no library allocations); kept reserved */
 
 #define RLP_ABI_VERSION 2  /* 2: caller-owned rollout / mlp_forward workspaces (round 5) */
 
@@ -608,7 +608,11 @@ int rlp_abi_version(void);
  * 11 ugv_oa, 12 dense_net, 13 ddpg_nets, 14 ddpg_cfg, 15 sac_nets, 16 sac_cfg): FFI bindings
  * verify their mirrors with it. */
 int64_t rlp_struct_size(int which);
-/* Tuning knob of rlp_rollout: 16-env sub-blocks per wave: 0 = auto (default; the f16x3 path
+/* The rlp_set_* knobs below are process-wide defaults (plain globals, not synchronised): set them
+ * before any thread launches work. Concurrent callers choose per call instead, through
+ * rlp_rollout_cfg's mlp_precision / physics / sub fields.
+ *
+ * Tuning knob of rlp_rollout: 16-env sub-blocks per wave: 0 = auto (default; the f16x3 path
  * takes 1 when 2 would leave fewer than two blocks per CU, e.g. 32 768 UAV envs), 1 (f16x3 only),
  * 2 or 4. */
 int rlp_set_rollout_sub(int sub);
