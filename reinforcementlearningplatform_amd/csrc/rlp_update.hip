@@ -129,6 +129,11 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
                     }
                 };
                 rd(0, 0);
+                // a group of its own for rd(0): without it the first pinned read group took rd(0)'s
+                // reads and every group was read, waited on and multiplied in turn (the ISA's
+                // ds_read -> first-use MFMA distance: 40 of ~130 groups pipelined -> 84; FD
+                // -0.5 to -1.4 %, same box, two repetitions: profiles/r5/r5ab1_fd_sgb_ab.txt)
+                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) {
                     if (grp + 1 < 4) {
