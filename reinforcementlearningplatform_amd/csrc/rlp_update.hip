@@ -816,6 +816,10 @@ __global__ void __launch_bounds__(64 * kWgWaves, 1) ppo2_wgrad_kernel(WArgs w) {
         lds_barrier();
         load_s(tile + 2 * (int64_t)gridDim.x, svn);
         half8 bh = frag(cur, 0, 0), bl = frag(cur, 0, 1);
+        // a pinned group of its own (as the FD's rd(0)): the tile's first steps then read one step
+        // ahead too (exposed reads per tile 10 -> 3, EXT 24 -> 9; wgrad -0.5 %, EXT -1.4 %:
+        // profiles/r5/r5ab3_wgrad_sgb_ab3.txt)
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             // A operands scaled by 2^sg and split
