@@ -21,7 +21,8 @@ def gaps(asm, name):
             pend[int(m.group(1))] = 0
             continue
         if line.startswith("v_mfma_f32_16x16x32_f16"):
-            srcs = [int(x) for x in re.findall(r"v\[(\d+):\d+\]", line)[1:3]]
+            ops = [o.strip() for o in line.split(None, 1)[1].split(",")]
+            srcs = [int(m.group(1)) for m in (re.match(r"v\[(\d+):\d+\]", o) for o in ops[1:3]) if m]
             for r in list(pend):
                 if r in srcs:
                     out.append(pend.pop(r))
