@@ -2695,7 +2695,7 @@ __device__ __forceinline__ int l1_row(int f, float invS) { return (int)(((float)
 // LDS. Wave w: rows 16 w .. 16 w + 15, all 16 neuron tiles (C = [neuron][row], 64 accumulators);
 // lane (g, e) stores neurons 16 t + 4 g .. + 3 of row e as one float4.
 template <int KS>
-__global__ void __launch_bounds__(256) l1_fwd_kernel(const float *__restrict__ s, int S, int64_t rows,
+__global__ void __launch_bounds__(256, 2) l1_fwd_kernel(const float *__restrict__ s, int S, int64_t rows,
                                                      const float *__restrict__ W1, int ldw,
                                                      const float *__restrict__ b1, float *__restrict__ h1) {
     __shared__ float w1t[4 * KS][kL1Ld];        // [k][neuron]
@@ -2707,6 +2707,21 @@ __global__ void __launch_bounds__(256) l1_fwd_kernel(const float *__restrict__ s
     }
     const float invS = 1.f / (float)S;
     const int64_t ntiles = (rows + kL1Rows - 1) / kL1Rows;
+    // the tile's s span (nr * S <= 64 * 4 KS floats, contiguous) in registers, loaded one tile ahead
+    // so that its latency hides under the current tile's MFMAs and stores
+    constexpr int NSV = (kL1Rows * 4 * KS + 255) / 256;
+    float sv[NSV];
+    auto load_s = [&](int64_t tile) {
+        const int64_t r0 = tile * kL1Rows;
+        const int n = tile < ntiles ? (int)(rows - r0 < kL1Rows ? rows - r0 : kL1Rows) * S : 0;
+        const float *src = s + r0 * S;
+#pragma unroll
+        for (int u = 0; u < NSV; ++u) {
+            const int f = t + 256 * u;
+            sv[u] = f < n ? src[f] : 0.f;
+        }
+    };
+    load_s(blockIdx.x);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t r0 = tile * kL1Rows;
         const int nr = (int)(rows - r0 < kL1Rows ? rows - r0 : kL1Rows);
@@ -2715,12 +2730,16 @@ __global__ void __launch_bounds__(256) l1_fwd_kernel(const float *__restrict__ s
             const int k = f / kL1Rows, r = f - k * kL1Rows;
             if (k >= S || r >= nr) st[k][r] = 0.f;
         }
-        const float *src = s + r0 * S;
-        for (int f = t; f < nr * S; f += 256) {  // the tile's contiguous span, coalesced
-            const int r = l1_row(f, invS);
-            st[f - r * S][r] = src[f];
+#pragma unroll
+        for (int u = 0; u < NSV; ++u) {  // the span transposed into st (row r, feature f - r S)
+            const int f = t + 256 * u;
+            if (f < nr * S) {
+                const int r = l1_row(f, invS);
+                st[f - r * S][r] = sv[u];
+            }
         }
         __syncthreads();
+        load_s(tile + gridDim.x);
         floatx4 acc[16];
 #pragma unroll
         for (int nt = 0; nt < 16; ++nt) {
@@ -2775,7 +2794,21 @@ __global__ void __launch_bounds__(256) l1_wgrad_kernel(const float *__restrict__
                                : floatx4{0.f, 0.f, 0.f, 0.f};
         }
     };
-    if (lo < hi) load(lo);
+    // the step's s span (nr * S <= 32 x 44 floats, contiguous) likewise one step ahead
+    constexpr int NSV = (kL1WRows * (kL1WLd - 4) + 255) / 256;
+    float sv[NSV];
+    auto load_s = [&](int64_t r0) {
+        const int n = r0 < hi ? (int)(hi - r0 < kL1WRows ? hi - r0 : kL1WRows) * S : 0;
+#pragma unroll
+        for (int u = 0; u < NSV; ++u) {
+            const int f = t + 256 * u;
+            sv[u] = f < n ? s[r0 * S + f] : 0.f;
+        }
+    };
+    if (lo < hi) {
+        load(lo);
+        load_s(lo);
+    }
     for (int64_t r0 = lo; r0 < hi; r0 += kL1WRows) {
         const int nr = (int)(hi - r0 < kL1WRows ? hi - r0 : kL1WRows);
         __syncthreads();  // the previous step's tiles are read
@@ -2789,13 +2822,19 @@ __global__ void __launch_bounds__(256) l1_wgrad_kernel(const float *__restrict__
             if (c >= S) sx[r][c] = (c == S && r < nr) ? 1.f : 0.f;
             else if (r >= nr) sx[r][c] = 0.f;
         }
-        const float *src = s + r0 * S;
-        for (int f = t; f < nr * S; f += 256) {
-            const int r = l1_row(f, invS);
-            sx[r][f - r * S] = src[f];
+#pragma unroll
+        for (int u = 0; u < NSV; ++u) {
+            const int f = t + 256 * u;
+            if (f < nr * S) {
+                const int r = l1_row(f, invS);
+                sx[r][f - r * S] = sv[u];
+            }
         }
         __syncthreads();
-        if (r0 + kL1WRows < hi) load(r0 + kL1WRows);  // next step, under this step's MFMAs
+        if (r0 + kL1WRows < hi) {  // next step, under this step's MFMAs
+            load(r0 + kL1WRows);
+            load_s(r0 + kL1WRows);
+        }
 #pragma unroll
         for (int k0 = 0; k0 < kL1WRows; k0 += 4) {
             float bv[FT];
