@@ -393,7 +393,14 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[j] = *reinterpret_cast<const floatx4 *>(B2c + 16 * j + 4 * gq);
         floatx4 p0, p1;  // layer-1 tiles of the next phase (pre), consumed by its B operands (bop)
+        // EXT: phase P's h1 quads in buffer P & 1, loaded two phases ahead (one phase ahead — half a
+        // phase before bop — left the global load latency exposed)
+        floatx4 q0[2], q1[2];
         x3_gemm16<false, kFdWaves, 1, kFdRing>(Xf, ring, my_part, acc, [&](int P, half8 &bh, half8 &bl) {
+            if constexpr (EXT) {
+                p0 = q0[P & 1];
+                p1 = q1[P & 1];
+            }
             float x[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -407,9 +414,13 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
             }
             split8(x, bh, bl);
         }, [&](int P) {
-            if constexpr (EXT) {  // neurons 32 P + 4 gq .. + 3 and 32 P + 16 + 4 gq .. + 3 of the row
-                p0 = *reinterpret_cast<const floatx4 *>(h1r + 32 * P + 4 * gq);
-                p1 = *reinterpret_cast<const floatx4 *>(h1r + 32 * P + 16 + 4 * gq);
+            if constexpr (EXT) {  // neurons 32 Q + 4 gq .. + 3 and 32 Q + 16 + 4 gq .. + 3 of the row
+                auto ld = [&](int Q) {
+                    q0[Q & 1] = *reinterpret_cast<const floatx4 *>(h1r + 32 * Q + 4 * gq);
+                    q1[Q & 1] = *reinterpret_cast<const floatx4 *>(h1r + 32 * Q + 16 + 4 * gq);
+                };
+                if (P == 0) ld(0);   // (pre(0) runs just before bop(0))
+                if (P + 1 < 8) ld(P + 1);
             } else {
                 p0 = layer1(2 * P);
                 p1 = layer1(2 * P + 1);
