@@ -2767,11 +2767,14 @@ __global__ void __launch_bounds__(256, 2) l1_fwd_kernel(const float *__restrict_
     }
 }
 
-// part[b][256][S + 1] = sum over block b's rows of g1[row] (x) [s_row | 1]: dW1 | db1 partials.
+// part[b][256][S + 1] = sum over block b's rows of g1[row] (x) [s_row | 1]: dW1 | db1 partials,
+// g1 = dL/dh1 * (1 - h1^2) formed here from the FD kernel's dL/dh1 rows and h1 (the same product
+// the FD tail formed before: (dL/dh1 * unscale) * fma(-h1, h1, 1), bit-identical).
 // Wave w owns neurons 64 w .. 64 w + 63 (4 tiles) x FT feature tiles (C = [neuron][feature]);
 // 32-row steps, the next step's g1 rows loaded into registers under the current step's MFMAs.
 template <int FT>
 __global__ void __launch_bounds__(256) l1_wgrad_kernel(const float *__restrict__ g1,
+                                                       const float *__restrict__ h1,
                                                        const float *__restrict__ s, int S, int64_t rows,
                                                        int64_t rpb, float *__restrict__ part) {
     __shared__ __attribute__((aligned(16))) float gt[kL1WRows][kL1Ld];  // [row][neuron]
@@ -2785,13 +2788,16 @@ __global__ void __launch_bounds__(256) l1_wgrad_kernel(const float *__restrict__
 #pragma unroll
         for (int j = 0; j < FT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     constexpr int NV = kL1WRows * 256 / 4 / 256;  // float4 of g1 per thread and step (8)
-    floatx4 v[NV];
+    floatx4 v[NV], hv[NV];
     auto load = [&](int64_t r0) {
 #pragma unroll
         for (int u = 0; u < NV; ++u) {
             const int i = t + 256 * u, r = i >> 6;
-            v[u] = r0 + r < hi ? *reinterpret_cast<const floatx4 *>(g1 + (r0 + r) * 256 + 4 * (i & 63))
-                               : floatx4{0.f, 0.f, 0.f, 0.f};
+            const bool in = r0 + r < hi;
+            v[u] = in ? *reinterpret_cast<const floatx4 *>(g1 + (r0 + r) * 256 + 4 * (i & 63))
+                      : floatx4{0.f, 0.f, 0.f, 0.f};
+            hv[u] = in ? *reinterpret_cast<const floatx4 *>(h1 + (r0 + r) * 256 + 4 * (i & 63))
+                       : floatx4{0.f, 0.f, 0.f, 0.f};
         }
     };
     // the step's s span (nr * S <= 32 x 44 floats, contiguous) likewise one step ahead
@@ -2815,7 +2821,10 @@ __global__ void __launch_bounds__(256) l1_wgrad_kernel(const float *__restrict__
 #pragma unroll
         for (int u = 0; u < NV; ++u) {
             const int i = t + 256 * u;
-            *reinterpret_cast<floatx4 *>(&gt[i >> 6][4 * (i & 63)]) = v[u];
+            floatx4 gz;  // dL/dz1 = dL/dh1 * (1 - h1^2)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) gz[c] = v[u][c] * __builtin_fmaf(-hv[u][c], hv[u][c], 1.f);
+            *reinterpret_cast<floatx4 *>(&gt[i >> 6][4 * (i & 63)]) = gz;
         }
         for (int f = t; f < kL1WRows * kL1WLd; f += 256) {  // ones column, zero padding
             const int r = f / kL1WLd, c = f - r * kL1WLd;
@@ -2873,12 +2882,12 @@ void ppo2_ext_h1(const float *W1, int ldw, const float *b1, int S, int H, const 
     const int grid = (int)(ntiles < 4096 ? ntiles : 4096);
     l1_fwd_kernel<11><<<grid, 256, 0, st>>>(s, S, rows, W1, ldw, b1, h1);
 }
-void ppo2_ext_dw1(const float *g1, const float *s, int S, int H, int64_t rows, float *part,
-                  float *gW, float *gb, hipStream_t st) {
+void ppo2_ext_dw1(const float *g1, const float *h1, const float *s, int S, int H, int64_t rows,
+                  float *part, float *gW, float *gb, hipStream_t st) {
     int64_t rpb = (rows + kL1WBlocks - 1) / kL1WBlocks;
     rpb = (rpb + kL1WRows - 1) / kL1WRows * kL1WRows;
     const int nb = (int)((rows + rpb - 1) / rpb);
-    l1_wgrad_kernel<3><<<nb, 256, 0, st>>>(g1, s, S, rows, rpb, part);
+    l1_wgrad_kernel<3><<<nb, 256, 0, st>>>(g1, h1, s, S, rows, rpb, part);
     wgrad_reduce(Layer{nullptr, nullptr, S, H}, part, nb, gW, gb, st);
 }
 

@@ -40,7 +40,7 @@ struct Ppo2Args {
     int p3;             // floats per wave partial: A*256 + A + 256*S + 256 (EXT: A*256 + A)
     double *lpart;      // [FD waves]: per-wave loss partials (summed in order by the reduce)
     const float *h1;    // EXT: [rows][256] tanh(W1 s + b1) (exact f32, rlp_dense.hip)
-    float *g1;          // EXT: [rows][256] dL/dz1, the dense dW1 | db1 GEMM's operand
+    float *g1;          // EXT: [rows][256] dL/dh1 (l1_wgrad_kernel applies 1 - h1^2: dL/dz1)
 };
 
 // block barrier for LDS hand-offs only: drains this wave's LDS ops, not its global loads (HIP's
@@ -576,20 +576,17 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
         // MFMAs first (their W1 / b1 reads in flight together), then the 64 independent tanh'
         // chains — tile by tile, each tile's LDS reads, MFMA latency and transcendental chain were
         // exposed in turn (r3x diag: g1 5.8k cycles per wave tile for ~2.5k of issue)
-        if constexpr (EXT) {  // g1 from the stored h1, to g.g1 (rows 4 gq + q, neuron 16 t + e)
+        if constexpr (EXT) {  // dL/dh1 to g.g1 (rows 4 gq + q, neuron 16 t + e); the tanh' factor
+            // (1 - h1^2) is applied by l1_wgrad_kernel, whose coalesced row loads take h1 beside g1:
+            // re-read here, the block's 128 KiB of h1 came in one burst with no MFMA work beside it
+            // (13-18 % of this kernel, profiles/r5/r5ab11_ext_tail_noload_diag.txt)
             const float unscale = __builtin_amdgcn_ldexpf(1.f, ex - 14) / sw;
             const int64_t r0 = bt * kFdRows + 16 * wv + 4 * gq;
-            float hv[16][4];
-#pragma unroll
-            for (int t = 0; t < 16; ++t)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    hv[t][q] = r0 + q < g.rows ? g.h1[(size_t)(r0 + q) * H + 16 * t + e] : 0.f;
 #pragma unroll
             for (int t = 0; t < 16; ++t)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const float v = dh1[t][q] * unscale * __builtin_fmaf(-hv[t][q], hv[t][q], 1.f);
+                    const float v = dh1[t][q] * unscale;
                     if (r0 + q < g.rows) g.g1[(size_t)(r0 + q) * H + 16 * t + e] = v;
                 }
         } else {
@@ -1027,8 +1024,8 @@ static int ppo2_grid() { return device_cus(); }  // wgrad / FD: one block per CU
 int64_t ppo2_ext_floats(int S, int H, int64_t rows);
 void ppo2_ext_h1(const float *W1, int ldw, const float *b1, int S, int H, const float *s,
                  int64_t rows, float *h1, hipStream_t st);
-void ppo2_ext_dw1(const float *g1, const float *s, int S, int H, int64_t rows, float *part,
-                  float *gW, float *gb, hipStream_t st);
+void ppo2_ext_dw1(const float *g1, const float *h1, const float *s, int S, int H, int64_t rows,
+                  float *part, float *gW, float *gb, hipStream_t st);
 
 // floats of a net's rlp_ppo2_grad workspace, in this order: G2 tiles | wgrad partials | FD
 // partials | g2max (16) | FD loss partials (f64) | EXT: h1 | g1 | dW1 partials
@@ -1152,7 +1149,7 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
     else ppo2_wgrad_kernel<2><<<grid, 64 * kWgWaves, 0, st>>>(w);
     RLP_CHECK_LAUNCH("rlp_ppo2_grad (wgrad)");
     if (ext)  // dW1 | db1 = G1^T [s | 1] on the dense GEMM, into grad's W1 / b1
-        ppo2_ext_dw1(g.g1, s, net.S, kUpdH, rows, workspace + wl.dw1, grad,
+        ppo2_ext_dw1(g.g1, g.h1, s, net.S, kUpdH, rows, workspace + wl.dw1, grad,
                      grad + (int64_t)kUpdH * net.S, st);
     const int64_t total = (int64_t)net.H * net.S + net.H + (int64_t)net.H * net.H + net.H +
                           (int64_t)net.A * net.H + net.A;
