@@ -658,8 +658,10 @@ def ugvoa_leg(rank, n=16384, steps=30, warmup=3, seed=5):
 def ugvoa_ppo2_leg(rank, n=16384, T=64, iters=3, seed=17):
     """UGVForwardObstacleAvoidance PPO2 rollout (the PPO2 demo's 41 -> 256 -> 256 -> 2 / -> 1 tanh
     nets, demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97) through
-    rlp_rollout: per step packed actor / critic forward (layer 1 on 11 K-steps of f32 MFMA),
-    Philox sample, lidar env step, map-generator resets; n envs per GPU (config 5: 131 072 / 8)."""
+    rlp_rollout: two launches per step (round 6) — oa_policy_kernel (actor + critic, layer 1 on
+    11 K-steps of exact f32 MFMA, the 256 x 256 hidden layer on the f16x3 split, the Philox sample)
+    and oa_step_kernel (lidar env step, success rule, the 37-beam scans, map-generator resets of the
+    ended envs); n envs per GPU (config 5: 131 072 / 8)."""
     kind = A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE
     p = A.default_params(kind, "ppo2")
     D, S, Ad = A.ENV_DIMS[kind]
@@ -691,16 +693,27 @@ def ugvoa_ppo2_leg(rank, n=16384, T=64, iters=3, seed=17):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     seg_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    rows = n * T + n   # actor + critic per env-step, the bootstrap critic per env
     flop = n * T * (mlp_flops(ad) + mlp_flops(cd)) + n * mlp_flops(cd)
+    hid = 2 * 256 * 256                     # the hidden layer's FLOP per row and net
+    f_hidden = (2 * n * T + n) * hid        # on the f16x3 split (the default arithmetic)
+    f_exact = flop - f_hidden               # layers 1 and 3: exact f32 MFMA / VALU
+    ideal_s = (f_exact / PEAK_FP32_MFMA_TFLOPS + f_hidden / PEAK_F16X3_TFLOPS) / 1e12
+    peak_mixed = flop / ideal_s / 1e12      # the FLOP-weighted ceiling of that arithmetic mix
     ach = flop / (seg_ms * 1e-3) / 1e12
     return {"value": n * T * iters / dt, "unit": "env-steps/s", "envs_per_gpu": n, "T": T,
             "ms_per_segment": dt / iters * 1e3, "episodes_per_segment": int(bufs["done"].sum()),
-            "roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_FP32_MFMA_TFLOPS,
-                         "unit": "TFLOP/s", "frac": ach / PEAK_FP32_MFMA_TFLOPS,
-                         "flop_per_segment": flop, "segment_ms": seg_ms,
-                         "peak_basis": "f32 MFMA dense (the per-step packed forwards: f32 MFMA)",
-                         "note": "whole segment (T x {critic + actor forward, sample, lidar env "
-                                 "step, resets} launches) against the nets' FLOPs"},
+            "roofline": {"bound": "mfma", "achieved": ach, "peak": peak_mixed,
+                         "unit": "TFLOP/s", "frac": ach / peak_mixed,
+                         "flop_per_segment": flop, "segment_ms": seg_ms, "rows": rows,
+                         "peak_basis": "mixed: layers 1 and 3 (%.3g FLOP) at the f32 MFMA peak "
+                                       "%.1f TF, the hidden layer (%.3g FLOP) at the f16x3 ceiling "
+                                       "%.1f TF" % (f_exact, PEAK_FP32_MFMA_TFLOPS, f_hidden,
+                                                    PEAK_F16X3_TFLOPS),
+                         "frac_vs_f32_peak": ach / PEAK_FP32_MFMA_TFLOPS,
+                         "note": "whole segment (T x {oa_policy_kernel, oa_step_kernel} + the "
+                                 "bootstrap critic), the lidar env's f64 work included, against "
+                                 "the nets' FLOPs"},
             "config": "UGVForwardObstacleAvoidance (PPO2 copy, 37-beam lidar, 10 circles) PPO2 "
                       "rollout, nets [41,256,256,2] / [41,256,256,1] tanh (rlp_rollout)"}
 

@@ -39,7 +39,9 @@ typedef void *rlp_stream_t; /* hipStream_t */
 #define RLP_EUNSUPPORTED (-1001)
 #define RLP_ENOMEM (-1002)  /* unused since ABI version 2 (no library allocations); kept reserved */
 
-#define RLP_ABI_VERSION 2  /* 2: caller-owned rollout / mlp_forward workspaces (round 5) */
+#define RLP_ABI_VERSION 3  /* 2: caller-owned rollout / mlp_forward workspaces (round 5);
+                              3: per-call mlp_precision of rlp_mfma_forward / rlp_value_fixup,
+                                 rlp_selftest_gemm_guard (round 6) */
 
 /* ------------------------------------------------------------------------------------------ */
 /* Environment kinds. Each kind is one specific reference env copy (copies diverge). */
@@ -356,16 +358,20 @@ int64_t rlp_rollout_workspace_bytes(int kind, const rlp_mlp_desc *actor_desc,
                                     const rlp_mlp_desc *critic_desc, const rlp_rollout_cfg *cfg);
 
 /* Batched forward of an MFMA-packed [S->H->H->A] net (H = 256): y[rows][A] (last-layer act
- * applied). Proximal_Policy_Optimization2.evaluate (:63-67) / critic(s) in learn() (:91-92). */
+ * applied). Proximal_Policy_Optimization2.evaluate (:63-67) / critic(s) in learn() (:91-92).
+ * mlp_precision (per call, as rlp_rollout_cfg.mlp_precision): 0 = the library-wide default
+ * (rlp_set_mlp_precision), 1 = RLP_MLP_FP32 (exact f32 MFMA), 2 = RLP_MLP_F16X3 (the rollout's
+ * split hidden layer). Concurrent callers pass 1 or 2 and never depend on the global. */
 int rlp_mfma_forward(const rlp_mlp_desc *desc, const float *packed, const float *x, float *y,
-                     int64_t rows, rlp_stream_t stream);
+                     int64_t rows, int mlp_precision, rlp_stream_t stream);
 
 /* Bootstrap values the rollout kernel cannot provide: value_next[i] = critic(obs_next[i]) for
  * rows with done[i] && !success[i] (e.g. CartPole time-outs); every other row is either written by
- * rlp_rollout (V(s'_t) == V(s_{t+1})) or multiplied by (1 - success) = 0 in the GAE (:93). */
+ * rlp_rollout (V(s'_t) == V(s_{t+1})) or multiplied by (1 - success) = 0 in the GAE (:93).
+ * mlp_precision: as rlp_mfma_forward. */
 int rlp_value_fixup(const rlp_mlp_desc *critic_desc, const float *critic_packed,
                     const float *obs_next, const uint8_t *done, const uint8_t *success,
-                    float *value_next, int64_t rows, rlp_stream_t stream);
+                    float *value_next, int64_t rows, int mlp_precision, rlp_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Learn-side scans (Proximal_Policy_Optimization2.learn, :84-100; utils/classes.py:626-656)   */
@@ -419,7 +425,14 @@ int rlp_adv_normalize(float *adv, int64_t count, double *adv_stats, int parts, r
 /* ------------------------------------------------------------------------------------------ */
 /* PPO2 update (Proximal_Policy_Optimization2.learn, algorithm/policy_base/
  * Proximal_Policy_Optimization2.py:102-163) for the drivers' [S -> 256 -> 256 -> A] tanh nets
- * (PPOActor_Gaussian / PPOCritic, demonstration/PPO2/PPO2-4-CartPole/train.py:39-125).
+ * (PPOActor_Gaussian / PPOCritic, demonstration/PPO2/PPO2-4-CartPole/train.py:39-125) with
+ * S <= 8 (CartPole, AngleOnly, SOI, UGV, UAV) or 41 <= S <= 44 (the obstacle-avoidance demos'
+ * 4 + 37 lidar inputs, demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97).
+ * For S <= 8 layer 1 runs inside the two kernels; for 41..44 inputs it runs on exact-f32 MFMA
+ * kernels of its own (h1 = tanh(W1 s + b1) stored once per call, dW1 | db1 from the stored
+ * dL/dh1 and h1), which needs contiguous rows: `index` must be NULL (RLP_EINVAL otherwise; the
+ * caller gathers a mini-batch first) and the workspace grows by 2 x rows x 256 floats (h1 and
+ * dL/dh1) plus the dW1 partials (rlp_ppo2_workspace_floats includes them).
  * rlp_ppo2_grad writes the gradient of ONE optimiser step's loss over `rows` samples, in the
  * flat torch parameter order (W1, b1, W2, b2, W3, b3 = rlp_mlp_forward's layout):
  *   RLP_LOSS_ACTOR:  mean(-min(r*adv, clamp(r, 1-eps, 1+eps)*adv) - entropy_coef * entropy),
@@ -449,8 +462,11 @@ int rlp_ppo2_grad(const rlp_mlp_desc *desc, const float *packed, const rlp_ppo2_
 /* The same gradient for any tanh Linear stack that rlp_ppo2_grad does not take (other widths, more
  * or fewer hidden layers, more inputs): the PPO2-SecondOrderIntegration demo's actor
  * 4 -> 128 -> 64 -> 32 -> A / critic 4 -> 64 -> 64 -> 1 (demonstration/PPO2/PPO2-4-
- * SecondOrderIntegration/train.py:37-125), the obstacle-avoidance demos' 41 -> 256 -> 256 -> A
- * (demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97). Hidden layers
+ * SecondOrderIntegration/train.py:37-125); also the exact-f32 alternative for nets that
+ * rlp_ppo2_grad takes (the obstacle-avoidance demos' 41 -> 256 -> 256 -> A go to rlp_ppo2_grad
+ * under the Python learner's 'auto' selection since round 5; update_kernels='dense' keeps them
+ * here). rlp_ppo2_grad has no arithmetic knob: its hidden layer is always the f16x3 split, and
+ * this entry point is the per-call exact-f32 choice. Hidden layers
  * tanh; the actor's last layer tanh (A <= 4), the critic's linear with one output; widths <= 1024.
  * `params` is the plain layout (rlp_mlp_param_count floats, torch order); rows are contiguous (a
  * mini-batch is gathered by the caller). Exact f32 MFMA products (v_mfma_f32_16x16x4_f32),
@@ -608,9 +624,16 @@ int rlp_abi_version(void);
  * 11 ugv_oa, 12 dense_net, 13 ddpg_nets, 14 ddpg_cfg, 15 sac_nets, 16 sac_cfg): FFI bindings
  * verify their mirrors with it. */
 int64_t rlp_struct_size(int which);
+/* Test hook of the launch-status plumbing: runs the dense GEMM launcher with `nprobs` problems,
+ * which must be outside its accepted range [1, 6], through a call chain that drops the launcher's
+ * return value (as the DDPG / SAC / PPO2-dense chains do), and returns the status that reaches the
+ * C-ABI (RLP_EINVAL; never RLP_OK). No device work. */
+int rlp_selftest_gemm_guard(int nprobs);
+
 /* The rlp_set_* knobs below are process-wide defaults (plain globals, not synchronised): set them
  * before any thread launches work. Concurrent callers choose per call instead, through
- * rlp_rollout_cfg's mlp_precision / physics / sub fields.
+ * rlp_rollout_cfg's mlp_precision / physics / sub fields and the mlp_precision argument of
+ * rlp_mfma_forward / rlp_value_fixup (rlp_ppo2_grad and the other entry points have no knob).
  *
  * Tuning knob of rlp_rollout: 16-env sub-blocks per wave: 0 = auto (default; the f16x3 path
  * takes 1 when 2 would leave fewer than two blocks per CU, e.g. 32 768 UAV envs), 1 (f16x3 only),
@@ -630,7 +653,8 @@ int rlp_set_rollout_physics(int shared);
  *     f32 accumulation — fp32-class accuracy (see tests/test_gpu_rollout.py) at 16/3 x the f32
  *     MFMA rate;
  *   RLP_MLP_FP32: exact f32-input MFMA (v_mfma_f32_16x16x4_f32).
- * The other kernels (rlp_mfma_forward, rlp_value_fixup, rlp_mlp_forward) are always fp32. */
+ * It is the default of rlp_rollout (cfg mlp_precision 0) and of rlp_mfma_forward / rlp_value_fixup
+ * (mlp_precision 0); rlp_mlp_forward is always fp32. */
 #define RLP_MLP_FP32 0
 #define RLP_MLP_F16X3 1
 int rlp_set_mlp_precision(int mode);

@@ -11,7 +11,7 @@ import torch  # import first: its libamdhip64 is the runtime librlp.so binds to 
 from . import _abi
 
 _LIB_NAME = "librlp.so"
-ABI_VERSION = 2  # include/rlp.h RLP_ABI_VERSION
+ABI_VERSION = 3  # include/rlp.h RLP_ABI_VERSION
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
 
@@ -44,8 +44,9 @@ def _declare(lib):
                                  vp]),
         "rlp_rollout": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "rlp_rollout_workspace_bytes": (i64, [i32, vp, vp, vp]),
-        "rlp_mfma_forward": (i32, [vp, vp, vp, vp, i64, vp]),
-        "rlp_value_fixup": (i32, [vp, vp, vp, vp, vp, vp, i64, vp]),
+        "rlp_mfma_forward": (i32, [vp, vp, vp, vp, i64, i32, vp]),
+        "rlp_value_fixup": (i32, [vp, vp, vp, vp, vp, vp, i64, i32, vp]),
+        "rlp_selftest_gemm_guard": (i32, [i32]),
         "rlp_set_rollout_sub": (i32, [i32]),
         "rlp_set_rollout_physics": (i32, [i32]),
         "rlp_set_mlp_precision": (i32, [i32]),

@@ -12,9 +12,18 @@ namespace rlp {
 // ------------------------------------------------------------------------------------------
 void set_error(const char *fmt, ...);
 int fail(int code, const char *fmt, ...);
+// Launch helpers that refuse a launch without a return path to the entry point (e.g. the dense
+// GEMM's gemm_multi, called from deep inside a chain) record their status here as well as in the
+// error string; RLP_CHECK_LAUNCH hands the first such status back through the C-ABI, so a refused
+// launch never reads as RLP_OK with unwritten outputs. take_pending() returns and clears it (entry
+// points call it first, so a status never leaks from one call into the next).
+int fail_pending(int code, const char *fmt, ...);
+int take_pending();
 
 #define RLP_CHECK_LAUNCH(what)                                                            \
     do {                                                                                  \
+        const int p_ = ::rlp::take_pending();                                             \
+        if (p_ != RLP_OK) return p_;                                                      \
         hipError_t e_ = hipGetLastError();                                                \
         if (e_ != hipSuccess) return ::rlp::fail(-(int)e_, "%s: %s", what, hipGetErrorString(e_)); \
     } while (0)

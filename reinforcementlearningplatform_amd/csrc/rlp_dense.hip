@@ -1235,12 +1235,14 @@ static hipError_t dense_gemm_attr() {
     return rc;
 }
 
-// problems qs[0 .. n) in one launch (0 < n <= kMaxProbs)
-void gemm_multi(const Prob *qs, int n, hipStream_t s) {
-    if (n < 1 || n > kMaxProbs || dense_gemm_attr() != hipSuccess) {
-        fail(RLP_EINVAL, "dense GEMM: %d problems (max %d) or LDS attribute not set", n, kMaxProbs);
-        return;
-    }
+// problems qs[0 .. n) in one launch (0 < n <= kMaxProbs). A refusal (nothing launched) returns
+// RLP_EINVAL and is also left pending (fail_pending), so the entry point's RLP_CHECK_LAUNCH returns
+// it through the C-ABI even where the caller's call chain drops this return value.
+int gemm_multi(const Prob *qs, int n, hipStream_t s) {
+    if (n < 1 || n > kMaxProbs)
+        return fail_pending(RLP_EINVAL, "dense GEMM: %d problems (1..%d)", n, kMaxProbs);
+    if (dense_gemm_attr() != hipSuccess)
+        return fail_pending(RLP_EINVAL, "dense GEMM: dynamic LDS attribute (%d B) not set", (int)kDenseLds);
     ProbSet ps{};
     int nb = 0;
     for (int i = 0; i < n; ++i) {
@@ -1251,12 +1253,26 @@ void gemm_multi(const Prob *qs, int n, hipStream_t s) {
     ps.start[n] = nb;
     ps.n = n;
     dense_gemm_kernel<<<nb, 256, kDenseLds, s>>>(ps);
+    return RLP_OK;
 }
-// one problem, or two (q1 != nullptr) in one launch; returns p0's slice count
+// one problem, or two (q1 != nullptr) in one launch; returns p0's slice count (a refused launch is
+// pending, see gemm_multi)
 int gemm_launch(const Prob &q0, const Prob *q1, hipStream_t s) {
     const Prob qs[2] = {q0, q1 ? *q1 : q0};
     gemm_multi(qs, q1 ? 2 : 1, s);
     return q0.nz;
+}
+
+// test hook (include/rlp.h rlp_selftest_gemm_guard): a refused gemm_multi inside a call chain that
+// drops its return value must still reach the caller as a non-OK status
+int selftest_gemm_guard(int nprobs) {
+    take_pending();
+    if (nprobs >= 1 && nprobs <= kMaxProbs)
+        return fail(RLP_EINVAL, "rlp_selftest_gemm_guard: only out-of-range counts (not %d)", nprobs);
+    Prob qs[kMaxProbs + 1] = {};
+    gemm_multi(qs, nprobs, nullptr);  // return value dropped, as chain_grad & co. do
+    RLP_CHECK_LAUNCH("rlp_selftest_gemm_guard");
+    return RLP_OK;
 }
 int gemm_impl(const Opnd &A, const Opnd &B, const Epi &e, const Opnd *A1, const Opnd *B1,
               const Epi *e1, int M, int N, int R, int splits, hipStream_t s) {
@@ -1724,6 +1740,7 @@ int64_t dense_mlp_scratch_floats(const rlp_mlp_desc &d, int n) {
 // activations in the caller's scratch (dense_mlp_scratch_floats)
 int dense_mlp_forward(const rlp_mlp_desc &d, const float *params, const float *x, float *y, int n,
                       float *scratch, hipStream_t s) {
+    take_pending();
     const int L = d.n_layers;
     if (mlp_chain_ok(d)) {
         int64_t off[RLP_MLP_MAX_LAYERS], o = 0;
@@ -1770,6 +1787,8 @@ using namespace rlp;
 
 extern "C" {
 
+int rlp_selftest_gemm_guard(int nprobs) { return selftest_gemm_guard(nprobs); }
+
 int64_t rlp_ddpg_workspace(const rlp_ddpg_nets *nets, int batch) {
     if (!nets || batch < 1 || !net_ok(nets->actor) || !net_ok(nets->critic)) return RLP_EINVAL;
     return ddpg_ws(*nets, batch).total;
@@ -1778,6 +1797,7 @@ int64_t rlp_ddpg_workspace(const rlp_ddpg_nets *nets, int batch) {
 int rlp_ddpg_update(const rlp_ddpg_nets *nets, const rlp_ddpg_cfg *cfg, const float *s, const float *a,
                     const float *r, const float *s_next, const float *end, float *work,
                     float *losses, rlp_stream_t stream) {
+    take_pending();
     RLP_REQUIRE(nets && cfg && s && a && r && s_next && end && work && losses,
                 "rlp_ddpg_update: null argument");
     const rlp_ddpg_nets &n = *nets;
@@ -1974,6 +1994,7 @@ int64_t rlp_sac_workspace(const rlp_sac_nets *nets, int batch) {
 int rlp_sac_update(const rlp_sac_nets *nets, const rlp_sac_cfg *cfg, const float *s, const float *a,
                    const float *r, const float *s_next, const float *dw, const float *noise,
                    float *work, float *losses, rlp_stream_t stream) {
+    take_pending();
     RLP_REQUIRE(nets && cfg && s && a && r && s_next && dw && work && losses,
                 "rlp_sac_update: null argument");
     const rlp_sac_nets &n = *nets;
@@ -2904,6 +2925,7 @@ int rlp_ppo2_dense_grad(const rlp_mlp_desc *desc, const float *params, const rlp
                         const float *s, const float *a, const float *a_logprob, const float *adv,
                         const float *v_target, int64_t rows, float *grad, double *loss_sum,
                         float *workspace, rlp_stream_t stream) {
+    take_pending();
     RLP_REQUIRE(desc && params && cfg && s && grad && workspace, "rlp_ppo2_dense_grad: null argument");
     const bool actor = cfg->kind == RLP_LOSS_ACTOR;
     RLP_REQUIRE(actor || cfg->kind == RLP_LOSS_CRITIC, "rlp_ppo2_dense_grad: loss kind %d", cfg->kind);

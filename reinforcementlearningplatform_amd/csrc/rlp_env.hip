@@ -30,6 +30,24 @@ int fail(int code, const char *fmt, ...) {
     return code;
 }
 
+// first refusal of a launch helper since the last take_pending() (thread-local, like g_err)
+static thread_local int g_pending = RLP_OK;
+
+int fail_pending(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    if (g_pending == RLP_OK) g_pending = code;
+    return code;
+}
+
+int take_pending() {
+    const int c = g_pending;
+    g_pending = RLP_OK;
+    return c;
+}
+
 template <int KIND>
 __global__ void __launch_bounds__(256) env_step_kernel(typename Env<KIND>::P p, double *state,
                                                        int n, const float *__restrict__ action,

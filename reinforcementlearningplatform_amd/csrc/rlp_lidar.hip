@@ -10,54 +10,23 @@
 // VGPRs (1 wave / SIMD, scratch spills) and leave most of the chip idle at 16 K envs; a beam per
 // lane keeps ~40 VGPRs of live state and launches 37x the lanes. The arithmetic of each beam is
 // Env<7>::beam — the same code the generic kernels run, restating the reference line by line.
-#include "rlp_envs.hpp"
+#include "rlp_lidar.hpp"
 
 namespace rlp {
 
-using OA = Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE>;
 constexpr int kOaThreads = 256;
-
-struct alignas(16) OaObstacle {
-    double x0, y0, r0, ref;  // ref = distance from the pose being scanned
-};
 
 template <int EB>
 struct OaLds {
-    OaObstacle ob[EB][OA::NOBS];
-    OA::Pose q[EB];
-    int coll[EB];
+    OaEnvLds e[EB];
 };
-
-// per-pose setup by the env's lane: obstacle distances, collision and the beam geometry
-template <int EB>
-__device__ __forceinline__ void oa_setup(const OA::P &p, OaLds<EB> &L, int t, const double *s) {
-    const double x = s[OA::X], y = s[OA::Y];
-    for (int k = 0; k < p.n_obs; ++k) {
-        const double dx = x - L.ob[t][k].x0, dy = y - L.ob[t][k].y0;
-        L.ob[t][k].ref = sqrt(dx * dx + dy * dy);
-    }
-    L.coll[t] = OA::collision_at(p, x, y, [&](int k, double &x0, double &y0, double &r0) {
-        x0 = L.ob[t][k].x0; y0 = L.ob[t][k].y0; r0 = L.ob[t][k].r0;
-    });
-    L.q[t] = OA::pose(p, x, y, s[OA::PHI]);
-}
 
 template <int EB>
 __device__ __forceinline__ void oa_scan(const OA::P &p, const OaLds<EB> &L, int e0, int ne,
                                         float *__restrict__ obs) {
-    const float blind = OA::beam_obs(p, p.laser_blind);
     for (int it = threadIdx.x; it < ne * OA::NL; it += kOaThreads) {
         const int e = it / OA::NL, i = it - e * OA::NL;
-        float v = blind;
-        if (!L.coll[e]) {
-            const OA::Pose q = L.q[e];
-            v = OA::beam_obs(p, OA::beam(p, q, i, [&](int k, double &x0, double &y0, double &r0,
-                                                      double &rf) {
-                const OaObstacle o = L.ob[e][k];
-                x0 = o.x0; y0 = o.y0; r0 = o.r0; rf = o.ref;
-            }));
-        }
-        obs[(size_t)(e0 + e) * OA::S + 4 + i] = v;
+        obs[(size_t)(e0 + e) * OA::S + 4 + i] = oa_beam(p, L.e[e], i);
     }
 }
 
@@ -90,19 +59,16 @@ __global__ void __launch_bounds__(kOaThreads) oa_kernel(OA::P p, double *state, 
 #pragma unroll
         for (int d = 0; d < OA::DW; ++d) s[d] = state[(size_t)d * n + i];
         for (int k = 0; k < p.n_obs; ++k) {
-            L.ob[t][k].x0 = state[(size_t)(OA::OB + 3 * k) * n + i];
-            L.ob[t][k].y0 = state[(size_t)(OA::OB + 3 * k + 1) * n + i];
-            L.ob[t][k].r0 = state[(size_t)(OA::OB + 3 * k + 2) * n + i];
+            L.e[t].ob[k].x0 = state[(size_t)(OA::OB + 3 * k) * n + i];
+            L.e[t].ob[k].y0 = state[(size_t)(OA::OB + 3 * k + 1) * n + i];
+            L.e[t].ob[k].r0 = state[(size_t)(OA::OB + 3 * k + 2) * n + i];
         }
     }
     float *first = STEP ? obs_cur : obs_next;
     if (first) {  // scan at the current pose (get_state / step's current_state)
         if (own) {
-            oa_setup(p, L, t, s);
-            float h[4];
-            OA::obs_head(p, s, OA::get_e(s), OA::e_phi(s), h);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) first[i * OA::S + j] = h[j];
+            oa_setup(p, L.e[t], s);
+            oa_head(p, s, first + i * OA::S);
         }
         __syncthreads();
         oa_scan(p, L, e0, ne, first);
@@ -117,7 +83,7 @@ __global__ void __launch_bounds__(kOaThreads) oa_kernel(OA::P p, double *state, 
             bool dn;
             OA::step_core(p, s, a, [&](double x, double y) {
                 return OA::collision_at(p, x, y, [&](int k, double &x0, double &y0, double &r0) {
-                    x0 = L.ob[t][k].x0; y0 = L.ob[t][k].y0; r0 = L.ob[t][k].r0;
+                    x0 = L.e[t].ob[k].x0; y0 = L.e[t].ob[k].y0; r0 = L.e[t].ob[k].r0;
                 });
             }, r, f, dn, e, eph);
 #pragma unroll
@@ -125,7 +91,7 @@ __global__ void __launch_bounds__(kOaThreads) oa_kernel(OA::P p, double *state, 
             reward[i] = r;
             flag[i] = f;
             done[i] = dn ? 1 : 0;
-            oa_setup(p, L, t, s);
+            oa_setup(p, L.e[t], s);
             float h[4];
             OA::obs_head(p, s, e, eph, h);
 #pragma unroll
@@ -175,18 +141,15 @@ int launch_ugvoa_observe_after(const rlp_ugv_oa_params &p, const double *state, 
                             nullptr, nullptr, st, reset, obs_next);
 }
 
-// reset(random=True) with one wave per env: each round, lane l tests try (round * 64 + l) of the
-// target / of obstacle k, and the lowest legal try wins — the sequential sampler's result
-// (Env<7>::reset) at ~1 round per draw instead of the wave waiting on its unluckiest lane.
+// reset(random=True) with one wave per env (oa_reset_wave); obs (nullable): also the reset env's
+// observation — the rollout's next observation of the envs it resets
 constexpr int kOaResetWaves = 4;
 
-// obs (nullable): also the reset env's observation (get_state: the head and the 37-beam scan of
-// the new pose, one beam per lane) — the rollout's next observation of the envs it resets
 __global__ void __launch_bounds__(64 * kOaResetWaves) oa_reset_kernel(
     OA::P p, double *state, int n, const uint8_t *mask, const double *init, uint64_t seed,
     uint64_t counter, uint64_t env_id0, float *obs) {
     __shared__ double obl[kOaResetWaves][OA::NOBS * 3];
-    __shared__ OaLds<kOaResetWaves> L;
+    __shared__ OaEnvLds L[kOaResetWaves];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int e = blockIdx.x * kOaResetWaves + w;
     if (e >= n || (mask && !mask[e])) return;  // uniform per wave
@@ -195,99 +158,8 @@ __global__ void __launch_bounds__(64 * kOaResetWaves) oa_reset_kernel(
         for (int d = lane; d < OA::D; d += 64) state[(size_t)d * n + i] = init[(size_t)d * n + i];
         return;
     }
-    const uint64_t id = env_id0 + (uint64_t)e;
-    double sx, sy;
-    OA::draw_point(p, seed, counter, id, OA::kTagStart, sx, sy);
-    double tx = sx, ty = sy;
-    if (!(0.0 >= p.safety_dis_st)) {  // terminal = start fails the distance test: redraw
-        for (int t0 = 0; t0 < p.max_tries; t0 += 64) {
-            const int t = t0 + lane;
-            double cx = 0, cy = 0;
-            bool ok = false;
-            if (t < p.max_tries) {
-                OA::draw_point(p, seed, counter, id, OA::kTagTarget + (uint32_t)t, cx, cy);
-                const double dx = cx - sx, dy = cy - sy;
-                ok = sqrt(dx * dx + dy * dy) >= p.safety_dis_st;
-            }
-            const uint64_t b = __ballot(ok);
-            const bool last = t0 + 64 >= p.max_tries;
-            if (b || last) {  // first legal try, else the last try drawn
-                const int src = b ? __ffsll((unsigned long long)b) - 1 : (p.max_tries - 1 - t0);
-                tx = __shfl(cx, src);
-                ty = __shfl(cy, src);
-                break;
-            }
-        }
-    }
-    for (int k = 0; k < OA::NOBS; ++k) {
-        double cx = OA::parked_x(k), cy = OA::kParkedY, r = p.r_min;
-        for (int t0 = 0; k < p.n_obs && t0 < p.max_tries; t0 += 64) {
-            const int t = t0 + lane;
-            double ccx = 0, ccy = 0, rr = 0;
-            bool ok = false;
-            if (t < p.max_tries) {
-                OA::draw_obstacle(p, seed, counter, id, k, t, ccx, ccy, rr);
-                ok = OA::legal(p, sx, sy, tx, ty, ccx, ccy, rr, k,
-                               [&](int j, double &x0, double &y0, double &r0) {
-                                   x0 = obl[w][3 * j]; y0 = obl[w][3 * j + 1]; r0 = obl[w][3 * j + 2];
-                               });
-            }
-            const uint64_t b = __ballot(ok);
-            if (b) {
-                const int src = __ffsll((unsigned long long)b) - 1;
-                cx = __shfl(ccx, src);
-                cy = __shfl(ccy, src);
-                r = __shfl(rr, src);
-                break;
-            }
-        }
-        if (lane == 0) {
-            obl[w][3 * k] = cx;
-            obl[w][3 * k + 1] = cy;
-            obl[w][3 * k + 2] = r;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    double u[2];
-    philox_u01_f64x2(seed, counter, id, OA::kTagPhi, u);
-    const double head[OA::DW] = {sx, sy, 0., -kPi + (kPi - -kPi) * u[0], 0., 0., tx, ty};
-    if (lane < OA::DW) {
-        double v = head[0];
-#pragma unroll
-        for (int d = 1; d < OA::DW; ++d) v = lane == d ? head[d] : v;
-        state[(size_t)lane * n + i] = v;
-    }
-    if (lane < OA::NOBS * 3) state[(size_t)(OA::OB + lane) * n + i] = obl[w][lane];
-    if (!obs) return;
-    if (lane == 0) {  // the per-pose setup of oa_kernel's observe, for this wave's env
-        for (int k = 0; k < p.n_obs; ++k) {
-            L.ob[w][k].x0 = obl[w][3 * k];
-            L.ob[w][k].y0 = obl[w][3 * k + 1];
-            L.ob[w][k].r0 = obl[w][3 * k + 2];
-        }
-        oa_setup(p, L, w, head);
-        float h[4];
-        OA::obs_head(p, head, OA::get_e(head), OA::e_phi(head), h);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) obs[i * OA::S + j] = h[j];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane < OA::NL) {  // oa_scan's beam, one per lane
-        float v = OA::beam_obs(p, p.laser_blind);
-        if (!L.coll[w]) {
-            const OA::Pose q = L.q[w];
-            v = OA::beam_obs(p, OA::beam(p, q, lane, [&](int k, double &x0, double &y0, double &r0,
-                                                         double &rf) {
-                const OaObstacle o = L.ob[w][k];
-                x0 = o.x0; y0 = o.y0; r0 = o.r0; rf = o.ref;
-            }));
-        }
-        obs[i * OA::S + 4 + lane] = v;
-    }
+    oa_reset_wave(p, state, n, i, seed, counter, env_id0 + (uint64_t)e,
+                  obs ? obs + i * OA::S : nullptr, obl[w], L[w]);
 }
 
 int launch_ugvoa_reset(const rlp_ugv_oa_params &p, double *state, int n, const uint8_t *mask,

@@ -10,6 +10,7 @@
 //   buffer.append(...)                 utils/classes.py:264-272, time-major [T][n][...]
 // The two MLPs are fp32 MFMA (v_mfma_f32_16x16x4_f32): this kernel is MFMA-bound.
 #include "rlp_envs.hpp"
+#include "rlp_lidar.hpp"
 #include "rlp_mfma_layout.hpp"
 #include "rlp_mfma_x3.hpp"
 
@@ -464,30 +465,39 @@ rollout_sp_kernel(SpArgs<KIND> args) {
 
 // ------------------------------------------------------------------------------------------
 // Packed-net forward over rows (evaluate(), learn()'s V(s) / V(s'), the value fix-up).
-// Each wave walks 16*SUB-row groups (grid-stride); with a row predicate, groups without an
-// active row are skipped wave-uniformly.
+// Exact f32 (X3 = false): each wave walks 16*SUB-row groups (grid-stride, its own W2 ring); with a
+// row predicate, groups without an active row are skipped wave-uniformly. f16x3 (X3 = true): the
+// hidden layer on the rollout's split (mlp_x3_forward), the block's 4 waves sharing one W2 chunk
+// ring, so the block walks 4 groups at a time (block-uniform trip count and skips).
 // ------------------------------------------------------------------------------------------
-template <int H, int SUB, int KS1, int NOUT, int MODE>  // MODE 0: all rows; 1: done && !success
+template <int H, int SUB, int KS1, int NOUT, int MODE, bool X3>  // MODE 0: all rows; 1: done && !success
 __global__ void __launch_bounds__(256, (SUB == 4 ? 1 : 2))
 packed_forward_kernel(const float *__restrict__ P, MfmaNet net, const float *__restrict__ x,
                       float *__restrict__ y, int64_t rows, const uint8_t *__restrict__ done,
                       const uint8_t *__restrict__ success, int apply_out_act) {
     constexpr int WROWS = 16 * SUB;
     constexpr int SMALL = mlp_small_floats<H, KS1, NOUT>(), PF = mlp_phase_floats<H>();
+    static_assert(4 * RING * PF == kX3RingFloats, "one LDS carve for both arithmetics");
     __shared__ __attribute__((aligned(16))) float lds[SMALL + 4 * RING * PF];
-    float *small = lds, *ring = lds + SMALL + (threadIdx.x >> 6) * RING * PF;
-    mlp_small_to_lds(P, net, small);
+    float *small = lds, *ring = lds + SMALL + (X3 ? 0 : (threadIdx.x >> 6) * RING * PF);
+    mlp_small_to_lds(P, net, small, X3);
     __syncthreads();
     const int lane = threadIdx.x & 63, g = lane >> 4, e = lane & 15;
     const int S = net.S;
     const int64_t nwaves = (int64_t)gridDim.x * 4;
-    for (int64_t grp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); grp * WROWS < rows;
-         grp += nwaves) {
+    // X3: group (bg * 4 + wave) for block-uniform bg; else the wave's own grid-stride groups
+    const int64_t g0 = X3 ? (int64_t)blockIdx.x * 4 : (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    for (int64_t gb = g0; gb * WROWS < rows; gb += nwaves) {
+        const int64_t grp = X3 ? gb + (threadIdx.x >> 6) : gb;
         const int64_t r0 = grp * WROWS;
         bool act_row = false;
         if (lane < WROWS && r0 + lane < rows)
             act_row = MODE == 0 ? true : (done[r0 + lane] && !success[r0 + lane]);
-        if (!__any(act_row)) continue;  // wave-uniform
+        if constexpr (X3) {
+            if (!__syncthreads_or(act_row)) continue;  // block-uniform
+        } else {
+            if (!__any(act_row)) continue;  // wave-uniform
+        }
         float bobs[SUB][KS1];
 #pragma unroll
         for (int sb = 0; sb < SUB; ++sb)
@@ -498,7 +508,10 @@ packed_forward_kernel(const float *__restrict__ P, MfmaNet net, const float *__r
                 bobs[sb][kk] = (row < rows && k < S) ? x[row * S + k] : 0.f;
             }
         float out[SUB][NOUT];
-        mlp_fused_forward<H, SUB, KS1, NOUT, RING>(P, small, ring, net, net.A, bobs, out);
+        if constexpr (X3)
+            mlp_x3_forward<H, SUB, KS1, NOUT>(P, small, ring, net, net.A, bobs, out);
+        else
+            mlp_fused_forward<H, SUB, KS1, NOUT, RING>(P, small, ring, net, net.A, bobs, out);
         // lane (sub-block g, row e) owns out[g]; lanes 0..WROWS-1 store their row
         float sel[NOUT];
 #pragma unroll
@@ -517,7 +530,7 @@ packed_forward_kernel(const float *__restrict__ P, MfmaNet net, const float *__r
     }
 }
 
-template <int MODE, int SUB>
+template <int MODE, int SUB, bool X3>
 static int launch_packed_forward_sub(const MfmaNet &net, const float *P, const float *x, float *y,
                                      int64_t rows, const uint8_t *done, const uint8_t *success,
                                      int apply_out_act, hipStream_t s) {
@@ -526,7 +539,7 @@ static int launch_packed_forward_sub(const MfmaNet &net, const float *P, const f
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) return RLP_OK;
 #define RLP_PF(KS1, NOUT)                                                                       \
-    packed_forward_kernel<256, SUB, KS1, NOUT, MODE><<<(int)blocks, 256, 0, s>>>(             \
+    packed_forward_kernel<256, SUB, KS1, NOUT, MODE, X3><<<(int)blocks, 256, 0, s>>>(         \
         P, net, x, y, rows, done, success, apply_out_act)
     if (net.ks1 == 1) {
         if (net.A == 1) RLP_PF(1, 1); else if (net.A == 2) RLP_PF(1, 2); else if (net.A == 3) RLP_PF(1, 3); else RLP_PF(1, 4);
@@ -541,16 +554,20 @@ static int launch_packed_forward_sub(const MfmaNet &net, const float *P, const f
     return RLP_OK;
 }
 
-// 64 rows per wave for large batches (learn()'s V(s) over a whole segment), 16 when that would
-// leave CUs idle (the lidar rollout's per-step forwards over n envs; the value fix-up)
+// exact f32: 64 rows per wave for large batches (learn()'s V(s) over a whole segment), 16 when
+// that would leave CUs idle (the value fix-up); f16x3: 32 rows per wave for large batches
 template <int MODE>
 static int launch_packed_forward(const MfmaNet &net, const float *P, const float *x, float *y,
                                  int64_t rows, const uint8_t *done, const uint8_t *success,
-                                 int apply_out_act, hipStream_t s) {
+                                 int apply_out_act, int prec, hipStream_t s) {
     if (net.H != 256) return fail(RLP_EUNSUPPORTED, "packed forward: hidden width %d", net.H);
-    if (MODE == 0 && rows >= (int64_t)64 * 4 * 2 * device_cus())
-        return launch_packed_forward_sub<MODE, 4>(net, P, x, y, rows, done, success, apply_out_act, s);
-    return launch_packed_forward_sub<MODE, 1>(net, P, x, y, rows, done, success, apply_out_act, s);
+    const bool big = MODE == 0 && rows >= (int64_t)64 * 4 * 2 * device_cus();
+    if (prec == RLP_MLP_F16X3) {
+        if (big) return launch_packed_forward_sub<MODE, 2, true>(net, P, x, y, rows, done, success, apply_out_act, s);
+        return launch_packed_forward_sub<MODE, 1, true>(net, P, x, y, rows, done, success, apply_out_act, s);
+    }
+    if (big) return launch_packed_forward_sub<MODE, 4, false>(net, P, x, y, rows, done, success, apply_out_act, s);
+    return launch_packed_forward_sub<MODE, 1, false>(net, P, x, y, rows, done, success, apply_out_act, s);
 }
 
 static int g_rollout_shared_physics = -1;  // rlp_set_rollout_physics (-1: auto)
@@ -646,110 +663,212 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
 // UGVForwardObstacleAvoidance PPO2 / DPPO2 rollout (demonstration/PPO2/PPO2-4-UGVForward
 // ObstacleAvoidance/train.py:48-50,95-97: 41 -> 256 -> 256 -> 2 actor, 41 -> 256 -> 256 -> 1
 // critic, tanh; DPPO2 copy likewise). The 41 inputs (4 + 37 lidar beams), the lidar scan and the
-// 38-double env state (10 obstacle circles travel with the env) do not fit the fused kernel's LDS,
-// so ONE rlp_rollout call runs the same driver loop as a sequence of kernels per step on the
-// caller's stream (no host round trip, no synchronisation):
-//   critic V(s_t), actor z_t            packed forward (layer 1 as 11 K-steps of 16x16x4 f32 MFMA)
-//   oa_sample_kernel                    mean = tanh(z) gain + off, Philox eps (the fused kernel's
-//                                       stream), clamp, log-prob; V(s'_{t-1}) = V(s_t) where the env
-//                                       did not end at t-1
-//   lidar env step (oa_kernel)          obs_next, reward, flag, done
-//   oa_post_kernel                      f32 reward, i8 flag, success rule
-//   reset of ended envs (map generator, counter step0 + t + 1) and the next observation (lidar)
-// and after the segment the bootstrap V(s'_{T-1}) of the envs still running. Same semantics, same
-// random draws and same buffers as the fused kernel; the MLPs run on the exact f32 MFMA path.
-using OA = Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE>;
+// 53-double env state (up to 15 obstacle circles travel with the env) do not fit the fused
+// kernel's LDS next to the 41-wide layer 1, so ONE rlp_rollout call runs the driver loop as TWO
+// launches per step on the caller's stream (no host round trip, no synchronisation):
+//   oa_policy_kernel   per 16-env wave: actor and critic forward (layer 1 as 11 K-steps of the
+//                      exact f32 16x16x4 MFMA, the 256 x 256 hidden layer on the f16x3 split of
+//                      the fused rollout, or exact f32 under RLP_MLP_FP32), then the Philox sample
+//                      (the fused kernel's stream), clamp, log-prob, V(s_t), and V(s'_{t-1}) =
+//                      V(s_t) where the env did not end at t-1
+//   oa_step_kernel     lidar env step (dynamics, terminal, reward: one lane per env), the
+//                      success rule, the 37-beam scan of s' (one (env, beam) pair per lane) into
+//                      obs_next and — for envs still running — obs_{t+1}; ended envs reset with the
+//                      map generator (one wave per env, counter step0 + t + 1) and scan the new pose
+//                      into obs_{t+1}
+// and after the segment the bootstrap V(s'_{T-1}) of the envs still running (oa_policy_kernel,
+// critic only). Same semantics, same random draws and same buffers as the fused kernels.
+struct OaPolicyArgs {
+    const float *actor, *critic;
+    MfmaNet an, cn;
+    RolloutArgs ra;
+    rlp_rollout_bufs b;
+    int t;     // step of this launch
+    int boot;  // 1: critic on obs_next[T-1] -> value_next of the envs still running
+};
 
-__global__ void __launch_bounds__(256) oa_sample_kernel(RolloutArgs ra, int t, int out_tanh,
-                                                        rlp_rollout_bufs b) {
-    const int i = blockIdx.x * 256 + threadIdx.x, n = ra.n;
-    if (i >= n) return;
-    constexpr int A = OA::A;
-    const int k = t * n + i;
-    float eps[A];
-    philox_normal_f32<A>(ra.seed, ra.step0 + (uint64_t)t, ra.env_id0 + (uint64_t)i, eps);
+#ifndef RLP_OA_DIAG
+#define RLP_OA_DIAG 0
+#endif
+constexpr int kOaPolWaves = 4;  // 16-env waves per block, one block per CU (1 wave per SIMD)
+constexpr int kOaKs1 = (OA::S + 3) / 4;
+constexpr int kOaSmall = mlp_small_floats<256, kOaKs1, OA::A>();
+constexpr int kOaRing = kX3Ring * kX3ChunkFloats;  // f32 path: kOaPolWaves x RING x phase, same size
+static_assert(kOaRing == kOaPolWaves * RING * mlp_phase_floats<256>(), "one LDS carve for both paths");
+
+template <bool X3>
+__global__ void __launch_bounds__(64 * kOaPolWaves, 1) oa_policy_kernel(OaPolicyArgs pa) {
+    constexpr int A = OA::A, S = OA::S, KS1 = kOaKs1, ROWS = 16 * kOaPolWaves;
+    __shared__ __attribute__((aligned(16))) float lds[2 * kOaSmall + kOaRing];
+    float *small_a = lds, *small_c = lds + kOaSmall, *ring0 = lds + 2 * kOaSmall;
+    const MfmaNet an = pa.an, cn = pa.cn;
+    if (!pa.boot) mlp_small_to_lds(pa.actor, an, small_a, X3);
+    mlp_small_to_lds(pa.critic, cn, small_c, X3);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, e = lane & 15;
+    float *ring = ring0 + (X3 ? 0 : wave * RING * mlp_phase_floats<256>());
+    const RolloutArgs &ra = pa.ra;
+    const int n = ra.n, t = pa.t;
+    const float *x = pa.boot ? pa.b.obs_next + (size_t)(ra.T - 1) * n * S : pa.b.obs + (size_t)t * n * S;
+    // block-uniform trip count (mlp_x3_forward's ring barriers need every wave in every call)
+    for (int r0 = blockIdx.x * ROWS; r0 < n; r0 += gridDim.x * ROWS) {
+        const int row = r0 + 16 * wave + e;
+        float bobs[1][KS1];
 #pragma unroll
-    for (int a = 0; a < A; ++a) {
-        const float mr = b.action[k * A + a];  // the actor's pre-activation, written in place
-        const float m = (out_tanh ? tanhf(mr) : mr) * ra.gain[a] + ra.off[a];
-        float x = m + ra.std_[a] * eps[a];
-        x = fmaxf(fminf(x, ra.a_max[a]), ra.a_min[a]);
-        b.action[k * A + a] = x;
-        b.logp[k * A + a] = normal_logp_c(x, m, ra.half_inv_var[a], ra.log_std[a]);
-    }
-    if (t > 0 && !b.done[k - n]) b.value_next[k - n] = b.value[k];  // V(s'_{t-1}) == V(s_t)
-}
-
-__global__ void __launch_bounds__(256) oa_post_kernel(RolloutArgs ra, int t, const double *r64,
-                                                      const int32_t *f32, rlp_rollout_bufs b,
-                                                      uint8_t *need_reset) {
-    const int i = blockIdx.x * 256 + threadIdx.x, n = ra.n;
-    if (i >= n) return;
-    const int k = t * n + i;
-    const bool dn = b.done[k] != 0;
-    b.reward[k] = (float)r64[i];
-    b.flag[k] = (int8_t)f32[i];
-    b.success[k] = success_of(ra.success_rule, ra.success_flag, dn, f32[i]);
-    if (t == ra.T - 1) need_reset[i] = dn;  // ended envs of the last step reset next segment
-    if (t + 1 < ra.T && !dn) {  // current_state = next_state (the reset kernel writes the others)
-        const float *src = b.obs_next + (size_t)k * OA::S;
-        float *dst = b.obs + (size_t)(k + n) * OA::S;
+        for (int kk = 0; kk < KS1; ++kk)
+            bobs[0][kk] = (row < n && 4 * kk + g < S) ? x[(size_t)row * S + 4 * kk + g] : 0.f;
+        float mraw[A] = {}, v = 0.f;
+#pragma unroll 1
+        for (int which = pa.boot ? 1 : 0; which < 2; ++which) {
+            float out[1][A];
+            if constexpr (X3)
+                mlp_x3_forward<256, 1, KS1, A>(which ? pa.critic : pa.actor, which ? small_c : small_a,
+                                               ring, which ? cn : an, which ? 1 : A, bobs, out);
+            else
+                mlp_fused_forward<256, 1, KS1, A, RING>(which ? pa.critic : pa.actor,
+                                                        which ? small_c : small_a, ring,
+                                                        which ? cn : an, which ? 1 : A, bobs, out);
+            if (which) v = out[0][0];
+            else
 #pragma unroll
-        for (int j = 0; j < OA::S; ++j) dst[j] = src[j];
+                for (int a = 0; a < A; ++a) mraw[a] = out[0][a];
+        }
+        if (g != 0 || row >= n) continue;  // lane e of group 0 owns env `row`
+        const rlp_rollout_bufs &b = pa.b;
+        if (pa.boot) {
+            const size_t k = (size_t)(ra.T - 1) * n + row;
+            if (!b.done[k]) b.value_next[k] = v;
+            continue;
+        }
+        const size_t k = (size_t)t * n + row;
+        float eps[A];
+        philox_normal_f32<A>(ra.seed, ra.step0 + (uint64_t)t, ra.env_id0 + (uint64_t)row, eps);
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            const float m = (an.out_tanh ? tanhf(mraw[a]) : mraw[a]) * ra.gain[a] + ra.off[a];
+            float xa = m + ra.std_[a] * eps[a];
+            xa = fmaxf(fminf(xa, ra.a_max[a]), ra.a_min[a]);
+            b.action[k * A + a] = xa;
+            b.logp[k * A + a] = normal_logp_c(xa, m, ra.half_inv_var[a], ra.log_std[a]);
+        }
+        b.value[k] = v;
+        if (t > 0 && !b.done[k - n]) b.value_next[k - n] = v;  // V(s'_{t-1}) == V(s_t)
     }
 }
 
-__global__ void __launch_bounds__(256) oa_boot_kernel(int T, int n, const float *v, rlp_rollout_bufs b) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const int k = (T - 1) * n + i;
-    if (!b.done[k]) b.value_next[k] = v[i];
-}
-
-inline int64_t rollout_oa_ws_bytes(int n) {
-    return (int64_t)n * (int64_t)(sizeof(double) + sizeof(int32_t) + sizeof(float));
+// EB envs per block: phase 1 one lane per env, phase 2 the EB x 37 (env, beam) pairs over the
+// block, phase 3 the ended envs' resets, one wave per env
+template <int EB>
+__global__ void __launch_bounds__(256) oa_step_kernel(OA::P p, double *state, uint8_t *need_reset,
+                                                      RolloutArgs ra, int t, rlp_rollout_bufs b) {
+    constexpr int S = OA::S, A = OA::A, NW = 4;
+    __shared__ OaEnvLds L[EB];
+    __shared__ OaEnvLds Lr[NW];
+    __shared__ double obl[NW][OA::NOBS * 3];
+    __shared__ uint8_t s_done[EB];
+    const int tid = threadIdx.x, n = ra.n;
+    const int e0 = blockIdx.x * EB, ne = n - e0 < EB ? n - e0 : EB;
+    const bool more = t + 1 < ra.T;  // a step t + 1 follows in this segment
+    const size_t k0 = (size_t)t * n;
+    if (tid < ne) {
+        const size_t i = (size_t)e0 + tid, k = k0 + i;
+        double s[OA::DW];
+#pragma unroll
+        for (int d = 0; d < OA::DW; ++d) s[d] = state[(size_t)d * n + i];
+        for (int kk = 0; kk < p.n_obs; ++kk) {
+            L[tid].ob[kk].x0 = state[(size_t)(OA::OB + 3 * kk) * n + i];
+            L[tid].ob[kk].y0 = state[(size_t)(OA::OB + 3 * kk + 1) * n + i];
+            L[tid].ob[kk].r0 = state[(size_t)(OA::OB + 3 * kk + 2) * n + i];
+        }
+        const float a[A] = {b.action[k * A], b.action[k * A + 1]};
+        double r, e, eph;
+        int f;
+        bool dn;
+        OA::step_core(p, s, a, [&](double x, double y) {
+            return OA::collision_at(p, x, y, [&](int kk, double &x0, double &y0, double &r0) {
+                x0 = L[tid].ob[kk].x0; y0 = L[tid].ob[kk].y0; r0 = L[tid].ob[kk].r0;
+            });
+        }, r, f, dn, e, eph);
+        if (!(dn && more)) {  // an env that resets below gets its whole state from the reset
+#pragma unroll
+            for (int d = 0; d < OA::DW; ++d) state[(size_t)d * n + i] = s[d];
+        }
+        b.reward[k] = (float)r;
+        b.flag[k] = (int8_t)f;
+        b.done[k] = dn;
+        b.success[k] = success_of(ra.success_rule, ra.success_flag, dn, f);
+        if (!more) need_reset[i] = dn;  // ended envs of the last step reset next segment
+        s_done[tid] = dn;
+        oa_setup(p, L[tid], s);
+        float h[4];
+        OA::obs_head(p, s, e, eph, h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b.obs_next[k * S + j] = h[j];
+        if (more && !dn) {  // current_state = next_state
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b.obs[(k + n) * S + j] = h[j];
+        }
+    }
+    __syncthreads();
+#if RLP_OA_DIAG & 2  // timing-only diagnostic build (wrong observations by construction)
+    for (int it = tid; it < 0; it += 256) {
+#else
+    for (int it = tid; it < ne * OA::NL; it += 256) {
+#endif
+        const int le = it / OA::NL, i = it - le * OA::NL;
+        const size_t k = k0 + e0 + le;
+        const float v = oa_beam(p, L[le], i);
+        b.obs_next[k * S + 4 + i] = v;
+        if (more && !s_done[le]) b.obs[(k + n) * S + 4 + i] = v;
+    }
+    if (!more) return;
+#if RLP_OA_DIAG & 1  // timing-only diagnostic build (no resets)
+    return;
+#endif
+    // the ended envs' resets (counter step0 + t + 1) and their obs_{t+1}: wave w takes the block's
+    // ended envs w, w + NW, ... in env order (s_done is final since the barrier above)
+    const int w = tid >> 6;
+    int c = 0;
+    for (int le = 0; le < ne; ++le) {
+        if (!s_done[le]) continue;
+        if (c++ % NW != w) continue;
+        const size_t i = (size_t)e0 + le;
+        oa_reset_wave(p, state, n, i, ra.seed, ra.step0 + (uint64_t)t + 1, ra.env_id0 + i,
+                      b.obs + (k0 + n + i) * S, obl[w], Lr[w]);
+    }
 }
 
 static int rollout_oa(const void *params, double *state, uint8_t *need_reset, const float *actor,
                       const MfmaNet &an, const float *critic, const MfmaNet &cn,
-                      const RolloutArgs &ra, const rlp_rollout_bufs &b, void *ws, hipStream_t s) {
+                      const RolloutArgs &ra, const rlp_rollout_bufs &b, int prec, hipStream_t s) {
     const auto &p = *static_cast<const OA::P *>(params);
     if (an.S != OA::S || cn.S != OA::S || an.A != OA::A || cn.A != 1)
         return fail(RLP_EINVAL, "rlp_rollout: net dims (S=%d,A=%d / S=%d,A=%d) != env (S=%d,A=%d)",
                     an.S, an.A, cn.S, cn.A, OA::S, OA::A);
     if (an.H != 256 || cn.H != 256)
         return fail(RLP_EUNSUPPORTED, "rlp_rollout: hidden width %d/%d (built for 256)", an.H, cn.H);
-    const int n = ra.n, T = ra.T, nb = (n + 255) / 256;
-    // the caller's scratch (rollout_oa_ws_bytes): the step's f64 reward, i32 flag, the bootstrap V
-    double *r64 = static_cast<double *>(ws);
-    int32_t *f32 = reinterpret_cast<int32_t *>(r64 + n);
-    float *vb = reinterpret_cast<float *>(f32 + n);
+    if (p.n_obs < 0 || p.n_obs > OA::NOBS)
+        return fail(RLP_EINVAL, "UGVForwardObstacleAvoidance: n_obs=%d (0..%d)", p.n_obs, OA::NOBS);
+    const int n = ra.n, T = ra.T;
+    const int cus = device_cus();
+    const int rows_pb = 16 * kOaPolWaves;
+    const int pblocks = (n + rows_pb - 1) / rows_pb < cus ? (n + rows_pb - 1) / rows_pb : cus;
+    // fewer envs per block when the batch is small, so every CU gets several blocks
+    const bool eb64 = (n + 63) / 64 >= 4 * cus;
+    auto policy = [&](int t, int boot) {
+        const OaPolicyArgs pa{actor, critic, an, cn, ra, b, t, boot};
+        if (prec == RLP_MLP_F16X3) oa_policy_kernel<true><<<pblocks, 64 * kOaPolWaves, 0, s>>>(pa);
+        else oa_policy_kernel<false><<<pblocks, 64 * kOaPolWaves, 0, s>>>(pa);
+    };
     int rc = launch_ugvoa_reset(p, state, n, need_reset, nullptr, ra.seed, ra.step0, ra.env_id0, s);
     if (rc == RLP_OK) rc = launch_ugvoa_observe(p, state, n, b.obs, s);
-    for (int t = 0; t < T && rc == RLP_OK; ++t) {
-        const size_t k0 = (size_t)t * n;
-        float *obs_t = b.obs + k0 * OA::S;
-        rc = launch_packed_forward<0>(cn, critic, obs_t, b.value + k0, n, nullptr, nullptr, 0, s);
-        if (rc == RLP_OK)
-            rc = launch_packed_forward<0>(an, actor, obs_t, b.action + k0 * OA::A, n, nullptr,
-                                          nullptr, 0, s);
-        if (rc != RLP_OK) break;
-        oa_sample_kernel<<<nb, 256, 0, s>>>(ra, t, an.out_tanh, b);
-        rc = launch_ugvoa_step(p, state, n, b.action + k0 * OA::A, nullptr, b.obs_next + k0 * OA::S,
-                               r64, f32, b.done + k0, s);
-        if (rc != RLP_OK) break;
-        oa_post_kernel<<<nb, 256, 0, s>>>(ra, t, r64, f32, b, need_reset);
-        if (t + 1 < T)  // the ended envs' reset with the next step's counter and their obs_{t+1}
-                        // (the others' obs_{t+1} = obs_next_t, copied by oa_post_kernel)
-            rc = launch_ugvoa_reset(p, state, n, b.done + k0, nullptr, ra.seed, ra.step0 + t + 1,
-                                    ra.env_id0, s, b.obs + (k0 + n) * OA::S);
-    }
-    if (rc == RLP_OK) {  // V(s'_{T-1}) of the envs still running
-        rc = launch_packed_forward<0>(cn, critic, b.obs_next + (size_t)(T - 1) * n * OA::S, vb, n,
-                                      nullptr, nullptr, 0, s);
-        if (rc == RLP_OK) oa_boot_kernel<<<nb, 256, 0, s>>>(T, n, vb, b);
-    }
     if (rc != RLP_OK) return rc;
+    for (int t = 0; t < T; ++t) {
+        policy(t, 0);
+        if (eb64) oa_step_kernel<64><<<(n + 63) / 64, 256, 0, s>>>(p, state, need_reset, ra, t, b);
+        else oa_step_kernel<16><<<(n + 15) / 16, 256, 0, s>>>(p, state, need_reset, ra, t, b);
+    }
+    policy(T - 1, 1);  // V(s'_{T-1}) of the envs still running
     RLP_CHECK_LAUNCH("rlp_rollout (UGVForwardObstacleAvoidance)");
     return RLP_OK;
 }
@@ -843,6 +962,13 @@ __global__ void __launch_bounds__(256) plain_step_kernel(typename Env<KIND>::P p
     for (int d = 0; d < E::D; ++d) state[(size_t)d * n + i] = s[d];
 }
 
+__global__ void __launch_bounds__(256) oa_boot_kernel(int T, int n, const float *v, rlp_rollout_bufs b) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int k = (T - 1) * n + i;
+    if (!b.done[k]) b.value_next[k] = v[i];
+}
+
 // the plain path's scratch: the bootstrap V, then rlp_mlp_forward's workspace (shared by the two
 // nets' forwards, which run one after the other on the stream)
 inline int64_t rollout_plain_ws_bytes(const rlp_mlp_desc &ad, const rlp_mlp_desc &cd, int n) {
@@ -924,27 +1050,40 @@ int rlp_set_rollout_sub(int sub) {
     return RLP_OK;
 }
 
+// per-call arithmetic (include/rlp.h): 0 = the library-wide default (rlp_set_mlp_precision),
+// else RLP_MLP_* + 1
+static int call_precision(int mlp_precision, int *prec, const char *what) {
+    if (mlp_precision < 0 || mlp_precision > 2)
+        return fail(RLP_EINVAL, "%s: mlp_precision %d (0 default, 1 fp32, 2 f16x3)", what, mlp_precision);
+    *prec = mlp_precision ? mlp_precision - 1 : g_mlp_precision;
+    return RLP_OK;
+}
+
 int rlp_mfma_forward(const rlp_mlp_desc *desc, const float *packed, const float *x, float *y,
-                     int64_t rows, rlp_stream_t stream) {
+                     int64_t rows, int mlp_precision, rlp_stream_t stream) {
     RLP_REQUIRE(desc && packed && x && y, "rlp_mfma_forward: null argument");
+    int prec;
+    if (const int rc = call_precision(mlp_precision, &prec, "rlp_mfma_forward")) return rc;
     MfmaNet net;
     if (!mfma_net_from_desc(*desc, &net))
         return fail(RLP_EUNSUPPORTED, "rlp_mfma_forward: need a [S->H->H->A] tanh MLP");
     if (rows <= 0) return rows == 0 ? RLP_OK : RLP_EINVAL;
-    return launch_packed_forward<0>(net, packed, x, y, rows, nullptr, nullptr, 1, as_stream(stream));
+    return launch_packed_forward<0>(net, packed, x, y, rows, nullptr, nullptr, 1, prec, as_stream(stream));
 }
 
 int rlp_value_fixup(const rlp_mlp_desc *critic_desc, const float *critic_packed,
                     const float *obs_next, const uint8_t *done, const uint8_t *success,
-                    float *value_next, int64_t rows, rlp_stream_t stream) {
+                    float *value_next, int64_t rows, int mlp_precision, rlp_stream_t stream) {
     RLP_REQUIRE(critic_desc && critic_packed && obs_next && done && success && value_next,
                 "rlp_value_fixup: null argument");
+    int prec;
+    if (const int rc = call_precision(mlp_precision, &prec, "rlp_value_fixup")) return rc;
     MfmaNet net;
     if (!mfma_net_from_desc(*critic_desc, &net) || net.A != 1)
         return fail(RLP_EUNSUPPORTED, "rlp_value_fixup: need a [S->H->H->1] critic");
     if (rows <= 0) return rows == 0 ? RLP_OK : RLP_EINVAL;
     return launch_packed_forward<1>(net, critic_packed, obs_next, value_next, rows, done, success,
-                                    1, as_stream(stream));
+                                    1, prec, as_stream(stream));
 }
 
 int64_t rlp_rollout_workspace_bytes(int kind, const rlp_mlp_desc *actor_desc,
@@ -952,7 +1091,7 @@ int64_t rlp_rollout_workspace_bytes(int kind, const rlp_mlp_desc *actor_desc,
     if (!actor_desc || !critic_desc || !cfg || cfg->n < 0 || cfg->T < 1) return RLP_EINVAL;
     if (cfg->net_layout == 1) return rollout_plain_ws_bytes(*actor_desc, *critic_desc, cfg->n);
     if (cfg->net_layout != 0) return RLP_EINVAL;
-    return kind == RLP_ENV_UGV_OBSTACLE_AVOIDANCE ? rollout_oa_ws_bytes(cfg->n) : 0;
+    return 0;  // the fused kernels and the lidar env's two launches per step need no scratch
 }
 
 int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_reset,
@@ -1048,7 +1187,7 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
                                                           b, sub, prec, physics, s);
     case RLP_ENV_UGV_OBSTACLE_AVOIDANCE:
         return rollout_oa(env_params, state, need_reset, actor_packed, an, critic_packed, cn, ra, b,
-                          cfg->workspace, s);
+                          prec, s);
     }
     return fail(RLP_EINVAL, "rlp_rollout: unknown env kind %d", kind);
 }

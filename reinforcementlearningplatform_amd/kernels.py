@@ -80,22 +80,30 @@ def mfma_pack(desc, params, out=None):
     return out
 
 
-def mfma_forward(desc, packed, x, out=None):
-    """Forward of an MFMA-packed [S->H->H->A] net (last-layer activation applied)."""
+def _call_precision(precision):
+    """include/rlp.h per-call mlp_precision: 'fp32' (exact f32 MFMA, the default here), 'f16x3'
+    (the rollout's split hidden layer) or 'default' (the library-wide rlp_set_mlp_precision)."""
+    return {"default": 0, "fp32": 1, "f16x3": 2}[precision]
+
+
+def mfma_forward(desc, packed, x, out=None, precision="fp32"):
+    """Forward of an MFMA-packed [S->H->H->A] net (last-layer activation applied); the hidden
+    layer's arithmetic is chosen per call (`precision`, see _call_precision)."""
     rows = x.shape[0]
     outn = desc.dims[desc.n_layers]
     out = out if out is not None else torch.empty((rows, outn), dtype=torch.float32, device=x.device)
     x_ = x.contiguous()
     check(lib().rlp_mfma_forward(C.byref(desc), ptr(packed), ptr(x_), ptr(out), rows,
-                                 stream_ptr()), "rlp_mfma_forward")
+                                 _call_precision(precision), stream_ptr()), "rlp_mfma_forward")
     return out
 
 
-def value_fixup(critic_desc, critic_packed, obs_next, done, success, value_next):
+def value_fixup(critic_desc, critic_packed, obs_next, done, success, value_next, precision="fp32"):
     """value_next[i] = critic(obs_next[i]) where done & !success (flattened [T*n] rows)."""
     rows = done.numel()
     check(lib().rlp_value_fixup(C.byref(critic_desc), ptr(critic_packed), ptr(obs_next),
-                                ptr(done), ptr(success), ptr(value_next), rows, stream_ptr()),
+                                ptr(done), ptr(success), ptr(value_next), rows,
+                                _call_precision(precision), stream_ptr()),
           "rlp_value_fixup")
     return value_next
 

@@ -53,6 +53,32 @@ def test_bad_arguments_return_status():
     assert lib.rlp_mlp_param_count(C.byref(d)) == d.param_count() == 67329
 
 
+def test_refused_dense_launch_reaches_the_abi():
+    """A dense-GEMM launch the launcher refuses (problem count outside [1, 6]) inside a call chain
+    that drops the launcher's return value still comes back as a non-OK status: the
+    refusal is left pending and every entry point's launch check returns it. No device work."""
+    lib = _native.lib()
+    for n in (0, 7, -3):
+        assert lib.rlp_selftest_gemm_guard(n) == _abi.RLP_EINVAL, n
+        assert b"dense GEMM" in lib.rlp_last_error_string()
+    assert lib.rlp_selftest_gemm_guard(2) == _abi.RLP_EINVAL   # in range: refused up front
+    assert b"only out-of-range" in lib.rlp_last_error_string()
+
+
+def test_per_call_precision_is_validated():
+    """rlp_mfma_forward / rlp_value_fixup take the hidden layer's arithmetic per call (ABI 3):
+    0 default, 1 fp32, 2 f16x3; anything else is refused on the host."""
+    lib = _native.lib()
+    dev = C.c_void_p(1 << 20)  # never dereferenced
+    d = _abi.MLPDesc.make([4, 256, 256, 1], [1, 1, 0])
+    for bad in (-1, 3, 7):
+        assert lib.rlp_mfma_forward(C.byref(d), dev, dev, dev, 16, bad, None) == _abi.RLP_EINVAL
+        assert b"mlp_precision" in lib.rlp_last_error_string()
+        assert lib.rlp_value_fixup(C.byref(d), dev, dev, dev, dev, dev, 16, bad, None) == _abi.RLP_EINVAL
+    for ok in (0, 1, 2):   # zero rows: validated, nothing launched
+        assert lib.rlp_mfma_forward(C.byref(d), dev, dev, dev, 0, ok, None) == 0
+
+
 def test_workspaces_are_caller_owned_and_checked():
     """The multi-launch paths take a caller-owned workspace (no per-call device allocation):
     the queries size it, and a too-small one is refused on the host before any launch."""
@@ -86,8 +112,9 @@ def test_workspaces_are_caller_owned_and_checked():
     cfg.net_layout = 0
     big = _abi.MLPDesc.make([41, 256, 256, 2], [1, 1, 1])
     bigc = _abi.MLPDesc.make([41, 256, 256, 1], [1, 1, 0])
+    # the lidar env's rollout (two launches per step since round 6) needs no scratch either
     assert lib.rlp_rollout_workspace_bytes(_abi.RLP_ENV_UGV_OBSTACLE_AVOIDANCE, C.byref(big),
-                                           C.byref(bigc), C.byref(cfg)) == 16 * n
+                                           C.byref(bigc), C.byref(cfg)) == 0
     assert lib.rlp_rollout_workspace_bytes(_abi.RLP_ENV_CARTPOLE, C.byref(big), C.byref(bigc),
                                            C.byref(cfg)) == 0
 

@@ -182,6 +182,90 @@ def test_mfma_forward_and_value_fixup(kind):
     assert (vn[~need] == -123.0).all()
 
 
+@pytest.mark.parametrize("kind", [A.RLP_ENV_CARTPOLE, A.RLP_ENV_UAV_HOVER_OUTER_LOOP,
+                                  A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE])
+def test_mfma_forward_f16x3_per_call(kind):
+    """rlp_mfma_forward / rlp_value_fixup with the f16x3 hidden layer chosen per call (ABI 3):
+    against the oracle's double-accumulated nets at the exact path's bounds (rtol 1e-5, atol 2e-6),
+    at a row count that takes the 32-row-wave launch, and a value fix-up on a masked subset."""
+    D, S, Ad = A.ENV_DIMS[kind]
+    ad, ap, cd, cp = nets(S, Ad, seed=12)
+    rng = np.random.default_rng(kind + 100)
+    rows = 140_001
+    x = rng.uniform(-2, 2, (rows, S)).astype(np.float32)
+    apk, cpk = K.mfma_pack(ad, dev(ap)), K.mfma_pack(cd, dev(cp))
+    for d, pk, prm in ((ad, apk, ap), (cd, cpk, cp)):
+        y = host(K.mfma_forward(d, pk, dev(x), precision="f16x3"))
+        ref = oracle.mlp_forward(d, prm, x)
+        np.testing.assert_allclose(y, ref, rtol=1e-5, atol=2e-6)
+        y32 = host(K.mfma_forward(d, pk, dev(x), precision="fp32"))
+        assert not np.array_equal(y, y32)   # the two arithmetics really differ
+    v = host(K.mfma_forward(cd, cpk, dev(x), precision="f16x3"))
+    done = (rng.uniform(0, 1, rows) < 0.05).astype(np.uint8)
+    succ = (done * (rng.uniform(0, 1, rows) < 0.5)).astype(np.uint8)
+    vn = torch.full((rows,), -123.0, device="cuda")
+    K.value_fixup(cd, cpk, dev(x), dev(done), dev(succ), vn, precision="f16x3")
+    vn = host(vn)
+    need = (done == 1) & (succ == 0)
+    np.testing.assert_array_equal(vn[need], v[need, 0])   # same kernel arithmetic, bit for bit
+    assert (vn[~need] == -123.0).all()
+
+
+def test_two_threads_choose_precision_per_call():
+    """Two host threads, each on its own stream, run rlp_mfma_forward and rlp_rollout with
+    different hidden-layer arithmetics concurrently (fp32 in one, f16x3 in the other) while the
+    library-wide default is flipped in between: every result equals the same call made alone,
+    bit for bit (no global state is read by calls that choose per call)."""
+    import threading
+    kind = A.RLP_ENV_CARTPOLE
+    p = A.cartpole_params()
+    ad, ap, cd, cp = nets(4, 1, seed=21)
+    apk, cpk = K.mfma_pack(ad, dev(ap)), K.mfma_pack(cd, dev(cp))
+    x = dev(np.random.default_rng(5).uniform(-2, 2, (70_001, 4)).astype(np.float32))
+    n, T = 8192, 16
+
+    def work(prec):
+        mode = _native.MLP_FP32 if prec == "fp32" else _native.MLP_F16X3
+        y = K.mfma_forward(cd, cpk, x, precision=prec)
+        cfg = K.make_rollout_cfg(T, n, 9, 0, 0, [8 / 3], [-8], [8], A.RLP_SUCCESS_DONE_AND_FLAG_NE, 3,
+                                 mlp_precision=mode)
+        st = K.new_state(kind, n)
+        need = torch.ones(n, dtype=torch.uint8, device="cuda")
+        bufs = K.rollout_buffers(kind, T, n)
+        K.rollout(kind, p, st, need, ad, apk, cd, cpk, cfg, bufs)
+        return y, bufs["value"], bufs["action"], st
+
+    alone = {q: [t.clone() for t in work(q)] for q in ("fp32", "f16x3")}
+    torch.cuda.synchronize()
+    assert not torch.equal(alone["fp32"][0], alone["f16x3"][0])
+    got, errs = {}, []
+
+    def thread(q):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for _ in range(4):
+                    got[q] = [t.clone() for t in work(q)]
+            s.synchronize()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+    old = _native.get_mlp_precision()
+    try:
+        th = [threading.Thread(target=thread, args=(q,)) for q in ("fp32", "f16x3")]
+        for t in th:
+            t.start()
+        for m in (_native.MLP_FP32, _native.MLP_F16X3, _native.MLP_FP32):
+            _native.set_mlp_precision(m)   # the global default must not matter
+        for t in th:
+            t.join()
+    finally:
+        _native.set_mlp_precision(old)
+    assert not errs, errs
+    for q in ("fp32", "f16x3"):
+        for a, b in zip(got[q], alone[q]):
+            assert torch.equal(a, b), q
+
+
 @pytest.mark.parametrize("kind", [A.RLP_ENV_CARTPOLE, A.RLP_ENV_UAV_HOVER_OUTER_LOOP])
 def test_mlp_precision_modes_vs_float64(kind):
     """rlp_rollout's two hidden-layer arithmetics against a float64 evaluation of the critic on the
