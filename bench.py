@@ -198,6 +198,40 @@ def learn_roofline(flop_per_row, batch, learn_ms):
                     "graph: latency-bound at this batch, far from the roof"}
 
 
+def offpolicy_reuse(make_loop, n, ref_rows, flop_per_row, configs=((4096, 64), (16384, 16)),
+                    steps=3, warmup=1):
+    """The off-policy loop at the reference driver's sample reuse or near it: per vector step of n
+    transitions, `iters` learn() iterations of `batch` rows (one captured graph replayed iters
+    times), so sampled rows per transition = batch * iters / n against the reference's
+    `ref_rows` per transition (one ref_rows-row learn() per env step). Both configurations give
+    ratio 1/16 at the bench's n; the second takes 4x fewer, 4x fatter updates."""
+    out = []
+    for batch, iters in configs:
+        loop, agent = make_loop(batch, iters)
+        for _ in range(warmup):
+            loop.step(learn=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loop.step(learn=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        agent.learn(iter=iters)
+        ev[1].record()
+        torch.cuda.synchronize()
+        lms = ev[0].elapsed_time(ev[1]) / iters
+        out.append({"value": n * steps / dt, "unit": "env-steps/s", "batch": batch,
+                    "learn_iters_per_step": iters, "learn_ms": lms,
+                    "step_ms": dt / steps * 1e3,
+                    "sampled_rows_per_transition": batch * iters / n,
+                    "ratio_vs_reference": batch * iters / n / ref_rows,
+                    "learn_roofline": learn_roofline(flop_per_row, batch, lms)})
+        del loop, agent
+    return out
+
+
 def _net_dims(module):
     lin = [m for m in module.modules() if isinstance(m, torch.nn.Linear)]
     return [lin[0].in_features] + [l.out_features for l in lin]
@@ -528,7 +562,8 @@ def demo_nets_e2e_leg(rank, which, iters=2, seed=19):
     return out
 
 
-def soi_ddpg_leg(rank, n=65536, steps=20, warmup=3, batch=4096, capacity=1 << 20, seed=11):
+def soi_ddpg_leg(rank, n=65536, steps=20, warmup=3, batch=4096, capacity=1 << 20, seed=11,
+                 reuse_legs=True):
     """BASELINE config 3: SecondOrderIntegration DDPG (DDPG copy), n envs, replay buffer in HBM.
     One step = actor forward (librlp MLP, ReLU) + exploration noise + env step + n transitions
     into the replay ring + auto-reset, then one DDPG update on `batch` rows sampled from HBM
@@ -595,9 +630,18 @@ def soi_ddpg_leg(rank, n=65536, steps=20, warmup=3, batch=4096, capacity=1 << 20
             ev[1].record()
             torch.cuda.synchronize()
             out["learn_ms"] = ev[0].elapsed_time(ev[1]) / steps
+    def make_loop(b, iters):
+        torch.manual_seed(seed)
+        nets = [Actor(1e-4, 4, 2, lo, hi), Actor(1e-4, 4, 2, lo, hi), Critic(3e-4, 4, 2),
+                Critic(3e-4, 4, 2)]
+        ag = DDPG(msg, 0.99, 0.005, 0.005, capacity, b, *nets, device="cuda", seed=seed,
+                  graph=True, native=True)
+        return VecDDPG(env, ag, learn_iters=iters), ag
+    reuse = offpolicy_reuse(make_loop, n, 64, ddpg_learn_flops()) if reuse_legs else []
     return {"value": out["with_learn"], "unit": "env-steps/s", "env_only": out["env_only"],
             "with_learn_torch_update": out["with_learn_torch_update"], "learn_ms": out["learn_ms"],
             "learn_roofline": learn_roofline(ddpg_learn_flops(), batch, out["learn_ms"]),
+            "reference_reuse": reuse,
             "envs_per_gpu": n, "replay_capacity": capacity, "batch": batch, "learn_iters_per_step": 1,
             "update_to_data": {"sampled_rows_per_transition": batch / n, "reference": 64,
                                "reference_basis": "DDPG-4-SecondOrderIntegration/train.py:180,237: "
@@ -718,7 +762,8 @@ def ugvoa_ppo2_leg(rank, n=16384, T=64, iters=3, seed=17):
                       "rollout, nets [41,256,256,2] / [41,256,256,1] tanh (rlp_rollout)"}
 
 
-def ugvoa_sac_leg(rank, n=16384, steps=20, warmup=3, batch=4096, capacity=1 << 20, seed=13):
+def ugvoa_sac_leg(rank, n=16384, steps=20, warmup=3, batch=4096, capacity=1 << 20, seed=13,
+                  reuse_legs=True):
     """BASELINE config 5 shard: UGVForwardObstacleAvoidance SAC, n envs per GPU (131 072 / 8),
     replay in HBM. One step = actor trunk + squashed-Gaussian sample (librlp) + env step with the
     lidar kernel + n transitions into the replay ring + auto-reset (GPU map generator), then one
@@ -761,9 +806,18 @@ def ugvoa_sac_leg(rank, n=16384, steps=20, warmup=3, batch=4096, capacity=1 << 2
             ev[1].record()
             torch.cuda.synchronize()
             out["learn_ms"] = ev[0].elapsed_time(ev[1]) / steps
+    def make_loop(b, iters):
+        torch.manual_seed(seed)
+        ag = SAC(msg, 0.99, 0.005, capacity, b,
+                 SACActor(S, Ad, lo, hi, std_min=0.05, std_scale=1.), SACCritic(S, Ad),
+                 SACCritic(S, Ad), 1e-4, 1e-4, 1e-4, True, device="cuda", seed=seed, graph=True,
+                 native=True)
+        return VecSAC(env, ag, learn_iters=iters), ag
+    reuse = offpolicy_reuse(make_loop, n, 256, sac_learn_flops(S, Ad)) if reuse_legs else []
     return {"value": out["with_learn"], "unit": "env-steps/s", "env_only": out["env_only"],
             "with_learn_torch_update": out["with_learn_torch_update"], "learn_ms": out["learn_ms"],
             "learn_roofline": learn_roofline(sac_learn_flops(S, Ad), batch, out["learn_ms"]),
+            "reference_reuse": reuse,
             "envs_per_gpu": n, "replay_capacity": capacity, "batch": batch,
             "learn_iters_per_step": 1,
             "update_to_data": {"sampled_rows_per_transition": batch / n, "reference": 256,

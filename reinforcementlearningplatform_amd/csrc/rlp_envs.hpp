@@ -836,6 +836,20 @@ template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
         c = c < 1 ? c : 1;
         return acos(c);
     }
+    // vec_rad(x1, y1, x2, y2) > pi / 2 (the beam's "obstacle behind the vehicle" test) without the
+    // two square roots, the division and the acos where the answer cannot depend on them: with
+    // c = cos of the angle, acos(c) > fl(pi / 2) exactly when c < 0 except for |c| below ~1e-16
+    // (acos rounds to fl(pi / 2) there), and vec_rad returns 0 (not > pi / 2) for a vector shorter
+    // than 1e-4. Outside a relative band of 1e-9 around those thresholds the sign of the dot
+    // product decides; inside it the reference's expression runs as written (bit-identical result).
+    __device__ static __forceinline__ bool behind(double x1, double y1, double x2, double y2) {
+        const double s1 = x1 * x1 + y1 * y1, s2 = x2 * x2 + y2 * y2, dot = x1 * x2 + y1 * y2;
+        const bool short_sure = s1 < 1e-8 * (1 - 1e-9) || s2 < 1e-8 * (1 - 1e-9);
+        const bool long_sure = s1 > 1e-8 * (1 + 1e-9) && s2 > 1e-8 * (1 + 1e-9);
+        if (short_sure) return false;
+        if (long_sure && dot * dot > 1e-18 * (s1 * s2)) return dot < 0;  // |c| > 1e-9
+        return vec_rad(x1, y1, x2, y2) > kPi / 2;
+    }
     // utils/functions.py:49-60 cal_vector_rad_oriented(v1 = [cos phi, sin phi], v2 = target - pos)
     __device__ static __forceinline__ double e_phi(const double *s) {
         const double c = cos(s[PHI]), sn = sin(s[PHI]);
@@ -888,7 +902,15 @@ template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
     // (stable for <= 16 values) and stops at the first hit; the same result is the hit with the
     // smallest (ref_dis, index), found here without sorting. ob(k, x0, y0, r0, ref) fetches
     // obstacle k and its distance to the vehicle.
-    template <class Ob>
+    // Two passes: the cheap filters of every obstacle (range, distance of the centre from the beam
+    // line) give a candidate mask; the intersection runs for the candidates only. DYN (obstacles
+    // in LDS, so a per-lane index is a plain gather): each lane walks its own candidates and a wave
+    // iterates max-over-lanes times (a few), instead of NOBS times with the intersection path run
+    // whenever any lane of the wave needs it; !DYN (obstacles in a register array) keeps the
+    // unrolled walk over compile-time indices.
+    // |m x0 - y0 + b| / sq > r0 (the line-distance filter) is decided by a product outside a
+    // relative band of 1e-12 and by the reference's division inside it: the same decision.
+    template <bool DYN = false, class Ob>
     __device__ static __forceinline__ double beam(const P &p, const Pose &q, int i, Ob &&ob) {
         const double x = q.x, y = q.y, xm = p.map_size[0], ym = p.map_size[1], L = p.laser_dis;
         double ph = i == NL - 1 ? q.stop : (double)i * q.step + q.start;
@@ -921,26 +943,45 @@ template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
         const double lo = x < tx ? x : tx, hi = x < tx ? tx : x;  // min/max(start, terminal)
         bool found = false;
         double val = 0, best = 0;
+        unsigned cand = 0;
 #pragma unroll
         for (int k = 0; k < NOBS; ++k) {
             if (k >= p.n_obs) continue;
             double x0, y0, r0, ref;
             ob(k, x0, y0, r0, ref);
-            if (found && !(ref < best)) continue;
             if (ref > L + r0) continue;
-            if (fabs(m * x0 - y0 + b) / sq > r0) continue;
-            if (vec_rad(tx - x, ty - y, x0 - x, y0 - y) > kPi / 2) continue;
+            const double a = fabs(m * x0 - y0 + b), rs = r0 * sq;
+            const bool far = a > rs * (1 + 1e-12) ? true : a < rs * (1 - 1e-12) ? false : a / sq > r0;
+            if (!far) cand |= 1u << k;
+        }
+        auto hit = [&](int k) {  // obstacle k's intersection (the reference's, bit for bit)
+            double x0, y0, r0, ref;
+            ob(k, x0, y0, r0, ref);
+            if (found && !(ref < best)) return;
+            if (behind(tx - x, ty - y, x0 - x, y0 - y)) return;
+            // (sqrt(m2 + 1) == sq: fl(m * m + 1) is fl(1 + m * m))
             const double fx = (x0 + m * y0 - m * b) / (m2 + 1);
             const double fy = (m * x0 + m2 * y0 + b) / (m2 + 1);
             const double ddx = fx - x0, ddy = fy - y0;
             const double rd = sqrt(ddx * ddx + ddy * ddy);
-            const double cross = fx - sg * sqrt(r0 * r0 - rd * rd) / sqrt(m2 + 1);
+            const double cross = fx - sg * sqrt(r0 * r0 - rd * rd) / sq;
             if (lo <= cross && cross <= hi) {
                 found = true;
                 best = ref;
-                const double dis = fabs(cross - x) * sqrt(m2 + 1);
+                const double dis = fabs(cross - x) * sq;
                 val = dis < p.laser_blind ? p.laser_blind : dis;
             }
+        };
+        if constexpr (DYN) {
+            while (cand) {  // ascending index, as the unrolled walk
+                const int k = __builtin_ctz(cand);
+                cand &= cand - 1;
+                hit(k);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NOBS; ++k)
+                if (cand >> k & 1u) hit(k);
         }
         if (!found) {
             const double dx = x - tx, dy = y - ty;
@@ -1119,13 +1160,14 @@ template <> struct Env<RLP_ENV_UGV_OBSTACLE_AVOIDANCE> {
         if (sqrt(dx * dx + dy * dy) <= r + p.safety_dis_st) return false;
         dx = tx - cx; dy = ty - cy;
         if (sqrt(dx * dx + dy * dy) <= r + p.safety_dis_st) return false;
+        bool ok = true;  // every placed obstacle tested (independent square roots, no early exit)
         for (int j = 0; j < k; ++j) {
             double x0, y0, r0;
             ob(j, x0, y0, r0);
             dx = x0 - cx; dy = y0 - cy;
-            if (sqrt(dx * dx + dy * dy) <= r0 + r + p.safety_dis_obs) return false;
+            ok &= !(sqrt(dx * dx + dy * dy) <= r0 + r + p.safety_dis_obs);
         }
-        return true;
+        return ok;
     }
     __device__ static __forceinline__ double parked_x(int k) { return -1000.0 - 10.0 * k; }
     static constexpr double kParkedY = -1000.0;

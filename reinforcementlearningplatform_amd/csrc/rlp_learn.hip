@@ -169,22 +169,36 @@ __global__ void __launch_bounds__(256) reward_merge_kernel(const float *__restri
             for (int k = 0; k < 4; ++k) rms[k] = carry[k];
         return;
     }
-    // per time step: combine the chunks in global env order
+    // per time step: combine the chunks in global env order (the chunk statistics loaded in
+    // groups of kRsPre ahead of the serial combine)
+    constexpr int kRsPre = 8;
     for (int t = threadIdx.x; t < T; t += 256) {
         double c = 0, mean = 0, m2 = 0;
-        for (int q = 0; q < world * P; ++q) {
-            const int rk = q / P, p = q - rk * P;
-            const double *pp = parts + (((size_t)rk * T + t) * P + p) * 2;
-            const double cb = min(kRsChunk, n - p * kRsChunk);
-            if (q == 0) {
-                c = cb; mean = pp[0]; m2 = pp[1];
-                continue;
+        const int Q = world * P;
+        for (int q0 = 0; q0 < Q; q0 += kRsPre) {
+            double pm[kRsPre], pq[kRsPre];
+#pragma unroll
+            for (int u = 0; u < kRsPre; ++u) {
+                const int q = q0 + u, rk = q / P, p = q - rk * P;
+                const double *pp = parts + (((size_t)rk * T + t) * P + p) * 2;
+                pm[u] = q < Q ? pp[0] : 0.0;
+                pq[u] = q < Q ? pp[1] : 0.0;
             }
-            const double nn = c + cb;
-            const double dl = pp[0] - mean;
-            mean = mean + dl * (cb / nn);
-            m2 = m2 + pp[1] + dl * dl * (c * cb / nn);
-            c = nn;
+#pragma unroll
+            for (int u = 0; u < kRsPre; ++u) {
+                const int q = q0 + u, p = q % P;
+                if (q >= Q) break;
+                const double cb = min(kRsChunk, n - p * kRsChunk);
+                if (q == 0) {
+                    c = cb; mean = pm[u]; m2 = pq[u];
+                    continue;
+                }
+                const double nn = c + cb;
+                const double dl = pm[u] - mean;
+                mean = mean + dl * (cb / nn);
+                m2 = m2 + pq[u] + dl * dl * (c * cb / nn);
+                c = nn;
+            }
         }
         agg[2 * t] = mean;
         agg[2 * t + 1] = m2;

@@ -22,6 +22,14 @@ struct OaEnvLds {
     int coll;
 };
 
+// the head of get_state (e, vel, e_phi, omega) of a pose
+__device__ __forceinline__ void oa_head(const OA::P &p, const double *s, float *row) {
+    float h[4];
+    OA::obs_head(p, s, OA::get_e(s), OA::e_phi(s), h);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) row[j] = h[j];
+}
+
 // per-pose setup by the env's lane: obstacle distances, collision and the beam geometry
 __device__ __forceinline__ void oa_setup(const OA::P &p, OaEnvLds &L, const double *s) {
     const double x = s[OA::X], y = s[OA::Y];
@@ -35,23 +43,51 @@ __device__ __forceinline__ void oa_setup(const OA::P &p, OaEnvLds &L, const doub
     L.q = OA::pose(p, x, y, s[OA::PHI]);
 }
 
+// the same setup of ONE env by a whole wave (wave-uniform call, every lane the same pose s): lane
+// k < n_obs obstacle k's distance and collision test (collision_at's any() as a ballot), lanes
+// 0..3 the four corner angles (one acos each), lane 4 the beam angles; lane 5 writes get_state's
+// head into head_row (nullable). The caller orders the LDS writes before any read (wave barrier).
+__device__ __forceinline__ void oa_setup_wave(const OA::P &p, OaEnvLds &L, const double *s,
+                                              float *head_row) {
+    const int lane = threadIdx.x & 63;
+    const double x = s[OA::X], y = s[OA::Y];
+    bool hit = false;
+    if (lane < p.n_obs) {
+        const double dx = x - L.ob[lane].x0, dy = y - L.ob[lane].y0;
+        const double d = sqrt(dx * dx + dy * dy);
+        L.ob[lane].ref = d;
+        hit = d <= L.ob[lane].r0 + p.r_vehicle;
+    }
+    const bool coll = __ballot(hit) != 0;
+    if (lane < 4) {  // pose(): th1 (xm, ym), th2 (0, ym), th3 -(0, 0), th4 -(xm, 0) corners
+        const double cx = (lane == 0 || lane == 3) ? p.map_size[0] - x : 0 - x;
+        const double cy = (lane == 0 || lane == 1) ? p.map_size[1] - y : 0 - y;
+        const double v = OA::vec_rad(1, 0, cx, cy);
+        if (lane == 0) L.q.th1 = v;
+        else if (lane == 1) L.q.th2 = v;
+        else if (lane == 2) L.q.th3 = -v;
+        else L.q.th4 = -v;
+    } else if (lane == 4) {
+        L.q.x = x;
+        L.q.y = y;
+        L.q.start = s[OA::PHI] - p.laser_range;
+        L.q.stop = s[OA::PHI] + p.laser_range;
+        L.q.step = (L.q.stop - L.q.start) / (OA::NL - 1);
+        L.coll = coll;
+    } else if (lane == 5 && head_row) {
+        oa_head(p, s, head_row);
+    }
+}
+
 // beam i of an env set up in L (get_state's normalised value)
 __device__ __forceinline__ float oa_beam(const OA::P &p, const OaEnvLds &L, int i) {
     if (L.coll) return OA::beam_obs(p, p.laser_blind);
     const OA::Pose q = L.q;
-    return OA::beam_obs(p, OA::beam(p, q, i, [&](int k, double &x0, double &y0, double &r0,
-                                                 double &rf) {
+    return OA::beam_obs(p, OA::beam<true>(p, q, i, [&](int k, double &x0, double &y0, double &r0,
+                                                       double &rf) {
         const OaObstacle o = L.ob[k];
         x0 = o.x0; y0 = o.y0; r0 = o.r0; rf = o.ref;
     }));
-}
-
-// the head of get_state (e, vel, e_phi, omega) of a pose
-__device__ __forceinline__ void oa_head(const OA::P &p, const double *s, float *row) {
-    float h[4];
-    OA::obs_head(p, s, OA::get_e(s), OA::e_phi(s), h);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) row[j] = h[j];
 }
 
 // reset(random=True) of env i by ONE wave (all 64 lanes, wave-uniform call): each round, lane l
@@ -87,14 +123,22 @@ __device__ __forceinline__ void oa_reset_wave(const OA::P &p, double *state, int
             }
         }
     }
+    // the first round's draw of obstacle k + 1 (try = lane) does not depend on where obstacle k
+    // lands: it is drawn before obstacle k's legality checks, so the chain per obstacle is the
+    // checks and the ballot, not the two Philox blocks (later rounds, rare, draw in turn)
+    double nx = 0, ny = 0, nr = 0;
+    if (p.n_obs > 0 && lane < p.max_tries) OA::draw_obstacle(p, seed, counter, id, 0, lane, nx, ny, nr);
     for (int k = 0; k < OA::NOBS; ++k) {
         double cx = OA::parked_x(k), cy = OA::kParkedY, r = p.r_min;
+        const double fx = nx, fy = ny, fr = nr;  // round 0 of obstacle k
+        if (k + 1 < p.n_obs && lane < p.max_tries)
+            OA::draw_obstacle(p, seed, counter, id, k + 1, lane, nx, ny, nr);
         for (int t0 = 0; k < p.n_obs && t0 < p.max_tries; t0 += 64) {
             const int t = t0 + lane;
-            double ccx = 0, ccy = 0, rr = 0;
+            double ccx = fx, ccy = fy, rr = fr;
             bool ok = false;
             if (t < p.max_tries) {
-                OA::draw_obstacle(p, seed, counter, id, k, t, ccx, ccy, rr);
+                if (t0 > 0) OA::draw_obstacle(p, seed, counter, id, k, t, ccx, ccy, rr);
                 ok = OA::legal(p, sx, sy, tx, ty, ccx, ccy, rr, k,
                                [&](int j, double &x0, double &y0, double &r0) {
                                    x0 = obl[3 * j]; y0 = obl[3 * j + 1]; r0 = obl[3 * j + 2];
@@ -129,15 +173,12 @@ __device__ __forceinline__ void oa_reset_wave(const OA::P &p, double *state, int
     }
     if (lane < OA::NOBS * 3) state[(size_t)(OA::OB + lane) * n + i] = obl[lane];
     if (!obs_row) return;
-    if (lane == 0) {  // the per-pose setup of the new pose, for this wave's env
-        for (int k = 0; k < p.n_obs; ++k) {
-            L.ob[k].x0 = obl[3 * k];
-            L.ob[k].y0 = obl[3 * k + 1];
-            L.ob[k].r0 = obl[3 * k + 2];
-        }
-        oa_setup(p, L, head);
-        oa_head(p, head, obs_row);
+    if (lane < p.n_obs) {  // the per-pose setup of the new pose, over the wave's lanes
+        L.ob[lane].x0 = obl[3 * lane];
+        L.ob[lane].y0 = obl[3 * lane + 1];
+        L.ob[lane].r0 = obl[3 * lane + 2];
     }
+    oa_setup_wave(p, L, head, obs_row);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

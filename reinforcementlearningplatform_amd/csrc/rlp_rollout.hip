@@ -690,6 +690,9 @@ struct OaPolicyArgs {
 #ifndef RLP_OA_DIAG
 #define RLP_OA_DIAG 0
 #endif
+#ifndef RLP_OA_POL1
+#define RLP_OA_POL1 0
+#endif
 constexpr int kOaPolWaves = 4;  // 16-env waves per block, one block per CU (1 wave per SIMD)
 constexpr int kOaKs1 = (OA::S + 3) / 4;
 constexpr int kOaSmall = mlp_small_floats<256, kOaKs1, OA::A>();
@@ -756,10 +759,78 @@ __global__ void __launch_bounds__(64 * kOaPolWaves, 1) oa_policy_kernel(OaPolicy
     }
 }
 
+// f16x3 policy with two waves per SIMD: 8-wave blocks over 64 rows, waves 0-3 run the actor and
+// sample, waves 4-7 the critic and the value bookkeeping, each group through its own W2 chunk ring
+// (the two groups execute the same barrier sequence: both nets have 16 chunks per pass). Boot
+// (critic only): both groups run the critic, on 128 rows per block. One wave per SIMD left the
+// layer-1 LDS reads, the ring waits and the tanh stretches of the single wave exposed.
+constexpr int kOaPol2Ring = 2;  // ring slots per group: both nets' resident parts + 2 x 2 slots fill the 160 KiB
+constexpr int kOaSmallA = mlp_small_floats<256, kOaKs1, OA::A>(), kOaSmallC = mlp_small_floats<256, kOaKs1, 1>();
+static_assert(4 * (kOaSmallA + kOaSmallC + 2 * kOaPol2Ring * kX3ChunkFloats) <= 160 * 1024,
+              "oa_policy2_kernel LDS");
+__global__ void __launch_bounds__(512, 1) oa_policy2_kernel(OaPolicyArgs pa) {
+    constexpr int A = OA::A, S = OA::S, KS1 = kOaKs1;
+    __shared__ __attribute__((aligned(16))) float lds[kOaSmallA + kOaSmallC + 2 * kOaPol2Ring * kX3ChunkFloats];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, e = lane & 15;
+    const int grp = __builtin_amdgcn_readfirstlane(wave >> 2), wq = wave & 3;
+    const bool boot = pa.boot != 0;
+    const bool critic = boot || grp == 1;
+    float *small0 = lds, *small1 = lds + kOaSmallA;
+    float *ring = lds + kOaSmallA + kOaSmallC + grp * kOaPol2Ring * kX3ChunkFloats;
+    // group 0's region holds the actor (boot: a second copy of the critic), group 1's the critic
+    mlp_small_to_lds(boot ? pa.critic : pa.actor, boot ? pa.cn : pa.an, small0, true);
+    mlp_small_to_lds(pa.critic, pa.cn, small1, true);
+    __syncthreads();
+    const float *P = critic ? pa.critic : pa.actor;
+    const MfmaNet &net = critic ? pa.cn : pa.an;
+    const float *small = grp ? small1 : small0;
+    const RolloutArgs &ra = pa.ra;
+    const int n = ra.n, t = pa.t;
+    const int rows_blk = boot ? 128 : 64;
+    const float *x = boot ? pa.b.obs_next + (size_t)(ra.T - 1) * n * S : pa.b.obs + (size_t)t * n * S;
+    for (int r0 = blockIdx.x * rows_blk; r0 < n; r0 += gridDim.x * rows_blk) {  // block-uniform
+        const int row = r0 + (boot ? 64 * grp : 0) + 16 * wq + e;
+        float bobs[1][KS1];
+#pragma unroll
+        for (int kk = 0; kk < KS1; ++kk)
+            bobs[0][kk] = (row < n && 4 * kk + g < S) ? x[(size_t)row * S + 4 * kk + g] : 0.f;
+        float out[1][A];
+        mlp_x3_forward<256, 1, KS1, A, kOaPol2Ring, 4, 1>(P, small, ring, net, critic ? 1 : A, bobs, out);
+        if (g != 0 || row >= n) continue;  // lane e of group 0 owns row `row`
+        const rlp_rollout_bufs &b = pa.b;
+        if (boot) {
+            const size_t k = (size_t)(ra.T - 1) * n + row;
+            if (!b.done[k]) b.value_next[k] = out[0][0];
+            continue;
+        }
+        const size_t k = (size_t)t * n + row;
+        if (critic) {
+            const float v = out[0][0];
+            b.value[k] = v;
+            if (t > 0 && !b.done[k - n]) b.value_next[k - n] = v;  // V(s'_{t-1}) == V(s_t)
+            continue;
+        }
+        float eps[A];
+        philox_normal_f32<A>(ra.seed, ra.step0 + (uint64_t)t, ra.env_id0 + (uint64_t)row, eps);
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            const float m = (pa.an.out_tanh ? tanhf(out[0][a]) : out[0][a]) * ra.gain[a] + ra.off[a];
+            float xa = m + ra.std_[a] * eps[a];
+            xa = fmaxf(fminf(xa, ra.a_max[a]), ra.a_min[a]);
+            b.action[k * A + a] = xa;
+            b.logp[k * A + a] = normal_logp_c(xa, m, ra.half_inv_var[a], ra.log_std[a]);
+        }
+    }
+}
+
 // EB envs per block: phase 1 one lane per env, phase 2 the EB x 37 (env, beam) pairs over the
 // block, phase 3 the ended envs' resets, one wave per env
+// 4 waves per SIMD (<= 128 registers, ~240 B of scratch spills): the kernel's phases are latency
+// chains (per-env f64 dynamics and setup, divergent beams, the map generator's rounds) that only
+// more resident waves hide: 16 384 x 64 segment 7.48 -> 6.66 ms against 2 waves per SIMD (213
+// registers, no spills), 6.75 ms at 3 (profiles/r6/r6d_lidar_occupancy_ab.txt)
 template <int EB>
-__global__ void __launch_bounds__(256) oa_step_kernel(OA::P p, double *state, uint8_t *need_reset,
+__global__ void __launch_bounds__(256, 4) oa_step_kernel(OA::P p, double *state, uint8_t *need_reset,
                                                       RolloutArgs ra, int t, rlp_rollout_bufs b) {
     constexpr int S = OA::S, A = OA::A, NW = 4;
     __shared__ OaEnvLds L[EB];
@@ -857,8 +928,16 @@ static int rollout_oa(const void *params, double *state, uint8_t *need_reset, co
     const bool eb64 = (n + 63) / 64 >= 4 * cus;
     auto policy = [&](int t, int boot) {
         const OaPolicyArgs pa{actor, critic, an, cn, ra, b, t, boot};
-        if (prec == RLP_MLP_F16X3) oa_policy_kernel<true><<<pblocks, 64 * kOaPolWaves, 0, s>>>(pa);
-        else oa_policy_kernel<false><<<pblocks, 64 * kOaPolWaves, 0, s>>>(pa);
+        if (prec == RLP_MLP_F16X3) {
+#if RLP_OA_POL1  // (A/B: the one-wave-per-SIMD form)
+            oa_policy_kernel<true><<<pblocks, 64 * kOaPolWaves, 0, s>>>(pa);
+#else
+            const int rb = boot ? 128 : 64, nb = (n + rb - 1) / rb;
+            oa_policy2_kernel<<<nb < cus ? nb : cus, 512, 0, s>>>(pa);
+#endif
+        } else {
+            oa_policy_kernel<false><<<pblocks, 64 * kOaPolWaves, 0, s>>>(pa);
+        }
     };
     int rc = launch_ugvoa_reset(p, state, n, need_reset, nullptr, ra.seed, ra.step0, ra.env_id0, s);
     if (rc == RLP_OK) rc = launch_ugvoa_observe(p, state, n, b.obs, s);

@@ -163,11 +163,10 @@ __device__ __forceinline__ void x3_gemm16(const gptr<float> Xw, float *ring, flo
 }
 
 // packed FP32 (v_pk_mul / v_pk_add / v_pk_fma_f32: two IEEE f32 results per instruction, each
-// rounded exactly as the scalar op) for the FD kernel's elementwise tails: the same values at half
-// the VALU issue slots (the tails are issue-bound: both waves of a SIMD run them together)
-#ifndef RLP_FD_PK
-#define RLP_FD_PK 1
-#endif
+// rounded exactly as the scalar op) for the FD kernel's elementwise work (layer-1 tanh, h2 tanh and
+// z3, dW3 products, g2, the backward operand scale, the g1 recompute, dW1): 2745 -> 2226 VALU per
+// 16-row wave tile in the ISA, FD -0.5 to -1.2 % (profiles/r6/r6b_fd_pk_lidar_ab.txt): the kernel is
+// not VALU-issue bound
 __device__ __forceinline__ float2v pk(float a, float b) { return (float2v){a, b}; }
 __device__ __forceinline__ float2v pk_fma(float2v a, float2v b, float2v c) {
     return __builtin_elementwise_fma(a, b, c);
@@ -328,7 +327,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
             for (int tt = 0; tt < 8; ++tt) {
                 const floatx4 gt = dh1[8 * h + tt];
-#if RLP_FD_PK
 #pragma unroll
                 for (int f = 0; f < 4 * KS; f += 2) {  // two features per packed op
                     float2v x = pk(gt[0], gt[0]) * pk(sv[0][f], sv[0][f + 1]);
@@ -337,15 +335,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
                     v[tt * NC + f] = x.x;
                     v[tt * NC + f + 1] = x.y;
                 }
-#else
-#pragma unroll
-                for (int f = 0; f < 4 * KS; ++f) {
-                    float x = gt[0] * sv[0][f];
-#pragma unroll
-                    for (int q = 1; q < 4; ++q) x = __builtin_fmaf(gt[q], sv[q][f], x);
-                    v[tt * NC + f] = x;
-                }
-#endif
                 v[tt * NC + 4 * KS] = (gt[0] + gt[1]) + (gt[2] + gt[3]);
             }
 #pragma unroll
@@ -430,7 +419,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
                 p1 = q1[P & 1];
             }
             float x[8];
-#if RLP_FD_PK
 #pragma unroll
             for (int i = 0; i < 8; i += 2) {
                 const float2v pre = i < 4 ? pk(p0[i], p0[i + 1]) : pk(p1[i - 4], p1[i - 3]);
@@ -444,18 +432,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
                 x[i] = xv.x;
                 x[i + 1] = xv.y;
             }
-#else
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float pre = i < 4 ? p0[i] : p1[i - 4];
-                if constexpr (EXT) {
-                    x[i] = pre * kX3HScale;  // h1 itself (exact power-of-two scale)
-                } else {
-                    const float ex = __builtin_amdgcn_exp2f(pre);  // pre = 2 h1 / ln 2 (small_r)
-                    x[i] = __builtin_fmaf(-2.0f * kX3HScale, __builtin_amdgcn_rcpf(1.0f + ex), kX3HScale);
-                }
-            }
-#endif
             split8(x, bh, bl);
         }, [&](int P) {
             if constexpr (EXT) {  // neurons 32 Q + 4 gq .. + 3 and 32 Q + 16 + 4 gq .. + 3 of the row
@@ -472,7 +448,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
         });
         // ---- h2 = tanh(z2), z3 = W3 h2 + b3 (every lane group ends with its row's z3)
         float z3[A];
-#if RLP_FD_PK
         float2v z3p[A];  // two partial sums per output (even / odd neurons of each quad)
 #pragma unroll
         for (int a = 0; a < A; ++a) z3p[a] = pk(0.f, 0.f);
@@ -493,24 +468,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
         }
 #pragma unroll
         for (int a = 0; a < A; ++a) z3[a] = z3p[a].x + z3p[a].y;
-#else
-#pragma unroll
-        for (int a = 0; a < A; ++a) z3[a] = 0.f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            floatx4 w3[A];
-#pragma unroll
-            for (int a = 0; a < A; ++a) w3[a] = *reinterpret_cast<const floatx4 *>(W3c + a * H + 16 * j + 4 * gq);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float ex = __builtin_amdgcn_exp2f(acc[j][q] * k_out);
-                const float h = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + ex), 1.0f);
-                acc[j][q] = h;
-#pragma unroll
-                for (int a = 0; a < A; ++a) z3[a] = __builtin_fmaf(w3[a][q], h, z3[a]);
-            }
-        }
-#endif
 #pragma unroll
         for (int a = 0; a < A; ++a) {
             z3[a] += __shfl_xor(z3[a], 16);
@@ -568,17 +525,12 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
 #pragma unroll
             for (int a = 0; a < A; ++a) {
                 float pv[64];
-#if RLP_FD_PK
 #pragma unroll
                 for (int i = 0; i < 64; i += 2) {
                     const float2v p2 = pk(g3[a], g3[a]) * pk(acc[i >> 2][i & 3], acc[i >> 2][(i & 3) + 1]);
                     pv[i] = p2.x;
                     pv[i + 1] = p2.y;
                 }
-#else
-#pragma unroll
-                for (int i = 0; i < 64; ++i) pv[i] = g3[a] * acc[i >> 2][i & 3];
-#endif
 #pragma unroll
                 for (int i = 0; i < 32; ++i) pv[i] = pair_sum_rows16<kDppRowMirror>(pv[i], pv[i + 32], b3);
 #pragma unroll
@@ -597,7 +549,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
             floatx4 w3[A];
 #pragma unroll
             for (int a = 0; a < A; ++a) w3[a] = *reinterpret_cast<const floatx4 *>(W3c + a * H + 16 * j + 4 * gq);
-#if RLP_FD_PK
 #pragma unroll
             for (int q = 0; q < 4; q += 2) {
                 const float2v h = pk(acc[j][q], acc[j][q + 1]);
@@ -608,16 +559,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
                 acc[j][q] = v.x;
                 acc[j][q + 1] = v.y;
             }
-#else
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float h = acc[j][q];
-                float dh = 0.f;
-#pragma unroll
-                for (int a = 0; a < A; ++a) dh = __builtin_fmaf(w3[a][q], g3[a], dh);
-                acc[j][q] = dh * __builtin_fmaf(-h, h, 1.f);  // tanh' = 1 - h^2, one rounding
-            }
-#endif
         }
         // one wave-uniform guard (8-wave blocks: the last pair's 2nd tile); a scalar tile base
         // advanced per j plus the lane's 32-bit offset (saddr stores, no 64-bit VALU addresses)
@@ -654,7 +595,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
         // (operands swapped: dh1 comes out "neuron on lane", dh1[t][q] = row 4 gq + q, neuron 16 t + e)
         x3_gemm16<true, kFdWaves, 1, kFdRing>(Xb, ring, my_part, dh1, [&](int P, half8 &bh, half8 &bl) {
             float x[8];
-#if RLP_FD_PK
 #pragma unroll
             for (int i = 0; i < 4; i += 2) {
                 const float2v u = pk(acc[2 * P][i], acc[2 * P][i + 1]) * sc;
@@ -662,13 +602,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
                 x[i] = u.x; x[i + 1] = u.y;
                 x[i + 4] = v.x; x[i + 5] = v.y;
             }
-#else
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                x[i] = acc[2 * P][i] * sc;
-                x[i + 4] = acc[2 * P + 1][i] * sc;
-            }
-#endif
             split8(x, bh, bl);
         }, [](int) {});
         // ---- g1 = dh1 * (1 - h1^2) and dW1 | db1 of this tile: the 16 neuron tiles' layer-1
@@ -692,7 +625,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
             floatx4 pre[16];
 #pragma unroll
             for (int t = 0; t < 16; ++t) pre[t] = layer1_t(t, bobs);
-#if RLP_FD_PK
 #pragma unroll
             for (int t = 0; t < 16; ++t)
 #pragma unroll
@@ -702,15 +634,6 @@ __global__ void __launch_bounds__(64 * kFdWaves, 1) ppo2_fd_kernel(Ppo2Args g) {
                     dh1[t][q] = v.x;
                     dh1[t][q + 1] = v.y;
                 }
-#else
-#pragma unroll
-            for (int t = 0; t < 16; ++t)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(pre[t][q]));
-                    dh1[t][q] = dh1[t][q] * unscale4 * __builtin_fmaf(-r, r, r);
-                }
-#endif
             dw1_acc(srw);
         }
     }
