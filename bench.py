@@ -241,16 +241,32 @@ def update_roofline(learner, rows, k_epochs, update_ms):
     """achieved TFLOP/s of the K-epoch update of one PPO2 iteration (both nets, full batch),
     priced against the arithmetic the update runs: the f16x3 kernels' 838.9 TF ceiling
     (rlp_ppo2_grad) or the f32 MFMA peak (rlp_ppo2_dense_grad, torch)."""
-    per_row = update_flops_per_row(_net_dims(learner.actor)) + update_flops_per_row(_net_dims(learner.critic))
+    dims = [_net_dims(learner.actor), _net_dims(learner.critic)]
+    per_row = sum(update_flops_per_row(d) for d in dims)
     flop = per_row * rows * k_epochs
-    dense = [getattr(getattr(learner, k, None), "dense", True) for k in ("net_a", "net_c")]
+    nets = [getattr(learner, k, None) for k in ("net_a", "net_c")]
+    dense = [getattr(m, "dense", True) for m in nets]
     f16x3 = type(learner).__name__ == "NativePPO2Learner" and not any(dense)
-    peak = PEAK_F16X3_TFLOPS if f16x3 else PEAK_FP32_MFMA_TFLOPS
+    ext = f16x3 and any(getattr(m, "ext", False) for m in nets)
     ach = flop / (update_ms * 1e-3) / 1e12
-    return {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
-            "flop_per_iteration": flop, "update_ms": update_ms,
-            "peak_basis": "f16x3 ceiling (f16 MFMA / 3)" if f16x3 else "f32 MFMA dense",
-            "flop_basis": "K x rows x (forward + backward data + weight gradients) of both nets"}
+    out = {"bound": "mfma", "achieved": ach, "unit": "TFLOP/s", "flop_per_iteration": flop,
+           "update_ms": update_ms,
+           "flop_basis": "K x rows x (forward + backward data + weight gradients) of both nets"}
+    if ext:
+        # the lidar nets' layer 1 (41 inputs: h1 forward and dW1) runs on exact-f32 MFMA and is
+        # HBM-bound; the rest on the f16x3 kernels: each share priced against its own arithmetic's
+        # peak (the time both would take at their peaks, combined)
+        flop1 = sum(2 * d[0] * d[1] + 2 * (d[0] + 1) * d[1] for d in dims) * rows * k_epochs
+        peak = flop / (flop1 / PEAK_FP32_MFMA_TFLOPS + (flop - flop1) / PEAK_F16X3_TFLOPS)
+        out.update(peak=peak, frac=ach / peak, layer1_flop_share=flop1 / flop,
+                   peak_basis="mixed: layer 1 (f32 MFMA, HBM-bound) at the f32 MFMA peak, the "
+                              "rest at the f16x3 ceiling (f16 MFMA / 3)",
+                   frac_vs_f16x3_ceiling=ach / PEAK_F16X3_TFLOPS)
+    else:
+        peak = PEAK_F16X3_TFLOPS if f16x3 else PEAK_FP32_MFMA_TFLOPS
+        out.update(peak=peak, frac=ach / peak,
+                   peak_basis="f16x3 ceiling (f16 MFMA / 3)" if f16x3 else "f32 MFMA dense")
+    return out
 
 
 def _template_args(name):
@@ -702,10 +718,10 @@ def ugvoa_leg(rank, n=16384, steps=30, warmup=3, seed=5):
 def ugvoa_ppo2_leg(rank, n=16384, T=64, iters=3, seed=17):
     """UGVForwardObstacleAvoidance PPO2 rollout (the PPO2 demo's 41 -> 256 -> 256 -> 2 / -> 1 tanh
     nets, demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97) through
-    rlp_rollout: two launches per step (round 6) — oa_policy_kernel (actor + critic, layer 1 on
-    11 K-steps of exact f32 MFMA, the 256 x 256 hidden layer on the f16x3 split, the Philox sample)
-    and oa_step_kernel (lidar env step, success rule, the 37-beam scans, map-generator resets of the
-    ended envs); n envs per GPU (config 5: 131 072 / 8)."""
+    rlp_rollout: ONE launch per segment (round 6, oa_rollout_kernel: each block owns 64 envs for
+    all T steps — actor + critic with layer 1 on 11 K-steps of exact f32 MFMA and the 256 x 256
+    hidden layer on the f16x3 split, the Philox sample, the lidar env step, the 37-beam scans and
+    the map-generator resets of the ended envs); n envs per GPU (config 5: 131 072 / 8)."""
     kind = A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE
     p = A.default_params(kind, "ppo2")
     D, S, Ad = A.ENV_DIMS[kind]
@@ -755,9 +771,10 @@ def ugvoa_ppo2_leg(rank, n=16384, T=64, iters=3, seed=17):
                                        "%.1f TF" % (f_exact, PEAK_FP32_MFMA_TFLOPS, f_hidden,
                                                     PEAK_F16X3_TFLOPS),
                          "frac_vs_f32_peak": ach / PEAK_FP32_MFMA_TFLOPS,
-                         "note": "whole segment (T x {oa_policy_kernel, oa_step_kernel} + the "
-                                 "bootstrap critic), the lidar env's f64 work included, against "
-                                 "the nets' FLOPs"},
+                         "kernel": "rlp::oa_rollout_kernel(rlp::OaSegArgs)",
+                         "note": "whole segment (the segment-start reset and observation, "
+                                 "oa_rollout_kernel's T steps + the bootstrap critic), the lidar "
+                                 "env's f64 work included, against the nets' FLOPs"},
             "config": "UGVForwardObstacleAvoidance (PPO2 copy, 37-beam lidar, 10 circles) PPO2 "
                       "rollout, nets [41,256,256,2] / [41,256,256,1] tanh (rlp_rollout)"}
 

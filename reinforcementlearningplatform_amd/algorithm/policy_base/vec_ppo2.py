@@ -188,9 +188,11 @@ class VecPPO2:
         if learner not in ("auto", "native", "torch"):
             raise ValueError(f"VecPPO2: learner {learner!r} (auto | native | torch)")
         from .native_ppo2 import NativePPO2Learner, dense_fits
-        if learner == "auto":  # librlp's update: f16x3 kernels for [S<=8 -> 256 -> 256 -> A<=4],
-            # exact-f32 dense GEMMs for other Linear/Tanh stacks (the lidar env's 41-input nets,
-            # the PPO2-SOI demo's 4-128-64-32 / 4-64-64 nets); anything else: torch autograd
+        if learner == "auto":  # librlp's update (native_ppo2._update_kind): the f16x3 FD / wgrad
+            # kernels for [S<=8 or 41..44 -> 256 -> 256 -> A<=4] tanh nets (the lidar env's
+            # 41-input nets included, their layer 1 on exact f32), the exact-f32 dense GEMMs for
+            # other Linear/Tanh stacks (the PPO2-SOI demo's 4-128-64-32 / 4-64-64 nets;
+            # ppo_msg['update_kernels'] = 'dense' opts any net into them); else torch autograd
             fits = all(dense_fits(m, a) for m, a in ((actor, True), (critic, False)))
             learner = "native" if fits else "torch"
         cls = NativePPO2Learner if learner == "native" else PPO2Learner

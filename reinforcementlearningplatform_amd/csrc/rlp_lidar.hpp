@@ -48,7 +48,7 @@ __device__ __forceinline__ void oa_setup(const OA::P &p, OaEnvLds &L, const doub
 // 0..3 the four corner angles (one acos each), lane 4 the beam angles; lane 5 writes get_state's
 // head into head_row (nullable). The caller orders the LDS writes before any read (wave barrier).
 __device__ __forceinline__ void oa_setup_wave(const OA::P &p, OaEnvLds &L, const double *s,
-                                              float *head_row) {
+                                              float *head_row, float *head_row2 = nullptr) {
     const int lane = threadIdx.x & 63;
     const double x = s[OA::X], y = s[OA::Y];
     bool hit = false;
@@ -76,6 +76,8 @@ __device__ __forceinline__ void oa_setup_wave(const OA::P &p, OaEnvLds &L, const
         L.coll = coll;
     } else if (lane == 5 && head_row) {
         oa_head(p, s, head_row);
+        if (head_row2)
+            for (int j = 0; j < 4; ++j) head_row2[j] = head_row[j];
     }
 }
 
@@ -98,7 +100,8 @@ __device__ __forceinline__ float oa_beam(const OA::P &p, const OaEnvLds &L, int 
 // wave's LDS scratch.
 __device__ __forceinline__ void oa_reset_wave(const OA::P &p, double *state, int n, size_t i,
                                               uint64_t seed, uint64_t counter, uint64_t id,
-                                              float *obs_row, double *obl, OaEnvLds &L) {
+                                              float *obs_row, double *obl, OaEnvLds &L,
+                                              float *obs_row2 = nullptr) {
     const int lane = threadIdx.x & 63;
     double sx, sy;
     OA::draw_point(p, seed, counter, id, OA::kTagStart, sx, sy);
@@ -178,11 +181,15 @@ __device__ __forceinline__ void oa_reset_wave(const OA::P &p, double *state, int
         L.ob[lane].y0 = obl[3 * lane + 1];
         L.ob[lane].r0 = obl[3 * lane + 2];
     }
-    oa_setup_wave(p, L, head, obs_row);
+    oa_setup_wave(p, L, head, obs_row, obs_row2);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane < OA::NL) obs_row[4 + lane] = oa_beam(p, L, lane);  // one beam per lane
+    if (lane < OA::NL) {  // one beam per lane
+        const float v = oa_beam(p, L, lane);
+        obs_row[4 + lane] = v;
+        if (obs_row2) obs_row2[4 + lane] = v;
+    }
 }
 
 }  // namespace rlp

@@ -336,11 +336,42 @@ def test_rollout_env_copies_teacher_forced(kind, variant):
         bound(gb["value"], ob["value"], 1e-5, 2e-6, "V(s)")
 
 
-@pytest.mark.parametrize("variant", ["env", "ppo2"])
-def test_rollout_lidar_env_teacher_forced(variant):
-    """UGVForwardObstacleAvoidance through rlp_rollout (the per-step kernel sequence: packed
-    forward with the 41-input layer 1 on 11 K-steps of f32 MFMA, Philox sample, lidar env step,
-    map-generator resets), the PPO2 demo's 41 -> 256 -> 256 -> 2 / -> 1 nets
+def test_rollout_lidar_env_teacher_forced_config5_shard():
+    """The lidar rollout at BASELINE config 5's shard size (131 072 / 8 = 16 384 envs), which takes
+    the one-launch-per-segment kernel with every CU busy: two chained segments with resets inside,
+    physics teacher-forced against the oracle for all envs (flags / done exact, state 1e-9,
+    observations 2 ulps, rewards), the oracle's own policy and critic on the first 1 024 envs."""
+    kind = A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE
+    D, S, Ad = A.ENV_DIMS[kind]
+    p = A.default_params(kind, "ppo2")
+    ad, ap, cd, cp = _nets(S, Ad, 91)
+    lo, hi = A.action_bounds(kind, p)
+    std = [(h - l) / 6 for l, h in zip(lo, hi)]
+    n, T = 16384, 24
+    cfg = K.make_rollout_cfg(T, n, 3409, 0, 0, std, lo, hi, A.RLP_SUCCESS_DONE_AND_FLAG_NE,
+                             A.timeout_flag(kind))
+    g, gst, gneed = _gpu_segment(kind, p, n, T, ad, ap, cd, cp, cfg, segments=2)
+    assert g[0]["done"].sum() + g[1]["done"].sum() > 100   # resets inside the segments
+    o, ost, oneed = _oracle_forced(kind, p, n, T, cfg, g)
+    _check_physics(kind, g, o, gst, ost, gneed, oneed, "lidar env config-5 shard")
+    m = 1024
+    sub = [{k: v[:, :m] for k, v in b.items()} for b in g]
+    cfg.n = m
+    o2, _, _ = _oracle_forced(kind, p, m, T, cfg, sub, ad, ap, cd, cp)
+    for gb, ob in zip(sub, o2):
+        a_tol, lp_tol = policy_bounds(ad, ap, gb["obs"], ob["action"], lo, hi, std)
+        bound_rows(gb["action"], ob["action"], 1e-5, a_tol, "action")
+        bound_rows(gb["logp"], ob["logp"], 1e-5, lp_tol, "log-prob")
+        bound(gb["value"], ob["value"], 1e-5, 2e-6, "V(s)")
+        nd = gb["done"] == 0
+        bound(gb["value_next"][nd], ob["value_next"][nd], 1e-5, 2e-6, "V(s')")
+
+
+@pytest.mark.parametrize("variant,precision", [("env", "f16x3"), ("ppo2", "f16x3"), ("ppo2", "fp32")])
+def test_rollout_lidar_env_teacher_forced(variant, precision):
+    """UGVForwardObstacleAvoidance through rlp_rollout (round 6: one launch per segment with the
+    f16x3 hidden layer, oa_rollout_kernel; exact f32: oa_policy_kernel + oa_step_kernel per step),
+    the PPO2 demo's 41 -> 256 -> 256 -> 2 / -> 1 nets
     (demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97), two chained
     segments with resets inside: physics teacher-forced against the oracle (flags / done exact,
     state 1e-9, observations 2 ulps), the oracle's own policy and critic on the kernel's
@@ -353,11 +384,12 @@ def test_rollout_lidar_env_teacher_forced(variant):
     std = [(h - l) / 6 for l, h in zip(lo, hi)]
     n, T = 1024 + 37, 40
     cfg = K.make_rollout_cfg(T, n, 3407, 0, 0, std, lo, hi, A.RLP_SUCCESS_DONE_AND_FLAG_NE,
-                             A.timeout_flag(kind))
+                             A.timeout_flag(kind), mlp_precision=(_native.MLP_F16X3 if precision == "f16x3"
+                                                                  else _native.MLP_FP32))
     g, gst, gneed = _gpu_segment(kind, p, n, T, ad, ap, cd, cp, cfg, segments=2)
     assert g[0]["done"].any() or g[1]["done"].any()
     o, ost, oneed = _oracle_forced(kind, p, n, T, cfg, g, ad, ap, cd, cp)
-    _check_physics(kind, g, o, gst, ost, gneed, oneed, f"lidar env {variant}")
+    _check_physics(kind, g, o, gst, ost, gneed, oneed, f"lidar env {variant} {precision}")
     for gb, ob in zip(g, o):
         a_tol, lp_tol = policy_bounds(ad, ap, gb["obs"], ob["action"], lo, hi, std)
         bound_rows(gb["action"], ob["action"], 1e-5, a_tol, "action")
