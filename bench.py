@@ -198,13 +198,13 @@ def learn_roofline(flop_per_row, batch, learn_ms):
                     "graph: latency-bound at this batch, far from the roof"}
 
 
-def offpolicy_reuse(make_loop, n, ref_rows, flop_per_row, configs=((4096, 64), (16384, 16)),
-                    steps=3, warmup=1):
+def offpolicy_reuse(make_loop, n, ref_rows, flop_per_row,
+                    configs=((4096, 64), (16384, 16), (65536, 4)), steps=3, warmup=1):
     """The off-policy loop at the reference driver's sample reuse or near it: per vector step of n
     transitions, `iters` learn() iterations of `batch` rows (one captured graph replayed iters
     times), so sampled rows per transition = batch * iters / n against the reference's
-    `ref_rows` per transition (one ref_rows-row learn() per env step). Both configurations give
-    ratio 1/16 at the bench's n; the second takes 4x fewer, 4x fatter updates."""
+    `ref_rows` per transition (one ref_rows-row learn() per env step). The configurations give
+    ratio 1/16 at the bench's n; each takes 4x fewer, 4x fatter updates than the one before."""
     out = []
     for batch, iters in configs:
         loop, agent = make_loop(batch, iters)
@@ -292,15 +292,21 @@ def pmc_traffic(workload, n, T, kernel=None):
     return e["hbm_bytes_per_launch"]
 
 
-def pmc_kernel_traffic(name):
+def pmc_kernel_traffic(name, kernel):
     """HBM bytes per launch of an hbm_legs kernel from the committed PMC pass
-    (profiles/pmc_traffic.json "hbm_kernels"), or None."""
+    (profiles/pmc_traffic.json "hbm_kernels"), or None — also when that pass profiled other
+    kernels than `kernel` (the leg's label, launches joined by " + ")."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         e = json.load(f).get("hbm_kernels", {}).get(name)
-    return None if e is None else e.get("hbm_bytes_per_launch")
+    if e is None:
+        return None
+    parts = kernel.split(" + ")
+    if len(parts) != len(e["kernels"]) or not all(p.startswith(k) for p, k in zip(parts, e["kernels"])):
+        return None
+    return e.get("hbm_bytes_per_launch")
 
 
 class Segment:
@@ -345,10 +351,14 @@ class Segment:
         b = self.bufs
         # V(s'_t) of terminal transitions (non-terminal ones were written by the rollout)
         K.value_fixup(self.cd, self.cpk, b["obs_next"], b["done"], b["success"], b["value_next"])
-        K.reward_norm(b["reward"], self.rms, self.work, out=self.rnorm)
-        K.gae(self.rnorm, b["value"], b["value_next"], b["done"], b["success"], 0.999, 0.95,
-              adv=self.adv, v_target=self.vt, stats=self.stats)
-        K.adv_normalize(self.adv, self.stats)
+        # one rank's learn side as VecPPO2.advantages runs it: the reward statistics in one launch,
+        # GAE over the raw rewards normalised on load (+ the advantage statistics' merge), the
+        # advantage normalisation
+        K.reward_norm_statistics(b["reward"], self.rms, self.work)
+        K.gae_normalized(b["reward"], self.work, b["value"], b["value_next"], b["done"],
+                         b["success"], 0.999, 0.95, adv=self.adv, v_target=self.vt,
+                         stats=self.stats, merge_stats=True)
+        K.adv_apply(self.adv, self.stats, self.n)
 
     def iteration(self):
         self.rollout()
@@ -718,10 +728,12 @@ def ugvoa_leg(rank, n=16384, steps=30, warmup=3, seed=5):
 def ugvoa_ppo2_leg(rank, n=16384, T=64, iters=3, seed=17):
     """UGVForwardObstacleAvoidance PPO2 rollout (the PPO2 demo's 41 -> 256 -> 256 -> 2 / -> 1 tanh
     nets, demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97) through
-    rlp_rollout: ONE launch per segment (round 6, oa_rollout_kernel: each block owns 64 envs for
-    all T steps — actor + critic with layer 1 on 11 K-steps of exact f32 MFMA and the 256 x 256
-    hidden layer on the f16x3 split, the Philox sample, the lidar env step, the 37-beam scans and
-    the map-generator resets of the ended envs); n envs per GPU (config 5: 131 072 / 8)."""
+    rlp_rollout: two launches per step (round 6: oa_policy2_kernel — actor + critic with layer 1
+    on 11 K-steps of exact f32 MFMA and the 256 x 256 hidden layer on the f16x3 split, the Philox
+    sample — and oa_step_kernel<64> — the lidar env step, the 37-beam scans and the map-generator
+    resets of the ended envs), or one launch per segment under RLP_OA_ONE_LAUNCH=1
+    (oa_rollout_kernel, opt-in: DESIGN.md §4 round 6); n envs per GPU (config 5: 131 072 / 8)."""
+    one_launch = os.environ.get("RLP_OA_ONE_LAUNCH", "") == "1"
     kind = A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE
     p = A.default_params(kind, "ppo2")
     D, S, Ad = A.ENV_DIMS[kind]
@@ -771,10 +783,11 @@ def ugvoa_ppo2_leg(rank, n=16384, T=64, iters=3, seed=17):
                                        "%.1f TF" % (f_exact, PEAK_FP32_MFMA_TFLOPS, f_hidden,
                                                     PEAK_F16X3_TFLOPS),
                          "frac_vs_f32_peak": ach / PEAK_FP32_MFMA_TFLOPS,
-                         "kernel": "rlp::oa_rollout_kernel(rlp::OaSegArgs)",
-                         "note": "whole segment (the segment-start reset and observation, "
-                                 "oa_rollout_kernel's T steps + the bootstrap critic), the lidar "
-                                 "env's f64 work included, against the nets' FLOPs"},
+                         "kernel": ("rlp::oa_rollout_kernel(rlp::OaSegArgs const*)" if one_launch
+                                    else "rlp::oa_policy2_kernel + rlp::oa_step_kernel<64> per step"),
+                         "note": "whole segment (the segment-start reset and observation, the T "
+                                 "steps + the bootstrap critic), the lidar env's f64 work "
+                                 "included, against the nets' FLOPs"},
             "config": "UGVForwardObstacleAvoidance (PPO2 copy, 37-beam lidar, 10 circles) PPO2 "
                       "rollout, nets [41,256,256,2] / [41,256,256,1] tanh (rlp_rollout)"}
 
@@ -881,15 +894,26 @@ def hbm_legs(seg, n_env=1 << 22, iters=10, warmup=2):
                           "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS}, **(extra or {}))
 
     b, smp = seg.bufs, seg.n * seg.T
-    ms = timed(lambda: K.gae(seg.rnorm, b["value"], b["value_next"], b["done"], b["success"], 0.999,
-                             0.95, adv=seg.adv, v_target=seg.vt, stats=seg.stats))
-    put("gae", "rlp::gae_kernel", smp * (3 * 4 + 2 + 2 * 4), ms, {"samples": smp})
     rms = torch.zeros(4, dtype=torch.float64, device="cuda")
+    # the learn side's three launches (Segment.learn_side), each priced alone
+    ms = timed(lambda: K.reward_norm_statistics(b["reward"], rms, seg.work))
+    put("reward_norm", "rlp::reward_stats_fused_kernel<true>", smp * 4, ms,
+        {"samples": smp, "note": "the running statistics in one launch (chunk statistics, per-step "
+                                 "merges by each step's last block, the scan by the last step's "
+                                 "block); the rewards are normalised inside gae_kernel's load"})
+    ms = timed(lambda: K.gae_normalized(b["reward"], seg.work, b["value"], b["value_next"],
+                                        b["done"], b["success"], 0.999, 0.95, adv=seg.adv,
+                                        v_target=seg.vt, stats=seg.stats, merge_stats=True))
+    put("gae", "rlp::gae_kernel<true, true>", smp * (3 * 4 + 2 + 2 * 4), ms,
+        {"samples": smp, "note": "raw reward normalised on load + the advantage statistics' merge "
+                                 "by the grid's last block"})
+    ms = timed(lambda: K.adv_apply(seg.adv, seg.stats, seg.n))
+    put("adv_normalize", "rlp::adv_norm_kernel<true>", smp * 8, ms, {"samples": smp})
+    # the round-5 three-stage form (stats / merge / apply launches, the normalised rewards stored
+    # and re-read by GAE), for comparison
     ms = timed(lambda: K.reward_norm(b["reward"], rms, seg.work, out=seg.rnorm))
-    put("reward_norm", "rlp::reward_stats_kernel + reward_merge_kernel + reward_apply_kernel",
-        smp * 12, ms, {"samples": smp})
-    ms = timed(lambda: K.adv_normalize(seg.adv, seg.stats))
-    put("adv_normalize", "rlp::adv_stats_merge_kernel + adv_norm_kernel", smp * 8, ms,
+    put("reward_norm_stored", "rlp::reward_stats_fused_kernel<true> + rlp::reward_apply_kernel<true>",
+        smp * 12, ms,
         {"samples": smp})
     for env, kind, pf, dw in (("soi", A.RLP_ENV_SOI, lambda: A.soi_params("env"), 5),
                               ("ugv", A.RLP_ENV_UGV_FORWARD,
@@ -1216,7 +1240,7 @@ def main():
     if args.hbm:
         out["hbm_kernels"] = hbm_legs(seg)
         for k, v in out["hbm_kernels"].items():
-            v["traffic"] = pmc_kernel_traffic(k)
+            v["traffic"] = pmc_kernel_traffic(k, v["kernel"])
             v["hbm_frac_pmc"] = (None if v["traffic"] is None else
                                  v["traffic"] / (v["avg_launch_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS)
     if args.ddpg and args.env == "cartpole":

@@ -219,7 +219,8 @@ class VecPPO2:
         self.need = torch.ones(self.n, dtype=torch.uint8, device=self.device)
         self.bufs = K.rollout_buffers(self.kind, self.T, self.n, self.device)
         f32 = dict(dtype=torch.float32, device=self.device)
-        self.rnorm = torch.empty((self.T, self.n), **f32)
+        self._rnorm = torch.empty((self.T, self.n), **f32)
+        self._rnorm_stale = False
         self.adv = torch.empty((self.T, self.n), **f32)
         self.v_target = torch.empty((self.T, self.n), **f32)
         self.rms = torch.zeros(4, dtype=torch.float64, device=self.device)
@@ -284,18 +285,35 @@ class VecPPO2:
                           b["success"], b["value_next"])
         if self.global_norm:
             parts = self._gather(K.reward_norm_stats(b["reward"], self.work))
-            K.reward_norm_finish(b["reward"], self.rms, self.work, parts, self.world, out=self.rnorm)
-        else:
-            K.reward_norm(b["reward"], self.rms, self.work, out=self.rnorm)
-        K.gae(self.rnorm, b["value"], b["value_next"], b["done"], b["success"], self.msg['gamma'],
-              self.msg['lmd'], adv=self.adv, v_target=self.v_target, stats=self.stats)
-        if self.msg['use_adv_norm']:
-            parts = self.adv_parts
-            if self.global_norm:
+            K.reward_norm_finish(b["reward"], self.rms, self.work, parts, self.world, out=self._rnorm)
+            self._rnorm_stale = False
+            K.gae(self._rnorm, b["value"], b["value_next"], b["done"], b["success"],
+                  self.msg['gamma'], self.msg['lmd'], adv=self.adv, v_target=self.v_target,
+                  stats=self.stats)
+            if self.msg['use_adv_norm']:
+                parts = self.adv_parts
                 local = self.stats[:3 * parts].clone()
                 self.stats[:3 * parts * self.world] = self._gather(local)
-                parts *= self.world
-            K.adv_normalize(self.adv, self.stats, parts)
+                K.adv_normalize(self.adv, self.stats, parts * self.world)
+        else:  # one rank's statistics: 3 launches, the rewards normalised as GAE loads them
+            K.reward_norm_statistics(b["reward"], self.rms, self.work)
+            self._rnorm_stale = True
+            K.gae_normalized(b["reward"], self.work, b["value"], b["value_next"], b["done"],
+                             b["success"], self.msg['gamma'], self.msg['lmd'], adv=self.adv,
+                             v_target=self.v_target, stats=self.stats,
+                             merge_stats=bool(self.msg['use_adv_norm']))
+            if self.msg['use_adv_norm']:
+                K.adv_apply(self.adv, self.stats, self.n)
+
+    @property
+    def rnorm(self):
+        """the normalised rewards learn() consumed (computed on demand on the one-rank path, which
+        normalises them inside the GAE scan instead of storing them; valid until the next
+        rollout() overwrites the rewards)"""
+        if self._rnorm_stale:
+            K.reward_norm_apply(self.bufs["reward"], self.work, out=self._rnorm)
+            self._rnorm_stale = False
+        return self._rnorm
 
     def update(self):
         b = self.bufs

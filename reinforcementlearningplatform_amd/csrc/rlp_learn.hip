@@ -117,6 +117,100 @@ __global__ void __launch_bounds__(256) reward_stats_kernel(const float *__restri
     }
 }
 
+// loads of statistics other blocks of the same launch wrote (L2, past this CU's L1)
+__device__ __forceinline__ double ld_agent(const double *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// time step t's chunk statistics of `world` ranks (rank-major [world][T][P][2]) combined in global
+// env order -> (mean, M2) of its world * n rewards (one thread; loads kRsPre ahead of the combine)
+template <bool AGENT>
+__device__ __forceinline__ void rs_step_merge(const double *parts, int T, int n, int world, int t,
+                                              double &mean, double &m2) {
+    constexpr int kRsPre = 8;
+    const int P = rs_chunks(n), Q = world * P;
+    double c = 0;
+    mean = 0;
+    m2 = 0;
+    for (int q0 = 0; q0 < Q; q0 += kRsPre) {
+        double pm[kRsPre], pq[kRsPre];
+#pragma unroll
+        for (int u = 0; u < kRsPre; ++u) {
+            const int q = q0 + u, rk = q / P, p = q - rk * P;
+            const double *pp = parts + (((size_t)rk * T + t) * P + p) * 2;
+            pm[u] = q < Q ? (AGENT ? ld_agent(pp) : pp[0]) : 0.0;
+            pq[u] = q < Q ? (AGENT ? ld_agent(pp + 1) : pp[1]) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kRsPre; ++u) {
+            const int q = q0 + u, p = q % P;
+            if (q >= Q) break;
+            const double cb = min(kRsChunk, n - p * kRsChunk);
+            if (q == 0) {
+                c = cb; mean = pm[u]; m2 = pq[u];
+                continue;
+            }
+            const double nn = c + cb;
+            const double dl = pm[u] - mean;
+            mean = mean + dl * (cb / nn);
+            m2 = m2 + pq[u] + dl * dl * (c * cb / nn);
+            c = nn;
+        }
+    }
+}
+
+// the running statistics over t (whole block, 256 threads): a block-wide inclusive scan of Chan
+// merges of the per-step aggregates agg [T][2] (world * n rewards each) onto rms; writes step t's
+// (mean_t, std_t) to out [T][2] and the final statistics to rms
+template <bool AGENT>
+__device__ __forceinline__ void rs_running_scan(const double *agg, int T, double ntot, double *rms,
+                                                double *out) {
+    __shared__ Moments wred[4];
+    __shared__ double carry[4];
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 4; ++k) carry[k] = rms[k];
+    __syncthreads();
+    Moments cr{carry[0], carry[1], carry[2]};
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    auto ag = [&](int i) { return AGENT ? ld_agent(agg + i) : agg[i]; };
+    for (int t0 = 0; t0 < T; t0 += kRsTile) {
+        const int ta = t0 + 2 * (int)threadIdx.x, tb = ta + 1;
+        const Moments e0 = ta < T ? Moments{ntot, ag(2 * ta), ag(2 * ta + 1)} : Moments{0, 0, 0};
+        const Moments e1 = tb < T ? Moments{ntot, ag(2 * tb), ag(2 * tb + 1)} : Moments{0, 0, 0};
+        Moments v = chan(e0, e1);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive scan inside the wave
+            const Moments u{__shfl_up(v.c, o), __shfl_up(v.m, o), __shfl_up(v.q, o)};
+            if (l >= o) v = chan(u, v);
+        }
+        Moments ex{__shfl_up(v.c, 1), __shfl_up(v.m, 1), __shfl_up(v.q, 1)};
+        if (l == 0) ex = Moments{0, 0, 0};
+        if (l == 63) wred[w] = v;
+        __syncthreads();
+        Moments base = cr;
+        for (int i = 0; i < w; ++i) base = chan(base, wred[i]);
+        base = chan(base, ex);
+        Moments tot = cr;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tot = chan(tot, wred[i]);
+        __syncthreads();
+        const Moments s0 = chan(base, e0), s1 = chan(s0, e1);
+        if (ta < T) {
+            out[2 * ta] = s0.m;
+            out[2 * ta + 1] = sqrt(s0.q / s0.c);
+        }
+        if (tb < T) {
+            out[2 * tb] = s1.m;
+            out[2 * tb + 1] = sqrt(s1.q / s1.c);
+        }
+        cr = tot;
+    }
+    if (threadIdx.x == 0) {
+        rms[0] = cr.c; rms[1] = cr.m; rms[2] = cr.q;
+        rms[3] = T > 0 ? sqrt(cr.q / cr.c) : carry[3];
+    }
+}
+
 // Welford for a single env (the reference exactly, first-call std = x quirk included, serial),
 // Chan's parallel merge otherwise (utils/classes.py:626-645 RunningMeanStd.update). `parts` holds
 // the chunk statistics of `world` ranks of n envs each, rank-major ([world][T][P][2]); per time
@@ -126,14 +220,13 @@ __global__ void __launch_bounds__(256) reward_merge_kernel(const float *__restri
                                                            int world, const double *parts,
                                                            double *rms, double *work) {
     __shared__ double sa[kRsTile], sb[kRsTile];
-    __shared__ Moments wred[4];
     __shared__ double carry[4];
     const int P = rs_chunks(n);
     double *agg = work + (size_t)T * P * 2, *out = agg + (size_t)T * 2;
     const double ntot = (double)n * world;
-    if (threadIdx.x == 0)
-        for (int k = 0; k < 4; ++k) carry[k] = rms[k];
     if (ntot == 1) {  // the reference's own shape: one reward per step, serial Welford
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 4; ++k) carry[k] = rms[k];
         __syncthreads();
         for (int t0 = 0; t0 < T; t0 += kRsTile) {
             const int tn = min(kRsTile, T - t0);
@@ -169,78 +262,80 @@ __global__ void __launch_bounds__(256) reward_merge_kernel(const float *__restri
             for (int k = 0; k < 4; ++k) rms[k] = carry[k];
         return;
     }
-    // per time step: combine the chunks in global env order (the chunk statistics loaded in
-    // groups of kRsPre ahead of the serial combine)
-    constexpr int kRsPre = 8;
     for (int t = threadIdx.x; t < T; t += 256) {
-        double c = 0, mean = 0, m2 = 0;
-        const int Q = world * P;
-        for (int q0 = 0; q0 < Q; q0 += kRsPre) {
-            double pm[kRsPre], pq[kRsPre];
-#pragma unroll
-            for (int u = 0; u < kRsPre; ++u) {
-                const int q = q0 + u, rk = q / P, p = q - rk * P;
-                const double *pp = parts + (((size_t)rk * T + t) * P + p) * 2;
-                pm[u] = q < Q ? pp[0] : 0.0;
-                pq[u] = q < Q ? pp[1] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < kRsPre; ++u) {
-                const int q = q0 + u, p = q % P;
-                if (q >= Q) break;
-                const double cb = min(kRsChunk, n - p * kRsChunk);
-                if (q == 0) {
-                    c = cb; mean = pm[u]; m2 = pq[u];
-                    continue;
-                }
-                const double nn = c + cb;
-                const double dl = pm[u] - mean;
-                mean = mean + dl * (cb / nn);
-                m2 = m2 + pq[u] + dl * dl * (c * cb / nn);
-                c = nn;
-            }
-        }
+        double mean, m2;
+        rs_step_merge<false>(parts, T, n, world, t, mean, m2);
         agg[2 * t] = mean;
         agg[2 * t + 1] = m2;
     }
     __syncthreads();
-    Moments cr{carry[0], carry[1], carry[2]};
-    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int t0 = 0; t0 < T; t0 += kRsTile) {
-        const int ta = t0 + 2 * (int)threadIdx.x, tb = ta + 1;
-        const Moments e0 = ta < T ? Moments{ntot, agg[2 * ta], agg[2 * ta + 1]} : Moments{0, 0, 0};
-        const Moments e1 = tb < T ? Moments{ntot, agg[2 * tb], agg[2 * tb + 1]} : Moments{0, 0, 0};
-        Moments v = chan(e0, e1);
+    rs_running_scan<false>(agg, T, ntot, rms, out);
+}
+
+// rlp_reward_norm_statistics (one rank, n > 1) in ONE launch: the chunk statistics of
+// reward_stats_kernel; the last of step t's P chunk blocks to finish (a wrapping per-step counter)
+// combines that step's chunks (rs_step_merge); the last step to be combined (a wrapping global
+// counter) runs the running scan with its whole block. Same arithmetic in the same order as the
+// stats + merge launches, so the statistics are bit-identical. The counters (T + 1 u32 after the
+// [T][2] out array) return to zero at the end of every launch: work is zero-filled once.
+template <bool VEC>
+__global__ void __launch_bounds__(256) reward_stats_fused_kernel(const float *__restrict__ r, int T,
+                                                                 int n, double *rms, double *work) {
+    __shared__ double red[4];
+    __shared__ int last;
+    const int p = blockIdx.x, P = gridDim.x;
+    const int lo = p * kRsChunk, cnt = min(kRsChunk, n - lo);
+    double *part = work, *agg = work + (size_t)T * P * 2, *out = agg + (size_t)T * 2;
+    unsigned *ctr = (unsigned *)(out + (size_t)T * 2);
+    for (int t = blockIdx.y; t < T; t += gridDim.y) {
+        const float *x = r + (size_t)t * n + lo;
+        float v[kRsPer];
+        if (VEC) {
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {  // inclusive scan inside the wave
-            const Moments u{__shfl_up(v.c, o), __shfl_up(v.m, o), __shfl_up(v.q, o)};
-            if (l >= o) v = chan(u, v);
-        }
-        Moments ex{__shfl_up(v.c, 1), __shfl_up(v.m, 1), __shfl_up(v.q, 1)};
-        if (l == 0) ex = Moments{0, 0, 0};
-        if (l == 63) wred[w] = v;
-        __syncthreads();
-        Moments base = cr;
-        for (int i = 0; i < w; ++i) base = chan(base, wred[i]);
-        base = chan(base, ex);
-        Moments tot = cr;
+            for (int j = 0; j < kRsPer / 4; ++j) {
+                const int i = (j * 256 + (int)threadIdx.x) * 4;
+                const float4 q = i < cnt ? *(const float4 *)(x + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[4 * j] = q.x; v[4 * j + 1] = q.y; v[4 * j + 2] = q.z; v[4 * j + 3] = q.w;
+            }
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) tot = chan(tot, wred[i]);
+            for (int j = 0; j < kRsPer; ++j) {
+                const int i = j * 256 + threadIdx.x;
+                v[j] = i < cnt ? x[i] : 0.f;
+            }
+        }
+        double s = 0;
+#pragma unroll
+        for (int j = 0; j < kRsPer; ++j) s += (double)v[j];
+        const double mean = block_sum<256>(s, red) / cnt;
+        double q = 0;
+#pragma unroll
+        for (int j = 0; j < kRsPer; ++j) {
+            const int i = VEC ? (j / 4 * 256 + (int)threadIdx.x) * 4 + (j & 3) : j * 256 + threadIdx.x;
+            const double d = (double)v[j] - mean;
+            if (i < cnt) q += d * d;
+        }
+        const double m2 = block_sum<256>(q, red);
+        if (threadIdx.x == 0) {
+            part[((size_t)t * P + p) * 2 + 0] = mean;
+            part[((size_t)t * P + p) * 2 + 1] = m2;
+            __threadfence();  // the chunk's statistics before its count
+            int l = 0;
+            if (atomicInc(ctr + t, (unsigned)(P - 1)) == (unsigned)(P - 1)) {
+                __threadfence();
+                double sm, sq;
+                rs_step_merge<true>(part, T, n, 1, t, sm, sq);
+                agg[2 * t] = sm;
+                agg[2 * t + 1] = sq;
+                __threadfence();
+                l = atomicInc(ctr + T, (unsigned)(T - 1)) == (unsigned)(T - 1);
+                if (l) __threadfence();
+            }
+            last = l;
+        }
         __syncthreads();
-        const Moments s0 = chan(base, e0), s1 = chan(s0, e1);
-        if (ta < T) {
-            out[2 * ta] = s0.m;
-            out[2 * ta + 1] = sqrt(s0.q / s0.c);
-        }
-        if (tb < T) {
-            out[2 * tb] = s1.m;
-            out[2 * tb + 1] = sqrt(s1.q / s1.c);
-        }
-        cr = tot;
-    }
-    if (threadIdx.x == 0) {
-        rms[0] = cr.c; rms[1] = cr.m; rms[2] = cr.q;
-        rms[3] = T > 0 ? sqrt(cr.q / cr.c) : carry[3];
+        if (last) rs_running_scan<true>(agg, T, (double)n, rms, out);  // block-uniform
+        __syncthreads();
     }
 }
 
@@ -271,11 +366,37 @@ __global__ void __launch_bounds__(256) reward_apply_kernel(const float *__restri
     }
 }
 
+// the partials combined in a fixed order by one 256-thread block: thread j folds parts
+// [j*per, (j+1)*per) left to right, then the block combine; (mean, unbiased std) after the partials
+template <bool AGENT>
+__device__ __forceinline__ void adv_merge_block(double *stats, int parts) {
+    __shared__ Moments red[4];
+    const int per = (parts + 255) / 256, lo = threadIdx.x * per, hi = min(parts, lo + per);
+    Moments a{0, 0, 0};
+    for (int j = lo; j < hi; ++j) {
+        const double *q = stats + 3 * j;
+        a = chan(a, AGENT ? Moments{ld_agent(q), ld_agent(q + 1), ld_agent(q + 2)}
+                          : Moments{q[0], q[1], q[2]});
+    }
+    a = block_moments<256>(a, red);
+    if (threadIdx.x == 0) {
+        stats[3 * parts] = a.m;
+        stats[3 * parts + 1] = a.c > 1 ? sqrt(a.q / (a.c - 1)) : 0.0;
+    }
+}
+
 // GAE backward scan, one env per lane; coalesced [T][n] rows. The recurrence is serial in t, so
 // each lane's loads are issued kGaeU steps ahead of the arithmetic (registers), which is what
 // keeps HBM busy with only n / 64 waves in the grid.
+// NORM: r is the raw reward and rs [T][2] step t's (mean_t, std_t) of rlp_reward_norm_statistics:
+// the reward is normalised as it is loaded, (float)((r - mean_t) / (std_t + 1e-8)) — the apply
+// pass's expression, so the normalised-reward array is neither written nor re-read.
+// MERGE: the grid's last block to finish (a wrapping counter after the (mean, std) slots) combines
+// the per-block partials (adv_merge_block), so rlp_adv_apply needs no merge launch.
 constexpr int kGaeU = 16;
+template <bool NORM, bool MERGE>
 __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
+                                                  const double *__restrict__ rs,
                                                   const float *__restrict__ v,
                                                   const float *__restrict__ vn,
                                                   const uint8_t *__restrict__ done,
@@ -283,6 +404,7 @@ __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
                                                   float c, int T, int n, float *__restrict__ adv,
                                                   float *__restrict__ vt, double *stats) {
     __shared__ Moments red[4];
+    __shared__ int last;
     const int i = blockIdx.x * 256 + threadIdx.x;
     double s1 = 0, s2 = 0, k0 = 0;  // sums of (adv - k0), k0 = the lane's first advantage
     if (i < n) {
@@ -291,17 +413,23 @@ __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
             const int u = min(kGaeU, t1);
             float rr[kGaeU], vv[kGaeU], vx[kGaeU];
             uint8_t dd[kGaeU], ss[kGaeU];
+            double rm[NORM ? kGaeU : 1], rd[NORM ? kGaeU : 1];
 #pragma unroll
             for (int j = 0; j < kGaeU; ++j) {
                 if (j < u) {
                     const size_t k = (size_t)(t1 - 1 - j) * n + i;
                     rr[j] = r[k]; vv[j] = v[k]; vx[j] = vn[k]; dd[j] = done[k]; ss[j] = success[k];
+                    if (NORM) {  // step t's statistics (uniform: scalar loads), with the rows
+                        rm[j] = rs[2 * (t1 - 1 - j)];
+                        rd[j] = rs[2 * (t1 - 1 - j) + 1];
+                    }
                 }
             }
 #pragma unroll
             for (int j = 0; j < kGaeU; ++j) {
                 if (j < u) {
                     const size_t k = (size_t)(t1 - 1 - j) * n + i;
+                    if (NORM) rr[j] = (float)(((double)rr[j] - rm[j]) / (rd[j] + 1e-8));
                     const float one_s = 1.0f - (float)ss[j];
                     float delta = rr[j] + (g32 * one_s) * vx[j];
                     delta = delta - vv[j];
@@ -329,22 +457,23 @@ __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
             stats[3 * blockIdx.x + 0] = mo.c;
             stats[3 * blockIdx.x + 1] = mo.m;
             stats[3 * blockIdx.x + 2] = mo.q;
+            if (MERGE) {
+                __threadfence();
+                unsigned *ctr = (unsigned *)(stats + 3 * (size_t)gridDim.x + 2);
+                const int l = atomicInc(ctr, gridDim.x - 1) == gridDim.x - 1;
+                if (l) __threadfence();
+                last = l;
+            }
+        }
+        if (MERGE) {
+            __syncthreads();
+            if (last) adv_merge_block<true>(stats, gridDim.x);  // block-uniform
         }
     }
 }
 
-// the partials combined in a fixed order: thread j folds parts [j*per, (j+1)*per) left to right,
-// then the block combine above; writes (mean, unbiased std) after the partials
 __global__ void __launch_bounds__(256) adv_stats_merge_kernel(double *stats, int parts) {
-    __shared__ Moments red[4];
-    const int per = (parts + 255) / 256, lo = threadIdx.x * per, hi = min(parts, lo + per);
-    Moments a{0, 0, 0};
-    for (int j = lo; j < hi; ++j) a = chan(a, Moments{stats[3 * j], stats[3 * j + 1], stats[3 * j + 2]});
-    a = block_moments<256>(a, red);
-    if (threadIdx.x == 0) {
-        stats[3 * parts] = a.m;
-        stats[3 * parts + 1] = a.c > 1 ? sqrt(a.q / (a.c - 1)) : 0.0;
-    }
+    adv_merge_block<false>(stats, parts);
 }
 
 // 4 advantages per lane as one 16-byte access (the tail of count % 4 by the first lanes) when
@@ -381,7 +510,8 @@ extern "C" {
 
 int64_t rlp_reward_norm_workspace(int T, int n) {
     if (T < 0 || n < 0) return RLP_EINVAL;
-    return (int64_t)T * (2 * (int64_t)rs_chunks(n > 0 ? n : 1) + 4);
+    // part [T][P][2] | agg [T][2] | out [T][2] | T + 1 u32 counters (reward_stats_fused_kernel)
+    return (int64_t)T * (2 * (int64_t)rs_chunks(n > 0 ? n : 1) + 4) + ((int64_t)T + 2) / 2;
 }
 
 int64_t rlp_reward_norm_parts(int T, int n) {
@@ -402,17 +532,27 @@ int rlp_reward_norm_stats(const float *reward_in, int T, int n, double *work, rl
     return RLP_OK;
 }
 
-int rlp_reward_norm_finish(const float *reward_in, int T, int n, int world, const double *parts,
-                           double *rms, double *work, float *reward_out, rlp_stream_t stream) {
-    RLP_REQUIRE(reward_in && rms && work && reward_out, "rlp_reward_norm_finish: null argument");
-    RLP_REQUIRE(T >= 0 && n >= 0 && world >= 1, "rlp_reward_norm_finish: T=%d n=%d world=%d", T, n,
-                world);
-    RLP_REQUIRE(parts || (world == 1 && n == 1), "rlp_reward_norm_finish: null parts");
+int rlp_reward_norm_statistics(const float *reward_in, int T, int n, double *rms, double *work,
+                               rlp_stream_t stream) {
+    RLP_REQUIRE(reward_in && rms && work, "rlp_reward_norm_statistics: null argument");
+    RLP_REQUIRE(T >= 0 && n >= 0, "rlp_reward_norm_statistics: T=%d n=%d", T, n);
     if (T == 0 || n == 0) return RLP_OK;
     hipStream_t s = as_stream(stream);
-    const int P = rs_chunks(n);
-    reward_merge_kernel<<<1, 256, 0, s>>>(reward_in, T, n, world, parts, rms, work);
-    const double *out_t = work + (size_t)T * P * 2 + (size_t)T * 2;
+    if (n == 1) {  // the serial Welford recurrence
+        reward_merge_kernel<<<1, 256, 0, s>>>(reward_in, T, n, 1, work, rms, work);
+    } else {
+        const dim3 grid(rs_chunks(n), T < 65535 ? T : 65535);
+        if (n % 4 == 0 && aligned16(reward_in))
+            reward_stats_fused_kernel<true><<<grid, 256, 0, s>>>(reward_in, T, n, rms, work);
+        else
+            reward_stats_fused_kernel<false><<<grid, 256, 0, s>>>(reward_in, T, n, rms, work);
+    }
+    RLP_CHECK_LAUNCH("rlp_reward_norm_statistics");
+    return RLP_OK;
+}
+
+static void reward_apply(const float *reward_in, int T, int n, const double *out_t,
+                         float *reward_out, hipStream_t s) {
     const bool vec = n % 4 == 0 && aligned16(reward_in) && aligned16(reward_out);
     const int per = vec ? 1024 : 256, bx = (n + per - 1) / per;
     const int cap = T >= 256 ? 64 : 16384 / (T > 0 ? T : 1);  // >= 16k blocks in flight
@@ -421,6 +561,22 @@ int rlp_reward_norm_finish(const float *reward_in, int T, int n, int world, cons
         reward_apply_kernel<true><<<grid, 256, 0, s>>>(reward_in, T, n, out_t, reward_out);
     else
         reward_apply_kernel<false><<<grid, 256, 0, s>>>(reward_in, T, n, out_t, reward_out);
+}
+
+static const double *reward_step_stats(const double *work, int T, int n) {
+    return work + (size_t)T * rs_chunks(n) * 2 + (size_t)T * 2;
+}
+
+int rlp_reward_norm_finish(const float *reward_in, int T, int n, int world, const double *parts,
+                           double *rms, double *work, float *reward_out, rlp_stream_t stream) {
+    RLP_REQUIRE(reward_in && rms && work && reward_out, "rlp_reward_norm_finish: null argument");
+    RLP_REQUIRE(T >= 0 && n >= 0 && world >= 1, "rlp_reward_norm_finish: T=%d n=%d world=%d", T, n,
+                world);
+    RLP_REQUIRE(parts || (world == 1 && n == 1), "rlp_reward_norm_finish: null parts");
+    if (T == 0 || n == 0) return RLP_OK;
+    hipStream_t s = as_stream(stream);
+    reward_merge_kernel<<<1, 256, 0, s>>>(reward_in, T, n, world, parts, rms, work);
+    reward_apply(reward_in, T, n, reward_step_stats(work, T, n), reward_out, s);
     RLP_CHECK_LAUNCH("rlp_reward_norm_finish");
     return RLP_OK;
 }
@@ -430,11 +586,21 @@ int rlp_reward_norm(const float *reward_in, int T, int n, double *rms, double *w
     RLP_REQUIRE(reward_in && rms && work && reward_out, "rlp_reward_norm: null argument");
     RLP_REQUIRE(T >= 0 && n >= 0, "rlp_reward_norm: T=%d n=%d", T, n);
     if (T == 0 || n == 0) return RLP_OK;
-    if (n > 1) {
-        const int rc = rlp_reward_norm_stats(reward_in, T, n, work, stream);
-        if (rc != RLP_OK) return rc;
-    }
-    return rlp_reward_norm_finish(reward_in, T, n, 1, work, rms, work, reward_out, stream);
+    const int rc = rlp_reward_norm_statistics(reward_in, T, n, rms, work, stream);
+    if (rc != RLP_OK) return rc;
+    reward_apply(reward_in, T, n, reward_step_stats(work, T, n), reward_out, as_stream(stream));
+    RLP_CHECK_LAUNCH("rlp_reward_norm");
+    return RLP_OK;
+}
+
+int rlp_reward_norm_apply(const float *reward_in, int T, int n, const double *work,
+                          float *reward_out, rlp_stream_t stream) {
+    RLP_REQUIRE(reward_in && work && reward_out, "rlp_reward_norm_apply: null argument");
+    RLP_REQUIRE(T >= 0 && n >= 0, "rlp_reward_norm_apply: T=%d n=%d", T, n);
+    if (T == 0 || n == 0) return RLP_OK;
+    reward_apply(reward_in, T, n, reward_step_stats(work, T, n), reward_out, as_stream(stream));
+    RLP_CHECK_LAUNCH("rlp_reward_norm_apply");
+    return RLP_OK;
 }
 
 int rlp_gae(const float *reward, const float *value, const float *value_next, const uint8_t *done,
@@ -446,14 +612,46 @@ int rlp_gae(const float *reward, const float *value, const float *value_next, co
     if (T == 0 || n == 0) return RLP_OK;
     const float g32 = (float)gamma;       // torch: gamma * (1 - success) in fp32
     const float c = (float)(gamma * lambda);  // numpy: (gamma * lmd) * gae, NEP-50 fp32
-    gae_kernel<<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(reward, value, value_next, done,
-                                                               success, g32, c, T, n, adv,
-                                                               v_target, adv_stats);
+    gae_kernel<false, false><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
+        reward, nullptr, value, value_next, done, success, g32, c, T, n, adv, v_target, adv_stats);
     RLP_CHECK_LAUNCH("rlp_gae");
     return RLP_OK;
 }
 
+int rlp_gae_normalized(const float *reward_raw, const double *reward_work, const float *value,
+                       const float *value_next, const uint8_t *done, const uint8_t *success,
+                       double gamma, double lambda, int T, int n, float *adv, float *v_target,
+                       double *adv_stats, int merge_adv_stats, rlp_stream_t stream) {
+    RLP_REQUIRE(reward_raw && reward_work && value && value_next && done && success && adv &&
+                v_target, "rlp_gae_normalized: null argument");
+    RLP_REQUIRE(T >= 0 && n >= 0, "rlp_gae_normalized: T=%d n=%d", T, n);
+    RLP_REQUIRE(!merge_adv_stats || adv_stats, "rlp_gae_normalized: merge_adv_stats without adv_stats");
+    if (T == 0 || n == 0) return RLP_OK;
+    const float g32 = (float)gamma, c = (float)(gamma * lambda);
+    const double *rs = reward_step_stats(reward_work, T, n);
+    hipStream_t s = as_stream(stream);
+    const int nb = (n + 255) / 256;
+    if (merge_adv_stats)
+        gae_kernel<true, true><<<nb, 256, 0, s>>>(reward_raw, rs, value, value_next, done, success,
+                                                   g32, c, T, n, adv, v_target, adv_stats);
+    else
+        gae_kernel<true, false><<<nb, 256, 0, s>>>(reward_raw, rs, value, value_next, done, success,
+                                                    g32, c, T, n, adv, v_target, adv_stats);
+    RLP_CHECK_LAUNCH("rlp_gae_normalized");
+    return RLP_OK;
+}
+
 int rlp_adv_stats_parts(int n) { return n < 0 ? RLP_EINVAL : (n + 255) / 256; }
+
+static void adv_apply(float *adv, int64_t count, const double *ms, hipStream_t s) {
+    if (aligned16(adv)) {
+        const int64_t b = (count / 4 + 255) / 256;
+        adv_norm_kernel<true><<<(int)(b < 1 ? 1 : b < 8192 ? b : 8192), 256, 0, s>>>(adv, count, ms);
+    } else {
+        const int64_t b = (count + 255) / 256;
+        adv_norm_kernel<false><<<(int)(b < 8192 ? b : 8192), 256, 0, s>>>(adv, count, ms);
+    }
+}
 
 int rlp_adv_normalize(float *adv, int64_t count, double *adv_stats, int parts,
                       rlp_stream_t stream) {
@@ -462,15 +660,16 @@ int rlp_adv_normalize(float *adv, int64_t count, double *adv_stats, int parts,
     if (count <= 1) return RLP_OK;
     hipStream_t s = as_stream(stream);
     adv_stats_merge_kernel<<<1, 256, 0, s>>>(adv_stats, parts);
-    const double *ms = adv_stats + 3 * (size_t)parts;
-    if (aligned16(adv)) {
-        const int64_t b = (count / 4 + 255) / 256;
-        adv_norm_kernel<true><<<(int)(b < 1 ? 1 : b < 8192 ? b : 8192), 256, 0, s>>>(adv, count, ms);
-    } else {
-        const int64_t b = (count + 255) / 256;
-        adv_norm_kernel<false><<<(int)(b < 8192 ? b : 8192), 256, 0, s>>>(adv, count, ms);
-    }
+    adv_apply(adv, count, adv_stats + 3 * (size_t)parts, s);
     RLP_CHECK_LAUNCH("rlp_adv_normalize");
+    return RLP_OK;
+}
+
+int rlp_adv_apply(float *adv, int64_t count, const double *mean_std, rlp_stream_t stream) {
+    RLP_REQUIRE(adv && mean_std, "rlp_adv_apply: null argument");
+    if (count <= 1) return RLP_OK;
+    adv_apply(adv, count, mean_std, as_stream(stream));
+    RLP_CHECK_LAUNCH("rlp_adv_apply");
     return RLP_OK;
 }
 

@@ -663,20 +663,23 @@ static int rollout_kind(const void *params, double *state, uint8_t *need_reset, 
 // UGVForwardObstacleAvoidance PPO2 / DPPO2 rollout (demonstration/PPO2/PPO2-4-UGVForward
 // ObstacleAvoidance/train.py:48-50,95-97: 41 -> 256 -> 256 -> 2 actor, 41 -> 256 -> 256 -> 1
 // critic, tanh; DPPO2 copy likewise). ONE rlp_rollout call runs the driver loop on the caller's
-// stream (no host round trip, no synchronisation). With the f16x3 hidden layer (the default) the
-// whole segment is one launch, oa_rollout_kernel (below). Under RLP_MLP_FP32 it is two launches
-// per step:
-//   oa_policy_kernel   per 16-env wave: actor and critic forward (layer 1 as 11 K-steps of the
-//                      exact f32 16x16x4 MFMA, the 256 x 256 hidden layer on exact f32 MFMA), then
-//                      the Philox sample (the fused kernel's stream), clamp, log-prob, V(s_t), and
+// stream (no host round trip, no synchronisation): two launches per step,
+//   oa_policy2_kernel  (f16x3, the default: 8-wave blocks over 64 rows, waves 0-3 the actor,
+//   / oa_policy_kernel 4-7 the critic; RLP_MLP_FP32: per 16-env wave, both nets in turn): actor
+//                      and critic forward (layer 1 as 11 K-steps of the exact f32 16x16x4 MFMA,
+//                      the 256 x 256 hidden layer on f16x3 / exact f32 MFMA), then the Philox
+//                      sample (the fused kernel's stream), clamp, log-prob, V(s_t), and
 //                      V(s'_{t-1}) = V(s_t) where the env did not end at t-1
 //   oa_step_kernel     lidar env step (dynamics, terminal, reward: one lane per env), the
 //                      success rule, the 37-beam scan of s' (one (env, beam) pair per lane) into
 //                      obs_next and — for envs still running — obs_{t+1}; ended envs reset with the
 //                      map generator (one wave per env, counter step0 + t + 1) and scan the new pose
 //                      into obs_{t+1}
-// and after the segment the bootstrap V(s'_{T-1}) of the envs still running (oa_policy_kernel,
-// critic only). Same semantics, same random draws and same buffers in both forms.
+// and after the segment the bootstrap V(s'_{T-1}) of the envs still running (the policy kernel,
+// critic only). RLP_OA_ONE_LAUNCH=1 runs the f16x3 segment as ONE launch instead
+// (oa_rollout_kernel, below: 5.31 against 6.66 ms per 16 384 x 64 segment), opt-in only: it
+// faulted (illegal address) when run after other streams of the process had run work; the cause
+// is not found. Same semantics, random draws and buffers in every form.
 struct OaPolicyArgs {
     const float *actor, *critic;
     MfmaNet an, cn;
@@ -821,6 +824,7 @@ __global__ void __launch_bounds__(512, 1) oa_policy2_kernel(OaPolicyArgs pa) {
 #define OA_GUARD(cond, what) true
 #endif
 constexpr int kOaSegEnvs = 64;
+constexpr int kOaArgsBytes = 1024;  // rlp_rollout_workspace_bytes of the lidar env
 
 // 4 waves per SIMD (<= 128 registers, ~240 B of scratch spills): the kernel's phases are latency
 // chains (per-env f64 dynamics and setup, divergent beams, the map generator's rounds) that only
@@ -932,7 +936,7 @@ struct OaSegArgs {
     rlp_rollout_bufs b;
 };
 
-// the two phases; the launch's arguments are re-read from the kernarg segment at each phase (an
+// the two phases; the launch's arguments are re-read from their workspace copy at each phase (an
 // opaque scalar pointer per phase), so no parameter is held in registers across the other phase
 __device__ __forceinline__ void oa_seg_policy(const OaSegArgs &g, OaSegLds &Z, float *small0,
                                                         float *small1, float *ring, float (*sact)[OA::A],
@@ -1074,18 +1078,44 @@ __device__ __forceinline__ void oa_seg_step(const OaSegArgs &g, OaSegLds &Z,
     }
 }
 
-__global__ void __launch_bounds__(512, 1) oa_rollout_kernel(OaSegArgs g) {
+// The launch's arguments are read from a copy in the caller's workspace (oa_args_kernel writes
+// it, stream-ordered, from its own kernarg segment), not from this launch's kernarg segment: a
+// multi-millisecond launch that re-reads its kernarg segment at every phase depends on the
+// runtime keeping that segment intact for the whole launch.
+static_assert(sizeof(OaSegArgs) <= kOaArgsBytes && sizeof(OaSegArgs) % 16 == 0, "OaSegArgs copy");
+__global__ void __launch_bounds__(64) oa_args_kernel(OaSegArgs a, OaSegArgs *dst) {
+    if (threadIdx.x == 0) *dst = a;
+}
+
+#ifdef RLP_OA_KCHECK  // diagnostic build: does this launch's kernarg segment change while it runs?
+struct OaKcheckArgs {  // the kernarg segment of the diagnostic build's oa_rollout_kernel
+    const OaSegArgs *ga;
+    OaSegArgs kg;
+    unsigned *diag;
+};
+#define OA_KCHECK_PARAMS , OaSegArgs kg, unsigned *diag
+#define OA_KCHECK_ARGS(a) , a, (unsigned *)nullptr
+#else
+#define OA_KCHECK_PARAMS
+#define OA_KCHECK_ARGS(a)
+#endif
+
+__global__ void __launch_bounds__(512, 1) oa_rollout_kernel(const OaSegArgs *ga OA_KCHECK_PARAMS) {
     constexpr int EB = kOaSegEnvs, S = OA::S;
     __shared__ __attribute__((aligned(16))) float lds[kOaSmallA + kOaSmallC + 2 * kOaPol2Ring * kX3ChunkFloats];
     __shared__ float sact[EB][OA::A];
     __shared__ uint8_t sdone[EB];  // done of the previous step (V(s'_{t-1}) bookkeeping)
     float *small0 = lds, *small1 = lds + kOaSmallA, *rings = lds + kOaSmallA + kOaSmallC;
     OaSegLds &Z = *reinterpret_cast<OaSegLds *>(rings);
+    const OaSegArgs &g = *ga;
     mlp_small_to_lds(g.actor, g.an, small0, true);
     mlp_small_to_lds(g.critic, g.cn, small1, true);
     const int tid = threadIdx.x, grp = __builtin_amdgcn_readfirstlane((tid >> 6) >> 2);
     float *ring = rings + grp * kOaPol2Ring * kX3ChunkFloats;
     const int n = g.ra.n, T = g.ra.T;
+#ifdef RLP_OA_KCHECK
+    bool reported = false;
+#endif
     for (int e0 = blockIdx.x * EB; e0 < n; e0 += gridDim.x * EB) {  // block-uniform
         const int ne = n - e0 < EB ? n - e0 : EB;
         __syncthreads();  // (the resident parts loaded; the previous group's last pass done)
@@ -1095,17 +1125,32 @@ __global__ void __launch_bounds__(512, 1) oa_rollout_kernel(OaSegArgs g) {
         }
         __syncthreads();
         for (int t = 0; t <= T; ++t) {
+#ifdef RLP_OA_KCHECK
+            if (tid == 0 && !reported) {
+                const auto *k = (const __attribute__((address_space(4))) OaKcheckArgs *)
+                    __builtin_amdgcn_kernarg_segment_ptr();
+                asm volatile("" : "+s"(k));
+                const bool same = k->kg.state == ga->state && k->kg.actor == ga->actor &&
+                                  k->kg.critic == ga->critic && k->kg.b.obs == ga->b.obs &&
+                                  k->kg.b.action == ga->b.action && k->kg.ra.n == ga->ra.n;
+                if (!same) {
+                    printf("oa_rollout_kernel: kernarg segment changed, block %d step %d\n",
+                           (int)blockIdx.x, t);
+                    reported = true;
+                }
+            }
+#endif
             {
-                auto ak = (const __attribute__((address_space(4))) OaSegArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-                asm volatile("" : "+s"(ak));
-                oa_seg_policy(*(const OaSegArgs *)ak, Z, small0, small1, ring, sact, sdone, e0, ne, t);
+                const OaSegArgs *gp = ga;
+                asm volatile("" : "+s"(gp));  // re-read per phase (scalar loads), not held
+                oa_seg_policy(*gp, Z, small0, small1, ring, sact, sdone, e0, ne, t);
             }
             __syncthreads();  // actions in LDS; every wave is done with the rings
             if (t == T) break;
             {
-                auto ak = (const __attribute__((address_space(4))) OaSegArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-                asm volatile("" : "+s"(ak));
-                oa_seg_step(*(const OaSegArgs *)ak, Z, sact, sdone, e0, ne, t);
+                const OaSegArgs *gp = ga;
+                asm volatile("" : "+s"(gp));
+                oa_seg_step(*gp, Z, sact, sdone, e0, ne, t);
             }
             // the state a reset wave wrote is read by another wave at the next step: stores done
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1114,8 +1159,8 @@ __global__ void __launch_bounds__(512, 1) oa_rollout_kernel(OaSegArgs g) {
     }
 }
 
-// RLP_OA_ONE_LAUNCH=1 selects the one-launch segment for the f16x3 hidden layer (read once; see
-// DESIGN.md §4 round 6 for why it is not the default)
+// RLP_OA_ONE_LAUNCH=1 selects the one-launch segment for the f16x3 hidden layer (read once).
+// Opt-in only: see the section comment above and DESIGN.md §4 round 6.
 static bool oa_one_launch() {
     static const bool on = [] {
         const char *v = getenv("RLP_OA_ONE_LAUNCH");
@@ -1126,7 +1171,8 @@ static bool oa_one_launch() {
 
 static int rollout_oa(const void *params, double *state, uint8_t *need_reset, const float *actor,
                       const MfmaNet &an, const float *critic, const MfmaNet &cn,
-                      const RolloutArgs &ra, const rlp_rollout_bufs &b, int prec, hipStream_t s) {
+                      const RolloutArgs &ra, const rlp_rollout_bufs &b, int prec, void *workspace,
+                      int64_t workspace_bytes, hipStream_t s) {
     const auto &p = *static_cast<const OA::P *>(params);
     if (an.S != OA::S || cn.S != OA::S || an.A != OA::A || cn.A != 1)
         return fail(RLP_EINVAL, "rlp_rollout: net dims (S=%d,A=%d / S=%d,A=%d) != env (S=%d,A=%d)",
@@ -1154,9 +1200,14 @@ static int rollout_oa(const void *params, double *state, uint8_t *need_reset, co
     if (rc == RLP_OK) rc = launch_ugvoa_observe(p, state, n, b.obs, s);
     if (rc != RLP_OK) return rc;
     if (prec == RLP_MLP_F16X3 && oa_one_launch()) {  // the whole segment in one launch
+        if (!workspace || workspace_bytes < kOaArgsBytes)
+            return fail(RLP_EINVAL, "rlp_rollout: the lidar segment needs %d workspace bytes",
+                        kOaArgsBytes);
         const int nb = (n + kOaSegEnvs - 1) / kOaSegEnvs;
-        oa_rollout_kernel<<<nb < cus ? nb : cus, 512, 0, s>>>(
-            OaSegArgs{p, state, need_reset, actor, critic, an, cn, ra, b});
+        const OaSegArgs a{p, state, need_reset, actor, critic, an, cn, ra, b};
+        OaSegArgs *ga = static_cast<OaSegArgs *>(workspace);
+        oa_args_kernel<<<1, 64, 0, s>>>(a, ga);
+        oa_rollout_kernel<<<nb < cus ? nb : cus, 512, 0, s>>>(ga OA_KCHECK_ARGS(a));
         RLP_CHECK_LAUNCH("rlp_rollout (UGVForwardObstacleAvoidance)");
         return RLP_OK;
     }
@@ -1388,7 +1439,8 @@ int64_t rlp_rollout_workspace_bytes(int kind, const rlp_mlp_desc *actor_desc,
     if (!actor_desc || !critic_desc || !cfg || cfg->n < 0 || cfg->T < 1) return RLP_EINVAL;
     if (cfg->net_layout == 1) return rollout_plain_ws_bytes(*actor_desc, *critic_desc, cfg->n);
     if (cfg->net_layout != 0) return RLP_EINVAL;
-    return 0;  // the fused kernels and the lidar env's two launches per step need no scratch
+    // the lidar segment kernel's argument copy; the other fused kernels need no scratch
+    return kind == RLP_ENV_UGV_OBSTACLE_AVOIDANCE ? kOaArgsBytes : 0;
 }
 
 int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_reset,
@@ -1484,7 +1536,7 @@ int rlp_rollout(int kind, const void *env_params, double *state, uint8_t *need_r
                                                           b, sub, prec, physics, s);
     case RLP_ENV_UGV_OBSTACLE_AVOIDANCE:
         return rollout_oa(env_params, state, need_reset, actor_packed, an, critic_packed, cn, ra, b,
-                          prec, s);
+                          prec, cfg->workspace, cfg->workspace_bytes, s);
     }
     return fail(RLP_EINVAL, "rlp_rollout: unknown env kind %d", kind);
 }

@@ -112,9 +112,9 @@ def test_workspaces_are_caller_owned_and_checked():
     cfg.net_layout = 0
     big = _abi.MLPDesc.make([41, 256, 256, 2], [1, 1, 1])
     bigc = _abi.MLPDesc.make([41, 256, 256, 1], [1, 1, 0])
-    # the lidar env's rollout (two launches per step since round 6) needs no scratch either
+    # the lidar env's rollout: 1 KiB, the one-launch segment kernel's copy of its arguments
     assert lib.rlp_rollout_workspace_bytes(_abi.RLP_ENV_UGV_OBSTACLE_AVOIDANCE, C.byref(big),
-                                           C.byref(bigc), C.byref(cfg)) == 0
+                                           C.byref(bigc), C.byref(cfg)) == 1024
     assert lib.rlp_rollout_workspace_bytes(_abi.RLP_ENV_CARTPOLE, C.byref(big), C.byref(bigc),
                                            C.byref(cfg)) == 0
 

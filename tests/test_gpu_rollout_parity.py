@@ -337,8 +337,8 @@ def test_rollout_env_copies_teacher_forced(kind, variant):
 
 
 def test_rollout_lidar_env_teacher_forced_config5_shard():
-    """The lidar rollout at BASELINE config 5's shard size (131 072 / 8 = 16 384 envs), which takes
-    the one-launch-per-segment kernel with every CU busy: two chained segments with resets inside,
+    """The lidar rollout at BASELINE config 5's shard size (131 072 / 8 = 16 384 envs), every CU
+    busy (oa_policy2_kernel + oa_step_kernel<64> per step): two chained segments with resets inside,
     physics teacher-forced against the oracle for all envs (flags / done exact, state 1e-9,
     observations 2 ulps, rewards), the oracle's own policy and critic on the first 1 024 envs."""
     kind = A.RLP_ENV_UGV_OBSTACLE_AVOIDANCE
@@ -369,8 +369,9 @@ def test_rollout_lidar_env_teacher_forced_config5_shard():
 
 @pytest.mark.parametrize("variant,precision", [("env", "f16x3"), ("ppo2", "f16x3"), ("ppo2", "fp32")])
 def test_rollout_lidar_env_teacher_forced(variant, precision):
-    """UGVForwardObstacleAvoidance through rlp_rollout (round 6: one launch per segment with the
-    f16x3 hidden layer, oa_rollout_kernel; exact f32: oa_policy_kernel + oa_step_kernel per step),
+    """UGVForwardObstacleAvoidance through rlp_rollout (round 6: two launches per step, the policy
+    — oa_policy2_kernel with the f16x3 hidden layer, oa_policy_kernel on exact f32 — and
+    oa_step_kernel),
     the PPO2 demo's 41 -> 256 -> 256 -> 2 / -> 1 nets
     (demonstration/PPO2/PPO2-4-UGVForwardObstacleAvoidance/train.py:48-50,95-97), two chained
     segments with resets inside: physics teacher-forced against the oracle (flags / done exact,
