@@ -351,14 +351,14 @@ class Segment:
         b = self.bufs
         # V(s'_t) of terminal transitions (non-terminal ones were written by the rollout)
         K.value_fixup(self.cd, self.cpk, b["obs_next"], b["done"], b["success"], b["value_next"])
-        # one rank's learn side as VecPPO2.advantages runs it: the reward statistics in one launch,
-        # GAE over the raw rewards normalised on load (+ the advantage statistics' merge), the
+        # one rank's learn side as VecPPO2.advantages runs it: the reward statistics, GAE over
+        # the raw rewards normalised on load (the normalised rewards are not stored), the
         # advantage normalisation
         K.reward_norm_statistics(b["reward"], self.rms, self.work)
         K.gae_normalized(b["reward"], self.work, b["value"], b["value_next"], b["done"],
                          b["success"], 0.999, 0.95, adv=self.adv, v_target=self.vt,
-                         stats=self.stats, merge_stats=True)
-        K.adv_apply(self.adv, self.stats, self.n)
+                         stats=self.stats)
+        K.adv_normalize(self.adv, self.stats)
 
     def iteration(self):
         self.rollout()
@@ -895,26 +895,26 @@ def hbm_legs(seg, n_env=1 << 22, iters=10, warmup=2):
 
     b, smp = seg.bufs, seg.n * seg.T
     rms = torch.zeros(4, dtype=torch.float64, device="cuda")
-    # the learn side's three launches (Segment.learn_side), each priced alone
+    # the learn side's calls (Segment.learn_side), each priced alone
     ms = timed(lambda: K.reward_norm_statistics(b["reward"], rms, seg.work))
-    put("reward_norm", "rlp::reward_stats_fused_kernel<true>", smp * 4, ms,
-        {"samples": smp, "note": "the running statistics in one launch (chunk statistics, per-step "
-                                 "merges by each step's last block, the scan by the last step's "
-                                 "block); the rewards are normalised inside gae_kernel's load"})
+    put("reward_norm", "rlp::reward_stats_kernel<true> + rlp::reward_merge_kernel", smp * 4, ms,
+        {"samples": smp, "note": "the running statistics (chunk statistics, then one block: the "
+                                 "per-step merges and the scan); the rewards are normalised inside "
+                                 "gae_kernel's load"})
     ms = timed(lambda: K.gae_normalized(b["reward"], seg.work, b["value"], b["value_next"],
                                         b["done"], b["success"], 0.999, 0.95, adv=seg.adv,
-                                        v_target=seg.vt, stats=seg.stats, merge_stats=True))
-    put("gae", "rlp::gae_kernel<true, true>", smp * (3 * 4 + 2 + 2 * 4), ms,
-        {"samples": smp, "note": "raw reward normalised on load + the advantage statistics' merge "
-                                 "by the grid's last block"})
-    ms = timed(lambda: K.adv_apply(seg.adv, seg.stats, seg.n))
-    put("adv_normalize", "rlp::adv_norm_kernel<true>", smp * 8, ms, {"samples": smp})
-    # the round-5 three-stage form (stats / merge / apply launches, the normalised rewards stored
-    # and re-read by GAE), for comparison
-    ms = timed(lambda: K.reward_norm(b["reward"], rms, seg.work, out=seg.rnorm))
-    put("reward_norm_stored", "rlp::reward_stats_fused_kernel<true> + rlp::reward_apply_kernel<true>",
-        smp * 12, ms,
+                                        v_target=seg.vt, stats=seg.stats))
+    put("gae", "rlp::gae_kernel<true>", smp * (3 * 4 + 2 + 2 * 4), ms,
+        {"samples": smp, "note": "the raw reward normalised on load"})
+    ms = timed(lambda: K.adv_normalize(seg.adv, seg.stats))
+    put("adv_normalize", "rlp::adv_stats_merge_kernel + rlp::adv_norm_kernel<true>", smp * 8, ms,
         {"samples": smp})
+    # the form that stores the normalised rewards (rlp_reward_norm: statistics + apply), which
+    # GAE then re-reads — the learn side before round 6
+    ms = timed(lambda: K.reward_norm(b["reward"], rms, seg.work, out=seg.rnorm))
+    put("reward_norm_stored",
+        "rlp::reward_stats_kernel<true> + rlp::reward_merge_kernel + rlp::reward_apply_kernel<true>",
+        smp * 12, ms, {"samples": smp})
     for env, kind, pf, dw in (("soi", A.RLP_ENV_SOI, lambda: A.soi_params("env"), 5),
                               ("ugv", A.RLP_ENV_UGV_FORWARD,
                                lambda: A.ugv_params(A.RLP_ENV_UGV_FORWARD, "ppo2"), 6),

@@ -42,8 +42,7 @@ typedef void *rlp_stream_t; /* hipStream_t */
 #define RLP_ABI_VERSION 3  /* 2: caller-owned rollout / mlp_forward workspaces (round 5);
                               3: per-call mlp_precision of rlp_mfma_forward / rlp_value_fixup,
                                  rlp_selftest_gemm_guard, rlp_reward_norm_statistics /
-                                 rlp_reward_norm_apply / rlp_gae_normalized / rlp_adv_apply
-                                 (round 6) */
+                                 rlp_reward_norm_apply / rlp_gae_normalized (round 6) */
 
 /* ------------------------------------------------------------------------------------------ */
 /* Environment kinds. Each kind is one specific reference env copy (copies diverge). */
@@ -384,17 +383,16 @@ int rlp_value_fixup(const rlp_mlp_desc *critic_desc, const float *critic_packed,
  * n == 1, reproducing the reference exactly including the first-call std = x quirk; Chan's
  * parallel merge otherwise), then every reward of step t is normalised with the statistics
  * after that merge. rms: device f64[4] = {count, mean, S, std}, in/out across segments.
- * work: device f64[rlp_reward_norm_workspace(T, n)] scratch, ZERO-FILLED before its first use
- * (its tail holds launch counters that every call leaves at zero again). reward_out may alias
- * reward_in. Two launches: rlp_reward_norm_statistics, then the elementwise normalisation. */
+ * work: device f64[rlp_reward_norm_workspace(T, n)] scratch. reward_out may alias reward_in.
+ * rlp_reward_norm_statistics, then the elementwise normalisation. */
 int64_t rlp_reward_norm_workspace(int T, int n);
 int rlp_reward_norm(const float *reward_in, int T, int n, double *rms, double *work,
                     float *reward_out, rlp_stream_t stream);
 
-/* The statistics half of rlp_reward_norm (one rank) in ONE launch: chunk statistics, per-step
- * merges and the running recurrence (rms updated; step t's (mean_t, std_t) kept in `work` for
- * rlp_gae_normalized), bit-identical to rlp_reward_norm's. The rewards themselves are not
- * written: rlp_gae_normalized normalises them as it loads them. */
+/* The statistics half of rlp_reward_norm (one rank): chunk statistics, per-step merges and the
+ * running recurrence (rms updated; step t's (mean_t, std_t) kept in `work` for
+ * rlp_gae_normalized). The rewards themselves are not written: rlp_gae_normalized normalises
+ * them as it loads them. */
 int rlp_reward_norm_statistics(const float *reward_in, int T, int n, double *rms, double *work,
                                rlp_stream_t stream);
 /* The normalised rewards themselves, from the statistics a preceding rlp_reward_norm_statistics
@@ -430,19 +428,14 @@ int rlp_gae(const float *reward, const float *value, const float *value_next, co
             const uint8_t *success, double gamma, double lambda, int T, int n, float *adv,
             float *v_target, double *adv_stats, rlp_stream_t stream);
 
-/* rlp_reward_norm + rlp_gae (+ the advantage statistics' merge) without the normalised-reward
- * array: reward_raw is the rollout's reward and reward_work the `work` of a preceding
- * rlp_reward_norm_statistics over it; each reward is normalised as it is loaded, with the same
- * expression as rlp_reward_norm, so adv / v_target / the partials are bit-identical to
- * rlp_reward_norm followed by rlp_gae. merge_adv_stats = 1 (one rank): the grid's last block also
- * combines the partials in rlp_adv_normalize's order and writes (mean, std) to
- * adv_stats[3 * parts], [3 * parts + 1] (adv_stats then needs 3 * parts + 3 doubles, zero-filled
- * before first use: the last one holds a counter that every call leaves at zero); rlp_adv_apply
- * then normalises. */
+/* rlp_reward_norm + rlp_gae without the normalised-reward array: reward_raw is the rollout's
+ * reward and reward_work the `work` of a preceding rlp_reward_norm_statistics over it; each
+ * reward is normalised as it is loaded, with the same expression as rlp_reward_norm, so adv /
+ * v_target / the partials are bit-identical to rlp_reward_norm followed by rlp_gae. */
 int rlp_gae_normalized(const float *reward_raw, const double *reward_work, const float *value,
                        const float *value_next, const uint8_t *done, const uint8_t *success,
                        double gamma, double lambda, int T, int n, float *adv, float *v_target,
-                       double *adv_stats, int merge_adv_stats, rlp_stream_t stream);
+                       double *adv_stats, rlp_stream_t stream);
 
 /* adv = (adv - mean) / (std_unbiased + 1e-5) (Trick 1, :99-100; torch's two-pass std over the
  * whole buffer), mean / std from the first `parts` partials of adv_stats combined in a fixed
@@ -450,11 +443,6 @@ int rlp_gae_normalized(const float *reward_raw, const double *reward_work, const
  * ranks, all-gather every rank's partials (rank-major) and pass parts = world * parts: the
  * normalisation is then global and identical on every rank. */
 int rlp_adv_normalize(float *adv, int64_t count, double *adv_stats, int parts, rlp_stream_t stream);
-
-/* The elementwise half of rlp_adv_normalize: adv = (adv - mean) / (std + 1e-5) with
- * mean_std = {mean, std} already merged (rlp_gae_normalized with merge_adv_stats, or a
- * preceding rlp_adv_normalize's adv_stats + 3 * parts). */
-int rlp_adv_apply(float *adv, int64_t count, const double *mean_std, rlp_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* PPO2 update (Proximal_Policy_Optimization2.learn, algorithm/policy_base/

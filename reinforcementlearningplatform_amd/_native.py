@@ -57,8 +57,7 @@ def _declare(lib):
         "rlp_adv_normalize": (i32, [vp, i64, vp, i32, vp]),
         "rlp_reward_norm_statistics": (i32, [vp, i32, i32, vp, vp, vp]),
         "rlp_reward_norm_apply": (i32, [vp, i32, i32, vp, vp, vp]),
-        "rlp_gae_normalized": (i32, [vp, vp, vp, vp, vp, vp, dbl, dbl, i32, i32, vp, vp, vp, i32, vp]),
-        "rlp_adv_apply": (i32, [vp, i64, vp, vp]),
+        "rlp_gae_normalized": (i32, [vp, vp, vp, vp, vp, vp, dbl, dbl, i32, i32, vp, vp, vp, vp]),
         "rlp_adv_stats_parts": (i32, [i32]),
         "rlp_reward_norm_parts": (i64, [i32, i32]),
         "rlp_reward_norm_stats": (i32, [vp, i32, i32, vp, vp]),

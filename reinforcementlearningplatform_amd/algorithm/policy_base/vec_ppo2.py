@@ -295,15 +295,14 @@ class VecPPO2:
                 local = self.stats[:3 * parts].clone()
                 self.stats[:3 * parts * self.world] = self._gather(local)
                 K.adv_normalize(self.adv, self.stats, parts * self.world)
-        else:  # one rank's statistics: 3 launches, the rewards normalised as GAE loads them
+        else:  # one rank's statistics: the rewards normalised as GAE loads them (not stored)
             K.reward_norm_statistics(b["reward"], self.rms, self.work)
             self._rnorm_stale = True
             K.gae_normalized(b["reward"], self.work, b["value"], b["value_next"], b["done"],
                              b["success"], self.msg['gamma'], self.msg['lmd'], adv=self.adv,
-                             v_target=self.v_target, stats=self.stats,
-                             merge_stats=bool(self.msg['use_adv_norm']))
+                             v_target=self.v_target, stats=self.stats)
             if self.msg['use_adv_norm']:
-                K.adv_apply(self.adv, self.stats, self.n)
+                K.adv_normalize(self.adv, self.stats, self.adv_parts)
 
     @property
     def rnorm(self):

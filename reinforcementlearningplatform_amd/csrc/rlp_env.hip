@@ -48,6 +48,9 @@ int take_pending() {
     return c;
 }
 
+// (the UAV step at 234 registers runs 2 waves per SIMD; compiled for 3 or 4 (168 / 128
+// registers, 204 / 416 B of spills) it took 764 / 1088 us against 528 us per 4M-env launch,
+// profiles/r6/r6l_learn_side_ab.txt)
 template <int KIND>
 __global__ void __launch_bounds__(256) env_step_kernel(typename Env<KIND>::P p, double *state,
                                                        int n, const float *__restrict__ action,

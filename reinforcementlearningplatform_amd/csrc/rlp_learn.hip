@@ -117,14 +117,8 @@ __global__ void __launch_bounds__(256) reward_stats_kernel(const float *__restri
     }
 }
 
-// loads of statistics other blocks of the same launch wrote (L2, past this CU's L1)
-__device__ __forceinline__ double ld_agent(const double *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // time step t's chunk statistics of `world` ranks (rank-major [world][T][P][2]) combined in global
 // env order -> (mean, M2) of its world * n rewards (one thread; loads kRsPre ahead of the combine)
-template <bool AGENT>
 __device__ __forceinline__ void rs_step_merge(const double *parts, int T, int n, int world, int t,
                                               double &mean, double &m2) {
     constexpr int kRsPre = 8;
@@ -138,8 +132,8 @@ __device__ __forceinline__ void rs_step_merge(const double *parts, int T, int n,
         for (int u = 0; u < kRsPre; ++u) {
             const int q = q0 + u, rk = q / P, p = q - rk * P;
             const double *pp = parts + (((size_t)rk * T + t) * P + p) * 2;
-            pm[u] = q < Q ? (AGENT ? ld_agent(pp) : pp[0]) : 0.0;
-            pq[u] = q < Q ? (AGENT ? ld_agent(pp + 1) : pp[1]) : 0.0;
+            pm[u] = q < Q ? pp[0] : 0.0;
+            pq[u] = q < Q ? pp[1] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < kRsPre; ++u) {
@@ -162,7 +156,6 @@ __device__ __forceinline__ void rs_step_merge(const double *parts, int T, int n,
 // the running statistics over t (whole block, 256 threads): a block-wide inclusive scan of Chan
 // merges of the per-step aggregates agg [T][2] (world * n rewards each) onto rms; writes step t's
 // (mean_t, std_t) to out [T][2] and the final statistics to rms
-template <bool AGENT>
 __device__ __forceinline__ void rs_running_scan(const double *agg, int T, double ntot, double *rms,
                                                 double *out) {
     __shared__ Moments wred[4];
@@ -172,7 +165,7 @@ __device__ __forceinline__ void rs_running_scan(const double *agg, int T, double
     __syncthreads();
     Moments cr{carry[0], carry[1], carry[2]};
     const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-    auto ag = [&](int i) { return AGENT ? ld_agent(agg + i) : agg[i]; };
+    auto ag = [&](int i) { return agg[i]; };
     for (int t0 = 0; t0 < T; t0 += kRsTile) {
         const int ta = t0 + 2 * (int)threadIdx.x, tb = ta + 1;
         const Moments e0 = ta < T ? Moments{ntot, ag(2 * ta), ag(2 * ta + 1)} : Moments{0, 0, 0};
@@ -264,79 +257,12 @@ __global__ void __launch_bounds__(256) reward_merge_kernel(const float *__restri
     }
     for (int t = threadIdx.x; t < T; t += 256) {
         double mean, m2;
-        rs_step_merge<false>(parts, T, n, world, t, mean, m2);
+        rs_step_merge(parts, T, n, world, t, mean, m2);
         agg[2 * t] = mean;
         agg[2 * t + 1] = m2;
     }
     __syncthreads();
-    rs_running_scan<false>(agg, T, ntot, rms, out);
-}
-
-// rlp_reward_norm_statistics (one rank, n > 1) in ONE launch: the chunk statistics of
-// reward_stats_kernel; the last of step t's P chunk blocks to finish (a wrapping per-step counter)
-// combines that step's chunks (rs_step_merge); the last step to be combined (a wrapping global
-// counter) runs the running scan with its whole block. Same arithmetic in the same order as the
-// stats + merge launches, so the statistics are bit-identical. The counters (T + 1 u32 after the
-// [T][2] out array) return to zero at the end of every launch: work is zero-filled once.
-template <bool VEC>
-__global__ void __launch_bounds__(256) reward_stats_fused_kernel(const float *__restrict__ r, int T,
-                                                                 int n, double *rms, double *work) {
-    __shared__ double red[4];
-    __shared__ int last;
-    const int p = blockIdx.x, P = gridDim.x;
-    const int lo = p * kRsChunk, cnt = min(kRsChunk, n - lo);
-    double *part = work, *agg = work + (size_t)T * P * 2, *out = agg + (size_t)T * 2;
-    unsigned *ctr = (unsigned *)(out + (size_t)T * 2);
-    for (int t = blockIdx.y; t < T; t += gridDim.y) {
-        const float *x = r + (size_t)t * n + lo;
-        float v[kRsPer];
-        if (VEC) {
-#pragma unroll
-            for (int j = 0; j < kRsPer / 4; ++j) {
-                const int i = (j * 256 + (int)threadIdx.x) * 4;
-                const float4 q = i < cnt ? *(const float4 *)(x + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-                v[4 * j] = q.x; v[4 * j + 1] = q.y; v[4 * j + 2] = q.z; v[4 * j + 3] = q.w;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < kRsPer; ++j) {
-                const int i = j * 256 + threadIdx.x;
-                v[j] = i < cnt ? x[i] : 0.f;
-            }
-        }
-        double s = 0;
-#pragma unroll
-        for (int j = 0; j < kRsPer; ++j) s += (double)v[j];
-        const double mean = block_sum<256>(s, red) / cnt;
-        double q = 0;
-#pragma unroll
-        for (int j = 0; j < kRsPer; ++j) {
-            const int i = VEC ? (j / 4 * 256 + (int)threadIdx.x) * 4 + (j & 3) : j * 256 + threadIdx.x;
-            const double d = (double)v[j] - mean;
-            if (i < cnt) q += d * d;
-        }
-        const double m2 = block_sum<256>(q, red);
-        if (threadIdx.x == 0) {
-            part[((size_t)t * P + p) * 2 + 0] = mean;
-            part[((size_t)t * P + p) * 2 + 1] = m2;
-            __threadfence();  // the chunk's statistics before its count
-            int l = 0;
-            if (atomicInc(ctr + t, (unsigned)(P - 1)) == (unsigned)(P - 1)) {
-                __threadfence();
-                double sm, sq;
-                rs_step_merge<true>(part, T, n, 1, t, sm, sq);
-                agg[2 * t] = sm;
-                agg[2 * t + 1] = sq;
-                __threadfence();
-                l = atomicInc(ctr + T, (unsigned)(T - 1)) == (unsigned)(T - 1);
-                if (l) __threadfence();
-            }
-            last = l;
-        }
-        __syncthreads();
-        if (last) rs_running_scan<true>(agg, T, (double)n, rms, out);  // block-uniform
-        __syncthreads();
-    }
+    rs_running_scan(agg, T, ntot, rms, out);
 }
 
 // [chunks x T] grid: the block row is the time step, so the per-step (mean, std) are two scalar
@@ -368,16 +294,11 @@ __global__ void __launch_bounds__(256) reward_apply_kernel(const float *__restri
 
 // the partials combined in a fixed order by one 256-thread block: thread j folds parts
 // [j*per, (j+1)*per) left to right, then the block combine; (mean, unbiased std) after the partials
-template <bool AGENT>
-__device__ __forceinline__ void adv_merge_block(double *stats, int parts) {
+__global__ void __launch_bounds__(256) adv_stats_merge_kernel(double *stats, int parts) {
     __shared__ Moments red[4];
     const int per = (parts + 255) / 256, lo = threadIdx.x * per, hi = min(parts, lo + per);
     Moments a{0, 0, 0};
-    for (int j = lo; j < hi; ++j) {
-        const double *q = stats + 3 * j;
-        a = chan(a, AGENT ? Moments{ld_agent(q), ld_agent(q + 1), ld_agent(q + 2)}
-                          : Moments{q[0], q[1], q[2]});
-    }
+    for (int j = lo; j < hi; ++j) a = chan(a, Moments{stats[3 * j], stats[3 * j + 1], stats[3 * j + 2]});
     a = block_moments<256>(a, red);
     if (threadIdx.x == 0) {
         stats[3 * parts] = a.m;
@@ -391,10 +312,12 @@ __device__ __forceinline__ void adv_merge_block(double *stats, int parts) {
 // NORM: r is the raw reward and rs [T][2] step t's (mean_t, std_t) of rlp_reward_norm_statistics:
 // the reward is normalised as it is loaded, (float)((r - mean_t) / (std_t + 1e-8)) — the apply
 // pass's expression, so the normalised-reward array is neither written nor re-read.
-// MERGE: the grid's last block to finish (a wrapping counter after the (mean, std) slots) combines
-// the per-block partials (adv_merge_block), so rlp_adv_apply needs no merge launch.
+// (Round 6 also tried merging the advantage partials in the grid's last block, and the reward
+// statistics' per-step merges and scan in the last blocks of the statistics launch, handing over
+// through atomic counters: the agent-scope release fence each block then needs writes back its
+// XCD's L2, and GAE went 31 -> 54 us, the statistics 17 -> 76 us (profiles/r6/r6l_learn_side_ab.txt).)
 constexpr int kGaeU = 16;
-template <bool NORM, bool MERGE>
+template <bool NORM>
 __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
                                                   const double *__restrict__ rs,
                                                   const float *__restrict__ v,
@@ -404,7 +327,6 @@ __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
                                                   float c, int T, int n, float *__restrict__ adv,
                                                   float *__restrict__ vt, double *stats) {
     __shared__ Moments red[4];
-    __shared__ int last;
     const int i = blockIdx.x * 256 + threadIdx.x;
     double s1 = 0, s2 = 0, k0 = 0;  // sums of (adv - k0), k0 = the lane's first advantage
     if (i < n) {
@@ -457,23 +379,8 @@ __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
             stats[3 * blockIdx.x + 0] = mo.c;
             stats[3 * blockIdx.x + 1] = mo.m;
             stats[3 * blockIdx.x + 2] = mo.q;
-            if (MERGE) {
-                __threadfence();
-                unsigned *ctr = (unsigned *)(stats + 3 * (size_t)gridDim.x + 2);
-                const int l = atomicInc(ctr, gridDim.x - 1) == gridDim.x - 1;
-                if (l) __threadfence();
-                last = l;
-            }
-        }
-        if (MERGE) {
-            __syncthreads();
-            if (last) adv_merge_block<true>(stats, gridDim.x);  // block-uniform
         }
     }
-}
-
-__global__ void __launch_bounds__(256) adv_stats_merge_kernel(double *stats, int parts) {
-    adv_merge_block<false>(stats, parts);
 }
 
 // 4 advantages per lane as one 16-byte access (the tail of count % 4 by the first lanes) when
@@ -510,8 +417,7 @@ extern "C" {
 
 int64_t rlp_reward_norm_workspace(int T, int n) {
     if (T < 0 || n < 0) return RLP_EINVAL;
-    // part [T][P][2] | agg [T][2] | out [T][2] | T + 1 u32 counters (reward_stats_fused_kernel)
-    return (int64_t)T * (2 * (int64_t)rs_chunks(n > 0 ? n : 1) + 4) + ((int64_t)T + 2) / 2;
+    return (int64_t)T * (2 * (int64_t)rs_chunks(n > 0 ? n : 1) + 4);  // part | agg | out
 }
 
 int64_t rlp_reward_norm_parts(int T, int n) {
@@ -537,16 +443,11 @@ int rlp_reward_norm_statistics(const float *reward_in, int T, int n, double *rms
     RLP_REQUIRE(reward_in && rms && work, "rlp_reward_norm_statistics: null argument");
     RLP_REQUIRE(T >= 0 && n >= 0, "rlp_reward_norm_statistics: T=%d n=%d", T, n);
     if (T == 0 || n == 0) return RLP_OK;
-    hipStream_t s = as_stream(stream);
-    if (n == 1) {  // the serial Welford recurrence
-        reward_merge_kernel<<<1, 256, 0, s>>>(reward_in, T, n, 1, work, rms, work);
-    } else {
-        const dim3 grid(rs_chunks(n), T < 65535 ? T : 65535);
-        if (n % 4 == 0 && aligned16(reward_in))
-            reward_stats_fused_kernel<true><<<grid, 256, 0, s>>>(reward_in, T, n, rms, work);
-        else
-            reward_stats_fused_kernel<false><<<grid, 256, 0, s>>>(reward_in, T, n, rms, work);
+    if (n > 1) {
+        const int rc = rlp_reward_norm_stats(reward_in, T, n, work, stream);
+        if (rc != RLP_OK) return rc;
     }
+    reward_merge_kernel<<<1, 256, 0, as_stream(stream)>>>(reward_in, T, n, 1, work, rms, work);
     RLP_CHECK_LAUNCH("rlp_reward_norm_statistics");
     return RLP_OK;
 }
@@ -612,7 +513,7 @@ int rlp_gae(const float *reward, const float *value, const float *value_next, co
     if (T == 0 || n == 0) return RLP_OK;
     const float g32 = (float)gamma;       // torch: gamma * (1 - success) in fp32
     const float c = (float)(gamma * lambda);  // numpy: (gamma * lmd) * gae, NEP-50 fp32
-    gae_kernel<false, false><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
+    gae_kernel<false><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
         reward, nullptr, value, value_next, done, success, g32, c, T, n, adv, v_target, adv_stats);
     RLP_CHECK_LAUNCH("rlp_gae");
     return RLP_OK;
@@ -621,37 +522,20 @@ int rlp_gae(const float *reward, const float *value, const float *value_next, co
 int rlp_gae_normalized(const float *reward_raw, const double *reward_work, const float *value,
                        const float *value_next, const uint8_t *done, const uint8_t *success,
                        double gamma, double lambda, int T, int n, float *adv, float *v_target,
-                       double *adv_stats, int merge_adv_stats, rlp_stream_t stream) {
+                       double *adv_stats, rlp_stream_t stream) {
     RLP_REQUIRE(reward_raw && reward_work && value && value_next && done && success && adv &&
                 v_target, "rlp_gae_normalized: null argument");
     RLP_REQUIRE(T >= 0 && n >= 0, "rlp_gae_normalized: T=%d n=%d", T, n);
-    RLP_REQUIRE(!merge_adv_stats || adv_stats, "rlp_gae_normalized: merge_adv_stats without adv_stats");
     if (T == 0 || n == 0) return RLP_OK;
     const float g32 = (float)gamma, c = (float)(gamma * lambda);
-    const double *rs = reward_step_stats(reward_work, T, n);
-    hipStream_t s = as_stream(stream);
-    const int nb = (n + 255) / 256;
-    if (merge_adv_stats)
-        gae_kernel<true, true><<<nb, 256, 0, s>>>(reward_raw, rs, value, value_next, done, success,
-                                                   g32, c, T, n, adv, v_target, adv_stats);
-    else
-        gae_kernel<true, false><<<nb, 256, 0, s>>>(reward_raw, rs, value, value_next, done, success,
-                                                    g32, c, T, n, adv, v_target, adv_stats);
+    gae_kernel<true><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
+        reward_raw, reward_step_stats(reward_work, T, n), value, value_next, done, success, g32, c,
+        T, n, adv, v_target, adv_stats);
     RLP_CHECK_LAUNCH("rlp_gae_normalized");
     return RLP_OK;
 }
 
 int rlp_adv_stats_parts(int n) { return n < 0 ? RLP_EINVAL : (n + 255) / 256; }
-
-static void adv_apply(float *adv, int64_t count, const double *ms, hipStream_t s) {
-    if (aligned16(adv)) {
-        const int64_t b = (count / 4 + 255) / 256;
-        adv_norm_kernel<true><<<(int)(b < 1 ? 1 : b < 8192 ? b : 8192), 256, 0, s>>>(adv, count, ms);
-    } else {
-        const int64_t b = (count + 255) / 256;
-        adv_norm_kernel<false><<<(int)(b < 8192 ? b : 8192), 256, 0, s>>>(adv, count, ms);
-    }
-}
 
 int rlp_adv_normalize(float *adv, int64_t count, double *adv_stats, int parts,
                       rlp_stream_t stream) {
@@ -660,16 +544,15 @@ int rlp_adv_normalize(float *adv, int64_t count, double *adv_stats, int parts,
     if (count <= 1) return RLP_OK;
     hipStream_t s = as_stream(stream);
     adv_stats_merge_kernel<<<1, 256, 0, s>>>(adv_stats, parts);
-    adv_apply(adv, count, adv_stats + 3 * (size_t)parts, s);
+    const double *ms = adv_stats + 3 * (size_t)parts;
+    if (aligned16(adv)) {
+        const int64_t b = (count / 4 + 255) / 256;
+        adv_norm_kernel<true><<<(int)(b < 1 ? 1 : b < 8192 ? b : 8192), 256, 0, s>>>(adv, count, ms);
+    } else {
+        const int64_t b = (count + 255) / 256;
+        adv_norm_kernel<false><<<(int)(b < 8192 ? b : 8192), 256, 0, s>>>(adv, count, ms);
+    }
     RLP_CHECK_LAUNCH("rlp_adv_normalize");
-    return RLP_OK;
-}
-
-int rlp_adv_apply(float *adv, int64_t count, const double *mean_std, rlp_stream_t stream) {
-    RLP_REQUIRE(adv && mean_std, "rlp_adv_apply: null argument");
-    if (count <= 1) return RLP_OK;
-    adv_apply(adv, count, mean_std, as_stream(stream));
-    RLP_CHECK_LAUNCH("rlp_adv_apply");
     return RLP_OK;
 }
 

@@ -210,10 +210,9 @@ def make_rollout_cfg(T, n, seed, step0, env_id0, std, a_min, a_max, success_rule
 
 
 def reward_norm_workspace(T, n, device=None):
-    """zero-filled (include/rlp.h: the tail holds launch counters the calls leave at zero)"""
     cnt = lib().rlp_reward_norm_workspace(int(T), int(n))
     check(cnt if cnt < 0 else 0, "rlp_reward_norm_workspace")
-    return torch.zeros(int(cnt), dtype=torch.float64, device=_dev(device))
+    return torch.empty(int(cnt), dtype=torch.float64, device=_dev(device))
 
 
 def reward_norm(reward, rms, work=None, out=None):
@@ -227,8 +226,8 @@ def reward_norm(reward, rms, work=None, out=None):
 
 
 def reward_norm_statistics(reward, rms, work):
-    """rlp_reward_norm_statistics: the running statistics over reward [T][n] in one launch, step
-    t's (mean_t, std_t) kept in `work` for gae_normalized (no normalised-reward array)."""
+    """rlp_reward_norm_statistics: the running statistics over reward [T][n], step t's
+    (mean_t, std_t) kept in `work` for gae_normalized (no normalised-reward array)."""
     T, n = reward.shape
     check(lib().rlp_reward_norm_statistics(ptr(reward), T, n, ptr(rms), ptr(work), stream_ptr()),
           "rlp_reward_norm_statistics")
@@ -267,9 +266,8 @@ def adv_stats_parts(n):
 
 
 def adv_stats_buffer(n, world=1, device=None):
-    """f64 buffer for rlp_gae's per-block (count, mean, M2) partials of `world` ranks + (mean, std)
-    + the merge counter of gae_normalized(merge_adv_stats=True) (zero-filled)."""
-    return torch.zeros(3 * adv_stats_parts(n) * world + 3, dtype=torch.float64, device=_dev(device))
+    """f64 buffer for rlp_gae's per-block (count, mean, M2) partials of `world` ranks + (mean, std)."""
+    return torch.zeros(3 * adv_stats_parts(n) * world + 2, dtype=torch.float64, device=_dev(device))
 
 
 def gae(reward, value, value_next, done, success, gamma, lmd, adv=None, v_target=None, stats=None):
@@ -284,35 +282,23 @@ def gae(reward, value, value_next, done, success, gamma, lmd, adv=None, v_target
 
 
 def gae_normalized(reward_raw, reward_work, value, value_next, done, success, gamma, lmd, adv=None,
-                   v_target=None, stats=None, merge_stats=False):
+                   v_target=None, stats=None):
     """rlp_gae_normalized: GAE over the raw rewards normalised on load with the statistics a
-    preceding reward_norm_statistics left in reward_work; merge_stats: the (mean, std) of the
-    advantages also land in stats (one rank) for adv_apply."""
+    preceding reward_norm_statistics left in reward_work."""
     T, n = reward_raw.shape
     adv = adv if adv is not None else torch.empty_like(reward_raw)
     v_target = v_target if v_target is not None else torch.empty_like(reward_raw)
-    if merge_stats and (stats is None or stats.numel() < 3 * adv_stats_parts(n) + 3):
-        raise ValueError("gae_normalized: merge_stats needs an adv_stats_buffer(n)")
     check(lib().rlp_gae_normalized(ptr(reward_raw), ptr(reward_work), ptr(value), ptr(value_next),
                                    ptr(done), ptr(success), float(gamma), float(lmd), T, n,
-                                   ptr(adv), ptr(v_target), ptr(stats), int(bool(merge_stats)),
-                                   stream_ptr()), "rlp_gae_normalized")
+                                   ptr(adv), ptr(v_target), ptr(stats), stream_ptr()),
+          "rlp_gae_normalized")
     return adv, v_target
-
-
-def adv_apply(adv, stats, n=None):
-    """rlp_adv_apply with the (mean, std) gae_normalized(merge_stats=True) merged into stats
-    (one rank's buffer: at 3 * adv_stats_parts(n))."""
-    parts = adv_stats_parts(adv.shape[-1] if n is None else n)
-    check(lib().rlp_adv_apply(ptr(adv), adv.numel(), ptr(stats[3 * parts:]), stream_ptr()),
-          "rlp_adv_apply")
-    return adv
 
 
 def adv_normalize(adv, stats, parts=None):
     """Normalise adv with the first `parts` partials of stats (default: one rank's, from the
     buffer's size); (mean, std) land at stats[3 * parts:3 * parts + 2]."""
-    parts = (stats.numel() - 3) // 3 if parts is None else int(parts)
+    parts = (stats.numel() - 2) // 3 if parts is None else int(parts)
     check(lib().rlp_adv_normalize(ptr(adv), adv.numel(), ptr(stats), parts, stream_ptr()),
           "rlp_adv_normalize")
     return adv

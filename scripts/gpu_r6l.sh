@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 6 (l): the whole GPU suite + smoke on the in-tree build (lidar rollout two launches per
 # step), then the rollout / UAV / HBM-legs bench, in-tree vs rlp_rollout.hip built without
-# MachineLICM (fewer registers in every rollout kernel), alternating, two repetitions.
+# MachineLICM (fewer registers in every rollout kernel) and the UAV env step compiled for 3 / 4
+# waves per SIMD (env3 / env4), alternating, two repetitions.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); TAG=${TAG:-r6l}; OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
@@ -20,9 +21,13 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/
 rc=$?; tail -1 "$OUT/smoke.log" | tee -a "$OUT/progress.log"; [ $rc -ne 0 ] && stop smoke $rc
 BA="--steps 10 --warmup 3 --no-cpu-baseline --e2e 0 --fp32-leg 0 --ddpg 0 --oa 0 --sac 0 --demo-e2e 0"
 for rep in 1 2; do
-  for lib in - nolicm; do
+  for lib in - nolicm env3 env4; do
     log "bench A/B rep $rep lib=$lib"
-    if [ "$lib" = - ]; then unset RLP_LIBRARY; else export RLP_LIBRARY=$NL; fi
+    case $lib in
+      -) unset RLP_LIBRARY ;;
+      nolicm) export RLP_LIBRARY=$NL ;;
+      *) export RLP_LIBRARY=$ROOT/reinforcementlearningplatform_amd/csrc/build/exp$lib/librlp.so ;;
+    esac
     timeout -k 10 300 python -u bench.py $BA > "$OUT/bench_$lib.log" 2>&1
     rc=$?; unset RLP_LIBRARY
     [ $rc -ne 0 ] && stop "bench $lib" $rc

@@ -25,12 +25,13 @@ WORKLOADS = {  # workload -> (kernel name prefix, envs per GPU, T, algorithmic b
 
 
 # bench.py hbm_legs kernels -> the kernel-name prefixes whose FETCH / WRITE add up to one launch
-# (round 6: the learn side's fused launches; bench.py checks these prefixes against its labels)
+# (round 6: the learn side's launches; bench.py checks these prefixes against its labels)
 HBM_KERNELS = {
-    "gae": ["rlp::gae_kernel<true, true>"],
-    "reward_norm": ["rlp::reward_stats_fused_kernel"],
-    "adv_normalize": ["rlp::adv_norm_kernel"],
-    "reward_norm_stored": ["rlp::reward_stats_fused_kernel", "rlp::reward_apply_kernel"],
+    "gae": ["rlp::gae_kernel<true>"],
+    "reward_norm": ["rlp::reward_stats_kernel", "rlp::reward_merge_kernel"],
+    "adv_normalize": ["rlp::adv_stats_merge_kernel", "rlp::adv_norm_kernel"],
+    "reward_norm_stored": ["rlp::reward_stats_kernel", "rlp::reward_merge_kernel",
+                           "rlp::reward_apply_kernel"],
     "env_step_soi": ["rlp::env_step_kernel<3>"],
     "env_step_ugv": ["rlp::env_step_kernel<4>"],
     "env_step_uav": ["rlp::env_step_kernel<6>"],
