@@ -208,7 +208,8 @@ def offpolicy_reuse(make_loop, n, ref_rows, flop_per_row,
     out = []
     for batch, iters in configs:
         loop, agent = make_loop(batch, iters)
-        for _ in range(warmup):
+        # enough warm-up steps to hold `batch` rows: learn() skips while the replay has fewer
+        for _ in range(max(warmup, -(-batch // n))):
             loop.step(learn=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()

@@ -317,7 +317,8 @@ __global__ void __launch_bounds__(256) adv_stats_merge_kernel(double *stats, int
 // through atomic counters: the agent-scope release fence each block then needs writes back its
 // XCD's L2, and GAE went 31 -> 54 us, the statistics 17 -> 76 us (profiles/r6/r6l_learn_side_ab.txt).)
 constexpr int kGaeU = 16;
-template <bool NORM>
+constexpr int kGaeLdsSteps = 512;  // NORM = 1: the per-step statistics staged in LDS (T <= this)
+template <int NORM>  // 0: r normalised already; 1: raw r, statistics from LDS; 2: from global
 __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
                                                   const double *__restrict__ rs,
                                                   const float *__restrict__ v,
@@ -327,6 +328,12 @@ __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
                                                   float c, int T, int n, float *__restrict__ adv,
                                                   float *__restrict__ vt, double *stats) {
     __shared__ Moments red[4];
+    __shared__ __attribute__((aligned(16))) double srs[NORM == 1 ? 2 * kGaeLdsSteps : 2];
+    if (NORM == 1) {  // (uniform per step: one LDS broadcast read instead of registers per step)
+        for (int j = threadIdx.x; j < 2 * T; j += 256) srs[j] = rs[j];
+        __syncthreads();
+    }
+    const double *st = NORM == 1 ? srs : rs;
     const int i = blockIdx.x * 256 + threadIdx.x;
     double s1 = 0, s2 = 0, k0 = 0;  // sums of (adv - k0), k0 = the lane's first advantage
     if (i < n) {
@@ -335,23 +342,24 @@ __global__ void __launch_bounds__(256) gae_kernel(const float *__restrict__ r,
             const int u = min(kGaeU, t1);
             float rr[kGaeU], vv[kGaeU], vx[kGaeU];
             uint8_t dd[kGaeU], ss[kGaeU];
-            double rm[NORM ? kGaeU : 1], rd[NORM ? kGaeU : 1];
+            double2 ms[NORM ? kGaeU : 1];  // step t's (mean_t, std_t), read with the rows
 #pragma unroll
             for (int j = 0; j < kGaeU; ++j) {
                 if (j < u) {
                     const size_t k = (size_t)(t1 - 1 - j) * n + i;
                     rr[j] = r[k]; vv[j] = v[k]; vx[j] = vn[k]; dd[j] = done[k]; ss[j] = success[k];
-                    if (NORM) {  // step t's statistics (uniform: scalar loads), with the rows
-                        rm[j] = rs[2 * (t1 - 1 - j)];
-                        rd[j] = rs[2 * (t1 - 1 - j) + 1];
-                    }
+                    if (NORM) ms[j] = *reinterpret_cast<const double2 *>(st + 2 * (t1 - 1 - j));
                 }
+            }
+            if (NORM) {  // the chunk's rewards normalised before the recurrence (independent: ILP)
+#pragma unroll
+                for (int j = 0; j < kGaeU; ++j)
+                    if (j < u) rr[j] = (float)(((double)rr[j] - ms[j].x) / (ms[j].y + 1e-8));
             }
 #pragma unroll
             for (int j = 0; j < kGaeU; ++j) {
                 if (j < u) {
                     const size_t k = (size_t)(t1 - 1 - j) * n + i;
-                    if (NORM) rr[j] = (float)(((double)rr[j] - rm[j]) / (rd[j] + 1e-8));
                     const float one_s = 1.0f - (float)ss[j];
                     float delta = rr[j] + (g32 * one_s) * vx[j];
                     delta = delta - vv[j];
@@ -513,7 +521,7 @@ int rlp_gae(const float *reward, const float *value, const float *value_next, co
     if (T == 0 || n == 0) return RLP_OK;
     const float g32 = (float)gamma;       // torch: gamma * (1 - success) in fp32
     const float c = (float)(gamma * lambda);  // numpy: (gamma * lmd) * gae, NEP-50 fp32
-    gae_kernel<false><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
+    gae_kernel<0><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
         reward, nullptr, value, value_next, done, success, g32, c, T, n, adv, v_target, adv_stats);
     RLP_CHECK_LAUNCH("rlp_gae");
     return RLP_OK;
@@ -528,9 +536,13 @@ int rlp_gae_normalized(const float *reward_raw, const double *reward_work, const
     RLP_REQUIRE(T >= 0 && n >= 0, "rlp_gae_normalized: T=%d n=%d", T, n);
     if (T == 0 || n == 0) return RLP_OK;
     const float g32 = (float)gamma, c = (float)(gamma * lambda);
-    gae_kernel<true><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
-        reward_raw, reward_step_stats(reward_work, T, n), value, value_next, done, success, g32, c,
-        T, n, adv, v_target, adv_stats);
+    const double *rs = reward_step_stats(reward_work, T, n);
+    if (T <= kGaeLdsSteps)
+        gae_kernel<1><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
+            reward_raw, rs, value, value_next, done, success, g32, c, T, n, adv, v_target, adv_stats);
+    else
+        gae_kernel<2><<<(n + 255) / 256, 256, 0, as_stream(stream)>>>(
+            reward_raw, rs, value, value_next, done, success, g32, c, T, n, adv, v_target, adv_stats);
     RLP_CHECK_LAUNCH("rlp_gae_normalized");
     return RLP_OK;
 }

@@ -127,7 +127,7 @@ if [ -n "${BENCH_TRACE:-}" ]; then
   kstats "$OUT/bt" > "$OUT/bt_stats.txt"; head -40 "$OUT/bt_stats.txt" | tee -a "$OUT/progress.log"
   cp "$(find "$OUT/bt" -name '*kernel_stats.csv' | head -1)" "$OUT/bt_kernel_stats.csv"
   if [ "${KEEP_TRACE:-0}" = 1 ]; then
-    python3 scripts/trace_check.py "$OUT/bt" > "$OUT/trace_check.json" 2>&1 || true
+    python3 scripts/trace_check.py "$OUT/bt" "$OUT/bench_traced.log" > "$OUT/trace_check.json" 2>&1 || true
   fi
   rm -rf "$OUT/bt"
 fi
