@@ -905,7 +905,7 @@ def hbm_legs(seg, n_env=1 << 22, iters=10, warmup=2):
     ms = timed(lambda: K.gae_normalized(b["reward"], seg.work, b["value"], b["value_next"],
                                         b["done"], b["success"], 0.999, 0.95, adv=seg.adv,
                                         v_target=seg.vt, stats=seg.stats))
-    put("gae", "rlp::gae_kernel<true>", smp * (3 * 4 + 2 + 2 * 4), ms,
+    put("gae", "rlp::gae_kernel<1>", smp * (3 * 4 + 2 + 2 * 4), ms,
         {"samples": smp, "note": "the raw reward normalised on load"})
     ms = timed(lambda: K.adv_normalize(seg.adv, seg.stats))
     put("adv_normalize", "rlp::adv_stats_merge_kernel + rlp::adv_norm_kernel<true>", smp * 8, ms,

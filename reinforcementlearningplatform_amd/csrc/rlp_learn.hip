@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(256) reward_stats_kernel(const float *__restri
 // env order -> (mean, M2) of its world * n rewards (one thread; loads kRsPre ahead of the combine)
 __device__ __forceinline__ void rs_step_merge(const double *parts, int T, int n, int world, int t,
                                               double &mean, double &m2) {
-    constexpr int kRsPre = 8;
+    constexpr int kRsPre = 16;  // one round of loads for n <= 65536 (P <= 16 chunks)
     const int P = rs_chunks(n), Q = world * P;
     double c = 0;
     mean = 0;

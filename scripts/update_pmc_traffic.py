@@ -27,7 +27,7 @@ WORKLOADS = {  # workload -> (kernel name prefix, envs per GPU, T, algorithmic b
 # bench.py hbm_legs kernels -> the kernel-name prefixes whose FETCH / WRITE add up to one launch
 # (round 6: the learn side's launches; bench.py checks these prefixes against its labels)
 HBM_KERNELS = {
-    "gae": ["rlp::gae_kernel<true>"],
+    "gae": ["rlp::gae_kernel<1>"],
     "reward_norm": ["rlp::reward_stats_kernel", "rlp::reward_merge_kernel"],
     "adv_normalize": ["rlp::adv_stats_merge_kernel", "rlp::adv_norm_kernel"],
     "reward_norm_stored": ["rlp::reward_stats_kernel", "rlp::reward_merge_kernel",
@@ -39,12 +39,21 @@ HBM_KERNELS = {
 
 
 def main(run_dir, profile, out_path=None):
+    # per kernel name, the dispatches of its largest grid only (the bench's hbm_legs shapes; the
+    # same kernel also runs at smaller shapes in other legs, which must not be averaged in)
     vals = defaultdict(lambda: defaultdict(list))
+    grid = {}
+    rows = []
     for f in glob.glob(os.path.join(run_dir, "p*", "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 name = row.get("Kernel_Name", "").replace("void ", "")
-                vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                g = int(row.get("Grid_Size", 0) or 0)
+                grid[name] = max(grid.get(name, 0), g)
+                rows.append((name, g, row["Counter_Name"], float(row["Counter_Value"])))
+    for name, g, c, v in rows:
+        if g == grid[name]:
+            vals[name][c].append(v)
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     with open(path) as f:
         d = json.load(f)
