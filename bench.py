@@ -199,7 +199,7 @@ def learn_roofline(flop_per_row, batch, learn_ms):
 
 
 def offpolicy_reuse(make_loop, n, ref_rows, flop_per_row,
-                    configs=((4096, 64), (16384, 16), (65536, 4)), steps=3, warmup=1):
+                    configs=((4096, 64), (16384, 16), (65536, 4), (131072, 2)), steps=3, warmup=1):
     """The off-policy loop at the reference driver's sample reuse or near it: per vector step of n
     transitions, `iters` learn() iterations of `batch` rows (one captured graph replayed iters
     times), so sampled rows per transition = batch * iters / n against the reference's
