@@ -2701,7 +2701,8 @@ __global__ void __launch_bounds__(64 * kFgWaves, 1) fg_grad_kernel(FgArgs g) {
 // row against 164 B of s): the s rows of a tile are one contiguous span, loaded coalesced and
 // transposed into LDS (the tiled GEMM's generic loader spent 46 VALU per MFMA on the 41-float rows:
 // 1.9 ms for the forward of 2^20 rows, profiles/r5/r5f_ext_pmc_shapes.txt).
-constexpr int kL1Rows = 64;        // rows per forward tile (16 per wave)
+constexpr int kL1Waves = 8;        // forward: 8-wave blocks share one W1^T copy in LDS
+constexpr int kL1Rows = 16 * kL1Waves;  // rows per forward tile (16 per wave)
 constexpr int kL1Ld = 256 + 16;    // LDS row of 256 floats: lane groups g, g + 1 16 banks apart
 constexpr int kL1SLd = kL1Rows + 16;
 constexpr int kL1WRows = 32;       // rows per weight-gradient step
@@ -2712,25 +2713,31 @@ constexpr int kL1WBlocks = 512;    // weight-gradient blocks (per-block partials
 // (f + 0.5) / S lies at least 0.5 / S from an integer, far beyond the float rounding for f < 2^20
 __device__ __forceinline__ int l1_row(int f, float invS) { return (int)(((float)f + 0.5f) * invS); }
 
-// h1[row][256] = tanh(W1 s_row + b1) for 64-row tiles (grid-stride), W1^T and the tile's s^T in
-// LDS. Wave w: rows 16 w .. 16 w + 15, all 16 neuron tiles (C = [neuron][row], 64 accumulators);
-// lane (g, e) stores neurons 16 t + 4 g .. + 3 of row e as one float4.
+// h1[row][256] = tanh(W1 s_row + b1) for 128-row tiles (grid-stride), W1^T and the tile's s^T in
+// LDS. Wave w: rows 16 w .. 16 w + 15, the 16 neuron tiles in two halves of 8 (C = [neuron][row],
+// 32 accumulators); lane (g, e) stores neurons 16 t + 4 g .. + 3 of row e as one float4. Eight
+// waves share the block's W1^T (48 KiB) and stay within 128 registers: two blocks per CU give 4
+// waves per SIMD to overlap one wave's MFMAs with another's tanh and h1 stores (4-wave blocks,
+// 64-row tiles, all 16 tiles at once: LDS and registers allowed 2 waves per SIMD).
 template <int KS>
-__global__ void __launch_bounds__(256, 2) l1_fwd_kernel(const float *__restrict__ s, int S, int64_t rows,
-                                                     const float *__restrict__ W1, int ldw,
-                                                     const float *__restrict__ b1, float *__restrict__ h1) {
+__global__ void __launch_bounds__(64 * kL1Waves, 4) l1_fwd_kernel(const float *__restrict__ s, int S,
+                                                                  int64_t rows,
+                                                                  const float *__restrict__ W1, int ldw,
+                                                                  const float *__restrict__ b1,
+                                                                  float *__restrict__ h1) {
+    constexpr int NT = 64 * kL1Waves;           // threads
     __shared__ float w1t[4 * KS][kL1Ld];        // [k][neuron]
     __shared__ float st[4 * KS][kL1SLd];        // [k][row]
     const int t = threadIdx.x, lane = t & 63, g = lane >> 4, e = lane & 15, w = t >> 6;
-    for (int i = t; i < 4 * KS * 256; i += 256) {
+    for (int i = t; i < 4 * KS * 256; i += NT) {
         const int n = i / (4 * KS), k = i - n * (4 * KS);
         w1t[k][n] = k < S ? W1[(int64_t)n * ldw + k] : 0.f;
     }
     const float invS = 1.f / (float)S;
     const int64_t ntiles = (rows + kL1Rows - 1) / kL1Rows;
-    // the tile's s span (nr * S <= 64 * 4 KS floats, contiguous) in registers, loaded one tile ahead
-    // so that its latency hides under the current tile's MFMAs and stores
-    constexpr int NSV = (kL1Rows * 4 * KS + 255) / 256;
+    // the tile's s span (nr * S <= 128 * 4 KS floats, contiguous) in registers, loaded one tile
+    // ahead so that its latency hides under the current tile's MFMAs and stores
+    constexpr int NSV = (kL1Rows * 4 * KS + NT - 1) / NT;
     float sv[NSV];
     auto load_s = [&](int64_t tile) {
         const int64_t r0 = tile * kL1Rows;
@@ -2738,7 +2745,7 @@ __global__ void __launch_bounds__(256, 2) l1_fwd_kernel(const float *__restrict_
         const float *src = s + r0 * S;
 #pragma unroll
         for (int u = 0; u < NSV; ++u) {
-            const int f = t + 256 * u;
+            const int f = t + NT * u;
             sv[u] = f < n ? src[f] : 0.f;
         }
     };
@@ -2747,13 +2754,13 @@ __global__ void __launch_bounds__(256, 2) l1_fwd_kernel(const float *__restrict_
         const int64_t r0 = tile * kL1Rows;
         const int nr = (int)(rows - r0 < kL1Rows ? rows - r0 : kL1Rows);
         __syncthreads();  // the previous tile's s^T is read
-        for (int f = t; f < kL1Rows * 4 * KS; f += 256) {  // zero the padding columns / rows first
+        for (int f = t; f < kL1Rows * 4 * KS; f += NT) {  // zero the padding columns / rows first
             const int k = f / kL1Rows, r = f - k * kL1Rows;
             if (k >= S || r >= nr) st[k][r] = 0.f;
         }
 #pragma unroll
         for (int u = 0; u < NSV; ++u) {  // the span transposed into st (row r, feature f - r S)
-            const int f = t + 256 * u;
+            const int f = t + NT * u;
             if (f < nr * S) {
                 const int r = l1_row(f, invS);
                 st[f - r * S][r] = sv[u];
@@ -2761,28 +2768,30 @@ __global__ void __launch_bounds__(256, 2) l1_fwd_kernel(const float *__restrict_
         }
         __syncthreads();
         load_s(tile + gridDim.x);
-        floatx4 acc[16];
-#pragma unroll
-        for (int nt = 0; nt < 16; ++nt) {
-            const floatx4 b = *reinterpret_cast<const floatx4 *>(b1 + 16 * nt + 4 * g);
-            acc[nt] = b;
-        }
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
-            const float bv = st[4 * kk + g][16 * w + e];
-#pragma unroll
-            for (int nt = 0; nt < 16; ++nt)
-                acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1t[4 * kk + g][16 * nt + e], bv, acc[nt], 0, 0, 0);
-        }
         const int r = 16 * w + e;
-        if (r < nr) {
-            float *dst = h1 + (r0 + r) * 256 + 4 * g;
+#pragma unroll 1
+        for (int hf = 0; hf < 2; ++hf) {  // neurons 128 hf .. 128 hf + 127: 32 accumulators
+            floatx4 acc[8];
 #pragma unroll
-            for (int nt = 0; nt < 16; ++nt) {
-                floatx4 v;
+            for (int nt = 0; nt < 8; ++nt)
+                acc[nt] = *reinterpret_cast<const floatx4 *>(b1 + 128 * hf + 16 * nt + 4 * g);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = tanh_x3(acc[nt][q]);
-                *reinterpret_cast<floatx4 *>(dst + 16 * nt) = v;
+            for (int kk = 0; kk < KS; ++kk) {
+                const float bv = st[4 * kk + g][16 * w + e];
+#pragma unroll
+                for (int nt = 0; nt < 8; ++nt)
+                    acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1t[4 * kk + g][128 * hf + 16 * nt + e],
+                                                                   bv, acc[nt], 0, 0, 0);
+            }
+            if (r < nr) {
+                float *dst = h1 + (r0 + r) * 256 + 128 * hf + 4 * g;
+#pragma unroll
+                for (int nt = 0; nt < 8; ++nt) {
+                    floatx4 v;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] = tanh_x3(acc[nt][q]);
+                    *reinterpret_cast<floatx4 *>(dst + 16 * nt) = v;
+                }
             }
         }
     }
@@ -2900,8 +2909,8 @@ void ppo2_ext_h1(const float *W1, int ldw, const float *b1, int S, int H, const 
                  int64_t rows, float *h1, hipStream_t st) {
     (void)H;
     const int64_t ntiles = (rows + kL1Rows - 1) / kL1Rows;
-    const int grid = (int)(ntiles < 4096 ? ntiles : 4096);
-    l1_fwd_kernel<11><<<grid, 256, 0, st>>>(s, S, rows, W1, ldw, b1, h1);
+    const int grid = (int)(ntiles < 2048 ? ntiles : 2048);
+    l1_fwd_kernel<11><<<grid, 64 * kL1Waves, 0, st>>>(s, S, rows, W1, ldw, b1, h1);
 }
 void ppo2_ext_dw1(const float *g1, const float *h1, const float *s, int S, int H, int64_t rows,
                   float *part, float *gW, float *gb, hipStream_t st) {
