@@ -90,11 +90,27 @@ __global__ void __launch_bounds__(1024) mfma_scale_kernel(MfmaNet net, const flo
     const int S = net.S, H = net.H;
     const float *W2 = P + S * H + H;
     float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int i0 = threadIdx.x; i0 < H * H; i0 += 8 * 1024) {
+    if ((((uintptr_t)W2) & 15) == 0) {  // 16-byte loads, all of a thread's in flight at once
+        const float4 *W4 = reinterpret_cast<const float4 *>(W2);  // (H * H % 4 == 0: H even)
+        for (int i0 = threadIdx.x; i0 < H * H / 4; i0 += 16 * 1024) {
+            float4 q[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = i0 + u * 1024;
-            if (i < H * H) m[u] = fmaxf(m[u], fabsf(W2[i]));
+            for (int u = 0; u < 16; ++u) {
+                const int i = i0 + u * 1024;
+                q[u] = i < H * H / 4 ? W4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                m[u & 7] = fmaxf(m[u & 7], fmaxf(fmaxf(fabsf(q[u].x), fabsf(q[u].y)),
+                                                 fmaxf(fabsf(q[u].z), fabsf(q[u].w))));
+        }
+    } else {
+        for (int i0 = threadIdx.x; i0 < H * H; i0 += 8 * 1024) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * 1024;
+                if (i < H * H) m[u] = fmaxf(m[u], fabsf(W2[i]));
+            }
         }
     }
     float mm = fmaxf(fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3])), fmaxf(fmaxf(m[4], m[5]), fmaxf(m[6], m[7])));
