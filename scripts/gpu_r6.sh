@@ -96,7 +96,7 @@ if [ "${FD_AB:-0}" = 1 ]; then
           -- python3 "$ROOT/bench.py" --no-cpu-baseline --ddpg 0 --sac 0 --oa 0 --fp32-leg 0 --hbm 0 --uav 0 \
              --demo-e2e ${FD_DEMO:-0} --e2e 1 --e2e-k30 1 --steps 3 --warmup 1) > "$OUT/fd$i.log" 2>&1
       rc=$?; step_rc $rc "FD A/B $lib"
-      kstats "$OUT/fd$i" | grep -E "ppo2_fd|ppo2_wgrad|rollout_sp|l1_|fg_grad|mfma_scale|mfma_pack" > "$OUT/fd${i}_stats.txt"
+      kstats "$OUT/fd$i" | grep -E "ppo2_fd|ppo2_wgrad|rollout_sp|l1_|fg_grad|mfma_scale|mfma_pack|ppo2_reduce" > "$OUT/fd${i}_stats.txt"
       python3 - "$OUT/fd$i.log" "$lib" >> "$OUT/progress.log" <<'PY'
 import json, sys
 for line in open(sys.argv[1]):
